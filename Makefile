@@ -1,0 +1,39 @@
+# Builds the MI355X engine (narwhal_amd/libnarwhal_amd.so, gfx950 only), the CPU oracle
+# (test infrastructure) and the host arithmetic check library (test infrastructure).
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -Inarwhal_amd/csrc -Wall -Wno-unused-function
+CSRC := narwhal_amd/csrc
+HDRS := $(wildcard $(CSRC)/*.hpp) $(CSRC)/nw_kernels.h include/narwhal_amd.h
+LIB := narwhal_amd/libnarwhal_amd.so
+BUILD := build
+
+all: $(LIB) oracle hostcheck
+
+$(BUILD)/nw_kernels.o: $(CSRC)/nw_kernels.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/nw_api.o: $(CSRC)/nw_api.cpp $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIB): $(BUILD)/nw_kernels.o $(BUILD)/nw_api.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+oracle:
+	$(MAKE) -s -C oracle
+
+hostcheck: tools/libnw_hostcheck.so
+tools/libnw_hostcheck.so: tools/hostcheck.hip $(HDRS)
+	$(HIPCC) --cuda-host-only -O2 -std=c++17 -fPIC -shared -Iinclude $< -o $@
+
+ubench: tools/ubench_valu
+tools/ubench_valu: tools/ubench_valu.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 $< -o $@
+
+clean:
+	rm -rf $(BUILD) $(LIB) tools/libnw_hostcheck.so
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all oracle hostcheck ubench clean

@@ -1,0 +1,123 @@
+/*
+ * narwhal_amd.h — C ABI of the MI355X (gfx950) verification engine for Narwhal's `crypto`
+ * crate hot path. Plain pointers and sizes only; thread-safe; no exceptions or aborts
+ * cross this boundary.
+ *
+ * Reference interface each entry point replaces (paths under /root/reference):
+ *   nw_signature_verify          crypto/src/lib.rs:200-204  Signature::verify(&Digest, &PublicKey)
+ *   nw_signature_verify_batch    crypto/src/lib.rs:206-219  Signature::verify_batch(&Digest, votes)
+ *   nw_verify_strict_many        crypto/src/lib.rs:200-204  (bulk form of verify, for the
+ *                                primary's header/vote stream, primary/src/core.rs:306-336)
+ *   nw_verify_batch_many         crypto/src/lib.rs:206-219  (bulk form of verify_batch, one
+ *                                batch per certificate, primary/src/messages.rs:214)
+ *   nw_sha512_digest32_many      worker/src/processor.rs:38, worker/src/batch_maker.rs:124-128,
+ *                                primary/src/messages.rs:70-84,145-153,226-234
+ *                                (Digest(Sha512::digest(bytes)[..32]))
+ *   nw_dev_*                     the same work on device-resident buffers, asynchronous on a
+ *                                caller stream (hipStream_t passed as void*)
+ *
+ * Return values: 0 (NW_OK) = valid / success; positive NW_ERR_* = the item is invalid
+ * (the reference's CryptoError, with the first failing check named); negative NW_E_* =
+ * runtime/device error, never conflated with "invalid". There is no CPU fallback: on a
+ * host without a usable gfx950 device every call returns NW_E_NO_DEVICE.
+ */
+#ifndef NARWHAL_AMD_H
+#define NARWHAL_AMD_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NW_ABI_VERSION 1
+
+/* Per-item verdicts (check order = the reference's, see DESIGN.md "Semantics"). */
+#define NW_OK 0
+#define NW_ERR_S_HIGH_BITS 1      /* sig[63] & 0xE0 (ed25519::Signature::from_bytes)        */
+#define NW_ERR_S_NONCANONICAL 2   /* s >= l (dalek check_scalar)                            */
+#define NW_ERR_A_DECODE 3         /* public key does not decompress                         */
+#define NW_ERR_R_DECODE 4         /* R does not decompress                                  */
+#define NW_ERR_A_SMALL_ORDER 5    /* verify (strict) only                                   */
+#define NW_ERR_R_SMALL_ORDER 6    /* verify (strict) only                                   */
+#define NW_ERR_EQUATION 7         /* strict: [s]B != R + [k]A; batch: RLC sum != identity   */
+
+/* Runtime errors. */
+#define NW_E_INVALID_ARG (-1)
+#define NW_E_NO_DEVICE (-2)
+#define NW_E_DEVICE (-3)
+#define NW_E_OUT_OF_MEMORY (-4)
+
+/* ---- runtime ----------------------------------------------------------------------- */
+/* Initialise every visible gfx950 device (idempotent). Returns the device count (>0) or a
+ * negative NW_E_*. All other calls initialise lazily. */
+int nw_init(void);
+/* Number of usable devices (0 if none). */
+int nw_device_count(void);
+/* Device used by the calling thread's host-buffer calls (default 0). */
+int nw_set_device(int device);
+int nw_get_device(void);
+/* Human-readable description of the calling thread's last error ("" if none). */
+const char* nw_last_error(void);
+/* "narwhal_amd <version> gfx950". */
+const char* nw_version(void);
+/* Wait for all work this thread queued on its device stream. */
+int nw_synchronize(void);
+
+/* ---- host-buffer (blocking) entry points: the drop-in ------------------------------ */
+
+/* Digest(Sha512(m_i)[..32]) for n messages at data + offsets[i], lengths[i] bytes.
+ * out32: n x 32 bytes. */
+int nw_sha512_digest32_many(const uint8_t* data, const uint64_t* offsets,
+                            const uint64_t* lengths, size_t n, uint8_t* out32);
+
+/* crypto::Signature::verify: sig = part1 (R) || part2 (s), 64 bytes; digest 32 bytes;
+ * pk 32 bytes. Returns NW_OK, an NW_ERR_* code, or a negative runtime error. */
+int nw_signature_verify(const uint8_t sig[64], const uint8_t digest[32], const uint8_t pk[32]);
+
+/* n strict verifications. digests: n x 32 bytes (digest_stride = 32) or one shared digest
+ * (digest_stride = 0). status_out (optional): n x int32 verdicts. bitmap_out (optional):
+ * ceil(n/8) bytes, bit i (LSB-first) set iff item i is valid. */
+int nw_verify_strict_many(const uint8_t* digests, size_t digest_stride, const uint8_t* pks,
+                          const uint8_t* sigs, size_t n, int32_t* status_out,
+                          uint8_t* bitmap_out);
+
+/* crypto::Signature::verify_batch(digest, votes) over n (pk, sig) pairs sharing one digest.
+ * z16: optional n x 16-byte little-endian 128-bit coefficients (deterministic tests); NULL =
+ * fresh coefficients from the OS CSPRNG (the reference draws them from thread_rng).
+ * Returns NW_OK (also for n == 0), the first failing check in reference order, or a
+ * negative runtime error. fail_index (optional): failing item, or n for the equation. */
+int nw_signature_verify_batch(const uint8_t digest[32], const uint8_t* pks,
+                              const uint8_t* sigs, size_t n, const uint8_t* z16,
+                              size_t* fail_index);
+
+/* nbatches independent verify_batch calls. Batch b = items [offsets[b], offsets[b+1]) of
+ * pks/sigs (and z16 if given) with digest digests + 32 b. status_out: nbatches x int32. */
+int nw_verify_batch_many(const uint8_t* digests, const uint8_t* pks, const uint8_t* sigs,
+                         const uint64_t* offsets, size_t nbatches, const uint8_t* z16,
+                         int32_t* status_out);
+
+/* ---- device-pointer (asynchronous) entry points ------------------------------------ */
+/* All pointers are device pointers on the current device; work is queued on `stream`
+ * (a hipStream_t; NULL = the library's per-thread stream) and the call returns without
+ * waiting. */
+int nw_dev_sha512_digest32_many(const void* data, const uint64_t* offsets,
+                                const uint64_t* lengths, size_t n, void* out32, void* stream);
+
+int nw_dev_verify_strict_many(const void* digests, size_t digest_stride, const void* pks,
+                              const void* sigs, size_t n, int32_t* status_out,
+                              void* bitmap_out, void* stream);
+
+/* Workspace bytes nw_dev_verify_batch_many needs for nitems items. */
+size_t nw_dev_verify_batch_workspace(size_t nitems);
+/* z16 NULL: coefficients drawn on the device from ChaCha20 keyed by zkey32 (32 bytes from
+ * the OS CSPRNG if zkey32 is NULL). fail_index (optional, device): nbatches x uint64. */
+int nw_dev_verify_batch_many(const void* digests, const void* pks, const void* sigs,
+                             const uint64_t* offsets, size_t nbatches, size_t nitems,
+                             const void* z16, const uint8_t* zkey32, void* workspace,
+                             int32_t* status_out, uint64_t* fail_index, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NARWHAL_AMD_H */

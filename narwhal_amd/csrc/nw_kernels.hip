@@ -1,0 +1,497 @@
+// nw_kernels.hip — gfx950 kernels for Narwhal's crypto hot path.
+//
+//   k_sha512_digest32     Digest(Sha512(m)[..32]) for many messages, one lane per message
+//                         (worker/src/processor.rs:38, primary/src/messages.rs:70-84 ...).
+//   k_verify_strict       crypto::Signature::verify (crypto/src/lib.rs:200-204), one lane per
+//                         signature: decompress A and R, small-order tests, k = H(R||A||M)
+//                         mod l, [s]B + [k](-A) by a joint signed-window ladder (A table in
+//                         per-lane scratch, 8-bit B table in LDS), projective compare with R.
+//   k_batch_items         per-vote half of crypto::Signature::verify_batch
+//                         (crypto/src/lib.rs:206-219 -> dalek verify_batch [ext]): parse and
+//                         decode flags, k_i, z_i, P_i = z_i R_i + (z_i k_i mod l) A_i,
+//                         b_i = z_i s_i mod l.
+//   k_batch_reduce        one workgroup per batch: first failure in reference order, else
+//                         sum P_i - (sum b_i) B == identity.
+//
+// Everything here is integer VALU work; no MFMA (modular arithmetic is not a contraction).
+#include "nw_kernels.h"
+#include "nw_point.hpp"
+#include "nw_scalar.hpp"
+#include "nw_sha512.hpp"
+#include "nw_ladder.hpp"
+#include "nw_consts.hpp"
+
+#include <mutex>
+
+namespace nw {
+
+struct dev_consts {
+  curve_consts k;
+  ge_niels btab[129];   // j * B, j = 0..128, affine niels (signed 8-bit windows)
+};
+
+__constant__ dev_consts g_consts;
+
+static constexpr int BT_WORDS = 129 * 30;
+
+// ---------------------------------------------------------------------------------------
+// Small helpers
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// Copy the B table from constant memory into LDS (all threads of the block).
+__device__ __forceinline__ void load_btab(ge_niels* s_btab) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&g_consts.btab[0]);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(s_btab);
+  for (int i = threadIdx.x; i < BT_WORDS; i += blockDim.x) dst[i] = src[i];
+}
+
+// SHA-512 of the 96-byte R || A || M (one block) -> 16 LE words of the digest.
+__device__ __forceinline__ void hram96(uint32_t x[16], const uint32_t R[8], const uint32_t A[8],
+                                       const uint32_t M[8]) {
+  uint64_t w[16], st[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    w[i] = ((uint64_t)bswap32(R[2 * i]) << 32) | bswap32(R[2 * i + 1]);
+    w[4 + i] = ((uint64_t)bswap32(A[2 * i]) << 32) | bswap32(A[2 * i + 1]);
+    w[8 + i] = ((uint64_t)bswap32(M[2 * i]) << 32) | bswap32(M[2 * i + 1]);
+  }
+  w[12] = 0x8000000000000000ULL;
+  w[13] = 0;
+  w[14] = 0;
+  w[15] = 96 * 8;
+  sha512_init(st);
+  sha512_compress(st, w);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    x[2 * i] = bswap32((uint32_t)(st[i] >> 32));
+    x[2 * i + 1] = bswap32((uint32_t)st[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// SHA-512 digests of many messages (lane per message)
+// ---------------------------------------------------------------------------------------
+// Loads 128 bytes starting at byte address p (any alignment) as 16 big-endian u64 words.
+// Only dwords that contain message bytes are read (no over-read past the message).
+__device__ __forceinline__ void load_block_full(uint64_t w[16], const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3) * 8;
+  uint32_t d[33];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) d[i] = q[i];
+  d[32] = sh ? q[32] : 0u;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    // little-endian message dwords, realigned by the byte offset
+    const uint32_t lo = __builtin_amdgcn_alignbit(d[2 * i + 1], d[2 * i], sh);
+    const uint32_t hi = __builtin_amdgcn_alignbit(d[2 * i + 2], d[2 * i + 1], sh);
+    w[i] = ((uint64_t)bswap32(lo) << 32) | bswap32(hi);
+  }
+}
+
+// Tail block(s): message bytes [base, len) followed by 0x80, zeros, and (if last) the
+// 128-bit big-endian bit length in the final 16 bytes.
+__device__ __forceinline__ void load_block_tail(uint64_t w[16], const uint8_t* msg, uint64_t base,
+                                                uint64_t len, bool last) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const uint64_t pos = base + 8 * i + b;
+      uint32_t byte = 0;
+      if (pos < len) byte = msg[pos];
+      else if (pos == len) byte = 0x80;
+      v = (v << 8) | byte;
+    }
+    w[i] = v;
+  }
+  if (last) {
+    w[14] = len >> 61;
+    w[15] = len << 3;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_sha512_digest32(const uint8_t* __restrict__ data,
+                                                         const uint64_t* __restrict__ offsets,
+                                                         const uint64_t* __restrict__ lengths,
+                                                         uint64_t n, uint32_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* msg = data + offsets[i];
+  const uint64_t len = lengths[i];
+  const uint64_t nblocks = (len + 17 + 127) / 128;
+  const uint64_t nfull = len / 128;   // blocks entirely inside the message
+  uint64_t st[8], w[16];
+  sha512_init(st);
+#pragma unroll 1
+  for (uint64_t k = 0; k < nfull; ++k) {
+    load_block_full(w, msg + 128 * k);
+    sha512_compress(st, w);
+  }
+#pragma unroll 1
+  for (uint64_t k = nfull; k < nblocks; ++k) {
+    load_block_tail(w, msg, 128 * k, len, k + 1 == nblocks);
+    sha512_compress(st, w);
+  }
+  uint32_t* o = out + 8 * i;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[2 * j] = bswap32((uint32_t)(st[j] >> 32));
+    o[2 * j + 1] = bswap32((uint32_t)st[j]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Strict verification
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int strict_status(bool s_high, bool okA, bool s_canon, bool okR,
+                                             bool smallR, bool smallA, bool eq) {
+  // Reference order: crypto/src/lib.rs:201 (s high bits), 202 (decompress A), then dalek
+  // verify_strict: check_scalar, decompress R, small order (R || A), equation.
+  if (s_high) return NW_ERR_S_HIGH_BITS;
+  if (!okA) return NW_ERR_A_DECODE;
+  if (!s_canon) return NW_ERR_S_NONCANONICAL;
+  if (!okR) return NW_ERR_R_DECODE;
+  if (smallR) return NW_ERR_R_SMALL_ORDER;
+  if (smallA) return NW_ERR_A_SMALL_ORDER;
+  if (!eq) return NW_ERR_EQUATION;
+  return NW_OK;
+}
+
+__global__ __launch_bounds__(256) void k_verify_strict(const uint32_t* __restrict__ msgs,
+                                                       uint32_t msg_stride_words,
+                                                       const uint32_t* __restrict__ pks,
+                                                       const uint32_t* __restrict__ sigs,
+                                                       uint64_t n, int32_t* __restrict__ status,
+                                                       uint64_t* __restrict__ bitmap) {
+  __shared__ ge_niels s_btab[129];
+  load_btab(s_btab);
+  __syncthreads();
+  const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = gi < n;
+  const uint64_t i = active ? gi : n - 1;
+  const curve_consts& K = g_consts.k;
+
+  uint32_t Aw[8], Rw[8], Sw[8], Mw[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    Aw[j] = pks[8 * i + j];
+    Rw[j] = sigs[16 * i + j];
+    Sw[j] = sigs[16 * i + 8 + j];
+    Mw[j] = msgs[(uint64_t)msg_stride_words * i + j];
+  }
+  const bool s_high = (Sw[7] >> 29) != 0;
+  sc s;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s.w[j] = Sw[j];
+  const bool s_canon = sc_is_canonical(s);
+
+  ge A, R;
+  const bool okA = ge_frombytes(A, Aw, K);
+  const bool okR = ge_frombytes(R, Rw, K);
+  const bool smallA = ge_is_small_order(A);
+  const bool smallR = ge_is_small_order(R);
+
+  uint32_t hx[16];
+  hram96(hx, Rw, Aw, Mw);
+  sc k;
+  sc_reduce512(k, hx);
+
+  // [s]B + [k](-A)
+  ge minusA;
+  ge_neg(minusA, A);
+  ge_cached tab[9];
+  build_table9(tab, minusA, K.d2);
+  sc s_use = s;
+  if (!s_canon || s_high) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s_use.w[j] = 0;   // keep digits in range; verdict is Err anyway
+  }
+  ge acc;
+  dsm_var_base(acc, tab, k, s_use, s_btab);
+  const bool eq = ge_eq_affine(acc, R);
+
+  const int st = strict_status(s_high, okA, s_canon, okR, smallR, smallA, eq);
+  if (active) status[gi] = st;
+  const uint64_t mask = __ballot(active && st == NW_OK);
+  if ((threadIdx.x & 63) == 0 && gi < n) bitmap[gi >> 6] = mask;
+}
+
+// ---------------------------------------------------------------------------------------
+// Batch verification (random linear combination)
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+
+// z_i = ChaCha20(key, nonce, block i/4) bytes [16 (i%4), 16 (i%4) + 16) (DJB layout).
+__device__ __forceinline__ void chacha20_z(uint32_t z[4], const uint32_t key[8],
+                                           uint64_t nonce, uint64_t i) {
+  uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key[0], key[1],
+                    key[2], key[3], key[4], key[5], key[6], key[7], (uint32_t)(i >> 2),
+                    (uint32_t)(i >> 34), (uint32_t)nonce, (uint32_t)(nonce >> 32)};
+  uint32_t x[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) x[j] = s[j];
+#define NW_QR(a, b, c, d)                                                   \
+  x[a] += x[b]; x[d] ^= x[a]; x[d] = rotl32(x[d], 16); x[c] += x[d];        \
+  x[b] ^= x[c]; x[b] = rotl32(x[b], 12); x[a] += x[b]; x[d] ^= x[a];        \
+  x[d] = rotl32(x[d], 8); x[c] += x[d]; x[b] ^= x[c]; x[b] = rotl32(x[b], 7);
+#pragma unroll 1
+  for (int r = 0; r < 10; ++r) {
+    NW_QR(0, 4, 8, 12) NW_QR(1, 5, 9, 13) NW_QR(2, 6, 10, 14) NW_QR(3, 7, 11, 15)
+    NW_QR(0, 5, 10, 15) NW_QR(1, 6, 11, 12) NW_QR(2, 7, 8, 13) NW_QR(3, 4, 9, 14)
+  }
+#undef NW_QR
+  const int q = (int)(i & 3) * 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint32_t v = x[0] + s[0];
+#pragma unroll
+    for (int t = 1; t < 16; ++t) v = (q + j == t) ? x[t] + s[t] : v;
+    z[j] = v;
+  }
+}
+
+// Per-item flags (bit set = check FAILED).
+enum : uint32_t { BF_S_HIGH = 1, BF_A_DECODE = 2, BF_S_NONCANON = 4, BF_R_DECODE = 8 };
+
+__global__ __launch_bounds__(256) void k_batch_items(
+    const uint32_t* __restrict__ digests, const uint64_t* __restrict__ offsets,
+    uint64_t nbatches, const uint32_t* __restrict__ pks, const uint32_t* __restrict__ sigs,
+    uint64_t nitems, const uint32_t* __restrict__ z16, z_key_t zkey,
+    ge* __restrict__ out_pts, sc* __restrict__ out_b, uint32_t* __restrict__ out_flags) {
+  const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi >= nitems) return;
+  const curve_consts& K = g_consts.k;
+  // batch of this item: largest b with offsets[b] <= gi
+  uint64_t lo = 0, hi = nbatches;
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (offsets[mid] <= gi) lo = mid; else hi = mid;
+  }
+  uint32_t Aw[8], Rw[8], Sw[8], Mw[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    Aw[j] = pks[8 * gi + j];
+    Rw[j] = sigs[16 * gi + j];
+    Sw[j] = sigs[16 * gi + 8 + j];
+    Mw[j] = digests[8 * lo + j];
+  }
+  uint32_t flags = 0;
+  if ((Sw[7] >> 29) != 0) flags |= BF_S_HIGH;
+  sc s;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s.w[j] = Sw[j];
+  if (!sc_is_canonical(s)) flags |= BF_S_NONCANON;
+  ge A, R;
+  if (!ge_frombytes(A, Aw, K)) flags |= BF_A_DECODE;
+  if (!ge_frombytes(R, Rw, K)) flags |= BF_R_DECODE;
+
+  uint32_t hx[16];
+  hram96(hx, Rw, Aw, Mw);
+  sc k;
+  sc_reduce512(k, hx);
+  sc z;
+  uint32_t zw[4];
+  if (z16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) zw[j] = z16[4 * gi + j];
+  } else {
+    chacha20_z(zw, zkey.key, zkey.nonce, gi);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z.w[j] = j < 4 ? zw[j] : 0u;
+  sc c, b;
+  sc_mul(c, z, k);   // (z_i k_i) mod l
+  if (flags & (BF_S_HIGH | BF_S_NONCANON)) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s.w[j] = 0;
+  }
+  sc_mul(b, z, s);   // (z_i s_i) mod l
+
+  // P_i = [z_i] R_i + [c_i] A_i, one joint ladder: 4-bit signed digits for both.
+  ge_cached tabA[9], tabR[9];
+  build_table9(tabA, A, K.d2);
+  build_table9(tabR, R, K.d2);
+  uint32_t cc[8], zz[8];
+  sc_recode(cc, c, 0x88888888u);
+  sc_recode(zz, z, 0x88888888u);
+  ge acc;
+  ge_identity(acc);
+#pragma unroll 1
+  for (int i = 63; i >= 0; --i) {
+    if (i != 63) {
+#pragma unroll 1
+      for (int t = 0; t < 3; ++t) ge_dbl(acc, acc, false);
+      ge_dbl(acc, acc, true);
+    }
+    const bool rdig = i <= 32;   // z < 2^128: digits above 32 are zero
+    const int da = (int)((sel8(cc, i >> 3) >> ((i & 7) * 4)) & 15u) - 8;
+    add_digit_cached(acc, tabA, da, true);
+    if (rdig) {
+      const int dr = (int)((sel8(zz, i >> 3) >> ((i & 7) * 4)) & 15u) - 8;
+      add_digit_cached(acc, tabR, dr, true);
+    }
+  }
+  out_pts[gi] = acc;
+  out_b[gi] = b;
+  out_flags[gi] = flags;
+}
+
+// One workgroup per batch.
+__global__ __launch_bounds__(256) void k_batch_reduce(const uint64_t* __restrict__ offsets,
+                                                      uint64_t nbatches,
+                                                      const ge* __restrict__ pts,
+                                                      const sc* __restrict__ bs,
+                                                      const uint32_t* __restrict__ flags,
+                                                      int32_t* __restrict__ status,
+                                                      uint64_t* __restrict__ fail_index) {
+  __shared__ ge_niels s_btab[129];
+  __shared__ ge s_pts[256];
+  __shared__ sc s_b[256];
+  __shared__ unsigned long long s_first[3];
+  load_btab(s_btab);
+  const uint64_t bidx = blockIdx.x;
+  const uint64_t beg = offsets[bidx], end = offsets[bidx + 1];
+  const int tid = threadIdx.x;
+  if (tid < 3) s_first[tid] = ~0ULL;
+  __syncthreads();
+  const curve_consts& K = g_consts.k;
+
+  // First failures, in reference order (crypto/src/lib.rs:214-217 then dalek):
+  //   [0] first vote whose signature parse (s high bits) or key decompression fails
+  //   [1] first non-canonical s (dalek InternalSignature::try_from)
+  //   [2] first R that fails to decompress (optional_multiscalar_mul -> None)
+  ge acc;
+  ge_identity(acc);
+  sc bsum;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bsum.w[j] = 0;
+  for (uint64_t i = beg + tid; i < end; i += blockDim.x) {
+    const uint32_t f = flags[i];
+    const unsigned long long rel = i - beg;
+    if (f & (BF_S_HIGH | BF_A_DECODE)) atomicMin(&s_first[0], rel);
+    if (f & BF_S_NONCANON) atomicMin(&s_first[1], rel);
+    if (f & BF_R_DECODE) atomicMin(&s_first[2], rel);
+    ge_cached c;
+    ge_to_cached(c, pts[i], K.d2);
+    ge_add_cached(acc, acc, c, true);
+    sc_add(bsum, bsum, bs[i]);
+  }
+  s_pts[tid] = acc;
+  s_b[tid] = bsum;
+  __syncthreads();
+  for (int stride = 128; stride > 0; stride >>= 1) {
+    if (tid < stride) {
+      ge_cached c;
+      ge_to_cached(c, s_pts[tid + stride], K.d2);
+      ge t;
+      ge_add_cached(t, s_pts[tid], c, true);
+      s_pts[tid] = t;
+      sc u;
+      sc_add(u, s_b[tid], s_b[tid + stride]);
+      s_b[tid] = u;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const uint64_t n = end - beg;
+    int st = NW_OK;
+    uint64_t idx = n;
+    if (s_first[0] != ~0ULL) {
+      idx = s_first[0];
+      st = (flags[beg + idx] & BF_S_HIGH) ? NW_ERR_S_HIGH_BITS : NW_ERR_A_DECODE;
+    } else if (s_first[1] != ~0ULL) {
+      idx = s_first[1];
+      st = NW_ERR_S_NONCANONICAL;
+    } else if (s_first[2] != ~0ULL) {
+      idx = s_first[2];
+      st = NW_ERR_R_DECODE;
+    } else if (n > 0) {
+      // total = sum P_i + [-(sum b_i)] B ; dalek: is_identity() ? Ok : VerifyError
+      sc nb;
+      sc_neg(nb, s_b[0]);
+      ge bB;
+      fixed_base_mul(bB, nb, s_btab);
+      ge_cached c;
+      ge_to_cached(c, bB, K.d2);
+      ge total;
+      ge_add_cached(total, s_pts[0], c, false);
+      st = ge_is_identity(total) ? NW_OK : NW_ERR_EQUATION;
+    }
+    status[bidx] = st;
+    if (fail_index) fail_index[bidx] = idx;
+  }
+}
+
+}  // namespace nw
+
+// ---------------------------------------------------------------------------------------
+// Host side: constants and launchers
+// ---------------------------------------------------------------------------------------
+namespace nw {
+
+hipError_t upload_consts() {
+  static dev_consts host;
+  static std::once_flag once;
+  std::call_once(once, [] { compute_consts(host.k, host.btab); });
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_consts), &host, sizeof(host), 0,
+                           hipMemcpyHostToDevice);
+}
+
+static inline unsigned grid_for(uint64_t n, unsigned block) {
+  return (unsigned)((n + block - 1) / block);
+}
+
+hipError_t launch_sha512_digest32(const uint8_t* data, const uint64_t* offsets,
+                                  const uint64_t* lengths, uint64_t n, uint32_t* out,
+                                  hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sha512_digest32, dim3(grid_for(n, 256)), dim3(256), 0, stream, data,
+                     offsets, lengths, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
+                                const uint32_t* pks, const uint32_t* sigs, uint64_t n,
+                                int32_t* status, uint64_t* bitmap, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_verify_strict, dim3(grid_for(n, 256)), dim3(256), 0, stream, msgs,
+                     msg_stride_words, pks, sigs, n, status, bitmap);
+  return hipGetLastError();
+}
+
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+size_t batch_workspace_bytes(uint64_t nitems) {
+  const uint64_t m = nitems ? nitems : 1;
+  return align256(sizeof(ge) * m) + align256(sizeof(sc) * m) + align256(sizeof(uint32_t) * m);
+}
+
+hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
+                               uint64_t nbatches, const uint32_t* pks, const uint32_t* sigs,
+                               uint64_t nitems, const uint32_t* z16, const z_key_t& zkey,
+                               void* workspace, int32_t* status, uint64_t* fail_index,
+                               hipStream_t stream) {
+  if (nbatches == 0) return hipSuccess;
+  const uint64_t m = nitems ? nitems : 1;
+  char* ws = static_cast<char*>(workspace);
+  ge* pts = reinterpret_cast<ge*>(ws);
+  sc* bs = reinterpret_cast<sc*>(ws + align256(sizeof(ge) * m));
+  uint32_t* flags =
+      reinterpret_cast<uint32_t*>(ws + align256(sizeof(ge) * m) + align256(sizeof(sc) * m));
+  if (nitems) {
+    hipLaunchKernelGGL(k_batch_items, dim3(grid_for(nitems, 256)), dim3(256), 0, stream,
+                       digests, offsets, nbatches, pks, sigs, nitems, z16, zkey, pts, bs,
+                       flags);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_batch_reduce, dim3((unsigned)nbatches), dim3(256), 0, stream, offsets,
+                     nbatches, pts, bs, flags, status, fail_index);
+  return hipGetLastError();
+}
+
+}  // namespace nw

@@ -1,0 +1,100 @@
+// nw_sha512.hpp — FIPS 180-4 SHA-512 compression for gfx950.
+//
+// 64-bit words live as 32-bit halves: a rotation is two v_alignbit_b32, Ch/Maj/xor3 are a
+// single v_bitop3_b32 each, additions are v_lshl_add_u64. Round constants are uniform
+// (wave-wide) and come from scalar loads.
+#pragma once
+#include "nw_field.hpp"
+
+namespace nw {
+
+__constant__ static const uint64_t SHA512_K[80] = {
+  0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
+  0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
+  0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+  0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,
+  0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+  0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+  0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,
+  0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,
+  0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+  0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+  0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,
+  0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+  0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,
+  0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,
+  0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+  0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,
+  0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,
+  0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+  0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
+  0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+
+static constexpr uint64_t SHA512_H0[8] = {
+  0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
+  0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+
+__device__ __forceinline__ uint64_t rotr64(uint64_t x, const int n) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  uint32_t rlo, rhi;
+  if (n < 32) {
+    rlo = __builtin_amdgcn_alignbit(hi, lo, n);
+    rhi = __builtin_amdgcn_alignbit(lo, hi, n);
+  } else {
+    rlo = __builtin_amdgcn_alignbit(lo, hi, n - 32);
+    rhi = __builtin_amdgcn_alignbit(hi, lo, n - 32);
+  }
+  return ((uint64_t)rhi << 32) | rlo;
+}
+__device__ __forceinline__ uint64_t shr64(uint64_t x, const int n) {   // n < 32
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return ((uint64_t)(hi >> n) << 32) | __builtin_amdgcn_alignbit(hi, lo, n);
+}
+__device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
+
+// 16 rounds; FIRST = the block words themselves, else the schedule is advanced in place.
+template <bool FIRST>
+__device__ __forceinline__ void sha512_16rounds(uint64_t& a, uint64_t& b, uint64_t& c,
+                                                uint64_t& d, uint64_t& e, uint64_t& f,
+                                                uint64_t& g, uint64_t& h, uint64_t w[16],
+                                                int r) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    uint64_t wj;
+    if (FIRST) {
+      wj = w[j];
+    } else {
+      const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+      const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ shr64(w15, 7);
+      const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ shr64(w2, 6);
+      wj = w[j] + s0 + w[(j + 9) & 15] + s1;
+      w[j] = wj;
+    }
+    const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
+    const uint64_t ch = (e & f) ^ (~e & g);
+    const uint64_t t1 = h + S1 + ch + SHA512_K[r + j] + wj;
+    const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
+    const uint64_t maj = (a & b) ^ (a & c) ^ (b & c);
+    const uint64_t t2 = S0 + maj;
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+}
+
+// One compression. w[16] = the block as big-endian 64-bit words (consumed as the
+// message-schedule window).
+__device__ __forceinline__ void sha512_compress(uint64_t st[8], uint64_t w[16]) {
+  uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6],
+           h = st[7];
+  sha512_16rounds<true>(a, b, c, d, e, f, g, h, w, 0);
+#pragma unroll 1
+  for (int r = 16; r < 80; r += 16) sha512_16rounds<false>(a, b, c, d, e, f, g, h, w, r);
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g;
+  st[7] += h;
+}
+
+__device__ __forceinline__ void sha512_init(uint64_t st[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) st[i] = SHA512_H0[i];
+}
+
+}  // namespace nw

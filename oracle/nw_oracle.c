@@ -451,6 +451,10 @@ static int ge_frombytes(ge* p, const uint8_t s[32]) {
 static ge GE_B;
 static ge GE_B_TABLE[16];   /* j * B, j = 0..15 */
 
+static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+static void init_constants(void);
+static inline void ensure_init(void);
+
 /* ------------------------------------------------------------------------------------ */
 /* Scalars mod l = 2^252 + 27742317777372353535851937790883648493 (u32 limbs, Barrett)   */
 /* ------------------------------------------------------------------------------------ */
@@ -535,12 +539,14 @@ static void sc_barrett(uint32_t out[8], const uint32_t x[16]) {
 }
 
 void nwo_scalar_reduce64(const uint8_t in[64], uint8_t out[32]) {
+  ensure_init();
   uint32_t x[16], o[8];
   bytes_to_u32(x, in, 16);
   sc_barrett(o, x);
   u32_to_bytes(out, o, 8);
 }
 void nwo_scalar_mul(const uint8_t a[32], const uint8_t b[32], uint8_t out[32]) {
+  ensure_init();
   uint32_t aw[8], bw[8], x[16], o[8];
   bytes_to_u32(aw, a, 8); bytes_to_u32(bw, b, 8);
   bn_mul(x, aw, 8, bw, 8);
@@ -548,6 +554,7 @@ void nwo_scalar_mul(const uint8_t a[32], const uint8_t b[32], uint8_t out[32]) {
   u32_to_bytes(out, o, 8);
 }
 void nwo_scalar_add(const uint8_t a[32], const uint8_t b[32], uint8_t out[32]) {
+  ensure_init();
   uint32_t aw[8], bw[8], x[16] = {0}, o[8];
   bytes_to_u32(aw, a, 8); bytes_to_u32(bw, b, 8);
   uint64_t c = 0;
@@ -658,7 +665,6 @@ static void ge_msm(ge* r, const uint8_t* scalars, const ge* pts, size_t n) {
 /* ------------------------------------------------------------------------------------ */
 /* Initialisation                                                                        */
 /* ------------------------------------------------------------------------------------ */
-static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 
 static void init_constants(void) {
   fe a, b, t;

@@ -1,0 +1,103 @@
+"""The kernels' arithmetic headers (narwhal_amd/csrc/nw_*.hpp), compiled as host code into
+tools/libnw_hostcheck.so (test infrastructure), against the CPU oracle on the golden
+fixtures and random inputs. Catches field/point/scalar/ladder bugs without a GPU; the GPU
+parity tests (test_gpu_parity.py) then check the kernels end to end."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "tools", "libnw_hostcheck.so")
+L = 2**252 + 27742317777372353535851937790883648493
+
+
+def _build():
+    srcs = [os.path.join(ROOT, "tools", "hostcheck.hip")] + [
+        os.path.join(ROOT, "narwhal_amd", "csrc", f) for f in os.listdir(os.path.join(ROOT, "narwhal_amd", "csrc"))
+        if f.endswith(".hpp")]
+    if os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(s) for s in srcs):
+        return
+    subprocess.run(["hipcc", "--cuda-host-only", "-O2", "-std=c++17", "-fPIC", "-shared",
+                    "-I" + os.path.join(ROOT, "include"), srcs[0], "-o", LIB], check=True)
+
+
+@pytest.fixture(scope="module")
+def hc():
+    _build()
+    lib = ctypes.CDLL(LIB)
+    for f in ("hc_decompress", "hc_is_small_order", "hc_dsm", "hc_verify_strict",
+              "hc_scalar_canonical"):
+        getattr(lib, f).restype = ctypes.c_int
+    return lib
+
+
+def _b(x):
+    return ctypes.c_char_p(bytes(x))
+
+
+def _out(n=32):
+    return ctypes.create_string_buffer(n)
+
+
+def test_decompress_and_small_order(hc, golden):
+    pts = set()
+    for it in golden["edge_corpus"]["items"]:
+        pts.add(bytes.fromhex(it["pk"]))
+        pts.add(bytes.fromhex(it["sig"])[:32])
+    rng = np.random.Generator(np.random.PCG64(1))
+    pts |= {rng.bytes(32) for _ in range(200)}
+    for p in pts:
+        o = _out()
+        ok = hc.hc_decompress(_b(p), o)
+        ref = O.decompress(p)
+        assert bool(ok) == (ref is not None), p.hex()
+        if ok:
+            assert o.raw == ref, p.hex()
+        assert hc.hc_is_small_order(_b(p)) == O.is_small_order(p), p.hex()
+
+
+def test_scalars(hc):
+    rng = np.random.Generator(np.random.PCG64(2))
+    edge = [bytes(64), (L).to_bytes(64, "little"), (L - 1).to_bytes(64, "little"),
+            (2**512 - 1).to_bytes(64, "little"), (L * (2**259)).to_bytes(64, "little")]
+    for x in edge + [rng.bytes(64) for _ in range(300)]:
+        o = _out()
+        hc.hc_reduce512(_b(x), o)
+        assert o.raw == O.scalar_reduce64(x)
+    for _ in range(300):
+        a, b = rng.bytes(32), rng.bytes(32)
+        o = _out()
+        hc.hc_scalar_mul(_b(a), _b(b), o)
+        assert o.raw == O.scalar_mul(a, b)
+        ar = O.scalar_reduce64(a + bytes(32))
+        br = O.scalar_reduce64(b + bytes(32))
+        hc.hc_scalar_add(_b(ar), _b(br), o)
+        assert o.raw == O.scalar_add(ar, br)
+    for v in [0, 1, L - 1, L, L + 1, 2**252, 2**253, 2**256 - 1]:
+        assert hc.hc_scalar_canonical(_b(v.to_bytes(32, "little"))) == (v < L)
+
+
+def test_fixed_base_and_dsm(hc):
+    rng = np.random.Generator(np.random.PCG64(3))
+    for i in range(60):
+        s = O.scalar_reduce64(rng.bytes(64))
+        o = _out()
+        hc.hc_fixed_base(_b(s), o)
+        assert o.raw == O.scalarmult_base(s)
+        a = O.scalar_reduce64(rng.bytes(64))
+        P = O.scalarmult_base(O.scalar_reduce64(rng.bytes(64)))
+        assert hc.hc_dsm(_b(a), _b(P), _b(s), o) == 1
+        ref = O.point_add(O.scalarmult_base(s), O.scalarmult(a, P))
+        assert o.raw == ref
+
+
+def test_verify_strict_edge_corpus(hc, golden):
+    for it in golden["edge_corpus"]["items"]:
+        m, pk, sig = (bytes.fromhex(it[k]) for k in ("msg", "pk", "sig"))
+        k = O.hram(sig[:32], pk, m)
+        assert hc.hc_verify_strict(_b(pk), _b(sig), _b(k)) == it["status"], it["class"]

@@ -1,0 +1,101 @@
+// hostcheck.hip — TEST INFRASTRUCTURE. Exposes the device arithmetic headers (compiled as
+// host code) through a C ABI so tests/test_hostcheck.py can compare the exact field /
+// point / scalar / ladder code the kernels run against the CPU oracle, without a GPU.
+// SHA-512 is device-only, so the verification entry takes k = H(R||A||M) mod l as input.
+#include <string.h>
+#include "../narwhal_amd/csrc/nw_consts.hpp"
+#include "../narwhal_amd/csrc/nw_ladder.hpp"
+
+using namespace nw;
+
+static curve_consts K;
+static ge_niels BT[129];
+static bool ready = false;
+static void init() { if (!ready) { compute_consts(K, BT); ready = true; } }
+
+static void load8(uint32_t w[8], const uint8_t* b) { memcpy(w, b, 32); }
+static void store8(uint8_t* b, const uint32_t w[8]) { memcpy(b, w, 32); }
+
+extern "C" {
+
+int hc_decompress(const uint8_t in[32], uint8_t out[32]) {
+  init();
+  uint32_t w[8]; load8(w, in);
+  ge p;
+  if (!ge_frombytes(p, w, K)) return 0;
+  uint32_t o[8]; ge_tobytes(o, p); store8(out, o);
+  return 1;
+}
+
+int hc_is_small_order(const uint8_t in[32]) {
+  init();
+  uint32_t w[8]; load8(w, in);
+  ge p;
+  if (!ge_frombytes(p, w, K)) return -1;
+  return ge_is_small_order(p) ? 1 : 0;
+}
+
+void hc_reduce512(const uint8_t in[64], uint8_t out[32]) {
+  uint32_t x[16]; memcpy(x, in, 64);
+  sc r; sc_reduce512(r, x); store8(out, r.w);
+}
+
+void hc_scalar_mul(const uint8_t a[32], const uint8_t b[32], uint8_t out[32]) {
+  sc x, y, r; load8(x.w, a); load8(y.w, b); sc_mul(r, x, y); store8(out, r.w);
+}
+
+void hc_scalar_add(const uint8_t a[32], const uint8_t b[32], uint8_t out[32]) {
+  sc x, y, r; load8(x.w, a); load8(y.w, b); sc_add(r, x, y); store8(out, r.w);
+}
+
+int hc_scalar_canonical(const uint8_t a[32]) { sc x; load8(x.w, a); return sc_is_canonical(x); }
+
+void hc_fixed_base(const uint8_t s[32], uint8_t out[32]) {
+  init();
+  sc x; load8(x.w, s);
+  ge r; fixed_base_mul(r, x, BT);
+  uint32_t o[8]; ge_tobytes(o, r); store8(out, o);
+}
+
+// [b]B + [a]P
+int hc_dsm(const uint8_t a[32], const uint8_t P[32], const uint8_t b[32], uint8_t out[32]) {
+  init();
+  uint32_t w[8]; load8(w, P);
+  ge p;
+  if (!ge_frombytes(p, w, K)) return 0;
+  ge_cached tab[9]; build_table9(tab, p, K.d2);
+  sc x, y; load8(x.w, a); load8(y.w, b);
+  ge r; dsm_var_base(r, tab, x, y, BT);
+  uint32_t o[8]; ge_tobytes(o, r); store8(out, o);
+  return 1;
+}
+
+// Strict verification with the kernel's check order; k supplied (device-only SHA).
+int hc_verify_strict(const uint8_t pk[32], const uint8_t sig[64], const uint8_t k32[32]) {
+  init();
+  uint32_t Aw[8], Rw[8], Sw[8];
+  load8(Aw, pk); load8(Rw, sig); load8(Sw, sig + 32);
+  const bool s_high = (Sw[7] >> 29) != 0;
+  sc s; memcpy(s.w, Sw, 32);
+  const bool s_canon = sc_is_canonical(s);
+  ge A, R;
+  const bool okA = ge_frombytes(A, Aw, K);
+  const bool okR = ge_frombytes(R, Rw, K);
+  const bool smallA = ge_is_small_order(A), smallR = ge_is_small_order(R);
+  sc k; load8(k.w, k32);
+  ge mA; ge_neg(mA, A);
+  ge_cached tab[9]; build_table9(tab, mA, K.d2);
+  if (!s_canon || s_high) memset(s.w, 0, 32);
+  ge acc; dsm_var_base(acc, tab, k, s, BT);
+  const bool eq = ge_eq_affine(acc, R);
+  if (s_high) return 1;
+  if (!okA) return 3;
+  if (!s_canon) return 2;
+  if (!okR) return 4;
+  if (smallR) return 6;
+  if (smallA) return 5;
+  if (!eq) return 7;
+  return 0;
+}
+
+}
