@@ -1,0 +1,358 @@
+#!/usr/bin/env python3
+"""bench.py — Narwhal crypto hot path on MI355X: Ed25519 verifies/s (+ SHA-512 GB/s).
+
+    python bench.py [--gpus N --steps K --warmup W --workload strict|sha]
+
+One process per GPU (torch.distributed.run for N > 1; RCCL only for the barrier and the
+max-over-ranks timing: the path shards, there is no data-path collective). Inputs are
+synthetic, generated on the device with the engine's own keygen/signing kernels, and are
+resident in HBM before the timed region; every timed step is one pass of the hot path
+over one batch of inputs through the C ABI (nw_dev_*), launched on torch's current
+stream so torch.cuda.Event brackets exactly the kernel launches.
+
+Workloads (BASELINE.json configs):
+  strict (default)  config 4: mixed corpus, 12.5M items per GPU (100M over 8 GPUs), 10%
+                    invalid / non-canonical / small-order. crypto::Signature::verify
+                    semantics per item; bitmap checked against the construction.
+  sha               config 3: 65,536 worker batches x 508,052 B (977 x 512 B txs,
+                    bincode layout), SHA-512 digests; checked against hashlib.
+The SHA-512 rate (config 3) is also reported as a secondary field of the strict line.
+
+Roofline work constants are SURVEY.md 8(d) (see DESIGN.md "Measurement").
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from narwhal_amd import _lib                 # noqa: E402
+from narwhal_amd import workloads as W       # noqa: E402
+
+METRIC = "Ed25519 verifies/sec (1/2/4/8 MI355X) + SHA-512 GB/s vs dalek on host cores"
+L_ORDER = 2**252 + 27742317777372353535851937790883648493
+P_FIELD = 2**255 - 19
+
+# implementation-independent work per unit.
+MAC_PER_STRICT_VERIFY = 3200 * 64          # 204,800 32x32->64 MACs
+SHA_OPS_PER_BLOCK = 4800                   # int32 ops per 128-B block
+# Peaks (DESIGN.md "Measurement"): v_mad_u64_u32 issues at half rate on gfx950
+# (profiles/r01_ubench_valu_4wps.txt), so MAC peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz.
+PEAK_TMAC = 256 * 4 * 16 * 2.4e9 / 1e12    # 39.32 TMAC/s
+PEAK_TOPS_FULL = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.64 T int32 lane-ops/s (full-rate ops)
+PEAK_HBM_GBS = 8000.0
+
+SMALL_ORDER = [
+    "0100000000000000000000000000000000000000000000000000000000000000",
+    "ecffffffffffffffffffffffffffffffffffffffffffffffffffffffffffff7f",
+    "0000000000000000000000000000000000000000000000000000000000000000",
+    "0000000000000000000000000000000000000000000000000000000000000080",
+    "26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05",
+    "26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc85",
+    "c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac037a",
+    "c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac03fa",
+]
+
+
+def enc_y(y: int, sign: int) -> bytes:
+    b = bytearray(y.to_bytes(32, "little"))
+    b[31] |= sign << 7
+    return bytes(b)
+
+
+def log(msg: str) -> None:
+    print(f"[bench r{os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
+
+
+def ptr(t: torch.Tensor) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what}: rc={rc} {_lib.lib().nw_last_error().decode()}")
+
+
+# ------------------------------------------------------------------------ corpus (config 4)
+def build_strict_corpus(dev, stream, uniq: int, nkeys: int, seed: int):
+    """Unique corpus on the device: keys and signatures by the engine's kernels, then 10%
+    of items turned into the Appendix A edge classes on the host (byte edits only).
+    Returns device tensors (msgs, pks, sigs) and the expected validity mask."""
+    L = _lib.lib()
+    rng = np.random.Generator(np.random.PCG64(seed))
+    seeds = torch.from_numpy(rng.integers(0, 256, size=(nkeys, 32), dtype=np.uint8)).to(dev)
+    pks_k = torch.empty((nkeys, 32), dtype=torch.uint8, device=dev)
+    check(L.nw_dev_keypair_from_seed_many(ptr(seeds), nkeys, ptr(pks_k), stream), "keygen")
+    sks_k = torch.cat([seeds, pks_k], dim=1).contiguous()
+    key_of = torch.from_numpy(rng.integers(0, nkeys, size=uniq)).to(dev)
+    sks = sks_k.index_select(0, key_of).contiguous()
+    msgs = torch.from_numpy(rng.integers(0, 256, size=(uniq, 32), dtype=np.uint8)).to(dev)
+    sigs = torch.empty((uniq, 64), dtype=torch.uint8, device=dev)
+    check(L.nw_dev_sign_many(ptr(sks), 64, ptr(msgs), 32, uniq, ptr(sigs), stream), "sign")
+    torch.cuda.synchronize()
+    m = msgs.cpu().numpy().copy()
+    p = sks[:, 32:].cpu().numpy().copy()
+    s = sigs.cpu().numpy().copy()
+    valid = np.ones(uniq, dtype=bool)
+    bad = rng.choice(uniq, uniq // 10, replace=False)
+    classes = 12
+    for j, i in enumerate(bad):
+        c = j % classes
+        if c == 0:     # wrong message
+            m[i, rng.integers(0, 32)] ^= np.uint8(1 << rng.integers(0, 8))
+        elif c == 1:   # bit flip in R
+            s[i, rng.integers(0, 32)] ^= np.uint8(1 << rng.integers(0, 8))
+        elif c == 2:   # bit flip in s (low 31 bytes: stays < 2^253)
+            s[i, 32 + rng.integers(0, 31)] ^= np.uint8(1 << rng.integers(0, 8))
+        elif c == 3:   # bit flip in A
+            p[i, rng.integers(0, 32)] ^= np.uint8(1 << rng.integers(0, 8))
+        elif c == 4:   # s + l (non-canonical scalar)
+            v = int.from_bytes(s[i, 32:].tobytes(), "little") + L_ORDER
+            s[i, 32:] = np.frombuffer(v.to_bytes(32, "little"), np.uint8)
+        elif c == 5:   # s with high bits set
+            s[i, 63] |= np.uint8(0x80 >> rng.integers(0, 3))
+        elif c == 6:   # small-order A (canonical / non-canonical encodings)
+            enc = SMALL_ORDER + [enc_y(P_FIELD, 0).hex(), enc_y(P_FIELD + 1, 1).hex(), enc_y(1, 1).hex()]
+            p[i] = np.frombuffer(bytes.fromhex(enc[j % len(enc)]), np.uint8)
+        elif c == 7:   # small-order R
+            s[i, :32] = np.frombuffer(bytes.fromhex(SMALL_ORDER[j % 8]), np.uint8)
+        elif c == 8:   # non-canonical large-order A (y = p + t): dalek decodes, no valid sig
+            t = [3, 4, 5, 6, 9, 10, 14, 15, 16, 18][j % 10]
+            p[i] = np.frombuffer(enc_y(P_FIELD + t, j & 1), np.uint8)
+        elif c == 9:   # Signature::default()
+            s[i] = 0
+        elif c == 10:  # A not on the curve
+            p[i] = np.frombuffer(enc_y([2, 7, 8][j % 3], j & 1), np.uint8)
+        else:          # R not on the curve
+            s[i, :32] = np.frombuffer(enc_y([2, 7, 8][j % 3], j & 1), np.uint8)
+        valid[i] = False
+    return (torch.from_numpy(m).to(dev), torch.from_numpy(p).to(dev), torch.from_numpy(s).to(dev),
+            valid)
+
+
+def tile(t: torch.Tensor, total: int) -> torch.Tensor:
+    reps = (total + t.shape[0] - 1) // t.shape[0]
+    return t.repeat((reps,) + (1,) * (t.dim() - 1))[:total].contiguous()
+
+
+# ------------------------------------------------------------------------ timing helpers
+def timed_steps(launch, steps: int, warmup: int, world: int):
+    for _ in range(warmup):
+        launch()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record()
+        launch()
+        e1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, kernel_ms
+
+
+# ------------------------------------------------------------------------ workloads
+def run_strict(args, dev, stream, rank, world):
+    L = _lib.lib()
+    n = args.items_per_gpu
+    log(f"building corpus: {args.unique} unique items, tiled to {n}")
+    msgs_u, pks_u, sigs_u, valid_u = build_strict_corpus(dev, stream, args.unique, 4096,
+                                                        seed=1000 + rank)
+    msgs, pks, sigs = tile(msgs_u, n), tile(pks_u, n), tile(sigs_u, n)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    bitmap = torch.zeros((n + 63) // 64 * 8, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+
+    def launch():
+        check(L.nw_dev_verify_strict_many(ptr(msgs), 32, ptr(pks), ptr(sigs), n, ptr(status),
+                                          ptr(bitmap), stream), "verify_strict")
+
+    elapsed, kernel_ms = timed_steps(launch, args.steps, args.warmup, world)
+    # full-size parity property: the verdict bitmap equals the construction
+    bits = np.unpackbits(bitmap.cpu().numpy(), bitorder="little")[:n].astype(bool)
+    exp = np.resize(valid_u, n)
+    ok = bool(np.array_equal(bits, exp))
+    st = status.cpu().numpy()
+    ok &= bool(np.array_equal(st == 0, exp))
+    return dict(n=n, elapsed=elapsed, kernel_ms=kernel_ms, parity=ok,
+                sample=(msgs_u, pks_u, sigs_u, st[: args.unique]))
+
+
+def run_sha(args, dev, stream, rank, world):
+    L = _lib.lib()
+    nb = args.sha_batches
+    uniq = min(args.sha_unique, nb)
+    log(f"building {uniq} unique worker batches ({W.BATCH_BYTES} B), tiled to {nb}")
+    ub = np.stack([W.worker_batch(i, seed=rank) for i in range(uniq)])
+    expect = [hashlib.sha512(ub[i].tobytes()).digest()[:32] for i in range(uniq)]
+    data_u = torch.from_numpy(ub).to(dev)
+    data = tile(data_u, nb).view(-1)
+    offs = torch.arange(nb, dtype=torch.int64, device=dev) * W.BATCH_BYTES
+    lens = torch.full((nb,), W.BATCH_BYTES, dtype=torch.int64, device=dev)
+    out = torch.empty((nb, 32), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+
+    def launch():
+        check(L.nw_dev_sha512_digest32_many(ptr(data), ptr(offs), ptr(lens), nb, ptr(out),
+                                            stream), "sha512")
+
+    elapsed, kernel_ms = timed_steps(launch, args.steps, args.warmup, world)
+    o = out.cpu().numpy()
+    ok = all(o[i].tobytes() == expect[i % uniq] for i in range(0, nb, max(1, nb // 997)))
+    ok &= all(o[i].tobytes() == expect[i % uniq] for i in range(uniq))
+    del data, data_u
+    return dict(n=nb, bytes=nb * W.BATCH_BYTES, elapsed=elapsed, kernel_ms=kernel_ms, parity=ok)
+
+
+def cpu_baseline_strict(sample, seconds: float):
+    """Oracle ('port', the dalek-equivalent restatement) on the host cores, bounded."""
+    from oracle import oracle as O
+    msgs_u, pks_u, sigs_u, gpu_st = sample
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    m, p, s = (t.cpu().numpy() for t in (msgs_u, pks_u, sigs_u))
+    n = min(len(m), 2048)
+    t0 = time.perf_counter()
+    st = O.verify_strict_many(m[:n], p[:n], s[:n], nthreads=threads)
+    dt = time.perf_counter() - t0
+    rate = n / dt
+    n2 = int(min(len(m), max(n, rate * seconds)))
+    if n2 > n:
+        t0 = time.perf_counter()
+        st = O.verify_strict_many(m[:n2], p[:n2], s[:n2], nthreads=threads)
+        dt = time.perf_counter() - t0
+        n = n2
+    agree = bool(np.array_equal(st, gpu_st[:n]))
+    return dict(value=n / dt, unit="verifies/s", cores=threads, kind="port",
+                sample=f"{n} mixed-corpus items (first {n} of the unique corpus), oracle "
+                       f"verify_strict_many, {threads} threads, {dt:.1f} s"), agree
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", choices=["strict", "sha"], default="strict")
+    ap.add_argument("--items-per-gpu", type=int, default=12_500_000)
+    ap.add_argument("--unique", type=int, default=1 << 18)
+    ap.add_argument("--sha-batches", type=int, default=65536)
+    ap.add_argument("--sha-unique", type=int, default=256)
+    ap.add_argument("--no-sha", action="store_true", help="skip the secondary SHA-512 leg")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    L = _lib.lib()
+    ndev = L.nw_init()
+    if ndev <= 0:
+        raise RuntimeError(f"nw_init failed: {ndev} {L.nw_last_error().decode()}")
+    check(L.nw_set_device(local), "nw_set_device")
+    # A dedicated (non-null) stream: the kernels launch on it and torch.cuda.Event records
+    # on it, so the events bracket exactly the kernel launches.
+    tstream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(tstream)
+    stream = ctypes.c_void_p(tstream.cuda_stream)
+    assert stream.value, "expected a non-null HIP stream"
+
+    result = {}
+    if args.workload == "strict":
+        r = run_strict(args, dev, stream, rank, world)
+        units = r["n"] * world
+        value = units / r["elapsed"] * args.steps
+        achieved = r["n"] * MAC_PER_STRICT_VERIFY / (r["kernel_ms"] * 1e-3) / 1e12
+        result = {
+            "metric": METRIC, "value": value, "unit": "verifies/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": r["elapsed"] / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": "config4_mixed_corpus_strict_verify",
+                       "items_per_gpu": r["n"], "unique_items": args.unique,
+                       "invalid_fraction": 0.1, "semantics": "crypto::Signature::verify (dalek verify_strict)",
+                       "parallelism": f"shard{world}"},
+            "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_TMAC,
+                         "unit": "TMAC/s", "frac": achieved / PEAK_TMAC, "traffic": None,
+                         "kernel": "k_verify_strict", "kernel_ms": r["kernel_ms"],
+                         "work_per_unit": f"{MAC_PER_STRICT_VERIFY} MAC/verify (SURVEY 8d)"},
+            "parity": "ok" if r["parity"] else "FAIL",
+        }
+        sample = r["sample"]
+        del r
+        torch.cuda.empty_cache()
+        if not args.no_sha:
+            s = run_sha(args, dev, stream, rank, world)
+            gbs = s["bytes"] * world / (s["elapsed"] / args.steps) / 1e9
+            kgbs = s["bytes"] / (s["kernel_ms"] * 1e-3) / 1e9
+            blocks = s["n"] * ((W.BATCH_BYTES + 17 + 127) // 128)
+            tops = blocks * SHA_OPS_PER_BLOCK / (s["kernel_ms"] * 1e-3) / 1e12
+            result["sha512"] = {"workload": "config3_worker_batch_digests",
+                                "batches_per_gpu": s["n"], "batch_bytes": W.BATCH_BYTES,
+                                "GB_per_s": gbs, "kernel_GB_per_s": kgbs,
+                                "hbm_frac": kgbs / PEAK_HBM_GBS,
+                                "valu_Tops": tops, "valu_frac": tops / PEAK_TOPS_FULL,
+                                "kernel_ms": s["kernel_ms"],
+                                "parity": "ok" if s["parity"] else "FAIL"}
+            if not s["parity"]:
+                result["parity"] = "FAIL"
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            cb, agree = cpu_baseline_strict(sample, args.cpu_seconds)
+            result["cpu_baseline"] = cb
+            if not agree:
+                result["parity"] = "FAIL"
+                log("oracle disagrees with GPU statuses on the cpu_baseline sample")
+    else:
+        s = run_sha(args, dev, stream, rank, world)
+        gbs = s["bytes"] * world / (s["elapsed"] / args.steps) / 1e9
+        kgbs = s["bytes"] / (s["kernel_ms"] * 1e-3) / 1e9
+        result = {
+            "metric": METRIC, "value": gbs, "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": s["elapsed"] / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": "config3_worker_batch_digests", "batches_per_gpu": s["n"],
+                       "batch_bytes": W.BATCH_BYTES, "parallelism": f"shard{world}"},
+            "roofline": {"bound": "hbm", "achieved": kgbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": kgbs / PEAK_HBM_GBS, "traffic": None,
+                         "kernel": "k_sha512_digest32", "kernel_ms": s["kernel_ms"]},
+            "parity": "ok" if s["parity"] else "FAIL",
+        }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if result.get("parity") != "ok":
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

@@ -97,6 +97,17 @@ int nw_verify_batch_many(const uint8_t* digests, const uint8_t* pks, const uint8
                          const uint64_t* offsets, size_t nbatches, const uint8_t* z16,
                          int32_t* status_out);
 
+/* crypto::generate_keypair given the CSPRNG's 32-byte seeds (crypto/src/lib.rs:167-175:
+ * dalek Keypair::generate fills the seed from the RNG): pks_out n x 32 bytes. The
+ * crypto::SecretKey bytes are seed || pk. */
+int nw_keypair_from_seed_many(const uint8_t* seeds, size_t n, uint8_t* pks_out);
+
+/* crypto::Signature::new(digest, secret) (crypto/src/lib.rs:185-191, RFC 8032). sks: n x 64
+ * bytes (seed || pk) or one shared key (sk_stride = 0); digests: n x 32 (digest_stride 32)
+ * or shared (0). sigs_out: n x 64 bytes (part1 || part2). */
+int nw_sign_many(const uint8_t* sks, size_t sk_stride, const uint8_t* digests,
+                 size_t digest_stride, size_t n, uint8_t* sigs_out);
+
 /* ---- device-pointer (asynchronous) entry points ------------------------------------ */
 /* All pointers are device pointers on the current device; work is queued on `stream`
  * (a hipStream_t; NULL = the library's per-thread stream) and the call returns without
@@ -107,6 +118,11 @@ int nw_dev_sha512_digest32_many(const void* data, const uint64_t* offsets,
 int nw_dev_verify_strict_many(const void* digests, size_t digest_stride, const void* pks,
                               const void* sigs, size_t n, int32_t* status_out,
                               void* bitmap_out, void* stream);
+
+int nw_dev_keypair_from_seed_many(const void* seeds, size_t n, void* pks_out, void* stream);
+
+int nw_dev_sign_many(const void* sks, size_t sk_stride, const void* digests,
+                     size_t digest_stride, size_t n, void* sigs_out, void* stream);
 
 /* Workspace bytes nw_dev_verify_batch_many needs for nitems items. */
 size_t nw_dev_verify_batch_workspace(size_t nitems);

@@ -54,6 +54,10 @@ def lib() -> ctypes.CDLL:
         "nw_verify_batch_many": ([P, P, P, P, S, P, P], I),
         "nw_dev_sha512_digest32_many": ([P, P, P, S, P, P], I),
         "nw_dev_verify_strict_many": ([P, S, P, P, S, P, P, P], I),
+        "nw_keypair_from_seed_many": ([P, S, P], I),
+        "nw_sign_many": ([P, S, P, S, S, P], I),
+        "nw_dev_keypair_from_seed_many": ([P, S, P, P], I),
+        "nw_dev_sign_many": ([P, S, P, S, S, P, P], I),
         "nw_dev_verify_batch_workspace": ([S], S),
         "nw_dev_verify_batch_many": ([P, P, P, P, S, S, P, P, P, P, P, P], I),
     }

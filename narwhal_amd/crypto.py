@@ -28,7 +28,8 @@ import numpy as np
 from . import _lib
 from ._lib import EngineError, check
 
-__all__ = ["Digest", "Hash", "PublicKey", "Signature", "CryptoError", "EngineError",
+__all__ = ["Digest", "Hash", "PublicKey", "SecretKey", "Signature", "CryptoError",
+           "EngineError", "generate_keypair", "keypair_from_seed_many", "sign_many",
            "sha512_digest", "sha512_digest32_many", "verify_strict_many",
            "verify_batch_many"]
 
@@ -92,6 +93,65 @@ class PublicKey:
         return self.encode_base64()
 
 
+class SecretKey:
+    """crypto::SecretKey (lib.rs:120-161): seed || public key, zeroised on drop."""
+
+    def __init__(self, raw: bytes):
+        if len(raw) != 64:
+            raise ValueError("SecretKey must be 64 bytes")
+        self._raw = bytearray(raw)
+
+    def encode_base64(self) -> str:
+        return base64.b64encode(bytes(self._raw)).decode()
+
+    @classmethod
+    def decode_base64(cls, s: str) -> "SecretKey":
+        raw = base64.b64decode(s)
+        if len(raw) < 64:
+            raise ValueError("InvalidLength")
+        return cls(raw[:64])
+
+    def __bytes__(self) -> bytes:
+        return bytes(self._raw)
+
+    def __eq__(self, other) -> bool:
+        return isinstance(other, SecretKey) and self._raw == other._raw
+
+    def __del__(self):
+        for i in range(len(self._raw)):
+            self._raw[i] = 0
+
+
+def keypair_from_seed_many(seeds: np.ndarray) -> np.ndarray:
+    """Public keys for n 32-byte seeds (dalek Keypair::generate given the RNG output)."""
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint8).reshape(-1, 32)
+    out = np.zeros_like(seeds)
+    if len(seeds):
+        check(_lib.lib().nw_keypair_from_seed_many(_ptr(seeds), len(seeds), _ptr(out)),
+              "nw_keypair_from_seed_many")
+    return out
+
+
+def generate_keypair(fill_bytes) -> tuple[PublicKey, SecretKey]:
+    """crypto::generate_keypair(csprng) (lib.rs:167-175); fill_bytes(n) -> n random bytes
+    plays the RNG (e.g. oracle.stdrng_seeds-compatible ChaCha20, or os.urandom)."""
+    seed = bytes(fill_bytes(32))
+    pk = keypair_from_seed_many(np.frombuffer(seed, np.uint8))[0].tobytes()
+    return PublicKey(pk), SecretKey(seed + pk)
+
+
+def sign_many(sks: np.ndarray, digests: np.ndarray, shared_key: bool = False,
+              shared_digest: bool = False) -> np.ndarray:
+    """n x Signature::new (RFC 8032 deterministic). Returns n x 64 bytes."""
+    sks = np.ascontiguousarray(sks, dtype=np.uint8)
+    digests = np.ascontiguousarray(digests, dtype=np.uint8)
+    n = max(1 if shared_key else sks.size // 64, 1 if shared_digest else digests.size // 32)
+    out = np.zeros((n, 64), np.uint8)
+    check(_lib.lib().nw_sign_many(_ptr(sks), 0 if shared_key else 64, _ptr(digests),
+                                  0 if shared_digest else 32, n, _ptr(out)), "nw_sign_many")
+    return out
+
+
 @dataclass(frozen=True)
 class Signature:
     part1: bytes = bytes(32)   # R
@@ -102,6 +162,14 @@ class Signature:
         if len(b) != 64:
             raise ValueError("signature must be 64 bytes")
         return cls(bytes(b[:32]), bytes(b[32:]))
+
+    @classmethod
+    def new(cls, digest: Digest, secret: SecretKey) -> "Signature":
+        """crypto::Signature::new (lib.rs:185-191)."""
+        sig = sign_many(np.frombuffer(bytes(secret), np.uint8),
+                        np.frombuffer(digest.value, np.uint8), shared_key=True,
+                        shared_digest=True)[0].tobytes()
+        return cls.from_bytes(sig)
 
     def flatten(self) -> bytes:
         return self.part1 + self.part2

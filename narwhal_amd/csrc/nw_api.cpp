@@ -304,6 +304,79 @@ int nw_signature_verify(const uint8_t sig[64], const uint8_t digest[32], const u
 }
 
 // ------------------------------------------------------------------------------------
+int nw_dev_keypair_from_seed_many(const void* seeds, size_t n, void* pks_out, void* stream) {
+  DevCtx* c;
+  int rc = begin(&c);
+  if (rc) return rc;
+  if (n && (!seeds || !pks_out)) return set_err(NW_E_INVALID_ARG, "null pointer");
+  NW_HIP(nw::launch_keypair(static_cast<const uint32_t*>(seeds), n,
+                            static_cast<uint32_t*>(pks_out), pick_stream(stream, c)),
+         "k_keypair launch");
+  return 0;
+}
+
+int nw_dev_sign_many(const void* sks, size_t sk_stride, const void* digests,
+                     size_t digest_stride, size_t n, void* sigs_out, void* stream) {
+  DevCtx* c;
+  int rc = begin(&c);
+  if (rc) return rc;
+  if (n && (!sks || !digests || !sigs_out)) return set_err(NW_E_INVALID_ARG, "null pointer");
+  if ((sk_stride != 0 && sk_stride != 64) || (digest_stride != 0 && digest_stride != 32))
+    return set_err(NW_E_INVALID_ARG, "sk_stride must be 0/64, digest_stride 0/32");
+  NW_HIP(nw::launch_sign(static_cast<const uint32_t*>(sks), (uint32_t)(sk_stride / 4),
+                         static_cast<const uint32_t*>(digests), (uint32_t)(digest_stride / 4),
+                         n, static_cast<uint32_t*>(sigs_out), pick_stream(stream, c)),
+         "k_sign launch");
+  return 0;
+}
+
+int nw_keypair_from_seed_many(const uint8_t* seeds, size_t n, uint8_t* pks_out) {
+  DevCtx* c;
+  int rc = begin(&c);
+  if (rc) return rc;
+  if (n == 0) return 0;
+  if (!seeds || !pks_out) return set_err(NW_E_INVALID_ARG, "null pointer");
+  rc = reserve(*c, 2 * a256(32 * n));
+  if (rc) return rc;
+  uint8_t* d_in = static_cast<uint8_t*>(c->dbuf);
+  uint8_t* d_out = d_in + a256(32 * n);
+  hipStream_t s = c->stream;
+  NW_HIP(hipMemcpyAsync(d_in, seeds, 32 * n, hipMemcpyHostToDevice, s), "H2D seeds");
+  NW_HIP(nw::launch_keypair(reinterpret_cast<const uint32_t*>(d_in), n,
+                            reinterpret_cast<uint32_t*>(d_out), s), "k_keypair launch");
+  NW_HIP(hipMemcpyAsync(pks_out, d_out, 32 * n, hipMemcpyDeviceToHost, s), "D2H pks");
+  NW_HIP(hipStreamSynchronize(s), "sync");
+  return 0;
+}
+
+int nw_sign_many(const uint8_t* sks, size_t sk_stride, const uint8_t* digests,
+                 size_t digest_stride, size_t n, uint8_t* sigs_out) {
+  DevCtx* c;
+  int rc = begin(&c);
+  if (rc) return rc;
+  if (n == 0) return 0;
+  if (!sks || !digests || !sigs_out) return set_err(NW_E_INVALID_ARG, "null pointer");
+  if ((sk_stride != 0 && sk_stride != 64) || (digest_stride != 0 && digest_stride != 32))
+    return set_err(NW_E_INVALID_ARG, "sk_stride must be 0/64, digest_stride 0/32");
+  const size_t nk = sk_stride ? n : 1, nm = digest_stride ? n : 1;
+  const size_t b_k = a256(64 * nk), b_m = a256(32 * nm), b_s = a256(64 * n);
+  rc = reserve(*c, b_k + b_m + b_s);
+  if (rc) return rc;
+  uint8_t* d_k = static_cast<uint8_t*>(c->dbuf);
+  uint8_t* d_m = d_k + b_k;
+  uint8_t* d_s = d_m + b_m;
+  hipStream_t s = c->stream;
+  NW_HIP(hipMemcpyAsync(d_k, sks, 64 * nk, hipMemcpyHostToDevice, s), "H2D sks");
+  NW_HIP(hipMemcpyAsync(d_m, digests, 32 * nm, hipMemcpyHostToDevice, s), "H2D digests");
+  NW_HIP(nw::launch_sign(reinterpret_cast<const uint32_t*>(d_k), (uint32_t)(sk_stride / 4),
+                         reinterpret_cast<const uint32_t*>(d_m), (uint32_t)(digest_stride / 4),
+                         n, reinterpret_cast<uint32_t*>(d_s), s), "k_sign launch");
+  NW_HIP(hipMemcpyAsync(sigs_out, d_s, 64 * n, hipMemcpyDeviceToHost, s), "D2H sigs");
+  NW_HIP(hipStreamSynchronize(s), "sync");
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------
 size_t nw_dev_verify_batch_workspace(size_t nitems) { return nw::batch_workspace_bytes(nitems); }
 
 static int fill_key(nw::z_key_t& k, const uint8_t* key32) {

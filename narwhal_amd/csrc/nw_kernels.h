@@ -25,6 +25,12 @@ hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
                                 const uint32_t* pks, const uint32_t* sigs, uint64_t n,
                                 int32_t* status, uint64_t* bitmap, hipStream_t stream);
 
+hipError_t launch_keypair(const uint32_t* seeds, uint64_t n, uint32_t* pks, hipStream_t stream);
+
+hipError_t launch_sign(const uint32_t* sks, uint32_t sk_stride_words, const uint32_t* msgs,
+                       uint32_t msg_stride_words, uint64_t n, uint32_t* sigs,
+                       hipStream_t stream);
+
 size_t batch_workspace_bytes(uint64_t nitems);
 
 hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,

@@ -221,6 +221,121 @@ __global__ __launch_bounds__(256) void k_verify_strict(const uint32_t* __restric
 }
 
 // ---------------------------------------------------------------------------------------
+// Key generation and signing (crypto::generate_keypair / Signature::new, lib.rs:167-191;
+// dalek Keypair::generate + ExpandedSecretKey::sign = RFC 8032)
+// ---------------------------------------------------------------------------------------
+// SHA-512 of nwords64 whole 64-bit words (<= 13, one block), words given big-endian.
+__device__ __forceinline__ void sha512_words(uint64_t st[8], const uint64_t* m, int nwords64) {
+  uint64_t w[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) w[i] = i < nwords64 ? m[i] : 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i == nwords64) w[i] = 0x8000000000000000ULL;
+  w[15] = (uint64_t)nwords64 * 64;
+  sha512_init(st);
+  sha512_compress(st, w);
+}
+
+__device__ __forceinline__ uint64_t be64_of_le_words(const uint32_t* x, int i) {
+  return ((uint64_t)bswap32(x[2 * i]) << 32) | bswap32(x[2 * i + 1]);
+}
+
+// Expanded secret: a = clamp(H(seed)[0..32]) mod l, prefix = H(seed)[32..64] (LE words).
+__device__ __forceinline__ void expand_seed(sc& a, uint32_t prefix[8], const uint32_t seed[8]) {
+  uint64_t m[4], st[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) m[i] = be64_of_le_words(seed, i);
+  sha512_words(st, m, 4);
+  uint32_t h[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    h[2 * i] = bswap32((uint32_t)(st[i] >> 32));
+    h[2 * i + 1] = bswap32((uint32_t)st[i]);
+  }
+  h[0] &= 0xfffffff8u;
+  h[7] = (h[7] & 0x7fffffffu) | 0x40000000u;
+  uint32_t x[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = i < 8 ? h[i] : 0u;
+  sc_reduce512(a, x);   // [a]B = [a mod l]B
+#pragma unroll
+  for (int i = 0; i < 8; ++i) prefix[i] = h[8 + i];
+}
+
+__global__ __launch_bounds__(256) void k_keypair(const uint32_t* __restrict__ seeds, uint64_t n,
+                                                 uint32_t* __restrict__ pks) {
+  __shared__ ge_niels s_btab[129];
+  load_btab(s_btab);
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t seed[8], prefix[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) seed[j] = seeds[8 * i + j];
+  sc a;
+  expand_seed(a, prefix, seed);
+  ge A;
+  fixed_base_mul(A, a, s_btab);
+  uint32_t Aw[8];
+  ge_tobytes(Aw, A);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) pks[8 * i + j] = Aw[j];
+}
+
+// sks: crypto::SecretKey bytes (seed || pk), stride sk_stride_words (16, or 0 = one key).
+__global__ __launch_bounds__(256) void k_sign(const uint32_t* __restrict__ sks,
+                                              uint32_t sk_stride_words,
+                                              const uint32_t* __restrict__ msgs,
+                                              uint32_t msg_stride_words, uint64_t n,
+                                              uint32_t* __restrict__ sigs) {
+  __shared__ ge_niels s_btab[129];
+  load_btab(s_btab);
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t seed[8], pk[8], M[8], prefix[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    seed[j] = sks[(uint64_t)sk_stride_words * i + j];
+    pk[j] = sks[(uint64_t)sk_stride_words * i + 8 + j];
+    M[j] = msgs[(uint64_t)msg_stride_words * i + j];
+  }
+  sc a;
+  expand_seed(a, prefix, seed);
+  // r = H(prefix || M) mod l
+  uint64_t m[8], st[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    m[j] = be64_of_le_words(prefix, j);
+    m[4 + j] = be64_of_le_words(M, j);
+  }
+  sha512_words(st, m, 8);
+  uint32_t hx[16];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    hx[2 * j] = bswap32((uint32_t)(st[j] >> 32));
+    hx[2 * j + 1] = bswap32((uint32_t)st[j]);
+  }
+  sc r;
+  sc_reduce512(r, hx);
+  ge R;
+  fixed_base_mul(R, r, s_btab);
+  uint32_t Rw[8];
+  ge_tobytes(Rw, R);
+  hram96(hx, Rw, pk, M);
+  sc k, ka, s;
+  sc_reduce512(k, hx);
+  sc_mul(ka, k, a);
+  sc_add(s, ka, r);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sigs[16 * i + j] = Rw[j];
+    sigs[16 * i + 8 + j] = s.w[j];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Batch verification (random linear combination)
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
@@ -460,6 +575,21 @@ hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_verify_strict, dim3(grid_for(n, 256)), dim3(256), 0, stream, msgs,
                      msg_stride_words, pks, sigs, n, status, bitmap);
+  return hipGetLastError();
+}
+
+hipError_t launch_keypair(const uint32_t* seeds, uint64_t n, uint32_t* pks, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_keypair, dim3(grid_for(n, 256)), dim3(256), 0, stream, seeds, n, pks);
+  return hipGetLastError();
+}
+
+hipError_t launch_sign(const uint32_t* sks, uint32_t sk_stride_words, const uint32_t* msgs,
+                       uint32_t msg_stride_words, uint64_t n, uint32_t* sigs,
+                       hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sign, dim3(grid_for(n, 256)), dim3(256), 0, stream, sks, sk_stride_words,
+                     msgs, msg_stride_words, n, sigs);
   return hipGetLastError();
 }
 

@@ -196,3 +196,24 @@ def test_batch_many_vs_oracle():
     ref = O.verify_batch_many(digests, pks, sigs, offsets, z16=z)
     assert np.array_equal(st, ref)
     assert st[3] != 0 and st[5] != 0 and st[0] == 0 and st[7] == 0
+
+
+# ---------------------------------------------------------------- keygen / signing
+def test_keygen_and_sign_vs_oracle(golden):
+    seeds = O.stdrng_seeds(300)
+    pks = C.keypair_from_seed_many(np.array([np.frombuffer(s, np.uint8) for s in seeds]))
+    for s, pk in zip(seeds, pks):
+        assert pk.tobytes() == O.keypair_from_seed(s)[0]
+    assert [p.tobytes().hex() for p in pks[:4]] == [k["pk"] for k in golden["keys"]["stdrng_zero_seed_keys"]]
+    rng = np.random.Generator(np.random.PCG64(8))
+    digests = rng.integers(0, 256, size=(300, 32), dtype=np.uint8)
+    sks = np.concatenate([np.array([np.frombuffer(s, np.uint8) for s in seeds]), pks], axis=1)
+    sigs = C.sign_many(sks, digests)
+    for i in range(300):
+        assert sigs[i].tobytes() == O.sign(sks[i].tobytes(), digests[i].tobytes())
+    # reference fixture: keys().pop() signs the "Hello, world!" digest
+    pk, sk = C.generate_keypair(lambda n: O.stdrng_seeds(4)[3])
+    d = C.Digest(O.digest32(b"Hello, world!"))
+    sig = C.Signature.new(d, sk)
+    assert sig.flatten().hex() == golden["keys"]["hello_sig_key3"]
+    sig.verify(d, pk)
