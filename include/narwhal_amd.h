@@ -42,6 +42,19 @@ extern "C" {
 #define NW_ERR_R_SMALL_ORDER 6    /* verify (strict) only                                   */
 #define NW_ERR_EQUATION 7         /* strict: [s]B != R + [k]A; batch: RLC sum != identity   */
 
+/* Message-level verdicts (primary::DagError variants, primary/src/error.rs:26-59), returned
+ * per item by the Header / Vote / Certificate entry points below. */
+#define NW_DAG_INVALID_HEADER_ID 16      /* DagError::InvalidHeaderId                        */
+#define NW_DAG_UNKNOWN_AUTHORITY 17      /* DagError::UnknownAuthority(pk)                   */
+#define NW_DAG_MALFORMED_HEADER 18       /* DagError::MalformedHeader(id): unknown worker id */
+#define NW_DAG_AUTHORITY_REUSE 19        /* DagError::AuthorityReuse(pk)                     */
+#define NW_DAG_REQUIRES_QUORUM 20        /* DagError::CertificateRequiresQuorum              */
+/* DagError::InvalidSignature(CryptoError): base + the NW_ERR_* of the first failing check.
+ * NW_DAG_INVALID_SIGNATURE: the message's own Signature::verify (header or vote);
+ * NW_DAG_INVALID_VOTES: the certificate's Signature::verify_batch over its votes. */
+#define NW_DAG_INVALID_SIGNATURE 32
+#define NW_DAG_INVALID_VOTES 48
+
 /* Runtime errors. */
 #define NW_E_INVALID_ARG (-1)
 #define NW_E_NO_DEVICE (-2)
@@ -108,6 +121,56 @@ int nw_keypair_from_seed_many(const uint8_t* seeds, size_t n, uint8_t* pks_out);
 int nw_sign_many(const uint8_t* sks, size_t sk_stride, const uint8_t* digests,
                  size_t digest_stride, size_t n, uint8_t* sigs_out);
 
+/* ---- primary messages: Header / Vote / Certificate verification -------------------- */
+/* config::Committee (config/src/lib.rs:139-173): authorities sorted by public-key bytes
+ * (BTreeMap order), their stake (config::Stake = u32) and worker ids (WorkerId = u32). */
+typedef struct nw_committee {
+  size_t nauth;
+  const uint8_t* pks;              /* nauth x 32, strictly increasing                     */
+  const uint32_t* stakes;          /* nauth                                               */
+  const uint64_t* worker_offsets;  /* nauth + 1: authority a owns worker_ids[wo[a]..wo[a+1]) */
+  const uint32_t* worker_ids;
+} nw_committee;
+
+/* A stream of n primary::Certificate (or Header) values in structure-of-arrays form.
+ * header_bytes holds, per header, exactly the bytes `Hash for Header` feeds SHA-512
+ * (primary/src/messages.rs:70-84): author 32 || round u64 LE || payload_counts[i] x
+ * (digest 32 || worker id u32 LE) in BTreeMap order || parents x 32 in BTreeSet order. */
+typedef struct nw_certificates {
+  size_t n;
+  const uint8_t* header_bytes;
+  const uint64_t* header_offsets;  /* n + 1; header i = header_bytes[ho[i]..ho[i+1])      */
+  const uint32_t* payload_counts;  /* n                                                   */
+  const uint8_t* ids;              /* n x 32: header.id as received                       */
+  const uint8_t* header_sigs;      /* n x 64: header.signature (part1 || part2)           */
+  const uint64_t* vote_offsets;    /* n + 1 (certificates only; NULL for headers)          */
+  const uint8_t* vote_pks;         /* vote_offsets[n] x 32: certificate.votes[j].0         */
+  const uint8_t* vote_sigs;        /* vote_offsets[n] x 64: certificate.votes[j].1         */
+  size_t header_bytes_len;         /* total bytes of header_bytes (device entry points)    */
+  size_t nvotes;                   /* vote_offsets[n] (device entry points)                */
+} nw_certificates;
+
+/* n x Certificate::verify(committee) (primary/src/messages.rs:189-215, with
+ * Header::verify 48-67 and Signature::verify_batch over Certificate::digest 226-234).
+ * status_out: n x int32 (0 = Ok, else NW_DAG_*), first failure in the reference's order.
+ * index_out (optional): n x uint64 — the vote index for UNKNOWN_AUTHORITY (UINT64_MAX =
+ * the header author) / AUTHORITY_REUSE / INVALID_VOTES (nvotes for the equation), the
+ * payload entry for MALFORMED_HEADER, else 0. z16 (optional): vote_offsets[n] x 16-byte
+ * batch coefficients (deterministic tests); NULL = OS CSPRNG as in the reference. */
+int nw_certificates_verify_many(const nw_committee* committee, const nw_certificates* certs,
+                                const uint8_t* z16, int32_t* status_out, uint64_t* index_out);
+
+/* n x Header::verify(committee) (primary/src/messages.rs:48-67); vote fields ignored. */
+int nw_headers_verify_many(const nw_committee* committee, const nw_certificates* headers,
+                           int32_t* status_out, uint64_t* index_out);
+
+/* n x Vote::verify(committee) (primary/src/messages.rs:131-142): stake(author) > 0, then
+ * Signature::verify(Vote::digest = Sha512(id || round LE || origin)[..32], author). */
+int nw_votes_verify_many(const nw_committee* committee, const uint8_t* ids,
+                         const uint64_t* rounds, const uint8_t* origins,
+                         const uint8_t* authors, const uint8_t* sigs, size_t n,
+                         int32_t* status_out);
+
 /* ---- device-pointer (asynchronous) entry points ------------------------------------ */
 /* All pointers are device pointers on the current device; work is queued on `stream`
  * (a hipStream_t; NULL = the library's per-thread stream) and the call returns without
@@ -132,6 +195,16 @@ int nw_dev_verify_batch_many(const void* digests, const void* pks, const void* s
                              const uint64_t* offsets, size_t nbatches, size_t nitems,
                              const void* z16, const uint8_t* zkey32, void* workspace,
                              int32_t* status_out, uint64_t* fail_index, void* stream);
+
+/* Device form of nw_certificates_verify_many: every pointer inside *committee and *certs
+ * (and z16, status_out, index_out, workspace) is a device pointer; the structs themselves
+ * are host memory. header_bytes_len and nvotes must be set. headers_only != 0 runs
+ * Header::verify instead of Certificate::verify. */
+size_t nw_dev_certificates_workspace(size_t n, size_t nvotes);
+int nw_dev_certificates_verify_many(const nw_committee* committee, const nw_certificates* certs,
+                                    int headers_only, const void* z16, const uint8_t* zkey32,
+                                    void* workspace, int32_t* status_out, uint64_t* index_out,
+                                    void* stream);
 
 #ifdef __cplusplus
 }

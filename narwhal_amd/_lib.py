@@ -17,6 +17,8 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "narwhal_amd.h")
 NW_OK = 0
 ERR_NAMES = {1: "S_HIGH_BITS", 2: "S_NONCANONICAL", 3: "A_DECODE", 4: "R_DECODE",
              5: "A_SMALL_ORDER", 6: "R_SMALL_ORDER", 7: "EQUATION"}
+DAG_NAMES = {16: "InvalidHeaderId", 17: "UnknownAuthority", 18: "MalformedHeader",
+             19: "AuthorityReuse", 20: "CertificateRequiresQuorum"}
 E_NAMES = {-1: "NW_E_INVALID_ARG", -2: "NW_E_NO_DEVICE", -3: "NW_E_DEVICE",
            -4: "NW_E_OUT_OF_MEMORY"}
 
@@ -60,6 +62,11 @@ def lib() -> ctypes.CDLL:
         "nw_dev_sign_many": ([P, S, P, S, S, P, P], I),
         "nw_dev_verify_batch_workspace": ([S], S),
         "nw_dev_verify_batch_many": ([P, P, P, P, S, S, P, P, P, P, P, P], I),
+        "nw_certificates_verify_many": ([P, P, P, P, P], I),
+        "nw_headers_verify_many": ([P, P, P, P], I),
+        "nw_votes_verify_many": ([P, P, P, P, P, P, S, P], I),
+        "nw_dev_certificates_workspace": ([S, S], S),
+        "nw_dev_certificates_verify_many": ([P, P, I, P, P, P, P, P, P], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

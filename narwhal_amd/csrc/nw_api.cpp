@@ -490,3 +490,278 @@ int nw_verify_batch_many(const uint8_t* digests, const uint8_t* pks, const uint8
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------
+// Primary messages: Header::verify / Vote::verify / Certificate::verify
+// (primary/src/messages.rs:48-67, 131-142, 189-215)
+// ------------------------------------------------------------------------------------
+namespace {
+
+struct CertWs {
+  uint32_t *hdr_digest, *authors, *cert_digest;
+  int32_t *pre1, *pre2, *hdr_st, *batch_st;
+  uint64_t *idx1, *idx2, *batch_idx, *bitmap;
+  void* batch_ws;
+};
+
+size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
+  const size_t m = n ? n : 1;
+  const size_t sizes[12] = {a256(32 * m), a256(32 * m), a256(32 * m), a256(4 * m), a256(4 * m),
+                            a256(4 * m),  a256(4 * m),  a256(8 * m),  a256(8 * m), a256(8 * m),
+                            a256(8 * ((m + 63) / 64)), a256(nw::batch_workspace_bytes(nvotes))};
+  size_t off[12], tot = 0;
+  for (int k = 0; k < 12; ++k) { off[k] = tot; tot += sizes[k]; }
+  if (w) {
+    w->hdr_digest = reinterpret_cast<uint32_t*>(base + off[0]);
+    w->authors = reinterpret_cast<uint32_t*>(base + off[1]);
+    w->cert_digest = reinterpret_cast<uint32_t*>(base + off[2]);
+    w->pre1 = reinterpret_cast<int32_t*>(base + off[3]);
+    w->pre2 = reinterpret_cast<int32_t*>(base + off[4]);
+    w->hdr_st = reinterpret_cast<int32_t*>(base + off[5]);
+    w->batch_st = reinterpret_cast<int32_t*>(base + off[6]);
+    w->idx1 = reinterpret_cast<uint64_t*>(base + off[7]);
+    w->idx2 = reinterpret_cast<uint64_t*>(base + off[8]);
+    w->batch_idx = reinterpret_cast<uint64_t*>(base + off[9]);
+    w->bitmap = reinterpret_cast<uint64_t*>(base + off[10]);
+    w->batch_ws = base + off[11];
+  }
+  return tot;
+}
+
+// The whole device pipeline; every pointer is a device pointer.
+int cert_pipeline(const nw_committee& com, const nw_certificates& cs, int headers_only,
+                  const void* z16, const nw::z_key_t& key, void* workspace, int32_t* status,
+                  uint64_t* index, hipStream_t s) {
+  const uint64_t n = cs.n;
+  if (n == 0) return 0;
+  CertWs w;
+  cert_ws_layout(n, headers_only ? 0 : cs.nvotes, static_cast<char*>(workspace), &w);
+  nw::cert_committee_t dc{com.nauth, reinterpret_cast<const uint32_t*>(com.pks), com.stakes,
+                          com.worker_offsets, com.worker_ids};
+  nw::cert_stream_t ds{n, cs.header_bytes, cs.header_offsets, cs.payload_counts,
+                       reinterpret_cast<const uint32_t*>(cs.ids), cs.vote_offsets,
+                       reinterpret_cast<const uint32_t*>(cs.vote_pks)};
+  NW_HIP(nw::launch_sha512_digest32(cs.header_bytes, cs.header_offsets, nullptr, n,
+                                    w.hdr_digest, s), "k_sha512 (header digests)");
+  NW_HIP(nw::launch_cert_prepare(dc, ds, headers_only, w.hdr_digest, w.authors, w.cert_digest,
+                                 w.pre1, w.pre2, w.idx1, w.idx2, s), "k_cert_prepare");
+  NW_HIP(nw::launch_verify_strict(reinterpret_cast<const uint32_t*>(cs.ids), 8, w.authors,
+                                  reinterpret_cast<const uint32_t*>(cs.header_sigs), n, w.hdr_st,
+                                  w.bitmap, s), "k_verify_strict (headers)");
+  if (!headers_only)
+    NW_HIP(nw::launch_verify_batch(w.cert_digest, cs.vote_offsets, n,
+                                   reinterpret_cast<const uint32_t*>(cs.vote_pks),
+                                   reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
+                                   static_cast<const uint32_t*>(z16), key, w.batch_ws,
+                                   w.batch_st, w.batch_idx, s), "verify_batch (votes)");
+  NW_HIP(nw::launch_cert_finalize(n, headers_only, w.pre1, w.pre2, w.idx1, w.idx2, w.hdr_st,
+                                  w.batch_st, w.batch_idx, status, index, s), "k_cert_finalize");
+  return 0;
+}
+
+int check_committee_host(const nw_committee* com) {
+  if (!com || (com->nauth && (!com->pks || !com->stakes || !com->worker_offsets)))
+    return set_err(NW_E_INVALID_ARG, "committee: null pointer");
+  for (size_t a = 1; a < com->nauth; ++a)
+    if (memcmp(com->pks + 32 * (a - 1), com->pks + 32 * a, 32) >= 0)
+      return set_err(NW_E_INVALID_ARG, "committee keys must be strictly increasing");
+  for (size_t a = 0; a < com->nauth; ++a)
+    if (com->worker_offsets[a + 1] < com->worker_offsets[a])
+      return set_err(NW_E_INVALID_ARG, "committee worker_offsets not monotone");
+  if (com->nauth && com->worker_offsets[com->nauth] && !com->worker_ids)
+    return set_err(NW_E_INVALID_ARG, "committee: null worker_ids");
+  return 0;
+}
+
+// Copies a host-memory committee into `p` (device), returns the device view.
+struct Stage {
+  char* p;
+  hipStream_t s;
+  int err = 0;
+  template <class T>
+  T* put(const T* src, size_t count) {
+    char* dst = p;
+    const size_t bytes = sizeof(T) * count;
+    if (bytes && !err) {
+      hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+      if (e != hipSuccess) err = set_err(NW_E_DEVICE, "H2D staging", e);
+    }
+    p += a256(bytes ? bytes : 1);
+    return reinterpret_cast<T*>(dst);
+  }
+};
+
+size_t committee_bytes(const nw_committee* com) {
+  const size_t na = com->nauth, nw_ = com->nauth ? com->worker_offsets[com->nauth] : 0;
+  return a256(32 * na + 1) + a256(4 * na + 1) + a256(8 * (na + 1)) + a256(4 * nw_ + 1);
+}
+
+nw_committee stage_committee(Stage& st, const nw_committee* com) {
+  nw_committee d;
+  d.nauth = com->nauth;
+  const size_t nwk = com->nauth ? com->worker_offsets[com->nauth] : 0;
+  d.pks = st.put(com->pks, 32 * com->nauth);
+  d.stakes = st.put(com->stakes, com->nauth);
+  d.worker_offsets = st.put(com->worker_offsets, com->nauth + 1);
+  d.worker_ids = st.put(com->worker_ids, nwk);
+  return d;
+}
+
+int certs_host(const nw_committee* com, const nw_certificates* cs, int headers_only,
+               const uint8_t* z16, int32_t* status_out, uint64_t* index_out) {
+  DevCtx* c;
+  int rc = begin(&c);
+  if (rc) return rc;
+  if (!cs || !status_out) return set_err(NW_E_INVALID_ARG, "null pointer");
+  rc = check_committee_host(com);
+  if (rc) return rc;
+  const size_t n = cs->n;
+  if (n == 0) return 0;
+  if (!cs->header_bytes || !cs->header_offsets || !cs->payload_counts || !cs->ids ||
+      !cs->header_sigs)
+    return set_err(NW_E_INVALID_ARG, "certificates: null pointer");
+  for (size_t i = 0; i < n; ++i) {
+    if (cs->header_offsets[i + 1] < cs->header_offsets[i])
+      return set_err(NW_E_INVALID_ARG, "header_offsets not monotone");
+    const uint64_t len = cs->header_offsets[i + 1] - cs->header_offsets[i];
+    const uint64_t fixed = 40 + 36 * (uint64_t)cs->payload_counts[i];
+    if (len < fixed || (len - fixed) % 32 != 0)
+      return set_err(NW_E_INVALID_ARG, "header bytes do not match payload_counts");
+  }
+  size_t nvotes = 0;
+  if (!headers_only) {
+    if (!cs->vote_offsets) return set_err(NW_E_INVALID_ARG, "vote_offsets is NULL");
+    if (cs->vote_offsets[0] != 0) return set_err(NW_E_INVALID_ARG, "vote_offsets[0] must be 0");
+    for (size_t i = 0; i < n; ++i)
+      if (cs->vote_offsets[i + 1] < cs->vote_offsets[i])
+        return set_err(NW_E_INVALID_ARG, "vote_offsets not monotone");
+    nvotes = cs->vote_offsets[n];
+    if (nvotes && (!cs->vote_pks || !cs->vote_sigs))
+      return set_err(NW_E_INVALID_ARG, "votes: null pointer");
+  }
+  const uint64_t hb0 = cs->header_offsets[0], hlen = cs->header_offsets[n] - hb0;
+  std::vector<uint64_t> ho(n + 1);
+  for (size_t i = 0; i <= n; ++i) ho[i] = cs->header_offsets[i] - hb0;
+  const size_t ws = cert_ws_layout(n, nvotes, nullptr, nullptr);
+  const size_t need = committee_bytes(com) + a256(hlen + 1) + a256(8 * (n + 1)) + a256(4 * n) +
+                      a256(32 * n) + a256(64 * n) + a256(8 * (n + 1)) + a256(32 * nvotes + 1) +
+                      a256(64 * nvotes + 1) + a256(16 * nvotes + 1) + a256(4 * n) +
+                      a256(8 * n) + a256(ws);
+  rc = reserve(*c, need);
+  if (rc) return rc;
+  hipStream_t s = c->stream;
+  Stage st{static_cast<char*>(c->dbuf), s};
+  nw_committee dcom = stage_committee(st, com);
+  nw_certificates d{};
+  d.n = n;
+  d.header_bytes = st.put(cs->header_bytes + hb0, hlen);
+  d.header_offsets = st.put(ho.data(), n + 1);
+  d.payload_counts = st.put(cs->payload_counts, n);
+  d.ids = st.put(cs->ids, 32 * n);
+  d.header_sigs = st.put(cs->header_sigs, 64 * n);
+  d.header_bytes_len = hlen;
+  const uint8_t* dz = nullptr;
+  if (!headers_only) {
+    d.vote_offsets = st.put(cs->vote_offsets, n + 1);
+    d.vote_pks = st.put(cs->vote_pks, 32 * nvotes);
+    d.vote_sigs = st.put(cs->vote_sigs, 64 * nvotes);
+    d.nvotes = nvotes;
+    if (z16) dz = st.put(z16, 16 * nvotes);
+  }
+  int32_t* dst = reinterpret_cast<int32_t*>(st.p); st.p += a256(4 * n);
+  uint64_t* dix = reinterpret_cast<uint64_t*>(st.p); st.p += a256(8 * n);
+  void* dws = st.p;
+  if (st.err) return st.err;
+  nw::z_key_t key;
+  rc = fill_key(key, nullptr);
+  if (rc) return rc;
+  rc = cert_pipeline(dcom, d, headers_only, dz, key, dws, dst, dix, s);
+  if (rc) return rc;
+  NW_HIP(hipMemcpyAsync(status_out, dst, 4 * n, hipMemcpyDeviceToHost, s), "D2H status");
+  if (index_out) NW_HIP(hipMemcpyAsync(index_out, dix, 8 * n, hipMemcpyDeviceToHost, s), "D2H index");
+  NW_HIP(hipStreamSynchronize(s), "sync");
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nw_certificates_verify_many(const nw_committee* committee, const nw_certificates* certs,
+                                const uint8_t* z16, int32_t* status_out, uint64_t* index_out) {
+  return certs_host(committee, certs, 0, z16, status_out, index_out);
+}
+
+int nw_headers_verify_many(const nw_committee* committee, const nw_certificates* headers,
+                           int32_t* status_out, uint64_t* index_out) {
+  return certs_host(committee, headers, 1, nullptr, status_out, index_out);
+}
+
+size_t nw_dev_certificates_workspace(size_t n, size_t nvotes) {
+  return cert_ws_layout(n, nvotes, nullptr, nullptr);
+}
+
+int nw_dev_certificates_verify_many(const nw_committee* committee, const nw_certificates* certs,
+                                    int headers_only, const void* z16, const uint8_t* zkey32,
+                                    void* workspace, int32_t* status_out, uint64_t* index_out,
+                                    void* stream) {
+  DevCtx* c;
+  int rc = begin(&c);
+  if (rc) return rc;
+  if (!committee || !certs || !workspace || !status_out)
+    return set_err(NW_E_INVALID_ARG, "null pointer");
+  if (certs->n == 0) return 0;
+  nw::z_key_t key;
+  rc = fill_key(key, zkey32);
+  if (rc) return rc;
+  return cert_pipeline(*committee, *certs, headers_only, z16, key, workspace, status_out,
+                       index_out, pick_stream(stream, c));
+}
+
+int nw_votes_verify_many(const nw_committee* committee, const uint8_t* ids,
+                         const uint64_t* rounds, const uint8_t* origins,
+                         const uint8_t* authors, const uint8_t* sigs, size_t n,
+                         int32_t* status_out) {
+  DevCtx* c;
+  int rc = begin(&c);
+  if (rc) return rc;
+  rc = check_committee_host(committee);
+  if (rc) return rc;
+  if (n == 0) return 0;
+  if (!ids || !rounds || !origins || !authors || !sigs || !status_out)
+    return set_err(NW_E_INVALID_ARG, "null pointer");
+  const size_t need = committee_bytes(committee) + a256(32 * n) + a256(8 * n) + a256(32 * n) +
+                      a256(32 * n) + a256(64 * n) + a256(32 * n) + 3 * a256(4 * n) +
+                      a256(8 * ((n + 63) / 64));
+  rc = reserve(*c, need);
+  if (rc) return rc;
+  hipStream_t s = c->stream;
+  Stage st{static_cast<char*>(c->dbuf), s};
+  nw_committee dcom = stage_committee(st, committee);
+  const uint8_t* d_id = st.put(ids, 32 * n);
+  const uint64_t* d_round = st.put(rounds, n);
+  const uint8_t* d_org = st.put(origins, 32 * n);
+  const uint8_t* d_au = st.put(authors, 32 * n);
+  const uint8_t* d_sig = st.put(sigs, 64 * n);
+  if (st.err) return st.err;
+  uint32_t* d_dig = reinterpret_cast<uint32_t*>(st.p); st.p += a256(32 * n);
+  int32_t* d_pre = reinterpret_cast<int32_t*>(st.p); st.p += a256(4 * n);
+  int32_t* d_sst = reinterpret_cast<int32_t*>(st.p); st.p += a256(4 * n);
+  int32_t* d_st = reinterpret_cast<int32_t*>(st.p); st.p += a256(4 * n);
+  uint64_t* d_bm = reinterpret_cast<uint64_t*>(st.p);
+  nw::cert_committee_t dc{dcom.nauth, reinterpret_cast<const uint32_t*>(dcom.pks), dcom.stakes,
+                          dcom.worker_offsets, dcom.worker_ids};
+  NW_HIP(nw::launch_vote_prepare(dc, n, reinterpret_cast<const uint32_t*>(d_id), d_round,
+                                 reinterpret_cast<const uint32_t*>(d_org),
+                                 reinterpret_cast<const uint32_t*>(d_au), d_dig, d_pre, s),
+         "k_vote_prepare");
+  NW_HIP(nw::launch_verify_strict(d_dig, 8, reinterpret_cast<const uint32_t*>(d_au),
+                                  reinterpret_cast<const uint32_t*>(d_sig), n, d_sst, d_bm, s),
+         "k_verify_strict (votes)");
+  NW_HIP(nw::launch_vote_finalize(n, d_pre, d_sst, d_st, s), "k_vote_finalize");
+  NW_HIP(hipMemcpyAsync(status_out, d_st, 4 * n, hipMemcpyDeviceToHost, s), "D2H status");
+  NW_HIP(hipStreamSynchronize(s), "sync");
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,269 @@
+// nw_cert.hip — primary message checks around the verification kernels.
+//
+//   k_cert_prepare    one lane per Header / Certificate (primary/src/messages.rs:48-67,
+//                     189-215): header id == Sha512(header bytes)[..32] (the digest comes
+//                     from k_sha512_digest32), committee checks (stake, worker ids, vote
+//                     reuse / stake / quorum, config/src/lib.rs:148-173), genesis rule, and
+//                     Certificate::digest = Sha512(id || round || origin)[..32] (226-234).
+//   k_cert_finalize   first failure in the reference's order, combining those checks with
+//                     the header's strict verdict (k_verify_strict) and the votes' batch
+//                     verdict (k_batch_*).
+//   k_vote_prepare    Vote::verify (131-153): stake(author) > 0 and Vote::digest.
+//   k_vote_finalize
+//
+// These are byte/integer bookkeeping kernels (a few hundred bytes per item); the
+// arithmetic lives in nw_kernels.hip.
+#include "nw_kernels.h"
+#include "nw_sha512.hpp"
+
+namespace nw {
+
+namespace {
+
+__device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// Committee lookup (BTreeMap<PublicKey, Authority>::get): binary search over the sorted
+// 32-byte keys; -1 if absent. key = 8 little-endian words of the public key bytes.
+__device__ int committee_find(const cert_committee_t& c, const uint32_t key[8]) {
+  uint32_t kb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) kb[j] = __builtin_bswap32(key[j]);   // lexicographic order
+  int lo = 0, hi = (int)c.nauth - 1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    const uint32_t* m = c.pks + 8 * (size_t)mid;
+    int cmp = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t mb = __builtin_bswap32(m[j]);
+      if (cmp == 0 && mb != kb[j]) cmp = mb < kb[j] ? -1 : 1;
+    }
+    if (cmp == 0) return mid;
+    if (cmp < 0) lo = mid + 1; else hi = mid - 1;
+  }
+  return -1;
+}
+
+__device__ __forceinline__ uint32_t committee_stake(const cert_committee_t& c, int a) {
+  return a < 0 ? 0u : c.stakes[a];
+}
+
+// Sha512(x32 || u64 LE || y32)[..32]: Vote::digest / Certificate::digest (72 bytes, 1 block).
+__device__ void digest_72(uint32_t out[8], const uint32_t x[8], uint64_t round,
+                          const uint32_t y[8]) {
+  uint64_t w[16], st[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    w[i] = ((uint64_t)__builtin_bswap32(x[2 * i]) << 32) | __builtin_bswap32(x[2 * i + 1]);
+    w[5 + i] = ((uint64_t)__builtin_bswap32(y[2 * i]) << 32) | __builtin_bswap32(y[2 * i + 1]);
+  }
+  w[4] = __builtin_bswap64(round);
+  w[9] = 0x8000000000000000ULL;
+#pragma unroll
+  for (int i = 10; i < 15; ++i) w[i] = 0;
+  w[15] = 72 * 8;
+  sha512_init(st);
+  sha512_compress(st, w);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    out[2 * i] = __builtin_bswap32((uint32_t)(st[i] >> 32));
+    out[2 * i + 1] = __builtin_bswap32((uint32_t)st[i]);
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com, cert_stream_t cs,
+                                                      int headers_only,
+                                                      const uint32_t* __restrict__ hdr_digest,
+                                                      uint32_t* __restrict__ authors,
+                                                      uint32_t* __restrict__ cert_digest,
+                                                      int32_t* __restrict__ pre1,
+                                                      int32_t* __restrict__ pre2,
+                                                      uint64_t* __restrict__ idx1,
+                                                      uint64_t* __restrict__ idx2) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cs.n) return;
+  const uint8_t* h = cs.header_bytes + cs.header_offsets[i];
+  uint32_t author[8], id[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    author[j] = ld_le32(h + 4 * j);
+    id[j] = cs.ids[8 * i + j];
+  }
+  const uint64_t round = (uint64_t)ld_le32(h + 32) | ((uint64_t)ld_le32(h + 36) << 32);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) authors[8 * i + j] = author[j];
+
+  const int a = committee_find(com, author);
+  int32_t p1 = 0, p2 = 0;
+  uint64_t x1 = 0, x2 = 0;
+  // Certificate::verify: genesis(committee).contains(self) compares (header.id, round,
+  // origin) with Certificate::genesis = (Digest::default(), 0, name) for every authority.
+  uint32_t idor = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) idor |= id[j];
+  const bool genesis = !headers_only && idor == 0 && round == 0 && a >= 0;
+  // Header::verify, in order: id well formed, author stake, worker ids.
+  bool id_ok = true;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) id_ok &= hdr_digest[8 * i + j] == id[j];
+  if (!id_ok) {
+    p1 = NW_DAG_INVALID_HEADER_ID;
+  } else if (committee_stake(com, a) == 0) {
+    p1 = NW_DAG_UNKNOWN_AUTHORITY;
+    x1 = ~0ULL;
+  } else {
+    const uint32_t np = cs.payload_counts[i];
+    const uint64_t wb = com.worker_offsets[a], we = com.worker_offsets[a + 1];
+    for (uint32_t e = 0; e < np && p1 == 0; ++e) {
+      const uint32_t wid = ld_le32(h + 40 + 36 * (uint64_t)e + 32);
+      bool found = false;
+      for (uint64_t w = wb; w < we; ++w) found |= com.worker_ids[w] == wid;
+      if (!found) { p1 = NW_DAG_MALFORMED_HEADER; x1 = e; }
+    }
+  }
+  if (!headers_only) {
+    // Quorum over the votes (messages.rs:199-211): reuse, then stake, per vote in order.
+    // Committee::quorum_threshold and the vote weight are config::Stake = u32 sums (wrapping
+    // as in a release build).
+    uint32_t total = 0;
+    for (uint64_t q = 0; q < com.nauth; ++q) total += com.stakes[q];
+    const uint32_t quorum = 2u * total / 3u + 1u;
+    const uint64_t vb = cs.vote_offsets[i], ve = cs.vote_offsets[i + 1];
+    uint32_t weight = 0;
+    for (uint64_t v = vb; v < ve && p2 == 0; ++v) {
+      uint32_t pk[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pk[j] = cs.vote_pks[8 * v + j];
+      bool reuse = false;
+      for (uint64_t u = vb; u < v && !reuse; ++u) {
+        bool eq = true;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) eq &= cs.vote_pks[8 * u + j] == pk[j];
+        reuse = eq;
+      }
+      if (reuse) { p2 = NW_DAG_AUTHORITY_REUSE; x2 = v - vb; break; }
+      const uint32_t st = committee_stake(com, committee_find(com, pk));
+      if (st == 0) { p2 = NW_DAG_UNKNOWN_AUTHORITY; x2 = v - vb; break; }
+      weight += st;
+    }
+    if (p2 == 0 && weight < quorum) p2 = NW_DAG_REQUIRES_QUORUM;
+    uint32_t cd[8];
+    digest_72(cd, id, round, author);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cert_digest[8 * i + j] = cd[j];
+  }
+  pre1[i] = genesis ? -1 : p1;
+  pre2[i] = p2;
+  idx1[i] = x1;
+  idx2[i] = x2;
+}
+
+__global__ __launch_bounds__(256) void k_cert_finalize(uint64_t n, int headers_only,
+                                                       const int32_t* __restrict__ pre1,
+                                                       const int32_t* __restrict__ pre2,
+                                                       const uint64_t* __restrict__ idx1,
+                                                       const uint64_t* __restrict__ idx2,
+                                                       const int32_t* __restrict__ hdr_status,
+                                                       const int32_t* __restrict__ batch_status,
+                                                       const uint64_t* __restrict__ batch_index,
+                                                       int32_t* __restrict__ status,
+                                                       uint64_t* __restrict__ index) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int32_t st = 0;
+  uint64_t ix = 0;
+  const int32_t p1 = pre1[i];
+  if (p1 < 0) {
+    st = 0;                                           // genesis certificate
+  } else if (p1 > 0) {
+    st = p1; ix = idx1[i];
+  } else if (hdr_status[i] != 0) {
+    st = NW_DAG_INVALID_SIGNATURE + hdr_status[i];
+  } else if (!headers_only) {
+    if (pre2[i] != 0) {
+      st = pre2[i]; ix = idx2[i];
+    } else if (batch_status[i] != 0) {
+      st = NW_DAG_INVALID_VOTES + batch_status[i]; ix = batch_index[i];
+    }
+  }
+  status[i] = st;
+  if (index) index[i] = ix;
+}
+
+__global__ __launch_bounds__(256) void k_vote_prepare(cert_committee_t com, uint64_t n,
+                                                      const uint32_t* __restrict__ ids,
+                                                      const uint64_t* __restrict__ rounds,
+                                                      const uint32_t* __restrict__ origins,
+                                                      const uint32_t* __restrict__ authors,
+                                                      uint32_t* __restrict__ digests,
+                                                      int32_t* __restrict__ pre) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t id[8], org[8], au[8], d[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    id[j] = ids[8 * i + j];
+    org[j] = origins[8 * i + j];
+    au[j] = authors[8 * i + j];
+  }
+  digest_72(d, id, rounds[i], org);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) digests[8 * i + j] = d[j];
+  pre[i] = committee_stake(com, committee_find(com, au)) == 0 ? NW_DAG_UNKNOWN_AUTHORITY : 0;
+}
+
+__global__ __launch_bounds__(256) void k_vote_finalize(uint64_t n, const int32_t* __restrict__ pre,
+                                                       const int32_t* __restrict__ sig_status,
+                                                       int32_t* __restrict__ status) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  status[i] = pre[i] ? pre[i] : (sig_status[i] ? NW_DAG_INVALID_SIGNATURE + sig_status[i] : 0);
+}
+
+static inline unsigned blocks_for(uint64_t n) { return (unsigned)((n + 255) / 256); }
+
+hipError_t launch_cert_prepare(const cert_committee_t& com, const cert_stream_t& cs,
+                               int headers_only, const uint32_t* hdr_digest, uint32_t* authors,
+                               uint32_t* cert_digest, int32_t* pre1, int32_t* pre2,
+                               uint64_t* idx1, uint64_t* idx2, hipStream_t stream) {
+  if (cs.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_cert_prepare, dim3(blocks_for(cs.n)), dim3(256), 0, stream, com, cs,
+                     headers_only, hdr_digest, authors, cert_digest, pre1, pre2, idx1, idx2);
+  return hipGetLastError();
+}
+
+hipError_t launch_cert_finalize(uint64_t n, int headers_only, const int32_t* pre1,
+                                const int32_t* pre2, const uint64_t* idx1, const uint64_t* idx2,
+                                const int32_t* hdr_status, const int32_t* batch_status,
+                                const uint64_t* batch_index, int32_t* status, uint64_t* index,
+                                hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_cert_finalize, dim3(blocks_for(n)), dim3(256), 0, stream, n,
+                     headers_only, pre1, pre2, idx1, idx2, hdr_status, batch_status,
+                     batch_index, status, index);
+  return hipGetLastError();
+}
+
+hipError_t launch_vote_prepare(const cert_committee_t& com, uint64_t n, const uint32_t* ids,
+                               const uint64_t* rounds, const uint32_t* origins,
+                               const uint32_t* authors, uint32_t* digests, int32_t* pre,
+                               hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_vote_prepare, dim3(blocks_for(n)), dim3(256), 0, stream, com, n, ids,
+                     rounds, origins, authors, digests, pre);
+  return hipGetLastError();
+}
+
+hipError_t launch_vote_finalize(uint64_t n, const int32_t* pre, const int32_t* sig_status,
+                                int32_t* status, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_vote_finalize, dim3(blocks_for(n)), dim3(256), 0, stream, n, pre,
+                     sig_status, status);
+  return hipGetLastError();
+}
+
+}  // namespace nw

@@ -17,6 +17,7 @@ struct z_key_t {
 // copies them to the current device's constant memory.
 hipError_t upload_consts();
 
+// lengths == nullptr: offsets has n + 1 entries and message i = [offsets[i], offsets[i+1]).
 hipError_t launch_sha512_digest32(const uint8_t* data, const uint64_t* offsets,
                                   const uint64_t* lengths, uint64_t n, uint32_t* out,
                                   hipStream_t stream);
@@ -38,5 +39,40 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                uint64_t nitems, const uint32_t* z16, const z_key_t& zkey,
                                void* workspace, int32_t* status, uint64_t* fail_index,
                                hipStream_t stream);
+
+// ---- primary messages (nw_cert.hip) ----------------------------------------------------
+struct cert_committee_t {
+  uint64_t nauth;
+  const uint32_t* pks;              // nauth x 8 words, sorted by bytes
+  const uint32_t* stakes;
+  const uint64_t* worker_offsets;   // nauth + 1
+  const uint32_t* worker_ids;
+};
+
+struct cert_stream_t {
+  uint64_t n;
+  const uint8_t* header_bytes;
+  const uint64_t* header_offsets;   // n + 1
+  const uint32_t* payload_counts;
+  const uint32_t* ids;              // n x 8 words
+  const uint64_t* vote_offsets;     // n + 1
+  const uint32_t* vote_pks;         // nvotes x 8 words
+};
+
+hipError_t launch_cert_prepare(const cert_committee_t& com, const cert_stream_t& cs,
+                               int headers_only, const uint32_t* hdr_digest, uint32_t* authors,
+                               uint32_t* cert_digest, int32_t* pre1, int32_t* pre2,
+                               uint64_t* idx1, uint64_t* idx2, hipStream_t stream);
+hipError_t launch_cert_finalize(uint64_t n, int headers_only, const int32_t* pre1,
+                                const int32_t* pre2, const uint64_t* idx1, const uint64_t* idx2,
+                                const int32_t* hdr_status, const int32_t* batch_status,
+                                const uint64_t* batch_index, int32_t* status, uint64_t* index,
+                                hipStream_t stream);
+hipError_t launch_vote_prepare(const cert_committee_t& com, uint64_t n, const uint32_t* ids,
+                               const uint64_t* rounds, const uint32_t* origins,
+                               const uint32_t* authors, uint32_t* digests, int32_t* pre,
+                               hipStream_t stream);
+hipError_t launch_vote_finalize(uint64_t n, const int32_t* pre, const int32_t* sig_status,
+                                int32_t* status, hipStream_t stream);
 
 }  // namespace nw

@@ -121,7 +121,7 @@ __global__ __launch_bounds__(256) void k_sha512_digest32(const uint8_t* __restri
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t* msg = data + offsets[i];
-  const uint64_t len = lengths[i];
+  const uint64_t len = lengths ? lengths[i] : offsets[i + 1] - offsets[i];
   const uint64_t nblocks = (len + 17 + 127) / 128;
   const uint64_t nfull = len / 128;   // blocks entirely inside the message
   uint64_t st[8], w[16];

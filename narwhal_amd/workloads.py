@@ -62,3 +62,73 @@ def ragged_messages(n: int, max_len: int, seed: int = 1) -> tuple[np.ndarray, np
     total = int(lengths.sum())
     data = rng.integers(0, 256, size=max(total, 1), dtype=np.uint8)
     return data, offsets, lengths
+
+
+# --------------------------------------------------------------------------------------
+# Certificate streams (BASELINE config 2): primary/src/messages.rs layouts.
+# --------------------------------------------------------------------------------------
+def quorum(n_auth: int) -> int:
+    """Votes needed at stake 1 each: Committee::quorum_threshold (config/src/lib.rs:167-173)."""
+    return 2 * n_auth // 3 + 1
+
+
+def _sort_digests(d: np.ndarray) -> np.ndarray:
+    """Sort [m, k, 32] digests along axis 1 in byte-lexicographic (BTreeSet) order."""
+    m, k = d.shape[:2]
+    rec = np.ascontiguousarray(d).view([("a", ">u8"), ("b", ">u8"), ("c", ">u8"), ("d", ">u8")])
+    return np.sort(rec.reshape(m, k), axis=1).view(np.uint8).reshape(m, k, 32)
+
+
+def certificate_stream(n_certs: int, keys: list[tuple[bytes, bytes]], sign_many, digest_many,
+                       payload: int = 0, seed: int = 0, n_votes: int | None = None) -> dict:
+    """n_certs honest certificates over the committee ``keys`` (list of (pk, sk)), stake 1
+    each, one worker (id 0) per authority. Certificate i: author = keys[i % N], round =
+    1 + i // N, ``payload`` (digest, worker 0) entries, q parents from a seeded stream
+    (sorted: BTreeSet order), votes by q distinct authorities (starting at the author) over
+    Certificate::digest. ``sign_many(sks[n,64], msgs[n,32]) -> sigs[n,64]`` and
+    ``digest_many(data, offsets[n+1]) -> [n,32]`` are supplied by the caller (the GPU
+    engine in bench.py, the oracle in tests), so this module computes nothing itself.
+
+    Returns the nw_certificates SoA dict (narwhal_amd.messages.pack_certificates layout)
+    plus 'committee' (pack_committee layout) and 'rounds', 'authors'."""
+    N = len(keys)
+    q = quorum(N) if n_votes is None else n_votes
+    rng = np.random.Generator(np.random.PCG64([seed, N, payload]))
+    order = sorted(range(N), key=lambda k: keys[k][0])
+    pk_sorted = np.array([np.frombuffer(keys[k][0], np.uint8) for k in order])
+    sks = np.array([np.frombuffer(keys[k][1], np.uint8) for k in range(N)])
+    pks = sks[:, 32:]
+    a = np.arange(n_certs) % N
+    rounds = (1 + np.arange(n_certs) // N).astype(np.uint64)
+    # header preimage: author || round || payload (sorted by digest) || parents (sorted)
+    L = 40 + 36 * payload + 32 * q
+    hb = np.zeros((n_certs, L), np.uint8)
+    hb[:, :32] = pks[a]
+    hb[:, 32:40] = rounds.astype("<u8").view(np.uint8).reshape(n_certs, 8)
+    if payload:
+        ent = np.zeros((n_certs, payload, 36), np.uint8)
+        ent[:, :, :32] = _sort_digests(rng.integers(0, 256, size=(n_certs, payload, 32),
+                                                    dtype=np.uint8))
+        hb[:, 40:40 + 36 * payload] = ent.reshape(n_certs, -1)
+    par = _sort_digests(rng.integers(0, 256, size=(n_certs, q, 32), dtype=np.uint8))
+    hb[:, 40 + 36 * payload:] = par.reshape(n_certs, -1)
+    ho = (np.arange(n_certs + 1) * L).astype(np.uint64)
+    ids = digest_many(hb.reshape(-1), ho)
+    hsig = sign_many(sks[a], ids)
+    cpre = np.zeros((n_certs, 72), np.uint8)
+    cpre[:, :32] = ids
+    cpre[:, 32:40] = hb[:, 32:40]
+    cpre[:, 40:] = pks[a]
+    cdig = digest_many(cpre.reshape(-1), (np.arange(n_certs + 1) * 72).astype(np.uint64))
+    voters = (a[:, None] + np.arange(q)[None, :]) % N
+    vsig = sign_many(sks[voters.reshape(-1)], np.repeat(cdig, q, axis=0))
+    return {
+        "header_bytes": hb.reshape(-1), "header_offsets": ho,
+        "payload_counts": np.full(n_certs, payload, np.uint32), "ids": ids,
+        "header_sigs": hsig, "vote_offsets": (np.arange(n_certs + 1) * q).astype(np.uint64),
+        "vote_pks": pks[voters.reshape(-1)].copy(), "vote_sigs": vsig,
+        "committee": {"pks": pk_sorted, "stakes": np.ones(N, np.uint32),
+                      "worker_offsets": np.arange(N + 1, dtype=np.uint64),
+                      "worker_ids": np.zeros(N, np.uint32)},
+        "rounds": rounds, "cert_digests": cdig, "q": q,
+    }

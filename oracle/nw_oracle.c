@@ -909,3 +909,156 @@ int nwo_msm(const uint8_t* scalars, const uint8_t* points, size_t n, uint8_t out
   free(pts);
   return 1;
 }
+
+/* ==================================================================================== */
+/* Primary messages (TEST INFRASTRUCTURE): Header::verify, Vote::verify,                */
+/* Certificate::verify — /root/reference/primary/src/messages.rs:48-67, 131-153,        */
+/* 189-234; Committee — /root/reference/config/src/lib.rs:139-173.                       */
+/* ==================================================================================== */
+
+/* BTreeMap<PublicKey, Authority>::get over the sorted keys: index or -1. */
+static long committee_find(const nwo_committee* c, const uint8_t pk[32]) {
+  long lo = 0, hi = (long)c->nauth - 1;
+  while (lo <= hi) {
+    long mid = (lo + hi) / 2;
+    int cmp = memcmp(c->pks + 32 * mid, pk, 32);
+    if (cmp == 0) return mid;
+    if (cmp < 0) lo = mid + 1; else hi = mid - 1;
+  }
+  return -1;
+}
+
+/* Committee::stake (lib.rs:148-151): 0 for unknown keys. */
+static uint32_t committee_stake(const nwo_committee* c, const uint8_t pk[32]) {
+  long a = committee_find(c, pk);
+  return a < 0 ? 0u : c->stakes[a];
+}
+
+/* Committee::quorum_threshold (lib.rs:167-173), config::Stake = u32 arithmetic. */
+static uint32_t committee_quorum(const nwo_committee* c) {
+  uint32_t total = 0;
+  for (size_t a = 0; a < c->nauth; ++a) total += c->stakes[a];
+  return 2u * total / 3u + 1u;
+}
+
+/* Sha512(x || round LE || y)[..32]: Vote::digest (messages.rs:145-153) and
+ * Certificate::digest (226-234). */
+void nwo_digest_72(const uint8_t x[32], uint64_t round, const uint8_t y[32], uint8_t out[32]) {
+  uint8_t buf[72], h[64];
+  memcpy(buf, x, 32);
+  for (int i = 0; i < 8; ++i) buf[32 + i] = (uint8_t)(round >> (8 * i));
+  memcpy(buf + 40, y, 32);
+  nwo_sha512(buf, 72, h);
+  memcpy(out, h, 32);
+}
+
+/* Header::verify (messages.rs:48-67). hb = author || round || P x (digest || wid) || parents. */
+static int header_verify(const nwo_committee* c, const uint8_t* hb, size_t hlen, uint32_t np,
+                         const uint8_t id[32], const uint8_t sig[64], uint64_t* index) {
+  uint8_t h[64];
+  nwo_sha512(hb, hlen, h);
+  if (memcmp(h, id, 32) != 0) return NWO_DAG_INVALID_HEADER_ID;
+  long a = committee_find(c, hb);
+  if (a < 0 || c->stakes[a] == 0) { *index = UINT64_MAX; return NWO_DAG_UNKNOWN_AUTHORITY; }
+  for (uint32_t e = 0; e < np; ++e) {
+    uint32_t wid = load32_le(hb + 40 + 36 * (size_t)e + 32);
+    int found = 0;
+    for (uint64_t w = c->worker_offsets[a]; w < c->worker_offsets[a + 1]; ++w)
+      found |= c->worker_ids[w] == wid;
+    if (!found) { *index = e; return NWO_DAG_MALFORMED_HEADER; }
+  }
+  int st = nwo_verify_strict(id, 32, hb, sig);
+  return st ? NWO_DAG_INVALID_SIGNATURE + st : 0;
+}
+
+int nwo_header_verify(const nwo_committee* c, const uint8_t* hb, size_t hlen, uint32_t np,
+                      const uint8_t id[32], const uint8_t sig[64], uint64_t* index) {
+  uint64_t ix = 0;
+  ensure_init();
+  int st = header_verify(c, hb, hlen, np, id, sig, &ix);
+  if (index) *index = ix;
+  return st;
+}
+
+int nwo_certificate_verify(const nwo_committee* c, const uint8_t* hb, size_t hlen,
+                           uint32_t np, const uint8_t id[32], const uint8_t hsig[64],
+                           const uint8_t* vote_pks, const uint8_t* vote_sigs, size_t nvotes,
+                           const uint8_t* z16, uint64_t* index) {
+  uint64_t ix = 0;
+  int st = 0;
+  ensure_init();
+  uint64_t round = 0;
+  for (int i = 0; i < 8; ++i) round |= (uint64_t)hb[32 + i] << (8 * i);
+  /* Genesis certificates are always valid: (id, round, origin) == (0, 0, authority). */
+  int idzero = 1;
+  for (int i = 0; i < 32; ++i) idzero &= id[i] == 0;
+  if (idzero && round == 0 && committee_find(c, hb) >= 0) goto done;
+  st = header_verify(c, hb, hlen, np, id, hsig, &ix);
+  if (st) goto done;
+  {
+    uint32_t weight = 0;
+    for (size_t v = 0; v < nvotes; ++v) {
+      for (size_t u = 0; u < v; ++u)
+        if (memcmp(vote_pks + 32 * u, vote_pks + 32 * v, 32) == 0) {
+          st = NWO_DAG_AUTHORITY_REUSE; ix = v; goto done;
+        }
+      uint32_t s = committee_stake(c, vote_pks + 32 * v);
+      if (s == 0) { st = NWO_DAG_UNKNOWN_AUTHORITY; ix = v; goto done; }
+      weight += s;
+    }
+    if (weight < committee_quorum(c)) { st = NWO_DAG_REQUIRES_QUORUM; goto done; }
+    uint8_t cd[32];
+    nwo_digest_72(id, round, hb, cd);
+    size_t fi = 0;
+    int b = nwo_verify_batch(cd, vote_pks, vote_sigs, nvotes, z16, &fi);
+    if (b) { st = NWO_DAG_INVALID_VOTES + b; ix = fi; }
+  }
+done:
+  if (index) *index = ix;
+  return st;
+}
+
+void nwo_certificates_verify_many(const nwo_committee* c, const uint8_t* header_bytes,
+                                  const uint64_t* header_offsets, const uint32_t* payload_counts,
+                                  const uint8_t* ids, const uint8_t* header_sigs,
+                                  const uint64_t* vote_offsets, const uint8_t* vote_pks,
+                                  const uint8_t* vote_sigs, size_t n, const uint8_t* z16,
+                                  int headers_only, int32_t* status, uint64_t* index,
+                                  int nthreads) {
+  ensure_init();
+#ifdef _OPENMP
+  if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 16) num_threads(nthreads)
+#endif
+  for (long i = 0; i < (long)n; ++i) {
+    const uint8_t* hb = header_bytes + header_offsets[i];
+    const size_t hl = header_offsets[i + 1] - header_offsets[i];
+    uint64_t ix = 0;
+    if (headers_only) {
+      status[i] = header_verify(c, hb, hl, payload_counts[i], ids + 32 * i, header_sigs + 64 * i,
+                                &ix);
+    } else {
+      const uint64_t vb = vote_offsets[i], nv = vote_offsets[i + 1] - vb;
+      status[i] = nwo_certificate_verify(c, hb, hl, payload_counts[i], ids + 32 * i,
+                                         header_sigs + 64 * i, vote_pks + 32 * vb,
+                                         vote_sigs + 64 * vb, nv, z16 ? z16 + 16 * vb : NULL,
+                                         &ix);
+    }
+    if (index) index[i] = ix;
+  }
+  (void)nthreads;
+}
+
+/* Vote::verify (messages.rs:131-142). */
+void nwo_votes_verify_many(const nwo_committee* c, const uint8_t* ids, const uint64_t* rounds,
+                           const uint8_t* origins, const uint8_t* authors, const uint8_t* sigs,
+                           size_t n, int32_t* status) {
+  ensure_init();
+  for (size_t i = 0; i < n; ++i) {
+    if (committee_stake(c, authors + 32 * i) == 0) { status[i] = NWO_DAG_UNKNOWN_AUTHORITY; continue; }
+    uint8_t d[32];
+    nwo_digest_72(ids + 32 * i, rounds[i], origins + 32 * i, d);
+    int st = nwo_verify_strict(d, 32, authors + 32 * i, sigs + 64 * i);
+    status[i] = st ? NWO_DAG_INVALID_SIGNATURE + st : 0;
+  }
+}

@@ -109,6 +109,43 @@ int nwo_point_add(const uint8_t P[32], const uint8_t Q[32], uint8_t out[32]);
 int nwo_msm(const uint8_t* scalars, const uint8_t* points, size_t n, uint8_t out[32],
             int* is_identity);
 
+/* ---- primary messages (primary/src/messages.rs:48-67, 131-153, 189-234) ---- */
+/* DagError codes; identical numbering to include/narwhal_amd.h (NW_DAG_*). */
+enum {
+  NWO_DAG_INVALID_HEADER_ID = 16,
+  NWO_DAG_UNKNOWN_AUTHORITY = 17,
+  NWO_DAG_MALFORMED_HEADER = 18,
+  NWO_DAG_AUTHORITY_REUSE = 19,
+  NWO_DAG_REQUIRES_QUORUM = 20,
+  NWO_DAG_INVALID_SIGNATURE = 32,   /* + NWO_ERR_* of the message's own signature    */
+  NWO_DAG_INVALID_VOTES = 48        /* + NWO_ERR_* of verify_batch over the votes      */
+};
+/* config::Committee (config/src/lib.rs:139-173), keys sorted by bytes. */
+typedef struct {
+  size_t nauth;
+  const uint8_t* pks;
+  const uint32_t* stakes;
+  const uint64_t* worker_offsets;
+  const uint32_t* worker_ids;
+} nwo_committee;
+void nwo_digest_72(const uint8_t x[32], uint64_t round, const uint8_t y[32], uint8_t out[32]);
+int nwo_header_verify(const nwo_committee* c, const uint8_t* hb, size_t hlen, uint32_t np,
+                      const uint8_t id[32], const uint8_t sig[64], uint64_t* index);
+int nwo_certificate_verify(const nwo_committee* c, const uint8_t* hb, size_t hlen,
+                           uint32_t np, const uint8_t id[32], const uint8_t hsig[64],
+                           const uint8_t* vote_pks, const uint8_t* vote_sigs, size_t nvotes,
+                           const uint8_t* z16, uint64_t* index);
+void nwo_certificates_verify_many(const nwo_committee* c, const uint8_t* header_bytes,
+                                  const uint64_t* header_offsets, const uint32_t* payload_counts,
+                                  const uint8_t* ids, const uint8_t* header_sigs,
+                                  const uint64_t* vote_offsets, const uint8_t* vote_pks,
+                                  const uint8_t* vote_sigs, size_t n, const uint8_t* z16,
+                                  int headers_only, int32_t* status, uint64_t* index,
+                                  int nthreads);
+void nwo_votes_verify_many(const nwo_committee* c, const uint8_t* ids, const uint64_t* rounds,
+                           const uint8_t* origins, const uint8_t* authors, const uint8_t* sigs,
+                           size_t n, int32_t* status);
+
 #ifdef __cplusplus
 }
 #endif

@@ -70,6 +70,9 @@ def lib() -> ctypes.CDLL:
         L.nwo_point_add.restype = I
         L.nwo_msm.argtypes = [P, P, S, P, ctypes.POINTER(I)]
         L.nwo_msm.restype = I
+        L.nwo_digest_72.argtypes = [P, ctypes.c_uint64, P, P]
+        L.nwo_certificates_verify_many.argtypes = [P, P, P, P, P, P, P, P, P, S, P, I, P, P, I]
+        L.nwo_votes_verify_many.argtypes = [P, P, P, P, P, P, S, P]
         _lib = L
     return _lib
 
@@ -247,3 +250,51 @@ def msm(scalars: list[bytes], points: list[bytes]) -> tuple[bytes, bool] | None:
     ok = lib().nwo_msm(_buf(b"".join(scalars)), _buf(b"".join(points)), n, out,
                        ctypes.byref(ident))
     return (out.raw, bool(ident.value)) if ok else None
+
+
+# ---- primary messages (primary/src/messages.rs:48-67, 131-153, 189-234) ----
+class _Committee(ctypes.Structure):
+    _fields_ = [("nauth", ctypes.c_size_t), ("pks", ctypes.c_void_p),
+                ("stakes", ctypes.c_void_p), ("worker_offsets", ctypes.c_void_p),
+                ("worker_ids", ctypes.c_void_p)]
+
+
+def _committee(c: dict) -> _Committee:
+    return _Committee(len(c["stakes"]), _np_ptr(c["pks"]), _np_ptr(c["stakes"]),
+                      _np_ptr(c["worker_offsets"]), _np_ptr(c["worker_ids"]))
+
+
+def digest_72(x: bytes, round_: int, y: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().nwo_digest_72(_buf(x), round_, _buf(y), out)
+    return out.raw
+
+
+def certificates_verify_many(committee: dict, p: dict, z16: np.ndarray | None = None,
+                             headers_only: bool = False, nthreads: int = 0
+                             ) -> tuple[np.ndarray, np.ndarray]:
+    """Certificate::verify (or Header::verify) over a packed stream (same SoA layout as
+    narwhal_amd.messages.pack_certificates / pack_committee)."""
+    n = len(p["header_offsets"]) - 1
+    st = np.zeros(max(n, 1), np.int32)
+    ix = np.zeros(max(n, 1), np.uint64)
+    cc = _committee(committee)
+    zp = None
+    if z16 is not None:
+        z16 = np.ascontiguousarray(z16, np.uint8)
+        zp = _np_ptr(z16)
+    lib().nwo_certificates_verify_many(
+        ctypes.byref(cc), _np_ptr(p["header_bytes"]), _np_ptr(p["header_offsets"]),
+        _np_ptr(p["payload_counts"]), _np_ptr(p["ids"]), _np_ptr(p["header_sigs"]),
+        _np_ptr(p["vote_offsets"]), _np_ptr(p["vote_pks"]), _np_ptr(p["vote_sigs"]), n, zp,
+        1 if headers_only else 0, _np_ptr(st), _np_ptr(ix), nthreads)
+    return st[:n], ix[:n]
+
+
+def votes_verify_many(committee: dict, p: dict, n: int) -> np.ndarray:
+    st = np.zeros(max(n, 1), np.int32)
+    cc = _committee(committee)
+    lib().nwo_votes_verify_many(ctypes.byref(cc), _np_ptr(p["ids"]), _np_ptr(p["rounds"]),
+                                _np_ptr(p["origins"]), _np_ptr(p["authors"]), _np_ptr(p["sigs"]),
+                                n, _np_ptr(st))
+    return st[:n]

@@ -1,0 +1,119 @@
+"""GPU parity for the primary-message entry points (nw_certificates_verify_many,
+nw_headers_verify_many, nw_votes_verify_many, nw_dev_certificates_verify_many) against the
+oracle: status codes AND indices bit-exact, with injected batch coefficients; verdicts
+equal with random coefficients on the deterministic set."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from narwhal_amd import _lib
+from narwhal_amd import messages as M
+from narwhal_amd import workloads as W
+from narwhal_amd.crypto import PublicKey, SecretKey, Signature
+from oracle import oracle as O
+
+from cert_cases import mutated_stream, oracle_digest_many, oracle_sign_many, votes_case
+from test_messages import HEADER_LEVEL, fixture_header
+
+pytestmark = pytest.mark.gpu
+
+
+class _Com:
+    """Adapter: a packed committee dict as a messages.Committee-like object."""
+
+    def __init__(self, p):
+        self._p = p
+
+    def packed(self):
+        return self._p
+
+
+def test_appendix_b_fixture_through_mirror():
+    keys, h = fixture_header()
+    committee = M.Committee({PublicKey(pk): M.Authority(1) for pk, _ in keys})
+    assert h.digest() == h.id                        # GPU SHA-512 over the header layout
+    h.verify(committee)
+    cert = M.Certificate(h)
+    cd = cert.digest()
+    cert.votes = [(PublicKey(pk), Signature.from_bytes(O.sign(sk, cd.value))) for pk, sk in keys]
+    cert.verify(committee)
+    for g in M.Certificate.genesis(committee):       # genesis certificates are always valid
+        g.verify(committee)
+    v = M.Vote.new(h, PublicKey(keys[0][0]), SecretKey(keys[0][1]))
+    v.verify(committee)
+    assert v.digest() == cd                          # Vote::digest == Certificate::digest
+    bad = M.Certificate(h, cert.votes[:2])
+    with pytest.raises(M.CertificateRequiresQuorum):
+        bad.verify(committee)
+    bad = M.Certificate(h, cert.votes[:2] + [cert.votes[0]])
+    with pytest.raises(M.AuthorityReuse):
+        bad.verify(committee)
+
+
+@pytest.mark.parametrize("N,copies", [(4, 3), (10, 2)])
+def test_certificates_vs_oracle(N, copies):
+    com, s, exp_st, exp_ix, cls = mutated_stream(N=N, copies=copies, seed=N)
+    z16 = np.random.Generator(np.random.PCG64(N)).integers(0, 256, size=(len(s["vote_pks"]), 16),
+                                                           dtype=np.uint8)
+    st, ix = M.verify_certificates_many(_Com(com), s, z16)
+    ost, oix = O.certificates_verify_many(com, s, z16)
+    assert np.array_equal(ost, exp_st) and np.array_equal(oix, exp_ix)
+    bad = [(c, int(a), int(b), int(x), int(y)) for c, a, b, x, y in zip(cls, st, ost, ix, oix)
+           if a != b or x != y]
+    assert not bad, bad
+    st2, ix2 = M.verify_certificates_many(_Com(com), s, None)   # CSPRNG coefficients
+    assert np.array_equal(st2, exp_st) and np.array_equal(ix2, exp_ix)
+
+
+def test_headers_vs_oracle():
+    com, s, exp_st, exp_ix, cls = mutated_stream(N=4, copies=2)
+    st, ix = M.verify_headers_many(_Com(com), s)
+    ost, oix = O.certificates_verify_many(com, s, headers_only=True)
+    assert np.array_equal(st, ost) and np.array_equal(ix, oix)
+    assert all((a != 0) == (c in HEADER_LEVEL or c.startswith("genesis"))
+               for a, c in zip(st, cls))
+
+
+def test_votes_vs_oracle():
+    com, p, n, exp = votes_case()
+    st = M.verify_votes_many(_Com(com), p)
+    assert st.tolist() == exp.tolist() == O.votes_verify_many(com, p, n).tolist()
+
+
+def test_certificate_stream_large_committee_payload():
+    keys = O.keys(50)
+    s = W.certificate_stream(40, keys, oracle_sign_many, oracle_digest_many, payload=3, seed=9)
+    st, ix = M.verify_certificates_many(_Com(s["committee"]), s)
+    assert st.tolist() == [0] * 40
+
+
+def test_device_entry_point_matches_host():
+    """nw_dev_certificates_verify_many on device-resident buffers (the bench path)."""
+    com, s, exp_st, exp_ix, cls = mutated_stream(N=4, copies=2, seed=11)
+    n = len(s["header_offsets"]) - 1
+    nv = int(s["vote_offsets"][-1])
+    z16 = np.random.Generator(np.random.PCG64(2)).integers(0, 256, size=(nv, 16), dtype=np.uint8)
+    dev = torch.device("cuda", 0)
+    T = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in s.items()}
+    C = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in com.items()}
+    zt = torch.from_numpy(z16).to(dev)
+    L = _lib.lib()
+    ws = torch.empty(L.nw_dev_certificates_workspace(n, nv), dtype=torch.uint8, device=dev)
+    st = torch.empty(n, dtype=torch.int32, device=dev)
+    ix = torch.empty(n, dtype=torch.int64, device=dev)
+    P = lambda t: t.data_ptr()
+    cc = M._CCommittee(len(com["stakes"]), P(C["pks"]), P(C["stakes"]), P(C["worker_offsets"]),
+                       P(C["worker_ids"]))
+    cs = M._CCertificates(n, P(T["header_bytes"]), P(T["header_offsets"]), P(T["payload_counts"]),
+                          P(T["ids"]), P(T["header_sigs"]), P(T["vote_offsets"]), P(T["vote_pks"]),
+                          P(T["vote_sigs"]), int(s["header_offsets"][-1]), nv)
+    torch.cuda.synchronize()
+    rc = L.nw_dev_certificates_verify_many(ctypes.byref(cc), ctypes.byref(cs), 0,
+                                           ctypes.c_void_p(P(zt)), None, ctypes.c_void_p(P(ws)),
+                                           ctypes.c_void_p(P(st)), ctypes.c_void_p(P(ix)), None)
+    assert rc == 0, L.nw_last_error()
+    assert L.nw_synchronize() == 0
+    assert st.cpu().numpy().tolist() == exp_st.tolist()
+    assert ix.cpu().numpy().astype(np.uint64).tolist() == exp_ix.tolist()
