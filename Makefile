@@ -14,6 +14,10 @@ $(BUILD)/nw_kernels.o: $(CSRC)/nw_kernels.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(BUILD)/nw_batch.o: $(CSRC)/nw_batch.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(BUILD)/nw_cert.o: $(CSRC)/nw_cert.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -22,7 +26,7 @@ $(BUILD)/nw_api.o: $(CSRC)/nw_api.cpp $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-$(LIB): $(BUILD)/nw_kernels.o $(BUILD)/nw_cert.o $(BUILD)/nw_api.o
+$(LIB): $(BUILD)/nw_kernels.o $(BUILD)/nw_batch.o $(BUILD)/nw_cert.o $(BUILD)/nw_api.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 oracle:

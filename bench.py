@@ -38,6 +38,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from narwhal_amd import _lib                 # noqa: E402
+from narwhal_amd import crypto as C          # noqa: E402
+from narwhal_amd import messages as M        # noqa: E402
 from narwhal_amd import workloads as W       # noqa: E402
 
 METRIC = "Ed25519 verifies/sec (1/2/4/8 MI355X) + SHA-512 GB/s vs dalek on host cores"
@@ -46,6 +48,8 @@ P_FIELD = 2**255 - 19
 
 # implementation-independent work per unit.
 MAC_PER_STRICT_VERIFY = 3200 * 64          # 204,800 32x32->64 MACs
+MAC_PER_BATCH_ITEM_LARGE = 1000 * 64       # batch item, n >= 10k (64,000 MACs)
+MAC_PER_BATCH_ITEM_SMALL = 2000 * 64       # batch item, small n (certificate votes)
 SHA_OPS_PER_BLOCK = 4800                   # int32 ops per 128-B block
 # Peaks (DESIGN.md "Measurement"): v_mad_u64_u32 issues at half rate on gfx950
 # (profiles/r01_ubench_valu_4wps.txt), so MAC peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz.
@@ -227,6 +231,145 @@ def run_sha(args, dev, stream, rank, world):
     return dict(n=nb, bytes=nb * W.BATCH_BYTES, elapsed=elapsed, kernel_ms=kernel_ms, parity=ok)
 
 
+def run_cert(args, dev, stream, rank, world, N: int):
+    """Config 2: Certificate::verify stream, committee N, q = 2N/3 + 1 votes per cert.
+    65,536 unique certificates (signed on the GPU), tiled to --certs; no dedup/caching."""
+    L = _lib.lib()
+    uniq = min(args.cert_unique, args.certs)
+    keys = [(bytes(pk), bytes(sd) + bytes(pk)) for sd, pk in
+            zip(W.fixture_seeds(N), C.keypair_from_seed_many(W.fixture_seeds(N)))]
+
+    def sign_many(sks, msgs):
+        return C.sign_many(sks, msgs)
+
+    def digest_many(data, offsets):
+        return C.sha512_digest32_many(data, offsets[:-1], np.diff(offsets))
+
+    log(f"cert stream N={N}: building {uniq} unique certificates, tiled to {args.certs}")
+    s = W.certificate_stream(uniq, keys, sign_many, digest_many, seed=rank)
+    q, n = s["q"], args.certs
+    Lh = int(s["header_offsets"][1])
+    reps = (n + uniq - 1) // uniq
+
+    def dev_tile(a, rows):
+        t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        return t.repeat((reps,) + (1,) * (t.dim() - 1))[:rows].contiguous()
+
+    T = {"header_bytes": dev_tile(s["header_bytes"].reshape(uniq, Lh), n).view(-1),
+         "ids": dev_tile(s["ids"], n), "header_sigs": dev_tile(s["header_sigs"], n),
+         "vote_pks": dev_tile(s["vote_pks"].reshape(uniq, q * 32), n).view(-1, 32),
+         "vote_sigs": dev_tile(s["vote_sigs"].reshape(uniq, q * 64), n).view(-1, 64),
+         "payload_counts": torch.zeros(n, dtype=torch.int32, device=dev),
+         "header_offsets": torch.arange(n + 1, dtype=torch.int64, device=dev) * Lh,
+         "vote_offsets": torch.arange(n + 1, dtype=torch.int64, device=dev) * q}
+    Cm = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in s["committee"].items()}
+    nv = n * q
+    host_vo = (np.arange(n + 1, dtype=np.uint64) * q)
+    ws = torch.empty(L.nw_dev_certificates_workspace(n, nv), dtype=torch.uint8, device=dev)
+    st = torch.empty(n, dtype=torch.int32, device=dev)
+    P = lambda t: t.data_ptr()
+    cc = M._CCommittee(N, P(Cm["pks"]), P(Cm["stakes"]), P(Cm["worker_offsets"]),
+                       P(Cm["worker_ids"]))
+    cs = M._CCertificates(n, P(T["header_bytes"]), P(T["header_offsets"]),
+                          P(T["payload_counts"]), P(T["ids"]), P(T["header_sigs"]),
+                          P(T["vote_offsets"]), P(T["vote_pks"]), P(T["vote_sigs"]), Lh * n, nv,
+                          host_vo.ctypes.data)
+    torch.cuda.synchronize()
+
+    def launch():
+        check(L.nw_dev_certificates_verify_many(ctypes.byref(cc), ctypes.byref(cs), 0, None, None,
+                                                ptr(ws), ptr(st), None, stream), "certificates")
+
+    elapsed, kernel_ms = timed_steps(launch, args.cert_steps, 1, world)
+    ok = bool((st == 0).all().item())
+    sec = elapsed / args.cert_steps
+    mac = MAC_PER_STRICT_VERIFY + q * MAC_PER_BATCH_ITEM_SMALL
+    res = {"committee": N, "quorum": q, "certs_per_gpu": n, "unique_certs": uniq,
+           "certs_per_s": n * world / sec, "sig_checks_per_s": n * (q + 1) * world / sec,
+           "ms_per_step": sec * 1e3, "achieved_TMAC_s": n * mac / (kernel_ms * 1e-3) / 1e12,
+           "work_per_cert": f"{mac} MAC (SURVEY 8d: strict + q x small-n batch item)",
+           "parity": "ok" if ok else "FAIL"}
+    del T, ws, st
+    torch.cuda.empty_cache()
+    return res
+
+
+def run_batch10k(args, dev, stream, rank, world):
+    """Config 1: crypto::Signature::verify_batch over 10,000 (PublicKey, Signature) pairs on
+    one digest (SHA-512("Hello, world!")[..32], crypto_tests.rs:55-56), keys = the StdRng
+    zero-seed fixture stream. Latency of one call through the host entry point (H2D +
+    kernels + D2H), plus device throughput with 64 such batches resident in HBM."""
+    L = _lib.lib()
+    n = 10_000
+    seeds = W.fixture_seeds(n)
+    pks = C.keypair_from_seed_many(seeds)
+    sks = np.concatenate([seeds, pks], axis=1)
+    digest = np.frombuffer(hashlib.sha512(b"Hello, world!").digest()[:32], np.uint8)
+    sigs = C.sign_many(sks, digest, shared_digest=True)
+    bad = sigs.copy()
+    bad[-1] = 0                                    # crypto_tests.rs:110-114: Signature::default()
+    idx = ctypes.c_size_t(0)
+
+    def call(sg):
+        return _lib.check(L.nw_signature_verify_batch(digest.ctypes.data_as(ctypes.c_void_p),
+                                                 pks.ctypes.data_as(ctypes.c_void_p),
+                                                 sg.ctypes.data_as(ctypes.c_void_p), n, None,
+                                                 ctypes.byref(idx)), "verify_batch")
+    ok = call(sigs) == 0 and call(bad) != 0
+    for _ in range(2):
+        call(sigs)
+    reps = 10
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ok &= call(sigs) == 0
+    lat = (time.perf_counter() - t0) / reps
+    # throughput: nb independent 10k batches resident on the device
+    nb = args.batch_many
+    d_pk = torch.from_numpy(pks).to(dev).repeat(nb, 1).contiguous()
+    d_sig = torch.from_numpy(sigs).to(dev).repeat(nb, 1).contiguous()
+    d_dig = torch.from_numpy(digest).to(dev).repeat(nb).contiguous()
+    d_off = torch.arange(nb + 1, dtype=torch.int64, device=dev) * n
+    host_off = np.arange(nb + 1, dtype=np.uint64) * n
+    ws = torch.empty(L.nw_dev_verify_batch_workspace(nb, nb * n), dtype=torch.uint8, device=dev)
+    d_st = torch.empty(nb, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    def launch():
+        check(L.nw_dev_verify_batch_many(ptr(d_dig), ptr(d_pk), ptr(d_sig), ptr(d_off),
+                                         host_off.ctypes.data_as(ctypes.c_void_p), nb,
+                                         nb * n, None, None, ptr(ws), ptr(d_st), None, stream),
+              "verify_batch_many")
+    elapsed, kernel_ms = timed_steps(launch, args.steps, 1, world)
+    ok &= bool((d_st == 0).all().item())
+    sec = elapsed / args.steps
+    res = {"items": n, "latency_ms": lat * 1e3, "verifies_per_s_one_call": n / lat,
+           "batches_resident": nb, "verifies_per_s_resident": nb * n * world / sec,
+           "achieved_TMAC_s": nb * n * MAC_PER_BATCH_ITEM_LARGE / (kernel_ms * 1e-3) / 1e12,
+           "work_per_item": f"{MAC_PER_BATCH_ITEM_LARGE} MAC (SURVEY 8d, n >= 10k)",
+           "parity": "ok" if ok else "FAIL"}
+    del d_pk, d_sig, ws
+    torch.cuda.empty_cache()
+    return res, (digest, pks, sigs)
+
+
+def cpu_baseline_batch(sample, seconds: float):
+    """Oracle verify_batch (the dalek-equivalent restatement, single thread like dalek's
+    verify_batch) on the same 10k batch, repeated for about ``seconds``."""
+    from oracle import oracle as O
+    digest, pks, sigs = sample
+    t0 = time.perf_counter()
+    k = 0
+    while True:
+        st, _ = O.verify_batch(digest.tobytes(), pks, sigs)
+        assert st == 0
+        k += 1
+        if time.perf_counter() - t0 > seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": k * len(pks) / dt, "unit": "verifies/s", "cores": 1, "kind": "port",
+            "sample": f"{k} x verify_batch over the 10k config-1 batch, 1 thread, {dt:.1f} s"}
+
+
 def cpu_baseline_strict(sample, seconds: float):
     """Oracle ('port', the dalek-equivalent restatement) on the host cores, bounded."""
     from oracle import oracle as O
@@ -255,13 +398,20 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["strict", "sha"], default="strict")
+    ap.add_argument("--workload", choices=["strict", "sha", "cert", "batch"], default="strict")
     ap.add_argument("--items-per-gpu", type=int, default=12_500_000)
     ap.add_argument("--unique", type=int, default=1 << 18)
     ap.add_argument("--sha-batches", type=int, default=65536)
     ap.add_argument("--sha-unique", type=int, default=256)
     ap.add_argument("--no-sha", action="store_true", help="skip the secondary SHA-512 leg")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--certs", type=int, default=1_000_000)
+    ap.add_argument("--cert-unique", type=int, default=65536)
+    ap.add_argument("--cert-steps", type=int, default=2)
+    ap.add_argument("--committees", default="4,10,50,100")
+    ap.add_argument("--no-cert", action="store_true", help="skip the config-2 certificate leg")
+    ap.add_argument("--no-batch", action="store_true", help="skip the config-1 verify_batch leg")
+    ap.add_argument("--batch-many", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -323,12 +473,48 @@ def main():
                                 "parity": "ok" if s["parity"] else "FAIL"}
             if not s["parity"]:
                 result["parity"] = "FAIL"
+        if not args.no_cert:
+            result["cert_stream"] = {}
+            for N in [int(x) for x in args.committees.split(",") if x]:
+                r2 = run_cert(args, dev, stream, rank, world, N)
+                result["cert_stream"][f"N{N}"] = r2
+                if r2["parity"] != "ok":
+                    result["parity"] = "FAIL"
+        if not args.no_batch:
+            r1, bsample = run_batch10k(args, dev, stream, rank, world)
+            result["verify_batch_10k"] = r1
+            if r1["parity"] != "ok":
+                result["parity"] = "FAIL"
+            if rank == 0 and world == 1 and not args.no_cpu_baseline:
+                r1["cpu_baseline"] = cpu_baseline_batch(bsample, min(5.0, args.cpu_seconds))
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             cb, agree = cpu_baseline_strict(sample, args.cpu_seconds)
             result["cpu_baseline"] = cb
             if not agree:
                 result["parity"] = "FAIL"
                 log("oracle disagrees with GPU statuses on the cpu_baseline sample")
+    elif args.workload == "cert":
+        res = {f"N{N}": run_cert(args, dev, stream, rank, world, N)
+               for N in [int(x) for x in args.committees.split(",") if x]}
+        last = list(res.values())[-1]
+        result = {"metric": METRIC, "value": last["sig_checks_per_s"], "unit": "verifies/s",
+                  "n_gpus": world, "steps": args.cert_steps, "warmup": 1,
+                  "ms_per_step": last["ms_per_step"], "higher_is_better": True,
+                  "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+                  "config": {"workload": "config2_certificate_stream",
+                             "certs_per_gpu": args.certs, "parallelism": f"shard{world}"},
+                  "cert_stream": res,
+                  "parity": "ok" if all(r["parity"] == "ok" for r in res.values()) else "FAIL"}
+    elif args.workload == "batch":
+        r1, bsample = run_batch10k(args, dev, stream, rank, world)
+        result = {"metric": METRIC, "value": r1["verifies_per_s_resident"], "unit": "verifies/s",
+                  "n_gpus": world, "steps": args.steps, "warmup": 1,
+                  "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
+                  "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+                  "config": {"workload": "config1_verify_batch_10k", "parallelism": f"shard{world}"},
+                  "verify_batch_10k": r1, "parity": r1["parity"]}
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline_batch(bsample, min(5.0, args.cpu_seconds))
     else:
         s = run_sha(args, dev, stream, rank, world)
         gbs = s["bytes"] * world / (s["elapsed"] / args.steps) / 1e9

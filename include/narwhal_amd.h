@@ -148,6 +148,8 @@ typedef struct nw_certificates {
   const uint8_t* vote_sigs;        /* vote_offsets[n] x 64: certificate.votes[j].1         */
   size_t header_bytes_len;         /* total bytes of header_bytes (device entry points)    */
   size_t nvotes;                   /* vote_offsets[n] (device entry points)                */
+  const uint64_t* host_vote_offsets; /* device entry points: host copy of vote_offsets
+                                        (optional; NULL = read back, blocking)             */
 } nw_certificates;
 
 /* n x Certificate::verify(committee) (primary/src/messages.rs:189-215, with
@@ -187,14 +189,20 @@ int nw_dev_keypair_from_seed_many(const void* seeds, size_t n, void* pks_out, vo
 int nw_dev_sign_many(const void* sks, size_t sk_stride, const void* digests,
                      size_t digest_stride, size_t n, void* sigs_out, void* stream);
 
-/* Workspace bytes nw_dev_verify_batch_many needs for nitems items. */
-size_t nw_dev_verify_batch_workspace(size_t nitems);
-/* z16 NULL: coefficients drawn on the device from ChaCha20 keyed by zkey32 (32 bytes from
+/* Workspace bytes nw_dev_verify_batch_many needs for nbatches batches of nitems votes in
+ * total (bounded: large calls are processed in slices of ~4M votes; a single batch may not
+ * exceed one slice). */
+size_t nw_dev_verify_batch_workspace(size_t nbatches, size_t nitems);
+/* offsets: device copy of the nbatches + 1 batch boundaries (offsets[0] = 0,
+ * offsets[nbatches] = nitems); host_offsets: the same values in host memory, used to plan
+ * the launch (NULL: read back from the device, which blocks until the stream is idle).
+ * z16 NULL: coefficients drawn on the device from ChaCha20 keyed by zkey32 (32 bytes from
  * the OS CSPRNG if zkey32 is NULL). fail_index (optional, device): nbatches x uint64. */
 int nw_dev_verify_batch_many(const void* digests, const void* pks, const void* sigs,
-                             const uint64_t* offsets, size_t nbatches, size_t nitems,
-                             const void* z16, const uint8_t* zkey32, void* workspace,
-                             int32_t* status_out, uint64_t* fail_index, void* stream);
+                             const uint64_t* offsets, const uint64_t* host_offsets,
+                             size_t nbatches, size_t nitems, const void* z16,
+                             const uint8_t* zkey32, void* workspace, int32_t* status_out,
+                             uint64_t* fail_index, void* stream);
 
 /* Device form of nw_certificates_verify_many: every pointer inside *committee and *certs
  * (and z16, status_out, index_out, workspace) is a device pointer; the structs themselves

@@ -60,8 +60,8 @@ def lib() -> ctypes.CDLL:
         "nw_sign_many": ([P, S, P, S, S, P], I),
         "nw_dev_keypair_from_seed_many": ([P, S, P, P], I),
         "nw_dev_sign_many": ([P, S, P, S, S, P, P], I),
-        "nw_dev_verify_batch_workspace": ([S], S),
-        "nw_dev_verify_batch_many": ([P, P, P, P, S, S, P, P, P, P, P, P], I),
+        "nw_dev_verify_batch_workspace": ([S, S], S),
+        "nw_dev_verify_batch_many": ([P, P, P, P, P, S, S, P, P, P, P, P, P], I),
         "nw_certificates_verify_many": ([P, P, P, P, P], I),
         "nw_headers_verify_many": ([P, P, P, P], I),
         "nw_votes_verify_many": ([P, P, P, P, P, P, S, P], I),

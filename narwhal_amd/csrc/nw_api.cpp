@@ -377,7 +377,9 @@ int nw_sign_many(const uint8_t* sks, size_t sk_stride, const uint8_t* digests,
 }
 
 // ------------------------------------------------------------------------------------
-size_t nw_dev_verify_batch_workspace(size_t nitems) { return nw::batch_workspace_bytes(nitems); }
+size_t nw_dev_verify_batch_workspace(size_t nbatches, size_t nitems) {
+  return nw::batch_workspace_bytes(nbatches, nitems);
+}
 
 static int fill_key(nw::z_key_t& k, const uint8_t* key32) {
   if (key32) {
@@ -390,10 +392,27 @@ static int fill_key(nw::z_key_t& k, const uint8_t* key32) {
   return 0;
 }
 
+// Host copy of the batch offsets: the caller's, or read back from the device (blocking).
+static int host_offsets_of(const uint64_t* dev_offsets, const uint64_t* host_offsets,
+                           size_t nbatches, hipStream_t s, std::vector<uint64_t>& tmp,
+                           const uint64_t** out) {
+  if (host_offsets) {
+    *out = host_offsets;
+    return 0;
+  }
+  tmp.resize(nbatches + 1);
+  NW_HIP(hipMemcpyAsync(tmp.data(), dev_offsets, 8 * (nbatches + 1), hipMemcpyDeviceToHost, s),
+         "D2H offsets");
+  NW_HIP(hipStreamSynchronize(s), "sync (offsets)");
+  *out = tmp.data();
+  return 0;
+}
+
 int nw_dev_verify_batch_many(const void* digests, const void* pks, const void* sigs,
-                             const uint64_t* offsets, size_t nbatches, size_t nitems,
-                             const void* z16, const uint8_t* zkey32, void* workspace,
-                             int32_t* status_out, uint64_t* fail_index, void* stream) {
+                             const uint64_t* offsets, const uint64_t* host_offsets,
+                             size_t nbatches, size_t nitems, const void* z16,
+                             const uint8_t* zkey32, void* workspace, int32_t* status_out,
+                             uint64_t* fail_index, void* stream) {
   DevCtx* c;
   int rc = begin(&c);
   if (rc) return rc;
@@ -403,11 +422,18 @@ int nw_dev_verify_batch_many(const void* digests, const void* pks, const void* s
   nw::z_key_t key;
   rc = fill_key(key, zkey32);
   if (rc) return rc;
-  NW_HIP(nw::launch_verify_batch(static_cast<const uint32_t*>(digests), offsets, nbatches,
+  hipStream_t s = pick_stream(stream, c);
+  std::vector<uint64_t> tmp;
+  const uint64_t* ho;
+  rc = host_offsets_of(offsets, host_offsets, nbatches, s, tmp, &ho);
+  if (rc) return rc;
+  if (ho[0] != 0 || ho[nbatches] != nitems)
+    return set_err(NW_E_INVALID_ARG, "offsets must run from 0 to nitems");
+  NW_HIP(nw::launch_verify_batch(static_cast<const uint32_t*>(digests), offsets, ho, nbatches,
                                  static_cast<const uint32_t*>(pks),
                                  static_cast<const uint32_t*>(sigs), nitems,
                                  static_cast<const uint32_t*>(z16), key, workspace, status_out,
-                                 fail_index, pick_stream(stream, c)),
+                                 fail_index, s),
          "verify_batch launch");
   return 0;
 }
@@ -423,7 +449,7 @@ static int batch_host(const uint8_t* digests, size_t ndig_bytes, const uint8_t* 
   const size_t b_d = a256(ndig_bytes), b_off = a256(8 * (nbatches + 1)),
                b_pk = a256(32 * (nitems ? nitems : 1)), b_sig = a256(64 * (nitems ? nitems : 1)),
                b_z = a256(16 * (nitems ? nitems : 1)), b_st = a256(4 * nbatches),
-               b_fi = a256(8 * nbatches), b_ws = a256(nw::batch_workspace_bytes(nitems));
+               b_fi = a256(8 * nbatches), b_ws = a256(nw::batch_workspace_bytes(nbatches, nitems));
   rc = reserve(*c, b_d + b_off + b_pk + b_sig + b_z + b_st + b_fi + b_ws);
   if (rc) return rc;
   char* p = static_cast<char*>(c->dbuf);
@@ -446,8 +472,8 @@ static int batch_host(const uint8_t* digests, size_t ndig_bytes, const uint8_t* 
   nw::z_key_t key;
   rc = fill_key(key, nullptr);
   if (rc) return rc;
-  NW_HIP(nw::launch_verify_batch(reinterpret_cast<const uint32_t*>(d_d), d_off, nbatches,
-                                 reinterpret_cast<const uint32_t*>(d_pk),
+  NW_HIP(nw::launch_verify_batch(reinterpret_cast<const uint32_t*>(d_d), d_off, offsets,
+                                 nbatches, reinterpret_cast<const uint32_t*>(d_pk),
                                  reinterpret_cast<const uint32_t*>(d_sig), nitems,
                                  z16 ? reinterpret_cast<const uint32_t*>(d_z) : nullptr, key,
                                  d_ws, d_st, d_fi, s),
@@ -508,7 +534,8 @@ size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
   const size_t m = n ? n : 1;
   const size_t sizes[12] = {a256(32 * m), a256(32 * m), a256(32 * m), a256(4 * m), a256(4 * m),
                             a256(4 * m),  a256(4 * m),  a256(8 * m),  a256(8 * m), a256(8 * m),
-                            a256(8 * ((m + 63) / 64)), a256(nw::batch_workspace_bytes(nvotes))};
+                            a256(8 * ((m + 63) / 64)),
+                            nvotes ? a256(nw::batch_workspace_bytes(n, nvotes)) : 256};
   size_t off[12], tot = 0;
   for (int k = 0; k < 12; ++k) { off[k] = tot; tot += sizes[k]; }
   if (w) {
@@ -529,9 +556,10 @@ size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
 }
 
 // The whole device pipeline; every pointer is a device pointer.
-int cert_pipeline(const nw_committee& com, const nw_certificates& cs, int headers_only,
-                  const void* z16, const nw::z_key_t& key, void* workspace, int32_t* status,
-                  uint64_t* index, hipStream_t s) {
+int cert_pipeline(const nw_committee& com, const nw_certificates& cs,
+                  const uint64_t* host_vote_offsets, int headers_only, const void* z16,
+                  const nw::z_key_t& key, void* workspace, int32_t* status, uint64_t* index,
+                  hipStream_t s) {
   const uint64_t n = cs.n;
   if (n == 0) return 0;
   CertWs w;
@@ -549,7 +577,7 @@ int cert_pipeline(const nw_committee& com, const nw_certificates& cs, int header
                                   reinterpret_cast<const uint32_t*>(cs.header_sigs), n, w.hdr_st,
                                   w.bitmap, s), "k_verify_strict (headers)");
   if (!headers_only)
-    NW_HIP(nw::launch_verify_batch(w.cert_digest, cs.vote_offsets, n,
+    NW_HIP(nw::launch_verify_batch(w.cert_digest, cs.vote_offsets, host_vote_offsets, n,
                                    reinterpret_cast<const uint32_t*>(cs.vote_pks),
                                    reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
                                    static_cast<const uint32_t*>(z16), key, w.batch_ws,
@@ -675,7 +703,7 @@ int certs_host(const nw_committee* com, const nw_certificates* cs, int headers_o
   nw::z_key_t key;
   rc = fill_key(key, nullptr);
   if (rc) return rc;
-  rc = cert_pipeline(dcom, d, headers_only, dz, key, dws, dst, dix, s);
+  rc = cert_pipeline(dcom, d, cs->vote_offsets, headers_only, dz, key, dws, dst, dix, s);
   if (rc) return rc;
   NW_HIP(hipMemcpyAsync(status_out, dst, 4 * n, hipMemcpyDeviceToHost, s), "D2H status");
   if (index_out) NW_HIP(hipMemcpyAsync(index_out, dix, 8 * n, hipMemcpyDeviceToHost, s), "D2H index");
@@ -714,8 +742,17 @@ int nw_dev_certificates_verify_many(const nw_committee* committee, const nw_cert
   nw::z_key_t key;
   rc = fill_key(key, zkey32);
   if (rc) return rc;
-  return cert_pipeline(*committee, *certs, headers_only, z16, key, workspace, status_out,
-                       index_out, pick_stream(stream, c));
+  hipStream_t s = pick_stream(stream, c);
+  std::vector<uint64_t> tmp;
+  const uint64_t* hvo = nullptr;
+  if (!headers_only) {
+    rc = host_offsets_of(certs->vote_offsets, certs->host_vote_offsets, certs->n, s, tmp, &hvo);
+    if (rc) return rc;
+    if (hvo[0] != 0 || hvo[certs->n] != certs->nvotes)
+      return set_err(NW_E_INVALID_ARG, "vote_offsets must run from 0 to nvotes");
+  }
+  return cert_pipeline(*committee, *certs, hvo, headers_only, z16, key, workspace, status_out,
+                       index_out, s);
 }
 
 int nw_votes_verify_many(const nw_committee* committee, const uint8_t* ids,

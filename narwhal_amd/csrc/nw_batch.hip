@@ -1,0 +1,569 @@
+// nw_batch.hip — crypto::Signature::verify_batch (crypto/src/lib.rs:206-219 -> dalek
+// verify_batch [ext]) for many independent batches, as a chunked Straus multi-scalar
+// multiplication:
+//
+//   sum_i z_i R_i + sum_i (z_i k_i mod l) A_i - (sum_i z_i s_i mod l) B == identity
+//
+//   k_bv_plan     one workgroup per slice: splits every batch into ceil(n_b / C) balanced
+//                 chunks (block-wide scan) and lists the batches that need a combine step.
+//   k_bv_items    one lane per vote: parse/decode flags, k_i = H(R||A||M) mod l, z_i
+//                 (ChaCha20 or injected), c_i = z_i k_i, b_i = z_i s_i, signed 4-bit
+//                 digits of c_i and z_i, and the tables j*A_i, j*R_i (j = 1..8, cached form)
+//                 written to HBM.
+//   k_bv_chunks   one lane per chunk: a Straus ladder shared by the chunk's 2m points and
+//                 B — 252 doublings per chunk instead of per vote — adding table entries
+//                 per 4-bit window and [-(sum b)]B by 8-bit windows over the LDS B table.
+//                 A batch that is a single chunk is finished here (identity test + first
+//                 failure in reference order).
+//   k_bv_combine  one wave per multi-chunk (or empty) batch: sums the chunk points, the
+//                 first failures, and tests the total.
+//
+// Work per vote: 2 decompressions, ~97 table additions and the tables (SURVEY 8(d):
+// 64,000 MAC/vote at n >= 10k); the 252 doublings and the B term are shared per chunk.
+#include "nw_kernels.h"
+#include "nw_point.hpp"
+#include "nw_scalar.hpp"
+#include "nw_sha512.hpp"
+#include "nw_ladder.hpp"
+#include "nw_consts.hpp"
+
+#include <stdlib.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+namespace nw {
+
+namespace {
+
+struct batch_consts {
+  curve_consts k;
+  ge_niels btab[129];
+};
+__constant__ batch_consts g_bc;
+
+constexpr int BT_WORDS = 129 * 30;
+constexpr uint64_t kSliceUnits = 4ull << 20;   // items + batches per slice (workspace bound)
+
+// Test hooks (tests/test_gpu_batch.py): NW_BATCH_SLICE_UNITS shrinks the slice, and
+// NW_BATCH_CHUNK fixes the chunk size, so small inputs exercise every path.
+uint64_t env_u64(const char* name, uint64_t dflt) {
+  const char* v = getenv(name);
+  if (!v || !*v) return dflt;
+  const unsigned long long x = strtoull(v, nullptr, 10);
+  return x ? (uint64_t)x : dflt;
+}
+uint64_t slice_units() { return env_u64("NW_BATCH_SLICE_UNITS", kSliceUnits); }
+constexpr uint32_t kMaxChunk = 128;
+constexpr uint32_t kNone = 0xffffffffu;
+
+// Per-vote record written by k_bv_items (96 bytes).
+struct bv_item {
+  uint32_t c[8];     // c_i + 0x88..8: signed 4-bit digits of z_i k_i mod l
+  uint32_t z[5];     // z_i + 0x88..8 (33 digits)
+  uint32_t flags;    // BF_* (check FAILED)
+  uint32_t pad[2];
+  uint32_t b[8];     // z_i s_i mod l
+};
+
+struct bv_chunk {
+  uint64_t start;    // first item (global index)
+  uint32_t batch;
+  uint32_t count;
+};
+
+struct bv_chunk_out {
+  ge P;              // partial sum (with T)
+  uint32_t first[3]; // first failing item per class, relative to the batch start
+  uint32_t pad;
+};
+
+enum : uint32_t { BF_S_HIGH = 1, BF_A_DECODE = 2, BF_S_NONCANON = 4, BF_R_DECODE = 8 };
+
+__device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+
+__device__ __forceinline__ void load_btab(ge_niels* s_btab) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&g_bc.btab[0]);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(s_btab);
+  for (int i = threadIdx.x; i < BT_WORDS; i += blockDim.x) dst[i] = src[i];
+}
+
+__device__ __forceinline__ void hram96(uint32_t x[16], const uint32_t R[8], const uint32_t A[8],
+                                       const uint32_t M[8]) {
+  uint64_t w[16], st[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    w[i] = ((uint64_t)bswap(R[2 * i]) << 32) | bswap(R[2 * i + 1]);
+    w[4 + i] = ((uint64_t)bswap(A[2 * i]) << 32) | bswap(A[2 * i + 1]);
+    w[8 + i] = ((uint64_t)bswap(M[2 * i]) << 32) | bswap(M[2 * i + 1]);
+  }
+  w[12] = 0x8000000000000000ULL;
+  w[13] = 0;
+  w[14] = 0;
+  w[15] = 96 * 8;
+  sha512_init(st);
+  sha512_compress(st, w);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    x[2 * i] = bswap((uint32_t)(st[i] >> 32));
+    x[2 * i + 1] = bswap((uint32_t)st[i]);
+  }
+}
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+
+// z_i = ChaCha20(key, nonce, block i/4) bytes [16 (i%4), 16 (i%4) + 16) (DJB layout).
+__device__ void chacha20_z(uint32_t z[4], const uint32_t key[8], uint64_t nonce, uint64_t i) {
+  const uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key[0], key[1],
+                          key[2], key[3], key[4], key[5], key[6], key[7], (uint32_t)(i >> 2),
+                          (uint32_t)(i >> 34), (uint32_t)nonce, (uint32_t)(nonce >> 32)};
+  uint32_t x[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) x[j] = s[j];
+#define NW_QR(a, b, c, d)                                                   \
+  x[a] += x[b]; x[d] ^= x[a]; x[d] = rotl32(x[d], 16); x[c] += x[d];        \
+  x[b] ^= x[c]; x[b] = rotl32(x[b], 12); x[a] += x[b]; x[d] ^= x[a];        \
+  x[d] = rotl32(x[d], 8); x[c] += x[d]; x[b] ^= x[c]; x[b] = rotl32(x[b], 7);
+#pragma unroll 1
+  for (int r = 0; r < 10; ++r) {
+    NW_QR(0, 4, 8, 12) NW_QR(1, 5, 9, 13) NW_QR(2, 6, 10, 14) NW_QR(3, 7, 11, 15)
+    NW_QR(0, 5, 10, 15) NW_QR(1, 6, 11, 12) NW_QR(2, 7, 8, 13) NW_QR(3, 4, 9, 14)
+  }
+#undef NW_QR
+  const int q = (int)(i & 3) * 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint32_t v = x[0] + s[0];
+#pragma unroll
+    for (int t = 1; t < 16; ++t) v = (q + j == t) ? x[t] + s[t] : v;
+    z[j] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------ plan
+// k_bv_plan: one workgroup (1024 threads) per slice of batches [b0, b1): chunk counts
+// k_b = ceil(n_b / C) (0 for an empty batch) and their exclusive block scan -> chunk_start
+// (nb + 1 entries), plus the list of batches that need k_bv_combine (k_b != 1).
+// k_bv_expand: one lane per chunk writes its descriptor (balanced split of the batch).
+__global__ __launch_bounds__(1024) void k_bv_plan(const uint64_t* __restrict__ offsets,
+                                                  uint64_t b0, uint64_t b1, uint32_t C,
+                                                  uint32_t* __restrict__ chunk_start,
+                                                  uint32_t* __restrict__ multi,
+                                                  uint32_t* __restrict__ multi_first) {
+  __shared__ uint32_t s_a[1024], s_b[1024];
+  __shared__ uint32_t s_base_a, s_base_b;
+  const int t = threadIdx.x;
+  if (t == 0) { s_base_a = 0; s_base_b = 0; }
+  __syncthreads();
+  for (uint64_t base = b0; base < b1; base += 1024) {
+    const uint64_t b = base + t;
+    uint32_t kb = 0;
+    if (b < b1) {
+      const uint32_t nb = (uint32_t)(offsets[b + 1] - offsets[b]);
+      kb = (nb + C - 1) / C;
+    }
+    const uint32_t mflag = (b < b1 && kb != 1) ? 1u : 0u;
+    s_a[t] = kb;
+    s_b[t] = mflag;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {   // Hillis-Steele inclusive scan of both counters
+      const uint32_t va = t >= d ? s_a[t - d] : 0u, vb = t >= d ? s_b[t - d] : 0u;
+      __syncthreads();
+      s_a[t] += va;
+      s_b[t] += vb;
+      __syncthreads();
+    }
+    const uint32_t ca = s_base_a + s_a[t] - kb, cb = s_base_b + s_b[t] - mflag;
+    if (b < b1) {
+      chunk_start[b - b0] = ca;
+      if (mflag) {
+        multi[cb] = (uint32_t)(b - b0);
+        multi_first[cb] = ca;
+      }
+    }
+    __syncthreads();
+    if (t == 1023) { s_base_a += s_a[1023]; s_base_b += s_b[1023]; }
+    __syncthreads();
+  }
+  if (t == 0) chunk_start[b1 - b0] = s_base_a;
+}
+
+__global__ __launch_bounds__(256) void k_bv_expand(const uint64_t* __restrict__ offsets,
+                                                   uint64_t b0, uint64_t nb, uint32_t nchunks,
+                                                   const uint32_t* __restrict__ chunk_start,
+                                                   bv_chunk* __restrict__ chunks) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nchunks) return;
+  // batch: largest lb with chunk_start[lb] <= c (empty batches share a start; the last
+  // of them is the one that owns chunk c)
+  uint64_t lo = 0, hi = nb;
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (chunk_start[mid] <= c) lo = mid; else hi = mid;
+  }
+  const uint64_t ob = offsets[b0 + lo], n = offsets[b0 + lo + 1] - ob;
+  const uint32_t kb = chunk_start[lo + 1] - chunk_start[lo], k = c - chunk_start[lo];
+  const uint64_t l = n * k / kb, h = n * (k + 1) / kb;
+  bv_chunk ch;
+  ch.start = ob + l;
+  ch.batch = (uint32_t)lo;
+  ch.count = (uint32_t)(h - l);
+  chunks[c] = ch;
+}
+
+// ------------------------------------------------------------------------------ items
+__global__ __launch_bounds__(256) void k_bv_items(
+    const uint32_t* __restrict__ digests, const uint64_t* __restrict__ offsets, uint64_t b0,
+    uint64_t b1, uint64_t i0, uint64_t i1, const uint32_t* __restrict__ pks,
+    const uint32_t* __restrict__ sigs, const uint32_t* __restrict__ z16, z_key_t zkey,
+    bv_item* __restrict__ items, ge_cached* __restrict__ tabs) {
+  const uint64_t gi = i0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi >= i1) return;
+  const uint64_t li = gi - i0;
+  const curve_consts& K = g_bc.k;
+  // batch of this item: largest b in [b0, b1) with offsets[b] <= gi
+  uint64_t lo = b0, hi = b1;
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (offsets[mid] <= gi) lo = mid; else hi = mid;
+  }
+  uint32_t Aw[8], Rw[8], Sw[8], Mw[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    Aw[j] = pks[8 * gi + j];
+    Rw[j] = sigs[16 * gi + j];
+    Sw[j] = sigs[16 * gi + 8 + j];
+    Mw[j] = digests[8 * lo + j];
+  }
+  uint32_t flags = 0;
+  if ((Sw[7] >> 29) != 0) flags |= BF_S_HIGH;
+  sc s;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s.w[j] = Sw[j];
+  if (!sc_is_canonical(s)) flags |= BF_S_NONCANON;
+  uint32_t hx[16];
+  hram96(hx, Rw, Aw, Mw);
+  sc k;
+  sc_reduce512(k, hx);
+  uint32_t zw[4];
+  if (z16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) zw[j] = z16[4 * gi + j];
+  } else {
+    chacha20_z(zw, zkey.key, zkey.nonce, gi);
+  }
+  sc z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z.w[j] = j < 4 ? zw[j] : 0u;
+  sc c, b;
+  sc_mul(c, z, k);
+  if (flags & (BF_S_HIGH | BF_S_NONCANON)) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s.w[j] = 0;   // verdict is decided by the flags
+  }
+  sc_mul(b, z, s);
+  bv_item it;
+  sc_recode(it.c, c, 0x88888888u);
+  uint32_t zr[8];
+  sc_recode(zr, z, 0x88888888u);
+#pragma unroll
+  for (int j = 0; j < 5; ++j) it.z[j] = zr[j];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) it.b[j] = b.w[j];
+
+  ge P;
+  ge_cached* tA = tabs + 16 * li;
+  if (!ge_frombytes(P, Aw, K)) flags |= BF_A_DECODE;
+  it.flags = flags;   // (R decode flag added below)
+  // tables j*P, j = 1..8 (cached form)
+#pragma unroll 1
+  for (int which = 0; which < 2; ++which) {
+    if (which == 1) {
+      if (!ge_frombytes(P, Rw, K)) flags |= BF_R_DECODE;
+      tA += 8;
+    }
+    ge_cached c1;
+    ge_to_cached(c1, P, K.d2);
+    tA[0] = c1;
+    ge acc;
+    ge_dbl(acc, P, true);
+    ge_cached cj;
+    ge_to_cached(cj, acc, K.d2);
+    tA[1] = cj;
+#pragma unroll 1
+    for (int j = 3; j <= 8; ++j) {
+      ge_add_cached(acc, acc, c1, true);
+      ge_to_cached(cj, acc, K.d2);
+      tA[j - 1] = cj;
+    }
+  }
+  it.flags = flags;
+  it.pad[0] = it.pad[1] = 0;
+  items[li] = it;
+}
+
+// ------------------------------------------------------------------------------ chunks
+__device__ __forceinline__ int digit4(uint32_t word, int j) {
+  return (int)((word >> ((j & 7) * 4)) & 15u) - 8;
+}
+
+__device__ __forceinline__ void add_entry(ge& acc, const ge_cached* tab, int d) {
+  if (d != 0) {
+    const int ad = d < 0 ? -d : d;
+    ge_cached e = tab[ad - 1];
+    ge_cached_cneg(e, d < 0);
+    ge_add_cached(acc, acc, e, true);
+  }
+}
+
+// Status of a batch from its first failures (reference order, crypto/src/lib.rs:214-218
+// then dalek: parse / decompress A (fail fast), check_scalar, decompress R) or the sum.
+__device__ __forceinline__ int batch_status(const uint32_t first[3], uint32_t flags0,
+                                            bool identity, uint64_t n, uint64_t* idx) {
+  if (first[0] != kNone) {
+    *idx = first[0];
+    return (flags0 & BF_S_HIGH) ? NW_ERR_S_HIGH_BITS : NW_ERR_A_DECODE;
+  }
+  if (first[1] != kNone) { *idx = first[1]; return NW_ERR_S_NONCANONICAL; }
+  if (first[2] != kNone) { *idx = first[2]; return NW_ERR_R_DECODE; }
+  *idx = n;
+  return identity ? NW_OK : NW_ERR_EQUATION;
+}
+
+__global__ __launch_bounds__(256) void k_bv_chunks(
+    const bv_chunk* __restrict__ chunks, uint32_t nchunks, const uint64_t* __restrict__ offsets,
+    uint64_t b0, uint64_t i0, const bv_item* __restrict__ items,
+    const ge_cached* __restrict__ tabs, bv_chunk_out* __restrict__ out,
+    int32_t* __restrict__ status, uint64_t* __restrict__ fail_index) {
+  __shared__ ge_niels s_btab[129];
+  load_btab(s_btab);
+  __syncthreads();
+  const uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ci >= nchunks) return;
+  const bv_chunk ch = chunks[ci];
+  const uint64_t bidx = b0 + ch.batch;
+  const uint64_t bstart = offsets[bidx];
+  const uint64_t bn = offsets[bidx + 1] - bstart;
+  const uint64_t l0 = ch.start - i0;
+  // first failures and sum of b_i over the chunk
+  uint32_t first[3] = {kNone, kNone, kNone};
+  uint32_t flags0 = 0;
+  sc bsum;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bsum.w[j] = 0;
+  for (uint32_t t = 0; t < ch.count; ++t) {
+    const bv_item* it = items + l0 + t;
+    const uint32_t f = it->flags;
+    const uint32_t rel = (uint32_t)(ch.start + t - bstart);
+    if ((f & (BF_S_HIGH | BF_A_DECODE)) && first[0] == kNone) { first[0] = rel; flags0 = f; }
+    if ((f & BF_S_NONCANON) && first[1] == kNone) first[1] = rel;
+    if ((f & BF_R_DECODE) && first[2] == kNone) first[2] = rel;
+    sc bi;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bi.w[j] = it->b[j];
+    sc_add(bsum, bsum, bi);
+  }
+  sc nb;
+  sc_neg(nb, bsum);
+  uint32_t bb[8];
+  sc_recode(bb, nb, 0x80808080u);
+
+  ge acc;
+  ge_identity(acc);
+#pragma unroll 1
+  for (int j = 63; j >= 0; --j) {
+    if (j != 63) {
+#pragma unroll 1
+      for (int t = 0; t < 3; ++t) ge_dbl(acc, acc, false);
+      ge_dbl(acc, acc, true);
+    }
+#pragma unroll 1
+    for (uint32_t t = 0; t < ch.count; ++t) {
+      const bv_item* it = items + l0 + t;
+      const ge_cached* tab = tabs + 16 * (l0 + t);
+      add_entry(acc, tab, digit4(it->c[j >> 3], j));
+      if (j <= 32) add_entry(acc, tab + 8, digit4(it->z[j >> 3], j));
+    }
+    if ((j & 1) == 0) {
+      const int e = (int)((sel8(bb, j >> 3) >> (((j >> 1) & 3) * 8)) & 255u) - 128;
+      add_digit_niels(acc, s_btab, e, true);
+    }
+  }
+  if (ch.count == bn) {   // the batch is this one chunk: finish it here
+    uint64_t idx;
+    const int st = batch_status(first, flags0, ge_is_identity(acc), bn, &idx);
+    status[bidx] = st;
+    if (fail_index) fail_index[bidx] = idx;
+  } else {
+    bv_chunk_out o;
+    o.P = acc;
+    o.first[0] = first[0];
+    o.first[1] = first[1];
+    o.first[2] = first[2];
+    o.pad = flags0;
+    out[ci] = o;
+  }
+}
+
+// ------------------------------------------------------------------------------ combine
+// One 256-thread workgroup per listed batch (k_b == 0 or >= 2): threads sum a strided
+// subset of the chunk points, then a tree through LDS.
+__global__ __launch_bounds__(256) void k_bv_combine(const uint32_t* __restrict__ multi,
+                                                    const uint32_t* __restrict__ multi_first,
+                                                    uint32_t nmulti, const uint64_t* __restrict__ offsets,
+                                                    uint64_t b0, uint32_t C,
+                                                    const bv_chunk_out* __restrict__ out,
+                                                    int32_t* __restrict__ status,
+                                                    uint64_t* __restrict__ fail_index) {
+  __shared__ ge s_p[256];
+  __shared__ uint32_t s_f[256][4];
+  const uint32_t m = blockIdx.x;
+  if (m >= nmulti) return;
+  const int tid = threadIdx.x;
+  const uint64_t bidx = b0 + multi[m];
+  const uint64_t bn = offsets[bidx + 1] - offsets[bidx];
+  const uint32_t kb = (uint32_t)((bn + C - 1) / C);
+  const uint32_t c0 = multi_first[m];
+  const curve_consts& K = g_bc.k;
+  ge acc;
+  ge_identity(acc);
+  uint32_t f[3] = {kNone, kNone, kNone};
+  uint32_t flags0 = 0;
+  for (uint32_t k = tid; k < kb; k += 256) {
+    const bv_chunk_out& o = out[c0 + k];
+    ge_cached c;
+    ge_to_cached(c, o.P, K.d2);
+    ge_add_cached(acc, acc, c, true);
+    if (o.first[0] < f[0]) { f[0] = o.first[0]; flags0 = o.pad; }
+    f[1] = min(f[1], o.first[1]);
+    f[2] = min(f[2], o.first[2]);
+  }
+  s_p[tid] = acc;
+  s_f[tid][0] = f[0]; s_f[tid][1] = f[1]; s_f[tid][2] = f[2]; s_f[tid][3] = flags0;
+  __syncthreads();
+  for (int stride = 128; stride > 0; stride >>= 1) {
+    if (tid < stride && (uint32_t)(tid + stride) < kb) {
+      ge_cached c;
+      ge_to_cached(c, s_p[tid + stride], K.d2);
+      ge t;
+      ge_add_cached(t, s_p[tid], c, true);
+      s_p[tid] = t;
+      if (s_f[tid + stride][0] < s_f[tid][0]) {
+        s_f[tid][0] = s_f[tid + stride][0];
+        s_f[tid][3] = s_f[tid + stride][3];
+      }
+      s_f[tid][1] = min(s_f[tid][1], s_f[tid + stride][1]);
+      s_f[tid][2] = min(s_f[tid][2], s_f[tid + stride][2]);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    uint64_t idx = 0;
+    int st = NW_OK;
+    if (bn > 0) {
+      const uint32_t ff[3] = {s_f[0][0], s_f[0][1], s_f[0][2]};
+      st = batch_status(ff, s_f[0][3], ge_is_identity(s_p[0]), bn, &idx);
+    }
+    status[bidx] = st;
+    if (fail_index) fail_index[bidx] = idx;
+  }
+}
+
+inline size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct bv_ws {
+  bv_item* items;
+  ge_cached* tabs;
+  bv_chunk* chunks;
+  bv_chunk_out* outs;
+  uint32_t* multi;
+  uint32_t* multi_first;
+  uint32_t* chunk_start;
+};
+
+size_t bv_layout(uint64_t units, char* base, bv_ws* w) {
+  const uint64_t u = units ? units : 1;
+  const size_t s_items = a256(sizeof(bv_item) * u), s_tabs = a256(sizeof(ge_cached) * 16 * u),
+               s_ch = a256(sizeof(bv_chunk) * u), s_out = a256(sizeof(bv_chunk_out) * u),
+               s_m = a256(4 * u);
+  if (w) {
+    char* p = base;
+    w->items = reinterpret_cast<bv_item*>(p); p += s_items;
+    w->tabs = reinterpret_cast<ge_cached*>(p); p += s_tabs;
+    w->chunks = reinterpret_cast<bv_chunk*>(p); p += s_ch;
+    w->outs = reinterpret_cast<bv_chunk_out*>(p); p += s_out;
+    w->multi = reinterpret_cast<uint32_t*>(p); p += s_m;
+    w->multi_first = reinterpret_cast<uint32_t*>(p); p += s_m;
+    w->chunk_start = reinterpret_cast<uint32_t*>(p);
+  }
+  return s_items + s_tabs + s_ch + s_out + 2 * s_m + a256(4 * (u + 1));
+}
+
+}  // namespace
+
+hipError_t upload_batch_consts() {
+  static batch_consts host;
+  static std::once_flag once;
+  std::call_once(once, [] { compute_consts(host.k, host.btab); });
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_bc), &host, sizeof(host), 0, hipMemcpyHostToDevice);
+}
+
+size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems) {
+  return bv_layout(std::min<uint64_t>(nitems + nbatches, slice_units()), nullptr, nullptr);
+}
+
+hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
+                               const uint64_t* host_offsets, uint64_t nbatches,
+                               const uint32_t* pks, const uint32_t* sigs, uint64_t nitems,
+                               const uint32_t* z16, const z_key_t& zkey, void* workspace,
+                               int32_t* status, uint64_t* fail_index, hipStream_t stream) {
+  if (nbatches == 0) return hipSuccess;
+  const uint64_t cap = std::min<uint64_t>(nitems + nbatches, slice_units());
+  bv_ws w;
+  bv_layout(cap, static_cast<char*>(workspace), &w);
+  // Chunk size: fill the chip (~2 waves per SIMD of chunk lanes) but share the 252
+  // doublings over as many votes as possible.
+  const uint64_t target_lanes = 256ull * 4 * 2 * 64;
+  uint32_t C = (uint32_t)std::min<uint64_t>(kMaxChunk, std::max<uint64_t>(1, nitems / target_lanes));
+  C = (uint32_t)std::min<uint64_t>(kMaxChunk, env_u64("NW_BATCH_CHUNK", C));
+  uint64_t b = 0;
+  while (b < nbatches) {
+    // slice [b, e): items + batches <= cap
+    uint64_t e = b, items = 0, chunks = 0, multi = 0;
+    while (e < nbatches) {
+      const uint64_t n = host_offsets[e + 1] - host_offsets[e];
+      if (e > b && items + n + (e - b + 1) > cap) break;
+      if (n + 1 > cap) return hipErrorInvalidValue;   // one batch larger than a slice
+      items += n;
+      const uint64_t kb = (n + C - 1) / C;
+      chunks += kb;
+      multi += kb != 1;
+      ++e;
+    }
+    const uint64_t i0 = host_offsets[b], i1 = host_offsets[e];
+    hipLaunchKernelGGL(k_bv_plan, dim3(1), dim3(1024), 0, stream, offsets, b, e, C,
+                       w.chunk_start, w.multi, w.multi_first);
+    if (chunks)
+      hipLaunchKernelGGL(k_bv_expand, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
+                         stream, offsets, b, e - b, (uint32_t)chunks, w.chunk_start, w.chunks);
+    if (i1 > i0)
+      hipLaunchKernelGGL(k_bv_items, dim3((unsigned)((i1 - i0 + 255) / 256)), dim3(256), 0,
+                         stream, digests, offsets, b, e, i0, i1, pks, sigs, z16, zkey, w.items,
+                         w.tabs);
+    if (chunks)
+      hipLaunchKernelGGL(k_bv_chunks, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
+                         stream, w.chunks, (uint32_t)chunks, offsets, b, i0, w.items, w.tabs,
+                         w.outs, status, fail_index);
+    if (multi)
+      hipLaunchKernelGGL(k_bv_combine, dim3((unsigned)multi), dim3(256), 0, stream, w.multi,
+                         w.multi_first, (uint32_t)multi, offsets, b, C, w.outs, status,
+                         fail_index);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+    b = e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace nw

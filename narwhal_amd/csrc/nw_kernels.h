@@ -32,13 +32,16 @@ hipError_t launch_sign(const uint32_t* sks, uint32_t sk_stride_words, const uint
                        uint32_t msg_stride_words, uint64_t n, uint32_t* sigs,
                        hipStream_t stream);
 
-size_t batch_workspace_bytes(uint64_t nitems);
-
+// crypto::Signature::verify_batch over many batches (nw_batch.hip). offsets: device copy,
+// host_offsets: the same nbatches + 1 values in host memory (used to plan the chunks and
+// the workspace slices).
+hipError_t upload_batch_consts();
+size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems);
 hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
-                               uint64_t nbatches, const uint32_t* pks, const uint32_t* sigs,
-                               uint64_t nitems, const uint32_t* z16, const z_key_t& zkey,
-                               void* workspace, int32_t* status, uint64_t* fail_index,
-                               hipStream_t stream);
+                               const uint64_t* host_offsets, uint64_t nbatches,
+                               const uint32_t* pks, const uint32_t* sigs, uint64_t nitems,
+                               const uint32_t* z16, const z_key_t& zkey, void* workspace,
+                               int32_t* status, uint64_t* fail_index, hipStream_t stream);
 
 // ---- primary messages (nw_cert.hip) ----------------------------------------------------
 struct cert_committee_t {

@@ -6,12 +6,7 @@
 //                         signature: decompress A and R, small-order tests, k = H(R||A||M)
 //                         mod l, [s]B + [k](-A) by a joint signed-window ladder (A table in
 //                         per-lane scratch, 8-bit B table in LDS), projective compare with R.
-//   k_batch_items         per-vote half of crypto::Signature::verify_batch
-//                         (crypto/src/lib.rs:206-219 -> dalek verify_batch [ext]): parse and
-//                         decode flags, k_i, z_i, P_i = z_i R_i + (z_i k_i mod l) A_i,
-//                         b_i = z_i s_i mod l.
-//   k_batch_reduce        one workgroup per batch: first failure in reference order, else
-//                         sum P_i - (sum b_i) B == identity.
+//   (crypto::Signature::verify_batch lives in nw_batch.hip.)
 //
 // Everything here is integer VALU work; no MFMA (modular arithmetic is not a contraction).
 #include "nw_kernels.h"
@@ -335,212 +330,6 @@ __global__ __launch_bounds__(256) void k_sign(const uint32_t* __restrict__ sks,
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Batch verification (random linear combination)
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
-
-// z_i = ChaCha20(key, nonce, block i/4) bytes [16 (i%4), 16 (i%4) + 16) (DJB layout).
-__device__ __forceinline__ void chacha20_z(uint32_t z[4], const uint32_t key[8],
-                                           uint64_t nonce, uint64_t i) {
-  uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key[0], key[1],
-                    key[2], key[3], key[4], key[5], key[6], key[7], (uint32_t)(i >> 2),
-                    (uint32_t)(i >> 34), (uint32_t)nonce, (uint32_t)(nonce >> 32)};
-  uint32_t x[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) x[j] = s[j];
-#define NW_QR(a, b, c, d)                                                   \
-  x[a] += x[b]; x[d] ^= x[a]; x[d] = rotl32(x[d], 16); x[c] += x[d];        \
-  x[b] ^= x[c]; x[b] = rotl32(x[b], 12); x[a] += x[b]; x[d] ^= x[a];        \
-  x[d] = rotl32(x[d], 8); x[c] += x[d]; x[b] ^= x[c]; x[b] = rotl32(x[b], 7);
-#pragma unroll 1
-  for (int r = 0; r < 10; ++r) {
-    NW_QR(0, 4, 8, 12) NW_QR(1, 5, 9, 13) NW_QR(2, 6, 10, 14) NW_QR(3, 7, 11, 15)
-    NW_QR(0, 5, 10, 15) NW_QR(1, 6, 11, 12) NW_QR(2, 7, 8, 13) NW_QR(3, 4, 9, 14)
-  }
-#undef NW_QR
-  const int q = (int)(i & 3) * 4;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    uint32_t v = x[0] + s[0];
-#pragma unroll
-    for (int t = 1; t < 16; ++t) v = (q + j == t) ? x[t] + s[t] : v;
-    z[j] = v;
-  }
-}
-
-// Per-item flags (bit set = check FAILED).
-enum : uint32_t { BF_S_HIGH = 1, BF_A_DECODE = 2, BF_S_NONCANON = 4, BF_R_DECODE = 8 };
-
-__global__ __launch_bounds__(256) void k_batch_items(
-    const uint32_t* __restrict__ digests, const uint64_t* __restrict__ offsets,
-    uint64_t nbatches, const uint32_t* __restrict__ pks, const uint32_t* __restrict__ sigs,
-    uint64_t nitems, const uint32_t* __restrict__ z16, z_key_t zkey,
-    ge* __restrict__ out_pts, sc* __restrict__ out_b, uint32_t* __restrict__ out_flags) {
-  const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gi >= nitems) return;
-  const curve_consts& K = g_consts.k;
-  // batch of this item: largest b with offsets[b] <= gi
-  uint64_t lo = 0, hi = nbatches;
-  while (hi - lo > 1) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (offsets[mid] <= gi) lo = mid; else hi = mid;
-  }
-  uint32_t Aw[8], Rw[8], Sw[8], Mw[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    Aw[j] = pks[8 * gi + j];
-    Rw[j] = sigs[16 * gi + j];
-    Sw[j] = sigs[16 * gi + 8 + j];
-    Mw[j] = digests[8 * lo + j];
-  }
-  uint32_t flags = 0;
-  if ((Sw[7] >> 29) != 0) flags |= BF_S_HIGH;
-  sc s;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s.w[j] = Sw[j];
-  if (!sc_is_canonical(s)) flags |= BF_S_NONCANON;
-  ge A, R;
-  if (!ge_frombytes(A, Aw, K)) flags |= BF_A_DECODE;
-  if (!ge_frombytes(R, Rw, K)) flags |= BF_R_DECODE;
-
-  uint32_t hx[16];
-  hram96(hx, Rw, Aw, Mw);
-  sc k;
-  sc_reduce512(k, hx);
-  sc z;
-  uint32_t zw[4];
-  if (z16) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) zw[j] = z16[4 * gi + j];
-  } else {
-    chacha20_z(zw, zkey.key, zkey.nonce, gi);
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) z.w[j] = j < 4 ? zw[j] : 0u;
-  sc c, b;
-  sc_mul(c, z, k);   // (z_i k_i) mod l
-  if (flags & (BF_S_HIGH | BF_S_NONCANON)) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s.w[j] = 0;
-  }
-  sc_mul(b, z, s);   // (z_i s_i) mod l
-
-  // P_i = [z_i] R_i + [c_i] A_i, one joint ladder: 4-bit signed digits for both.
-  ge_cached tabA[9], tabR[9];
-  build_table9(tabA, A, K.d2);
-  build_table9(tabR, R, K.d2);
-  uint32_t cc[8], zz[8];
-  sc_recode(cc, c, 0x88888888u);
-  sc_recode(zz, z, 0x88888888u);
-  ge acc;
-  ge_identity(acc);
-#pragma unroll 1
-  for (int i = 63; i >= 0; --i) {
-    if (i != 63) {
-#pragma unroll 1
-      for (int t = 0; t < 3; ++t) ge_dbl(acc, acc, false);
-      ge_dbl(acc, acc, true);
-    }
-    const bool rdig = i <= 32;   // z < 2^128: digits above 32 are zero
-    const int da = (int)((sel8(cc, i >> 3) >> ((i & 7) * 4)) & 15u) - 8;
-    add_digit_cached(acc, tabA, da, true);
-    if (rdig) {
-      const int dr = (int)((sel8(zz, i >> 3) >> ((i & 7) * 4)) & 15u) - 8;
-      add_digit_cached(acc, tabR, dr, true);
-    }
-  }
-  out_pts[gi] = acc;
-  out_b[gi] = b;
-  out_flags[gi] = flags;
-}
-
-// One workgroup per batch.
-__global__ __launch_bounds__(256) void k_batch_reduce(const uint64_t* __restrict__ offsets,
-                                                      uint64_t nbatches,
-                                                      const ge* __restrict__ pts,
-                                                      const sc* __restrict__ bs,
-                                                      const uint32_t* __restrict__ flags,
-                                                      int32_t* __restrict__ status,
-                                                      uint64_t* __restrict__ fail_index) {
-  __shared__ ge_niels s_btab[129];
-  __shared__ ge s_pts[256];
-  __shared__ sc s_b[256];
-  __shared__ unsigned long long s_first[3];
-  load_btab(s_btab);
-  const uint64_t bidx = blockIdx.x;
-  const uint64_t beg = offsets[bidx], end = offsets[bidx + 1];
-  const int tid = threadIdx.x;
-  if (tid < 3) s_first[tid] = ~0ULL;
-  __syncthreads();
-  const curve_consts& K = g_consts.k;
-
-  // First failures, in reference order (crypto/src/lib.rs:214-217 then dalek):
-  //   [0] first vote whose signature parse (s high bits) or key decompression fails
-  //   [1] first non-canonical s (dalek InternalSignature::try_from)
-  //   [2] first R that fails to decompress (optional_multiscalar_mul -> None)
-  ge acc;
-  ge_identity(acc);
-  sc bsum;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bsum.w[j] = 0;
-  for (uint64_t i = beg + tid; i < end; i += blockDim.x) {
-    const uint32_t f = flags[i];
-    const unsigned long long rel = i - beg;
-    if (f & (BF_S_HIGH | BF_A_DECODE)) atomicMin(&s_first[0], rel);
-    if (f & BF_S_NONCANON) atomicMin(&s_first[1], rel);
-    if (f & BF_R_DECODE) atomicMin(&s_first[2], rel);
-    ge_cached c;
-    ge_to_cached(c, pts[i], K.d2);
-    ge_add_cached(acc, acc, c, true);
-    sc_add(bsum, bsum, bs[i]);
-  }
-  s_pts[tid] = acc;
-  s_b[tid] = bsum;
-  __syncthreads();
-  for (int stride = 128; stride > 0; stride >>= 1) {
-    if (tid < stride) {
-      ge_cached c;
-      ge_to_cached(c, s_pts[tid + stride], K.d2);
-      ge t;
-      ge_add_cached(t, s_pts[tid], c, true);
-      s_pts[tid] = t;
-      sc u;
-      sc_add(u, s_b[tid], s_b[tid + stride]);
-      s_b[tid] = u;
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    const uint64_t n = end - beg;
-    int st = NW_OK;
-    uint64_t idx = n;
-    if (s_first[0] != ~0ULL) {
-      idx = s_first[0];
-      st = (flags[beg + idx] & BF_S_HIGH) ? NW_ERR_S_HIGH_BITS : NW_ERR_A_DECODE;
-    } else if (s_first[1] != ~0ULL) {
-      idx = s_first[1];
-      st = NW_ERR_S_NONCANONICAL;
-    } else if (s_first[2] != ~0ULL) {
-      idx = s_first[2];
-      st = NW_ERR_R_DECODE;
-    } else if (n > 0) {
-      // total = sum P_i + [-(sum b_i)] B ; dalek: is_identity() ? Ok : VerifyError
-      sc nb;
-      sc_neg(nb, s_b[0]);
-      ge bB;
-      fixed_base_mul(bB, nb, s_btab);
-      ge_cached c;
-      ge_to_cached(c, bB, K.d2);
-      ge total;
-      ge_add_cached(total, s_pts[0], c, false);
-      st = ge_is_identity(total) ? NW_OK : NW_ERR_EQUATION;
-    }
-    status[bidx] = st;
-    if (fail_index) fail_index[bidx] = idx;
-  }
-}
-
 }  // namespace nw
 
 // ---------------------------------------------------------------------------------------
@@ -552,8 +341,9 @@ hipError_t upload_consts() {
   static dev_consts host;
   static std::once_flag once;
   std::call_once(once, [] { compute_consts(host.k, host.btab); });
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_consts), &host, sizeof(host), 0,
-                           hipMemcpyHostToDevice);
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_consts), &host, sizeof(host), 0,
+                                   hipMemcpyHostToDevice);
+  return e != hipSuccess ? e : upload_batch_consts();
 }
 
 static inline unsigned grid_for(uint64_t n, unsigned block) {
@@ -590,37 +380,6 @@ hipError_t launch_sign(const uint32_t* sks, uint32_t sk_stride_words, const uint
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_sign, dim3(grid_for(n, 256)), dim3(256), 0, stream, sks, sk_stride_words,
                      msgs, msg_stride_words, n, sigs);
-  return hipGetLastError();
-}
-
-static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
-
-size_t batch_workspace_bytes(uint64_t nitems) {
-  const uint64_t m = nitems ? nitems : 1;
-  return align256(sizeof(ge) * m) + align256(sizeof(sc) * m) + align256(sizeof(uint32_t) * m);
-}
-
-hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
-                               uint64_t nbatches, const uint32_t* pks, const uint32_t* sigs,
-                               uint64_t nitems, const uint32_t* z16, const z_key_t& zkey,
-                               void* workspace, int32_t* status, uint64_t* fail_index,
-                               hipStream_t stream) {
-  if (nbatches == 0) return hipSuccess;
-  const uint64_t m = nitems ? nitems : 1;
-  char* ws = static_cast<char*>(workspace);
-  ge* pts = reinterpret_cast<ge*>(ws);
-  sc* bs = reinterpret_cast<sc*>(ws + align256(sizeof(ge) * m));
-  uint32_t* flags =
-      reinterpret_cast<uint32_t*>(ws + align256(sizeof(ge) * m) + align256(sizeof(sc) * m));
-  if (nitems) {
-    hipLaunchKernelGGL(k_batch_items, dim3(grid_for(nitems, 256)), dim3(256), 0, stream,
-                       digests, offsets, nbatches, pks, sigs, nitems, z16, zkey, pts, bs,
-                       flags);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL(k_batch_reduce, dim3((unsigned)nbatches), dim3(256), 0, stream, offsets,
-                     nbatches, pts, bs, flags, status, fail_index);
   return hipGetLastError();
 }
 

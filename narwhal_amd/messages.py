@@ -162,7 +162,7 @@ class _CCertificates(ctypes.Structure):
                 ("ids", ctypes.c_void_p), ("header_sigs", ctypes.c_void_p),
                 ("vote_offsets", ctypes.c_void_p), ("vote_pks", ctypes.c_void_p),
                 ("vote_sigs", ctypes.c_void_p), ("header_bytes_len", ctypes.c_size_t),
-                ("nvotes", ctypes.c_size_t)]
+                ("nvotes", ctypes.c_size_t), ("host_vote_offsets", ctypes.c_void_p)]
 
 
 def _p(a: np.ndarray | None):
@@ -306,7 +306,7 @@ def certificates_struct(p: dict[str, np.ndarray], n: int) -> _CCertificates:
     return _CCertificates(n, _p(p["header_bytes"]), _p(p["header_offsets"]),
                           _p(p["payload_counts"]), _p(p["ids"]), _p(p["header_sigs"]),
                           _p(p["vote_offsets"]), _p(p["vote_pks"]), _p(p["vote_sigs"]),
-                          int(p["header_offsets"][-1]), int(p["vote_offsets"][-1]))
+                          int(p["header_offsets"][-1]), int(p["vote_offsets"][-1]), None)
 
 
 def verify_certificates_many(committee: Committee, certs: Sequence[Certificate] | dict,

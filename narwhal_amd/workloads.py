@@ -132,3 +132,38 @@ def certificate_stream(n_certs: int, keys: list[tuple[bytes, bytes]], sign_many,
                       "worker_ids": np.zeros(N, np.uint32)},
         "rounds": rounds, "cert_digests": cdig, "q": q,
     }
+
+
+# --------------------------------------------------------------------------------------
+# Fixture keys (BASELINE config 1): rand 0.7 StdRng::from_seed([0; 32]) =
+# ChaCha20(key = 0^32, nonce = 0) keystream; seed i = bytes [32 i, 32 i + 32)
+# (primary/src/tests/common.rs:28-32 keys(), extended to 10,000 keys).
+# --------------------------------------------------------------------------------------
+def chacha20_keystream(key: bytes, nblocks: int, counter: int = 0) -> bytes:
+    """DJB ChaCha20 (64-bit counter, 64-bit nonce = 0) keystream, vectorised over blocks."""
+    def rotl(x, n):
+        return (x << np.uint32(n)) | (x >> np.uint32(32 - n))
+    k = np.frombuffer(key, "<u4")
+    ctr = np.arange(counter, counter + nblocks, dtype=np.uint64)
+    s = np.zeros((16, nblocks), np.uint32)
+    s[0:4] = np.array([0x61707865, 0x3320646E, 0x79622D32, 0x6B206574], np.uint32)[:, None]
+    s[4:12] = k[:, None]
+    s[12] = (ctr & 0xFFFFFFFF).astype(np.uint32)
+    s[13] = (ctr >> 32).astype(np.uint32)
+    x = s.copy()
+
+    def qr(a, b, c, d):
+        x[a] += x[b]; x[d] = rotl(x[d] ^ x[a], 16)
+        x[c] += x[d]; x[b] = rotl(x[b] ^ x[c], 12)
+        x[a] += x[b]; x[d] = rotl(x[d] ^ x[a], 8)
+        x[c] += x[d]; x[b] = rotl(x[b] ^ x[c], 7)
+    for _ in range(10):
+        qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15)
+        qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14)
+    return (x + s).T.astype("<u4").tobytes()
+
+
+def fixture_seeds(count: int) -> np.ndarray:
+    """[count, 32] seeds of the reference keys() fixture generator (StdRng zero seed)."""
+    ks = chacha20_keystream(bytes(32), (32 * count + 63) // 64)
+    return np.frombuffer(ks[:32 * count], np.uint8).reshape(count, 32).copy()

@@ -89,8 +89,10 @@ def test_certificate_stream_large_committee_payload():
     assert st.tolist() == [0] * 40
 
 
-def test_device_entry_point_matches_host():
-    """nw_dev_certificates_verify_many on device-resident buffers (the bench path)."""
+@pytest.mark.parametrize("case_host", [True, False])
+def test_device_entry_point_matches_host(case_host):
+    """nw_dev_certificates_verify_many on device-resident buffers (the bench path), with and
+    without the host copy of the vote offsets."""
     com, s, exp_st, exp_ix, cls = mutated_stream(N=4, copies=2, seed=11)
     n = len(s["header_offsets"]) - 1
     nv = int(s["vote_offsets"][-1])
@@ -108,7 +110,8 @@ def test_device_entry_point_matches_host():
                        P(C["worker_ids"]))
     cs = M._CCertificates(n, P(T["header_bytes"]), P(T["header_offsets"]), P(T["payload_counts"]),
                           P(T["ids"]), P(T["header_sigs"]), P(T["vote_offsets"]), P(T["vote_pks"]),
-                          P(T["vote_sigs"]), int(s["header_offsets"][-1]), nv)
+                          P(T["vote_sigs"]), int(s["header_offsets"][-1]), nv,
+                          s["vote_offsets"].ctypes.data if case_host else None)
     torch.cuda.synchronize()
     rc = L.nw_dev_certificates_verify_many(ctypes.byref(cc), ctypes.byref(cs), 0,
                                            ctypes.c_void_p(P(zt)), None, ctypes.c_void_p(P(ws)),
