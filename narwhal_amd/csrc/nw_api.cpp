@@ -31,6 +31,7 @@ struct DevCtx {
   hipStream_t stream = nullptr;
   void* dbuf = nullptr;
   size_t dcap = 0;
+  void* strict_ws = nullptr;   // per-lane tables of k_verify_strict (fixed size)
 };
 
 struct ThreadState {
@@ -42,6 +43,7 @@ struct ThreadState {
       if (ctx[i].stream || ctx[i].dbuf) {
         (void)hipSetDevice(g_dev_ids[i]);
         if (ctx[i].dbuf) (void)hipFree(ctx[i].dbuf);
+        if (ctx[i].strict_ws) (void)hipFree(ctx[i].strict_ws);
         if (ctx[i].stream) (void)hipStreamDestroy(ctx[i].stream);
       }
     }
@@ -124,6 +126,19 @@ int reserve(DevCtx& c, size_t bytes) {
 }
 
 inline size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// The strict kernel's per-lane table workspace (allocated once per thread and device).
+int strict_ws(DevCtx& c, void** out) {
+  if (!c.strict_ws) {
+    hipError_t e = hipMalloc(&c.strict_ws, nw::strict_workspace_bytes());
+    if (e != hipSuccess) {
+      c.strict_ws = nullptr;
+      return set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (strict workspace)", e);
+    }
+  }
+  *out = c.strict_ws;
+  return 0;
+}
 
 int os_random(void* buf, size_t n) {
   size_t got = 0;
@@ -249,11 +264,14 @@ int nw_dev_verify_strict_many(const void* digests, size_t digest_stride, const v
     return set_err(NW_E_INVALID_ARG, "null pointer (status_out and bitmap_out are required)");
   if (digest_stride != 0 && digest_stride != 32)
     return set_err(NW_E_INVALID_ARG, "digest_stride must be 0 or 32");
+  void* ws;
+  rc = strict_ws(*c, &ws);
+  if (rc) return rc;
   NW_HIP(nw::launch_verify_strict(static_cast<const uint32_t*>(digests),
                                   (uint32_t)(digest_stride / 4),
                                   static_cast<const uint32_t*>(pks),
                                   static_cast<const uint32_t*>(sigs), n, status_out,
-                                  static_cast<uint64_t*>(bitmap_out), pick_stream(stream, c)),
+                                  static_cast<uint64_t*>(bitmap_out), ws, pick_stream(stream, c)),
          "k_verify_strict launch");
   return 0;
 }
@@ -284,10 +302,13 @@ int nw_verify_strict_many(const uint8_t* digests, size_t digest_stride, const ui
   NW_HIP(hipMemcpyAsync(d_m, digests, 32 * nmsg, hipMemcpyHostToDevice, s), "H2D digests");
   NW_HIP(hipMemcpyAsync(d_pk, pks, 32 * n, hipMemcpyHostToDevice, s), "H2D pks");
   NW_HIP(hipMemcpyAsync(d_sig, sigs, 64 * n, hipMemcpyHostToDevice, s), "H2D sigs");
+  void* ws;
+  rc = strict_ws(*c, &ws);
+  if (rc) return rc;
   NW_HIP(nw::launch_verify_strict(reinterpret_cast<const uint32_t*>(d_m),
                                   (uint32_t)(digest_stride / 4),
                                   reinterpret_cast<const uint32_t*>(d_pk),
-                                  reinterpret_cast<const uint32_t*>(d_sig), n, d_st, d_bm, s),
+                                  reinterpret_cast<const uint32_t*>(d_sig), n, d_st, d_bm, ws, s),
          "k_verify_strict launch");
   if (status_out)
     NW_HIP(hipMemcpyAsync(status_out, d_st, 4 * n, hipMemcpyDeviceToHost, s), "D2H status");
@@ -556,7 +577,7 @@ size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
 }
 
 // The whole device pipeline; every pointer is a device pointer.
-int cert_pipeline(const nw_committee& com, const nw_certificates& cs,
+int cert_pipeline(DevCtx& ctx, const nw_committee& com, const nw_certificates& cs,
                   const uint64_t* host_vote_offsets, int headers_only, const void* z16,
                   const nw::z_key_t& key, void* workspace, int32_t* status, uint64_t* index,
                   hipStream_t s) {
@@ -573,9 +594,12 @@ int cert_pipeline(const nw_committee& com, const nw_certificates& cs,
                                     w.hdr_digest, s), "k_sha512 (header digests)");
   NW_HIP(nw::launch_cert_prepare(dc, ds, headers_only, w.hdr_digest, w.authors, w.cert_digest,
                                  w.pre1, w.pre2, w.idx1, w.idx2, s), "k_cert_prepare");
+  void* sws;
+  int rc = strict_ws(ctx, &sws);
+  if (rc) return rc;
   NW_HIP(nw::launch_verify_strict(reinterpret_cast<const uint32_t*>(cs.ids), 8, w.authors,
                                   reinterpret_cast<const uint32_t*>(cs.header_sigs), n, w.hdr_st,
-                                  w.bitmap, s), "k_verify_strict (headers)");
+                                  w.bitmap, sws, s), "k_verify_strict (headers)");
   if (!headers_only)
     NW_HIP(nw::launch_verify_batch(w.cert_digest, cs.vote_offsets, host_vote_offsets, n,
                                    reinterpret_cast<const uint32_t*>(cs.vote_pks),
@@ -703,7 +727,7 @@ int certs_host(const nw_committee* com, const nw_certificates* cs, int headers_o
   nw::z_key_t key;
   rc = fill_key(key, nullptr);
   if (rc) return rc;
-  rc = cert_pipeline(dcom, d, cs->vote_offsets, headers_only, dz, key, dws, dst, dix, s);
+  rc = cert_pipeline(*c, dcom, d, cs->vote_offsets, headers_only, dz, key, dws, dst, dix, s);
   if (rc) return rc;
   NW_HIP(hipMemcpyAsync(status_out, dst, 4 * n, hipMemcpyDeviceToHost, s), "D2H status");
   if (index_out) NW_HIP(hipMemcpyAsync(index_out, dix, 8 * n, hipMemcpyDeviceToHost, s), "D2H index");
@@ -751,8 +775,8 @@ int nw_dev_certificates_verify_many(const nw_committee* committee, const nw_cert
     if (hvo[0] != 0 || hvo[certs->n] != certs->nvotes)
       return set_err(NW_E_INVALID_ARG, "vote_offsets must run from 0 to nvotes");
   }
-  return cert_pipeline(*committee, *certs, hvo, headers_only, z16, key, workspace, status_out,
-                       index_out, s);
+  return cert_pipeline(*c, *committee, *certs, hvo, headers_only, z16, key, workspace,
+                       status_out, index_out, s);
 }
 
 int nw_votes_verify_many(const nw_committee* committee, const uint8_t* ids,
@@ -792,8 +816,12 @@ int nw_votes_verify_many(const nw_committee* committee, const uint8_t* ids,
                                  reinterpret_cast<const uint32_t*>(d_org),
                                  reinterpret_cast<const uint32_t*>(d_au), d_dig, d_pre, s),
          "k_vote_prepare");
+  void* sws;
+  rc = strict_ws(*c, &sws);
+  if (rc) return rc;
   NW_HIP(nw::launch_verify_strict(d_dig, 8, reinterpret_cast<const uint32_t*>(d_au),
-                                  reinterpret_cast<const uint32_t*>(d_sig), n, d_sst, d_bm, s),
+                                  reinterpret_cast<const uint32_t*>(d_sig), n, d_sst, d_bm, sws,
+                                  s),
          "k_verify_strict (votes)");
   NW_HIP(nw::launch_vote_finalize(n, d_pre, d_sst, d_st, s), "k_vote_finalize");
   NW_HIP(hipMemcpyAsync(status_out, d_st, 4 * n, hipMemcpyDeviceToHost, s), "D2H status");

@@ -2,7 +2,7 @@
 // definitions (d = -121665/121666, sqrt(-1) = 2^((p-1)/4), B = (x >= 0, 4/5)) with the same
 // arithmetic the kernels use. Computed once on the host and uploaded to constant memory.
 #pragma once
-#include "nw_point.hpp"
+#include "nw_strict.hpp"
 
 namespace nw {
 
@@ -10,6 +10,20 @@ NW_HD void fe_from_u32(fe& h, uint32_t x) {
   fe_0(h);
   h.v[0] = x & M26;
   h.v[1] = x >> 26;
+}
+
+// tab[j] = j * P for j = 0..128 (affine niels).
+inline void niels_multiples(ge_niels tab[129], const ge& P, const fe& d2) {
+  ge_niels_identity(tab[0]);
+  ge_cached cP;
+  ge_to_cached(cP, P, d2);
+  ge acc = P;
+  for (int j = 1; j <= 128; ++j) {
+    ge_to_niels(tab[j], acc, d2);
+    ge nxt;
+    ge_add_cached(nxt, acc, cP, true);
+    acc = nxt;
+  }
 }
 
 // btab[j] = j * B for j = 0..128 (affine niels).
@@ -44,6 +58,48 @@ inline void compute_consts(curve_consts& k, ge_niels btab[129]) {
     ge_add_cached(nxt, acc, cB, true);
     acc = nxt;
   }
+}
+
+// The 128-bit half-size verification constants (nw_strict.hpp): canonical y of the small-
+// order points, and b128[j] = j * 2^128 B.
+inline void compute_strict_consts(strict_consts& sk, ge_niels b128[129]) {
+  ge_niels btab[129];
+  compute_consts(sk.k, btab);
+  static const uint8_t y8_enc[32] = {0x26, 0xe8, 0x95, 0x8f, 0xc2, 0xb2, 0x27, 0xb0,
+                                     0x45, 0xc3, 0xf4, 0x89, 0xf2, 0xef, 0x98, 0xf0,
+                                     0xd5, 0xdf, 0xac, 0x05, 0xd3, 0xc6, 0x33, 0x39,
+                                     0xb1, 0x38, 0x02, 0x88, 0x6d, 0x53, 0xfc, 0x05};
+  uint32_t w[8];
+  for (int i = 0; i < 8; ++i)
+    w[i] = (uint32_t)y8_enc[4 * i] | ((uint32_t)y8_enc[4 * i + 1] << 8) |
+           ((uint32_t)y8_enc[4 * i + 2] << 16) | ((uint32_t)y8_enc[4 * i + 3] << 24);
+  fe y8, t, one;
+  fe_frombytes(y8, w);
+  fe_0(t);
+  fe_canonical(sk.small_y[0], t);                 // y = 0 (order 4)
+  fe_1(one);
+  fe_canonical(sk.small_y[1], one);               // identity
+  fe_neg(t, one);
+  fe_canonical(sk.small_y[2], t);                 // order 2
+  fe_canonical(sk.small_y[3], y8);                // order 8
+  fe_neg(t, y8);
+  fe_canonical(sk.small_y[4], t);                 // order 8
+  // B = (x >= 0, 4/5); B128 = 2^128 B
+  fe a, b;
+  fe_from_u32(a, 4);
+  fe_from_u32(b, 5);
+  fe_invert(t, b);
+  fe_mul(a, a, t);
+  uint32_t yw[8];
+  fe_tobytes(yw, a);
+  ge B;
+  ge_frombytes(B, yw, sk.k);
+  for (int i = 0; i < 128; ++i) {
+    ge d;
+    ge_dbl(d, B, true);
+    B = d;
+  }
+  niels_multiples(b128, B, sk.k.d2);
 }
 
 }  // namespace nw

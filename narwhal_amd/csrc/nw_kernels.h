@@ -22,9 +22,13 @@ hipError_t launch_sha512_digest32(const uint8_t* data, const uint64_t* offsets,
                                   const uint64_t* lengths, uint64_t n, uint32_t* out,
                                   hipStream_t stream);
 
+// Strict verification; workspace = strict_workspace_bytes() of device memory (per-lane
+// tables; reusable across launches on one stream).
+size_t strict_workspace_bytes();
 hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
                                 const uint32_t* pks, const uint32_t* sigs, uint64_t n,
-                                int32_t* status, uint64_t* bitmap, hipStream_t stream);
+                                int32_t* status, uint64_t* bitmap, void* workspace,
+                                hipStream_t stream);
 
 hipError_t launch_keypair(const uint32_t* seeds, uint64_t n, uint32_t* pks, hipStream_t stream);
 

@@ -16,6 +16,7 @@
 #include "nw_ladder.hpp"
 #include "nw_consts.hpp"
 
+#include <algorithm>
 #include <mutex>
 
 namespace nw {
@@ -23,6 +24,8 @@ namespace nw {
 struct dev_consts {
   curve_consts k;
   ge_niels btab[129];   // j * B, j = 0..128, affine niels (signed 8-bit windows)
+  strict_consts sk;     // nw_strict.hpp: small-order y values
+  ge_niels b128[129];   // j * 2^128 B
 };
 
 __constant__ dev_consts g_consts;
@@ -34,12 +37,25 @@ static constexpr int BT_WORDS = 129 * 30;
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-// Copy the B table from constant memory into LDS (all threads of the block).
-__device__ __forceinline__ void load_btab(ge_niels* s_btab) {
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(&g_consts.btab[0]);
-  uint32_t* dst = reinterpret_cast<uint32_t*>(s_btab);
+// Copy a 129-entry niels table from constant memory into LDS (all threads of the block).
+__device__ __forceinline__ void load_table(ge_niels* dst_tab, const ge_niels* src_tab) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(src_tab);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(dst_tab);
   for (int i = threadIdx.x; i < BT_WORDS; i += blockDim.x) dst[i] = src[i];
 }
+__device__ __forceinline__ void load_btab(ge_niels* s_btab) { load_table(s_btab, g_consts.btab); }
+
+// Maximum of a per-lane value over the wave (wave-uniform result).
+struct WaveMax {
+  __device__ int operator()(int w) const {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const int x = __shfl_xor(w, o);
+      w = x > w ? x : w;
+    }
+    return __builtin_amdgcn_readfirstlane(w);
+  }
+};
 
 // SHA-512 of the 96-byte R || A || M (one block) -> 16 LE words of the digest.
 __device__ __forceinline__ void hram96(uint32_t x[16], const uint32_t R[8], const uint32_t A[8],
@@ -142,77 +158,48 @@ __global__ __launch_bounds__(256) void k_sha512_digest32(const uint8_t* __restri
 // ---------------------------------------------------------------------------------------
 // Strict verification
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ int strict_status(bool s_high, bool okA, bool s_canon, bool okR,
-                                             bool smallR, bool smallA, bool eq) {
-  // Reference order: crypto/src/lib.rs:201 (s high bits), 202 (decompress A), then dalek
-  // verify_strict: check_scalar, decompress R, small order (R || A), equation.
-  if (s_high) return NW_ERR_S_HIGH_BITS;
-  if (!okA) return NW_ERR_A_DECODE;
-  if (!s_canon) return NW_ERR_S_NONCANONICAL;
-  if (!okR) return NW_ERR_R_DECODE;
-  if (smallR) return NW_ERR_R_SMALL_ORDER;
-  if (smallA) return NW_ERR_A_SMALL_ORDER;
-  if (!eq) return NW_ERR_EQUATION;
-  return NW_OK;
-}
 
-__global__ __launch_bounds__(256) void k_verify_strict(const uint32_t* __restrict__ msgs,
+// Persistent: the grid covers the resident waves once and strides over the items, so the
+// per-lane tables j*A, j*R live in a fixed workspace (16 entries x 160 B per lane slot, lane-
+// contiguous: a lookup reads 160 consecutive bytes per lane instead of 40 scattered dwords).
+__global__ __launch_bounds__(256, 2) void k_verify_strict(const uint32_t* __restrict__ msgs,
                                                        uint32_t msg_stride_words,
                                                        const uint32_t* __restrict__ pks,
                                                        const uint32_t* __restrict__ sigs,
                                                        uint64_t n, int32_t* __restrict__ status,
-                                                       uint64_t* __restrict__ bitmap) {
+                                                       uint64_t* __restrict__ bitmap,
+                                                       ge_cached* __restrict__ tabs) {
   __shared__ ge_niels s_btab[129];
-  load_btab(s_btab);
+  __shared__ ge_niels s_b128[129];
+  load_table(s_btab, g_consts.btab);
+  load_table(s_b128, g_consts.b128);
   __syncthreads();
-  const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = gi < n;
-  const uint64_t i = active ? gi : n - 1;
-  const curve_consts& K = g_consts.k;
-
-  uint32_t Aw[8], Rw[8], Sw[8], Mw[8];
+  ge_cached* tabA = tabs + 16 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  ge_cached* tabR = tabA + 8;
+#pragma unroll 1
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n;
+       base += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t gi = base + threadIdx.x;
+    const bool active = gi < n;
+    const uint64_t i = active ? gi : n - 1;
+    uint32_t Aw[8], Rw[8], Sw[8], Mw[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    Aw[j] = pks[8 * i + j];
-    Rw[j] = sigs[16 * i + j];
-    Sw[j] = sigs[16 * i + 8 + j];
-    Mw[j] = msgs[(uint64_t)msg_stride_words * i + j];
+    for (int j = 0; j < 8; ++j) {
+      Aw[j] = pks[8 * i + j];
+      Rw[j] = sigs[16 * i + j];
+      Sw[j] = sigs[16 * i + 8 + j];
+      Mw[j] = msgs[(uint64_t)msg_stride_words * i + j];
+    }
+    uint32_t hx[16];
+    hram96(hx, Rw, Aw, Mw);
+    sc k;
+    sc_reduce512(k, hx);
+    const int st = strict_verify_core(Aw, Rw, Sw, k, g_consts.sk, s_btab, s_b128, tabA, tabR,
+                                      WaveMax{});
+    if (active) status[gi] = st;
+    const uint64_t mask = __ballot(active && st == NW_OK);
+    if ((threadIdx.x & 63) == 0 && gi < n) bitmap[gi >> 6] = mask;
   }
-  const bool s_high = (Sw[7] >> 29) != 0;
-  sc s;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s.w[j] = Sw[j];
-  const bool s_canon = sc_is_canonical(s);
-
-  ge A, R;
-  const bool okA = ge_frombytes(A, Aw, K);
-  const bool okR = ge_frombytes(R, Rw, K);
-  const bool smallA = ge_is_small_order(A);
-  const bool smallR = ge_is_small_order(R);
-
-  uint32_t hx[16];
-  hram96(hx, Rw, Aw, Mw);
-  sc k;
-  sc_reduce512(k, hx);
-
-  // [s]B + [k](-A)
-  ge minusA;
-  ge_neg(minusA, A);
-  ge_cached tab[9];
-  build_table9(tab, minusA, K.d2);
-  sc s_use = s;
-  if (!s_canon || s_high) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s_use.w[j] = 0;   // keep digits in range; verdict is Err anyway
-  }
-  ge acc;
-  dsm_var_base(acc, tab, k, s_use, s_btab);
-  const bool eq = ge_eq_affine(acc, R);
-
-  const int st = strict_status(s_high, okA, s_canon, okR, smallR, smallA, eq);
-  if (active) status[gi] = st;
-  const uint64_t mask = __ballot(active && st == NW_OK);
-  if ((threadIdx.x & 63) == 0 && gi < n) bitmap[gi >> 6] = mask;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -340,7 +327,10 @@ namespace nw {
 hipError_t upload_consts() {
   static dev_consts host;
   static std::once_flag once;
-  std::call_once(once, [] { compute_consts(host.k, host.btab); });
+  std::call_once(once, [] {
+    compute_consts(host.k, host.btab);
+    compute_strict_consts(host.sk, host.b128);
+  });
   hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_consts), &host, sizeof(host), 0,
                                    hipMemcpyHostToDevice);
   return e != hipSuccess ? e : upload_batch_consts();
@@ -359,12 +349,38 @@ hipError_t launch_sha512_digest32(const uint8_t* data, const uint64_t* offsets,
   return hipGetLastError();
 }
 
+// Resident 256-thread blocks of k_verify_strict on the current device (occupancy query,
+// once per device).
+static unsigned strict_grid() {
+  static int cached[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (!cached[dev]) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_verify_strict, 256, 0) !=
+            hipSuccess || per_cu <= 0)
+      per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    cached[dev] = per_cu * cus;
+  }
+  return (unsigned)cached[dev];
+}
+
+size_t strict_workspace_bytes() {
+  return (size_t)strict_grid() * 256 * 16 * sizeof(ge_cached);
+}
+
 hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
                                 const uint32_t* pks, const uint32_t* sigs, uint64_t n,
-                                int32_t* status, uint64_t* bitmap, hipStream_t stream) {
+                                int32_t* status, uint64_t* bitmap, void* workspace,
+                                hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_verify_strict, dim3(grid_for(n, 256)), dim3(256), 0, stream, msgs,
-                     msg_stride_words, pks, sigs, n, status, bitmap);
+  const unsigned grid = std::min<uint64_t>(strict_grid(), grid_for(n, 256));
+  hipLaunchKernelGGL(k_verify_strict, dim3(grid), dim3(256), 0, stream, msgs, msg_stride_words,
+                     pks, sigs, n, status, bitmap, static_cast<ge_cached*>(workspace));
   return hipGetLastError();
 }
 

@@ -164,3 +164,185 @@ NW_HD void sc_recode(uint32_t out[8], const sc& s, uint32_t m_word) {
 }
 
 }  // namespace nw
+
+namespace nw {
+
+// ---------------------------------------------------------------------------------------
+// Half-size scalars for strict verification (Antipa et al., "Accelerated verification of
+// ECDSA signatures", SAC 2005; Pornin, "Optimized lattice basis reduction in dimension 2,
+// and fast Schnorr and EdDSA signature verification", 2020).
+//
+// Find (u, v) with u = v k (mod 8l), v odd, |u|, |v| ~ 2^128, by the extended Euclidean
+// algorithm on (8l, k) stopped at the first remainder below 2^128. Then for ANY point D on
+// the curve (group order 8l): [v] D = 0 <=> D = 0, because gcd(v, 8l) = 1 — so
+//   R + [k]A - [s]B == 0   <=>   [v]R + [u]A - [v s mod l]B == 0
+// exactly, torsion components included (mixed-order A keeps dalek's verify_strict
+// verdict), while the shared ladder is ~128 doublings instead of 252.
+//
+// State: X = (xr, -xt), Y = (yr, +-yt) lattice vectors r = t k (mod 8l) with opposite-sign
+// t; quotients are estimated in f64 and never overshoot. If the remainder does not drop
+// below 2^128 within the iteration cap (a quotient >= 2^32 somewhere, i.e. a ground k), the
+// result is the trivial vector (k, 1): correct, only slower.
+// ---------------------------------------------------------------------------------------
+static constexpr uint32_t L8_W[8] = {0xe7ae9f68u, 0xc09318d2u, 0x17bce6b2u, 0xa6f7cef5u,
+                                      0u, 0u, 0u, 0x80000000u};   // 8 l
+
+struct sc_half {
+  uint32_t u[8];    // u >= 0, u < 2^253
+  uint32_t v[5];    // |v|, odd
+  bool vneg;        // v < 0
+};
+
+NW_HD double bn8_to_f64(const uint32_t w[8]) {
+  double d = 0.0;
+#pragma unroll
+  for (int i = 7; i >= 0; --i) d = d * 4294967296.0 + (double)w[i];
+  return d;
+}
+
+NW_HD bool bn8_lt(const uint32_t a[8], const uint32_t b[8]) {
+  // a < b  <=>  a - b borrows
+  uint64_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) borrow = ((uint64_t)a[i] - b[i] - borrow) >> 63;
+  return borrow != 0;
+}
+
+NW_HD int bn_bits(const uint32_t* w, int n) {
+  int b = 0;
+  for (int i = 0; i < n; ++i)
+    if (w[i]) b = 32 * i + 32 - __builtin_clz(w[i]);
+  return b;
+}
+NW_HD bool bn_lt(const uint32_t* a, const uint32_t* b, int n) {
+  uint64_t borrow = 0;
+  for (int i = 0; i < n; ++i) borrow = ((uint64_t)a[i] - b[i] - borrow) >> 63;
+  return borrow != 0;
+}
+NW_HD void bn_add(uint32_t* r, const uint32_t* a, const uint32_t* b, int n) {
+  uint64_t c = 0;
+  for (int i = 0; i < n; ++i) { c += (uint64_t)a[i] + b[i]; r[i] = (uint32_t)c; c >>= 32; }
+}
+NW_HD void bn_sub(uint32_t* r, const uint32_t* a, const uint32_t* b, int n) {
+  uint64_t borrow = 0;
+  for (int i = 0; i < n; ++i) {
+    const uint64_t d = (uint64_t)a[i] - b[i] - borrow;
+    r[i] = (uint32_t)d;
+    borrow = (d >> 63) & 1;
+  }
+}
+// r = a - q b (no underflow), r = a + q b
+NW_HD void bn_submul(uint32_t* r, const uint32_t* a, const uint32_t* b, uint32_t q, int n) {
+  uint64_t c = 0, borrow = 0;
+  for (int i = 0; i < n; ++i) {
+    const uint64_t p = (uint64_t)q * b[i] + c;
+    c = p >> 32;
+    const uint64_t d = (uint64_t)a[i] - (uint32_t)p - borrow;
+    r[i] = (uint32_t)d;
+    borrow = (d >> 63) & 1;
+  }
+}
+NW_HD void bn_addmul(uint32_t* r, const uint32_t* a, const uint32_t* b, uint32_t q, int n) {
+  uint64_t c = 0;
+  for (int i = 0; i < n; ++i) {
+    const uint64_t p = (uint64_t)q * b[i] + a[i] + c;
+    r[i] = (uint32_t)p;
+    c = p >> 32;
+  }
+}
+
+NW_HD void sc_half_split(sc_half& out, const sc& k) {
+  uint32_t xr[8], yr[8], xt[5], yt[5];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { xr[i] = L8_W[i]; yr[i] = k.w[i]; }
+#pragma unroll
+  for (int i = 0; i < 5; ++i) { xt[i] = 0; yt[i] = i == 0 ? 1u : 0u; }
+  bool yneg = false, done = false;
+#pragma unroll 1
+  for (int it = 0; it < 400; ++it) {
+    done = (yr[4] | yr[5] | yr[6] | yr[7]) == 0;
+    if (done) break;
+    // q <= floor(xr / yr): relative error of the f64 quotient < 2^-49.
+    const double qd = floor(bn8_to_f64(xr) / bn8_to_f64(yr) * (1.0 - 0x1p-46));
+    const uint32_t q = qd >= 4294967295.0 ? 0xffffffffu : (qd < 1.0 ? 1u : (uint32_t)qd);
+    // xr -= q yr (never negative), xt += q yt
+    uint64_t c = 0, borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint64_t p = (uint64_t)q * yr[i] + c;
+      c = p >> 32;
+      const uint64_t d = (uint64_t)xr[i] - (uint32_t)p - borrow;
+      xr[i] = (uint32_t)d;
+      borrow = (d >> 63) & 1;
+    }
+    c = 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const uint64_t p = (uint64_t)q * yt[i] + xt[i] + c;
+      xt[i] = (uint32_t)p;
+      c = p >> 32;
+    }
+    if (bn8_lt(xr, yr)) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { const uint32_t t = xr[i]; xr[i] = yr[i]; yr[i] = t; }
+#pragma unroll
+      for (int i = 0; i < 5; ++i) { const uint32_t t = xt[i]; xt[i] = yt[i]; yt[i] = t; }
+      yneg = !yneg;
+    }
+  }
+  if (done && (yt[0] & 1u)) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out.u[i] = yr[i];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) out.v[i] = yt[i];
+    out.vneg = yneg;
+  } else if (done) {
+    // Y's t is even, so X's is odd (consecutive cofactors are coprime) and every vector
+    // X + a Y has an odd t. Take the shortest (max bit length of u, |v|) of X - Y, X + Y,
+    // Z = X - q Y, Z + Y, Y - Z (q <= floor(xr / yr) as in the loop).
+    int best = 1 << 30;
+    uint32_t r[8], t[5];
+    auto consider = [&](bool neg) {
+      const int m = bn_bits(r, 8) > bn_bits(t, 5) ? bn_bits(r, 8) : bn_bits(t, 5);
+      if (m < best) {
+        best = m;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) out.u[i] = r[i];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) out.v[i] = t[i];
+        out.vneg = neg;
+      }
+    };
+    bn_sub(r, xr, yr, 8);  bn_add(t, xt, yt, 5);  consider(!yneg);              // X - Y
+    bn_add(r, xr, yr, 8);                                                       // X + Y
+    const bool y_ge_x = !bn_lt(yt, xt, 5);
+    if (y_ge_x) bn_sub(t, yt, xt, 5); else bn_sub(t, xt, yt, 5);
+    consider(y_ge_x ? yneg : !yneg);
+    if (yr[0] | yr[1] | yr[2] | yr[3]) {
+      const double qd = floor(bn8_to_f64(xr) / bn8_to_f64(yr) * (1.0 - 0x1p-46));
+      const uint32_t q = qd >= 4294967295.0 ? 0xffffffffu : (qd < 1.0 ? 1u : (uint32_t)qd);
+      uint32_t zr[8], zt[5];
+      bn_submul(zr, xr, yr, q, 8);                                              // Z
+      bn_addmul(zt, xt, yt, q, 5);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[i] = zr[i];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) t[i] = zt[i];
+      consider(!yneg);
+      bn_add(r, zr, yr, 8);  bn_sub(t, zt, yt, 5);  consider(!yneg);            // Z + Y
+      if (bn_lt(zr, yr, 8)) {                                                   // Y - Z
+        bn_sub(r, yr, zr, 8);  bn_add(t, zt, yt, 5);  consider(yneg);
+      }
+    }
+  }
+  // Fallback (iteration cap, or u >= 2^252 / |v| >= 2^160): the trivial vector (k, 1).
+  if (!done || (out.u[7] >> 28) != 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out.u[i] = k.w[i];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) out.v[i] = i == 0 ? 1u : 0u;
+    out.vneg = false;
+  }
+}
+
+}  // namespace nw

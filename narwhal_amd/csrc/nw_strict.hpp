@@ -1,0 +1,171 @@
+// nw_strict.hpp — crypto::Signature::verify (crypto/src/lib.rs:200-204: ed25519
+// Signature::from_bytes, dalek PublicKey::from_bytes, verify_strict [ext]) for one lane.
+//
+// Shared by k_verify_strict and the host self-check (tools/hostcheck.hip), so the exact
+// code the GPU runs is also checked against the oracle on the CPU.
+//
+//   1. s high bits, s < l, decompress A and R (dalek semantics, y >= p accepted),
+//      small-order tests (8P == 0 <=> y mod p in {0, 1, -1, y8, -y8} for a decoded P).
+//   2. k = H(R || A || M) mod l (computed by the caller: SHA-512 is device code).
+//   3. Half-size scalars (nw_scalar.hpp sc_half_split): u = v k (mod 8l), v odd, and
+//      w = -v s mod l; then  R + [k]A - [s]B == 0  <=>  [v]R + [u]A + [w]B == 0.
+//   4. One ladder of ~128 doublings: signed 4-bit windows over u (table j*A) and |v|
+//      (table j*(+-R)), per-lane tables in private memory; w = w0 + 2^128 w1 by signed
+//      8-bit windows over two affine tables (j*B and j*2^128 B, LDS).
+#pragma once
+#include "narwhal_amd.h"
+#include "nw_ladder.hpp"
+
+namespace nw {
+
+struct strict_consts {
+  curve_consts k;
+  fe small_y[5];   // canonical y of the 8 small-order points: 0, 1, -1, y8, -y8
+};
+
+// 8P == identity for a decoded point (y as loaded; the x sign does not matter).
+NW_HD bool small_order_by_y(const fe& y, const fe small_y[5]) {
+  fe t;
+  fe_canonical(t, y);
+  bool hit = false;
+#pragma unroll
+  for (int c = 0; c < 5; ++c) {
+    uint32_t d = 0;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) d |= t.v[i] ^ small_y[c].v[i];
+    hit |= d == 0;
+  }
+  return hit;
+}
+
+NW_HD int digit4_of(const uint32_t* w, int nwords, int j) {
+  uint32_t word = w[0];
+  for (int t = 1; t < 8; ++t) word = (t < nwords && (j >> 3) == t) ? w[t] : word;
+  return (int)((word >> ((j & 7) * 4)) & 15u) - 8;
+}
+
+NW_HD void add_table_digit(ge& acc, const ge_cached* tab, int d, bool want_t) {
+  // tab[e - 1] = e * P, e = 1..8; d = 0 adds nothing.
+  if (d != 0) {
+    const int ad = d < 0 ? -d : d;
+    ge_cached c = tab[ad - 1];
+    ge_cached_cneg(c, d < 0);
+    ge_add_cached(acc, acc, c, want_t);
+  }
+}
+
+NW_HD void build_table8(ge_cached tab[8], const ge& P, const fe& d2) {
+  ge_to_cached(tab[0], P, d2);
+  ge acc;
+  ge_dbl(acc, P, true);
+  ge_to_cached(tab[1], acc, d2);
+#pragma unroll 1
+  for (int j = 3; j <= 8; ++j) {
+    ge_add_cached(acc, acc, tab[0], true);
+    ge_to_cached(tab[j - 1], acc, d2);
+  }
+}
+
+// Status of one strict verification. wave_max maps this lane's ladder length (in 4-bit
+// windows) to the wave's maximum (identity on the host). tabA/tabR: 8 entries each of
+// per-lane scratch. s_btab / s_b128: j*B and j*2^128 B, j = 0..128.
+template <class WaveMax>
+NW_HD int strict_verify_core(const uint32_t Aw[8], const uint32_t Rw[8], const uint32_t Sw[8],
+                             const sc& k, const strict_consts& K, const ge_niels* s_btab,
+                             const ge_niels* s_b128, ge_cached* tabA, ge_cached* tabR,
+                             WaveMax wave_max) {
+  const bool s_high = (Sw[7] >> 29) != 0;
+  sc s;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s.w[j] = Sw[j];
+  const bool s_canon = sc_is_canonical(s);
+
+  ge P;
+  const bool okA = ge_frombytes(P, Aw, K.k);
+  const bool smallA = small_order_by_y(P.Y, K.small_y);
+  build_table8(tabA, P, K.k.d2);
+
+  sc_half h;
+  sc_half_split(h, k);
+  const bool okR = ge_frombytes(P, Rw, K.k);
+  const bool smallR = small_order_by_y(P.Y, K.small_y);
+  if (h.vneg) ge_neg(P, P);
+  build_table8(tabR, P, K.k.d2);
+
+  // w = -v s mod l (s zeroed when invalid: the verdict is already decided)
+  sc vm, w;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) vm.w[j] = j < 5 ? h.v[j] : 0u;
+  if (!s_canon || s_high) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s.w[j] = 0;
+  }
+  sc_mul(w, vm, s);
+  if (!h.vneg) sc_neg(w, w);
+  // signed digits: u, |v| in 4-bit windows; w0 = w mod 2^128, w1 = w >> 128 in 8-bit windows
+  sc ur, vr;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { ur.w[j] = h.u[j]; vr.w[j] = vm.w[j]; }
+  uint32_t ud[8], vd[8], wd[8];
+  sc_recode(ud, ur, 0x88888888u);
+  sc_recode(vd, vr, 0x88888888u);
+  {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      c += (uint64_t)w.w[i] + 0x80808080u;
+      wd[i] = (uint32_t)c;
+      c >>= 32;
+    }
+#pragma unroll
+    for (int i = 4; i < 8; ++i) {
+      c += (uint64_t)w.w[i] + 0x80808080u;
+      wd[i] = (uint32_t)c;
+      c >>= 32;
+    }
+  }
+  // ladder length in 4-bit windows: up to the highest nonzero signed digit of u and |v|
+  // (digit j is nonzero iff nibble j of the recoded word is not 8), at least 32 for the
+  // two 128-bit halves of w
+  uint32_t xu[8], xv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { xu[j] = ud[j] ^ 0x88888888u; xv[j] = vd[j] ^ 0x88888888u; }
+  const int bu = bn_bits(xu, 8), bv = bn_bits(xv, 5);
+  int W = ((bu > bv ? bu : bv) + 3) / 4;
+  if (W < 32) W = 32;
+  W = wave_max(W);
+
+  ge acc;
+  ge_identity(acc);
+#pragma unroll 1
+  for (int j = W - 1; j >= 0; --j) {
+    if (j != W - 1) {
+#pragma unroll 1
+      for (int t = 0; t < 3; ++t) ge_dbl(acc, acc, false);
+      ge_dbl(acc, acc, true);
+    }
+    add_table_digit(acc, tabA, digit4_of(ud, 8, j), true);
+    add_table_digit(acc, tabR, j < 40 ? digit4_of(vd, 5, j) : 0, true);
+    if ((j & 1) == 0 && j < 32) {
+      const int m = j >> 1;   // 8-bit window m of w0 (word m / 4) and of w1 (word 4 + m / 4)
+      const int sh = (m & 3) * 8;
+      const int e0 = (int)((sel8(wd, m >> 2) >> sh) & 255u) - 128;
+      const int e1 = (int)((sel8(wd, 4 + (m >> 2)) >> sh) & 255u) - 128;
+      add_digit_niels(acc, s_btab, e0, true);
+      add_digit_niels(acc, s_b128, e1, true);
+    }
+  }
+  const bool eq = ge_is_identity(acc);
+  // Reference order: crypto/src/lib.rs:201 (s high bits), 202 (decompress A), then dalek
+  // verify_strict: check_scalar, decompress R, small order (R || A), equation.
+  if (s_high) return NW_ERR_S_HIGH_BITS;
+  if (!okA) return NW_ERR_A_DECODE;
+  if (!s_canon) return NW_ERR_S_NONCANONICAL;
+  if (!okR) return NW_ERR_R_DECODE;
+  if (smallR) return NW_ERR_R_SMALL_ORDER;
+  if (smallA) return NW_ERR_A_SMALL_ORDER;
+  if (!eq) return NW_ERR_EQUATION;
+  return NW_OK;
+}
+
+}  // namespace nw

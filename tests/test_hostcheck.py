@@ -31,7 +31,7 @@ def hc():
     _build()
     lib = ctypes.CDLL(LIB)
     for f in ("hc_decompress", "hc_is_small_order", "hc_dsm", "hc_verify_strict",
-              "hc_scalar_canonical"):
+              "hc_scalar_canonical", "hc_half_split", "hc_verify_strict_half"):
         getattr(lib, f).restype = ctypes.c_int
     return lib
 
@@ -101,3 +101,64 @@ def test_verify_strict_edge_corpus(hc, golden):
         m, pk, sig = (bytes.fromhex(it[k]) for k in ("msg", "pk", "sig"))
         k = O.hram(sig[:32], pk, m)
         assert hc.hc_verify_strict(_b(pk), _b(sig), _b(k)) == it["status"], it["class"]
+
+
+L_ORDER = 2**252 + 27742317777372353535851937790883648493
+
+
+def _half(hc, k: int):
+    u, v = _out(32), _out(20)
+    neg = hc.hc_half_split(_b(k.to_bytes(32, "little")), u, v)
+    vv = int.from_bytes(v.raw, "little")
+    return int.from_bytes(u.raw, "little"), -vv if neg else vv
+
+
+def _adversarial_k():
+    """k whose continued fraction of k / 8l has a huge partial quotient near the stopping
+    point (forces the iteration cap / fallback path)."""
+    n = 8 * L_ORDER
+    return [(n * (2**126 + 1)) // (2**128 + 3) % L_ORDER, n // (2**127 + 1) % L_ORDER,
+            (2**128 - 1), 2**128, 2**252, L_ORDER - 1, 0, 1, 2, 7]
+
+
+def test_half_split_lattice(hc):
+    """u = v k (mod 8l), v odd, |u|, |v| < 2^129 for random k; edge / adversarial k
+    still satisfy the congruence (fallback (k, 1) allowed)."""
+    n = 8 * L_ORDER
+    rng = np.random.Generator(np.random.PCG64(11))
+    sizes = []
+    for i in range(3000):
+        k = int.from_bytes(rng.bytes(32), "little") % L_ORDER
+        u, v = _half(hc, k)
+        assert (u - v * k) % n == 0 and v % 2 == 1 and u >= 0
+        sizes.append(max(u.bit_length(), abs(v).bit_length()))
+    sizes = np.array(sizes)
+    # the best odd vector is <= 129 bits for ~96% of k (Python model of the same search:
+    # 95.7%), and never far above
+    assert (sizes > 129).mean() < 0.06 and sizes.max() <= 140
+    for k in _adversarial_k():
+        u, v = _half(hc, k)
+        assert (u - v * k) % n == 0 and v % 2 == 1 and 0 <= u < 2**253, k
+
+
+def test_strict_half_edge_corpus(hc, golden):
+    for it in golden["edge_corpus"]["items"]:
+        m, pk, sig = (bytes.fromhex(it[k]) for k in ("msg", "pk", "sig"))
+        k = O.hram(sig[:32], pk, m)
+        assert hc.hc_verify_strict_half(_b(pk), _b(sig), _b(k)) == it["status"], it["class"]
+
+
+def test_strict_half_random_and_tampered(hc):
+    rng = np.random.Generator(np.random.PCG64(12))
+    for i in range(120):
+        seed = rng.bytes(32)
+        pk, sk = O.keypair_from_seed(seed)
+        m = rng.bytes(32)
+        sig = bytearray(O.sign(sk, m))
+        if i % 3 == 1:
+            sig[32 + int(rng.integers(0, 31))] ^= 1 << int(rng.integers(0, 8))
+        elif i % 3 == 2:
+            sig[int(rng.integers(0, 32))] ^= 1 << int(rng.integers(0, 8))
+        k = O.hram(bytes(sig[:32]), pk, m)
+        assert hc.hc_verify_strict_half(_b(pk), _b(bytes(sig)), _b(k)) == \
+            O.verify_strict(m, pk, bytes(sig))

@@ -10,8 +10,16 @@ using namespace nw;
 
 static curve_consts K;
 static ge_niels BT[129];
+static strict_consts SK;
+static ge_niels B128[129];
 static bool ready = false;
-static void init() { if (!ready) { compute_consts(K, BT); ready = true; } }
+static void init() {
+  if (!ready) {
+    compute_consts(K, BT);
+    compute_strict_consts(SK, B128);
+    ready = true;
+  }
+}
 
 static void load8(uint32_t w[8], const uint8_t* b) { memcpy(w, b, 32); }
 static void store8(uint8_t* b, const uint32_t w[8]) { memcpy(b, w, 32); }
@@ -96,6 +104,25 @@ int hc_verify_strict(const uint8_t pk[32], const uint8_t sig[64], const uint8_t 
   if (smallA) return 5;
   if (!eq) return 7;
   return 0;
+}
+
+
+// Half-size scalar split (nw_scalar.hpp): u (32 bytes), |v| (20 bytes), sign.
+int hc_half_split(const uint8_t k32[32], uint8_t u32[32], uint8_t v20[20]) {
+  sc k; load8(k.w, k32);
+  sc_half h; sc_half_split(h, k);
+  memcpy(u32, h.u, 32); memcpy(v20, h.v, 20);
+  return h.vneg ? 1 : 0;
+}
+
+// The kernel's strict verification (nw_strict.hpp), k supplied (device-only SHA).
+int hc_verify_strict_half(const uint8_t pk[32], const uint8_t sig[64], const uint8_t k32[32]) {
+  init();
+  uint32_t Aw[8], Rw[8], Sw[8];
+  load8(Aw, pk); load8(Rw, sig); load8(Sw, sig + 32);
+  sc k; load8(k.w, k32);
+  ge_cached ta[8], tr[8];
+  return strict_verify_core(Aw, Rw, Sw, k, SK, BT, B128, ta, tr, [](int w) { return w; });
 }
 
 }
