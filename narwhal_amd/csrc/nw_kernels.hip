@@ -103,21 +103,41 @@ __device__ __forceinline__ void load_block_full(uint64_t w[16], const uint8_t* p
 }
 
 // Tail block(s): message bytes [base, len) followed by 0x80, zeros, and (if last) the
-// 128-bit big-endian bit length in the final 16 bytes.
+// 128-bit big-endian bit length in the final 16 bytes. Reads only the aligned dwords that
+// hold a message byte (such a dword never crosses a page, so nothing past the buffer can
+// fault) and masks the bytes at or beyond len.
 __device__ __forceinline__ void load_block_tail(uint64_t w[16], const uint8_t* msg, uint64_t base,
                                                 uint64_t len, bool last) {
+  const uintptr_t a0 = (uintptr_t)(msg + base);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(a0 & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a0 & 3) * 8;
+  // message bytes in this block; negative for a padding-only block after the 0x80 block
+  const int64_t rem = (int64_t)len - (int64_t)base;
+  // dword q[i] covers block bytes [4 i - sh/8, 4 i - sh/8 + 4)
+  uint32_t prev = 0;
+#pragma unroll 1
+  for (int i = 0; i < 33; ++i) {
+    const int64_t first = 4 * (int64_t)i - (int64_t)(sh >> 3);   // block byte of q[i]'s byte 0
+    const uint32_t cur = first < rem ? q[i] : 0u;
+    if (i > 0) {
+      // block dword i-1 = bytes [4(i-1), 4i): LE word realigned from q[i-1], q[i]
+      uint32_t lo = __builtin_amdgcn_alignbit(cur, prev, sh);
+      const int64_t k0 = 4 * (int64_t)(i - 1);                 // its first block byte
+      // keep bytes < rem, put 0x80 at byte rem
+      uint32_t keep = 0, pad = 0;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    uint64_t v = 0;
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const uint64_t pos = base + 8 * i + b;
-      uint32_t byte = 0;
-      if (pos < len) byte = msg[pos];
-      else if (pos == len) byte = 0x80;
-      v = (v << 8) | byte;
+      for (int b = 0; b < 4; ++b) {
+        const int64_t pos = k0 + b;
+        keep |= (pos < rem ? 0xffu : 0u) << (8 * b);
+        pad |= (pos == rem ? 0x80u : 0u) << (8 * b);
+      }
+      lo = (lo & keep) | pad;
+      const int wi = (i - 1) >> 1;
+      const uint64_t be = (uint64_t)__builtin_bswap32(lo);
+      if ((i - 1) & 1) w[wi] = (w[wi] & 0xffffffff00000000ull) | be;
+      else w[wi] = be << 32;
     }
-    w[i] = v;
+    prev = cur;
   }
   if (last) {
     w[14] = len >> 61;

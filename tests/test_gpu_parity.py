@@ -48,6 +48,21 @@ def test_sha512_ragged_unaligned():
     assert np.array_equal(out2, ref)
 
 
+def test_sha512_every_tail_length_and_alignment():
+    """Every length 0..400 (one, two and three padding layouts per block boundary, incl.
+    len % 128 in [112, 128) where the length field spills into a padding-only block) at
+    each of the 4 byte alignments."""
+    lens = np.arange(0, 401, dtype=np.uint64)
+    rng = np.random.Generator(np.random.PCG64(5))
+    for shift in range(4):
+        offs = (np.concatenate([[0], np.cumsum(lens)[:-1]]) + shift).astype(np.uint64)
+        data = rng.integers(0, 256, size=int(lens.sum()) + shift + 1, dtype=np.uint8)
+        out = C.sha512_digest32_many(data, offs, lens)
+        for i in range(len(lens)):
+            m = data[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes()
+            assert out[i].tobytes() == hashlib.sha512(m).digest()[:32], (shift, i)
+
+
 def test_sha512_reference_processor_fixture():
     """worker/src/tests/processor_tests.rs: digest == Sha512(serialized_batch)[..32]."""
     m = W.reference_serialized_batch()
