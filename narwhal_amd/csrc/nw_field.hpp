@@ -29,6 +29,17 @@ static constexpr uint32_t M25 = (1u << 25) - 1;
 
 NW_HD uint64_t mul32(uint32_t a, uint32_t b) { return (uint64_t)a * b; }
 
+// acc + a * b as one v_mad_u64_u32. The empty asm makes the accumulator opaque so the
+// compiler keeps the chain in the written order (a column's carry-in stays its first
+// addend) instead of re-associating it into a product tree plus a separate 64-bit add.
+NW_HD uint64_t mac(uint64_t acc, uint32_t a, uint32_t b) {
+  uint64_t r = acc + (uint64_t)a * b;
+#ifdef __HIP_DEVICE_COMPILE__
+  asm("" : "+v"(r));
+#endif
+  return r;
+}
+
 NW_HD void fe_0(fe& h) {
 #pragma unroll
   for (int i = 0; i < 10; ++i) h.v[i] = 0;
@@ -93,6 +104,23 @@ NW_HD void fe_sub(fe& h, const fe& f, const fe& g) {
 }
 NW_HD void fe_neg(fe& h, const fe& f) { fe z; fe_0(z); fe_sub(h, z, f); }
 
+// Carry-folded column reduction (fe_mul / fe_sq). Columns 0-4 and 5-9 are accumulated as
+// two interleaved chains (independent v_mad_u64_u32 streams, so no dependent-issue wait
+// states); inside a chain each column's carry is the initial accumulator of the next one,
+// so no separate 64-bit add per step. fe_join finishes: a = column 4 (its carry goes into
+// limb 5), b = column 9 (its carry wraps to limb 0 times 19). Every column stays < 2^63
+// (input bounds above), so carries are < 2^39 and limbs land in T.
+NW_HD void fe_join(fe& h, uint64_t a, uint64_t b) {
+  h.v[4] = (uint32_t)a & M26;
+  h.v[9] = (uint32_t)b & M25;
+  const uint64_t t5 = (uint64_t)h.v[5] + (a >> 26);
+  h.v[5] = (uint32_t)t5 & M25;
+  h.v[6] += (uint32_t)(t5 >> 25);
+  const uint64_t t0 = (uint64_t)h.v[0] + (b >> 25) * 19;
+  h.v[0] = (uint32_t)t0 & M26;
+  h.v[1] += (uint32_t)(t0 >> 26);
+}
+
 NW_HD void fe_mul(fe& h, const fe& f, const fe& g) {
   const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
   const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
@@ -102,37 +130,63 @@ NW_HD void fe_mul(fe& h, const fe& f, const fe& g) {
                  g5_19 = 19 * g5, g6_19 = 19 * g6, g7_19 = 19 * g7, g8_19 = 19 * g8,
                  g9_19 = 19 * g9;
   const uint32_t f1_2 = 2 * f1, f3_2 = 2 * f3, f5_2 = 2 * f5, f7_2 = 2 * f7, f9_2 = 2 * f9;
-  uint64_t h0 = mul32(f0, g0) + mul32(f1_2, g9_19) + mul32(f2, g8_19) + mul32(f3_2, g7_19) +
-                mul32(f4, g6_19) + mul32(f5_2, g5_19) + mul32(f6, g4_19) + mul32(f7_2, g3_19) +
-                mul32(f8, g2_19) + mul32(f9_2, g1_19);
-  uint64_t h1 = mul32(f0, g1) + mul32(f1, g0) + mul32(f2, g9_19) + mul32(f3, g8_19) +
-                mul32(f4, g7_19) + mul32(f5, g6_19) + mul32(f6, g5_19) + mul32(f7, g4_19) +
-                mul32(f8, g3_19) + mul32(f9, g2_19);
-  uint64_t h2 = mul32(f0, g2) + mul32(f1_2, g1) + mul32(f2, g0) + mul32(f3_2, g9_19) +
-                mul32(f4, g8_19) + mul32(f5_2, g7_19) + mul32(f6, g6_19) + mul32(f7_2, g5_19) +
-                mul32(f8, g4_19) + mul32(f9_2, g3_19);
-  uint64_t h3 = mul32(f0, g3) + mul32(f1, g2) + mul32(f2, g1) + mul32(f3, g0) +
-                mul32(f4, g9_19) + mul32(f5, g8_19) + mul32(f6, g7_19) + mul32(f7, g6_19) +
-                mul32(f8, g5_19) + mul32(f9, g4_19);
-  uint64_t h4 = mul32(f0, g4) + mul32(f1_2, g3) + mul32(f2, g2) + mul32(f3_2, g1) +
-                mul32(f4, g0) + mul32(f5_2, g9_19) + mul32(f6, g8_19) + mul32(f7_2, g7_19) +
-                mul32(f8, g6_19) + mul32(f9_2, g5_19);
-  uint64_t h5 = mul32(f0, g5) + mul32(f1, g4) + mul32(f2, g3) + mul32(f3, g2) +
-                mul32(f4, g1) + mul32(f5, g0) + mul32(f6, g9_19) + mul32(f7, g8_19) +
-                mul32(f8, g7_19) + mul32(f9, g6_19);
-  uint64_t h6 = mul32(f0, g6) + mul32(f1_2, g5) + mul32(f2, g4) + mul32(f3_2, g3) +
-                mul32(f4, g2) + mul32(f5_2, g1) + mul32(f6, g0) + mul32(f7_2, g9_19) +
-                mul32(f8, g8_19) + mul32(f9_2, g7_19);
-  uint64_t h7 = mul32(f0, g7) + mul32(f1, g6) + mul32(f2, g5) + mul32(f3, g4) +
-                mul32(f4, g3) + mul32(f5, g2) + mul32(f6, g1) + mul32(f7, g0) +
-                mul32(f8, g9_19) + mul32(f9, g8_19);
-  uint64_t h8 = mul32(f0, g8) + mul32(f1_2, g7) + mul32(f2, g6) + mul32(f3_2, g5) +
-                mul32(f4, g4) + mul32(f5_2, g3) + mul32(f6, g2) + mul32(f7_2, g1) +
-                mul32(f8, g0) + mul32(f9_2, g9_19);
-  uint64_t h9 = mul32(f0, g9) + mul32(f1, g8) + mul32(f2, g7) + mul32(f3, g6) +
-                mul32(f4, g5) + mul32(f5, g4) + mul32(f6, g3) + mul32(f7, g2) +
-                mul32(f8, g1) + mul32(f9, g0);
-  fe_carry64(h, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
+  // Two interleaved carry-folded chains: columns 0-4 (a) and 5-9 (b).
+  uint64_t a = 0, b = 0;
+  a = mac(a, f0, g0); b = mac(b, f0, g5);
+  a = mac(a, f1_2, g9_19); b = mac(b, f1, g4);
+  a = mac(a, f2, g8_19); b = mac(b, f2, g3);
+  a = mac(a, f3_2, g7_19); b = mac(b, f3, g2);
+  a = mac(a, f4, g6_19); b = mac(b, f4, g1);
+  a = mac(a, f5_2, g5_19); b = mac(b, f5, g0);
+  a = mac(a, f6, g4_19); b = mac(b, f6, g9_19);
+  a = mac(a, f7_2, g3_19); b = mac(b, f7, g8_19);
+  a = mac(a, f8, g2_19); b = mac(b, f8, g7_19);
+  a = mac(a, f9_2, g1_19); b = mac(b, f9, g6_19);
+  h.v[0] = (uint32_t)a & M26; a >>= 26; h.v[5] = (uint32_t)b & M25; b >>= 25;
+  a = mac(a, f0, g1); b = mac(b, f0, g6);
+  a = mac(a, f1, g0); b = mac(b, f1_2, g5);
+  a = mac(a, f2, g9_19); b = mac(b, f2, g4);
+  a = mac(a, f3, g8_19); b = mac(b, f3_2, g3);
+  a = mac(a, f4, g7_19); b = mac(b, f4, g2);
+  a = mac(a, f5, g6_19); b = mac(b, f5_2, g1);
+  a = mac(a, f6, g5_19); b = mac(b, f6, g0);
+  a = mac(a, f7, g4_19); b = mac(b, f7_2, g9_19);
+  a = mac(a, f8, g3_19); b = mac(b, f8, g8_19);
+  a = mac(a, f9, g2_19); b = mac(b, f9_2, g7_19);
+  h.v[1] = (uint32_t)a & M25; a >>= 25; h.v[6] = (uint32_t)b & M26; b >>= 26;
+  a = mac(a, f0, g2); b = mac(b, f0, g7);
+  a = mac(a, f1_2, g1); b = mac(b, f1, g6);
+  a = mac(a, f2, g0); b = mac(b, f2, g5);
+  a = mac(a, f3_2, g9_19); b = mac(b, f3, g4);
+  a = mac(a, f4, g8_19); b = mac(b, f4, g3);
+  a = mac(a, f5_2, g7_19); b = mac(b, f5, g2);
+  a = mac(a, f6, g6_19); b = mac(b, f6, g1);
+  a = mac(a, f7_2, g5_19); b = mac(b, f7, g0);
+  a = mac(a, f8, g4_19); b = mac(b, f8, g9_19);
+  a = mac(a, f9_2, g3_19); b = mac(b, f9, g8_19);
+  h.v[2] = (uint32_t)a & M26; a >>= 26; h.v[7] = (uint32_t)b & M25; b >>= 25;
+  a = mac(a, f0, g3); b = mac(b, f0, g8);
+  a = mac(a, f1, g2); b = mac(b, f1_2, g7);
+  a = mac(a, f2, g1); b = mac(b, f2, g6);
+  a = mac(a, f3, g0); b = mac(b, f3_2, g5);
+  a = mac(a, f4, g9_19); b = mac(b, f4, g4);
+  a = mac(a, f5, g8_19); b = mac(b, f5_2, g3);
+  a = mac(a, f6, g7_19); b = mac(b, f6, g2);
+  a = mac(a, f7, g6_19); b = mac(b, f7_2, g1);
+  a = mac(a, f8, g5_19); b = mac(b, f8, g0);
+  a = mac(a, f9, g4_19); b = mac(b, f9_2, g9_19);
+  h.v[3] = (uint32_t)a & M25; a >>= 25; h.v[8] = (uint32_t)b & M26; b >>= 26;
+  a = mac(a, f0, g4); b = mac(b, f0, g9);
+  a = mac(a, f1_2, g3); b = mac(b, f1, g8);
+  a = mac(a, f2, g2); b = mac(b, f2, g7);
+  a = mac(a, f3_2, g1); b = mac(b, f3, g6);
+  a = mac(a, f4, g0); b = mac(b, f4, g5);
+  a = mac(a, f5_2, g9_19); b = mac(b, f5, g4);
+  a = mac(a, f6, g8_19); b = mac(b, f6, g3);
+  a = mac(a, f7_2, g7_19); b = mac(b, f7, g2);
+  a = mac(a, f8, g6_19); b = mac(b, f8, g1);
+  a = mac(a, f9_2, g5_19); b = mac(b, f9, g0);
+  fe_join(h, a, b);
 }
 
 NW_HD void fe_sq(fe& h, const fe& f) {
@@ -142,32 +196,47 @@ NW_HD void fe_sq(fe& h, const fe& f) {
                  f5_2 = 2 * f5, f6_2 = 2 * f6, f7_2 = 2 * f7;
   const uint32_t f5_38 = 38 * f5, f6_19 = 19 * f6, f7_38 = 38 * f7, f8_19 = 19 * f8,
                  f9_38 = 38 * f9;
-  uint64_t h0 = mul32(f0, f0) + mul32(f1_2, f9_38) + mul32(f2_2, f8_19) + mul32(f3_2, f7_38) +
-                mul32(f4_2, f6_19) + mul32(f5, f5_38);
-  uint64_t h1 = mul32(f0_2, f1) + mul32(f2, f9_38) + mul32(f3_2, f8_19) + mul32(f4, f7_38) +
-                mul32(f5_2, f6_19);
-  uint64_t h2 = mul32(f0_2, f2) + mul32(f1_2, f1) + mul32(f3_2, f9_38) + mul32(f4_2, f8_19) +
-                mul32(f5_2, f7_38) + mul32(f6, f6_19);
-  uint64_t h3 = mul32(f0_2, f3) + mul32(f1_2, f2) + mul32(f4, f9_38) + mul32(f5_2, f8_19) +
-                mul32(f6, f7_38);
-  uint64_t h4 = mul32(f0_2, f4) + mul32(f1_2, f3_2) + mul32(f2, f2) + mul32(f5_2, f9_38) +
-                mul32(f6_2, f8_19) + mul32(f7, f7_38);
-  uint64_t h5 = mul32(f0_2, f5) + mul32(f1_2, f4) + mul32(f2_2, f3) + mul32(f6, f9_38) +
-                mul32(f7_2, f8_19);
-  uint64_t h6 = mul32(f0_2, f6) + mul32(f1_2, f5_2) + mul32(f2_2, f4) + mul32(f3_2, f3) +
-                mul32(f7_2, f9_38) + mul32(f8, f8_19);
-  uint64_t h7 = mul32(f0_2, f7) + mul32(f1_2, f6) + mul32(f2_2, f5) + mul32(f3_2, f4) +
-                mul32(f8, f9_38);
-  uint64_t h8 = mul32(f0_2, f8) + mul32(f1_2, f7_2) + mul32(f2_2, f6) + mul32(f3_2, f5_2) +
-                mul32(f4, f4) + mul32(f9, f9_38);
-  uint64_t h9 = mul32(f0_2, f9) + mul32(f1_2, f8) + mul32(f2_2, f7) + mul32(f3_2, f6) +
-                mul32(f4_2, f5);
-  fe_carry64(h, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
+  // Two interleaved carry-folded chains: columns 0-4 (a) and 5-9 (b).
+  uint64_t a = 0, b = 0;
+  a = mac(a, f0, f0); b = mac(b, f0_2, f5);
+  a = mac(a, f1_2, f9_38); b = mac(b, f1_2, f4);
+  a = mac(a, f2_2, f8_19); b = mac(b, f2_2, f3);
+  a = mac(a, f3_2, f7_38); b = mac(b, f6, f9_38);
+  a = mac(a, f4_2, f6_19); b = mac(b, f7_2, f8_19);
+  a = mac(a, f5, f5_38); h.v[5] = (uint32_t)b & M25; b >>= 25;
+  h.v[0] = (uint32_t)a & M26; a >>= 26; b = mac(b, f0_2, f6);
+  a = mac(a, f0_2, f1); b = mac(b, f1_2, f5_2);
+  a = mac(a, f2, f9_38); b = mac(b, f2_2, f4);
+  a = mac(a, f3_2, f8_19); b = mac(b, f3_2, f3);
+  a = mac(a, f4, f7_38); b = mac(b, f7_2, f9_38);
+  a = mac(a, f5_2, f6_19); b = mac(b, f8, f8_19);
+  h.v[1] = (uint32_t)a & M25; a >>= 25; h.v[6] = (uint32_t)b & M26; b >>= 26;
+  a = mac(a, f0_2, f2); b = mac(b, f0_2, f7);
+  a = mac(a, f1_2, f1); b = mac(b, f1_2, f6);
+  a = mac(a, f3_2, f9_38); b = mac(b, f2_2, f5);
+  a = mac(a, f4_2, f8_19); b = mac(b, f3_2, f4);
+  a = mac(a, f5_2, f7_38); b = mac(b, f8, f9_38);
+  a = mac(a, f6, f6_19); h.v[7] = (uint32_t)b & M25; b >>= 25;
+  h.v[2] = (uint32_t)a & M26; a >>= 26; b = mac(b, f0_2, f8);
+  a = mac(a, f0_2, f3); b = mac(b, f1_2, f7_2);
+  a = mac(a, f1_2, f2); b = mac(b, f2_2, f6);
+  a = mac(a, f4, f9_38); b = mac(b, f3_2, f5_2);
+  a = mac(a, f5_2, f8_19); b = mac(b, f4, f4);
+  a = mac(a, f6, f7_38); b = mac(b, f9, f9_38);
+  h.v[3] = (uint32_t)a & M25; a >>= 25; h.v[8] = (uint32_t)b & M26; b >>= 26;
+  a = mac(a, f0_2, f4); b = mac(b, f0_2, f9);
+  a = mac(a, f1_2, f3_2); b = mac(b, f1_2, f8);
+  a = mac(a, f2, f2); b = mac(b, f2_2, f7);
+  a = mac(a, f5_2, f9_38); b = mac(b, f3_2, f6);
+  a = mac(a, f6_2, f8_19); b = mac(b, f4_2, f5);
+  a = mac(a, f7, f7_38);
+  fe_join(h, a, b);
 }
 
 // h = f^(2^n), rolled loop (keeps code size down inside the exponentiations).
 NW_HD void fe_sqn(fe& h, const fe& f, int n) {
   fe_sq(h, f);
+#pragma unroll 1
   for (int i = 1; i < n; ++i) fe_sq(h, h);
 }
 

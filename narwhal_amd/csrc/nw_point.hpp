@@ -91,6 +91,27 @@ NW_HD void ge_add_niels(ge& r, const ge& p, const ge_niels& q, bool want_t) {
   if (want_t) fe_mul(r.T, e, h);
 }
 
+// r = p + q with T, q either cached or (affine, wave-uniform) an affine niels point held
+// in cached form (q.Z2 unused: 2 Z1 Z2 = 2 Z1). One routine for every ladder term.
+NW_HD void ge_add_any(ge& r, const ge& p, const ge_cached& q, bool affine) {
+  fe a, b, c, d, e, f, g, h;
+  fe_sub(a, p.Y, p.X);
+  fe_mul(a, a, q.YmX);
+  fe_add(b, p.Y, p.X);
+  fe_mul(b, b, q.YpX);
+  fe_mul(c, p.T, q.T2d);
+  if (affine) fe_add(d, p.Z, p.Z);
+  else fe_mul(d, p.Z, q.Z2);
+  fe_sub(e, b, a);
+  fe_sub(f, d, c);
+  fe_add(g, d, c);
+  fe_add(h, b, a);
+  fe_mul(r.X, e, f);
+  fe_mul(r.Y, g, h);
+  fe_mul(r.Z, f, g);
+  fe_mul(r.T, e, h);
+}
+
 // Conditionally negate a niels point: -(x, y) = (-x, y) -> swap y+x / y-x, negate 2dxy.
 NW_HD void ge_niels_cneg(ge_niels& n, bool neg) {
   fe t;

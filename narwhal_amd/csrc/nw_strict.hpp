@@ -80,17 +80,23 @@ NW_HD int strict_verify_core(const uint32_t Aw[8], const uint32_t Rw[8], const u
   for (int j = 0; j < 8; ++j) s.w[j] = Sw[j];
   const bool s_canon = sc_is_canonical(s);
 
-  ge P;
-  const bool okA = ge_frombytes(P, Aw, K.k);
-  const bool smallA = small_order_by_y(P.Y, K.small_y);
-  build_table8(tabA, P, K.k.d2);
-
+  // Decompress A, then R, in one rolled loop (one copy of the sqrt_ratio_i chain in the
+  // code object): P, its small-order flag and its 8-entry table.
   sc_half h;
   sc_half_split(h, k);
-  const bool okR = ge_frombytes(P, Rw, K.k);
-  const bool smallR = small_order_by_y(P.Y, K.small_y);
-  if (h.vneg) ge_neg(P, P);
-  build_table8(tabR, P, K.k.d2);
+  bool okA = false, smallA = false, okR = false, smallR = false;
+#pragma unroll 1
+  for (int pt = 0; pt < 2; ++pt) {
+    uint32_t x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = pt ? Rw[i] : Aw[i];
+    ge P;
+    const bool ok = ge_frombytes(P, x, K.k);
+    const bool small = small_order_by_y(P.Y, K.small_y);
+    if (pt == 0) { okA = ok; smallA = small; } else { okR = ok; smallR = small; }
+    if (pt == 1 && h.vneg) ge_neg(P, P);
+    build_table8(pt ? tabR : tabA, P, K.k.d2);
+  }
 
   // w = -v s mod l (s zeroed when invalid: the verdict is already decided)
   sc vm, w;
@@ -135,24 +141,43 @@ NW_HD int strict_verify_core(const uint32_t Aw[8], const uint32_t Rw[8], const u
   if (W < 32) W = 32;
   W = wave_max(W);
 
+  // One rolled doubling and one addition routine serve every term (code size: the ladder
+  // body stays inside the instruction cache). Per 4-bit window j: 4 doublings, then the
+  // A digit, the R digit and, on even j < 32, the two 8-bit B digits.
   ge acc;
   ge_identity(acc);
 #pragma unroll 1
   for (int j = W - 1; j >= 0; --j) {
     if (j != W - 1) {
 #pragma unroll 1
-      for (int t = 0; t < 3; ++t) ge_dbl(acc, acc, false);
-      ge_dbl(acc, acc, true);
+      for (int t = 0; t < 4; ++t) ge_dbl(acc, acc, t == 3);
     }
-    add_table_digit(acc, tabA, digit4_of(ud, 8, j), true);
-    add_table_digit(acc, tabR, j < 40 ? digit4_of(vd, 5, j) : 0, true);
-    if ((j & 1) == 0 && j < 32) {
-      const int m = j >> 1;   // 8-bit window m of w0 (word m / 4) and of w1 (word 4 + m / 4)
-      const int sh = (m & 3) * 8;
-      const int e0 = (int)((sel8(wd, m >> 2) >> sh) & 255u) - 128;
-      const int e1 = (int)((sel8(wd, 4 + (m >> 2)) >> sh) & 255u) - 128;
-      add_digit_niels(acc, s_btab, e0, true);
-      add_digit_niels(acc, s_b128, e1, true);
+    const int nslots = ((j & 1) == 0 && j < 32) ? 4 : 2;
+#pragma unroll 1
+    for (int slot = 0; slot < nslots; ++slot) {
+      int d;
+      if (slot == 0) {
+        d = digit4_of(ud, 8, j);
+      } else if (slot == 1) {
+        d = j < 40 ? digit4_of(vd, 5, j) : 0;
+      } else {
+        const int m = j >> 1;   // 8-bit window m of w0 (word m / 4) and of w1 (word 4 + m / 4)
+        d = (int)((sel8(wd, (slot == 2 ? 0 : 4) + (m >> 2)) >> ((m & 3) * 8)) & 255u) - 128;
+      }
+      if (d != 0) {
+        const int ad = d < 0 ? -d : d;
+        ge_cached e;
+        if (slot < 2) {
+          e = (slot == 0 ? tabA : tabR)[ad - 1];
+        } else {
+          const ge_niels& nb = (slot == 2 ? s_btab : s_b128)[ad];
+          fe_copy(e.YpX, nb.ypx);
+          fe_copy(e.YmX, nb.ymx);
+          fe_copy(e.T2d, nb.xy2d);
+        }
+        ge_cached_cneg(e, d < 0);
+        ge_add_any(acc, acc, e, slot >= 2);
+      }
     }
   }
   const bool eq = ge_is_identity(acc);
