@@ -104,6 +104,19 @@ NW_HD void fe_sub(fe& h, const fe& f, const fe& g) {
 }
 NW_HD void fe_neg(fe& h, const fe& f) { fe z; fe_0(z); fe_sub(h, z, f); }
 
+// h = f - g + 4p WITHOUT the carry pass ("S" bound: limbs <= f + 4p, about 2^28.3 for
+// f <= T, 2^28.6 for f <= L). Only for values whose every use is the FIRST operand of
+// fe_mul (scaled by 2 in 32 bits; the second operand is scaled by 19 and must be <= 1.5L).
+// Worst-case columns over the limb bounds (tests/test_field_bounds.py) stay below 2^64
+// with their carry-in.
+NW_HD void fe_sub_nc(fe& h, const fe& f, const fe& g) {
+  h.v[0] = (f.v[0] + 0xfffffb4u) - g.v[0];
+#pragma unroll
+  for (int i = 1; i < 10; ++i)
+    h.v[i] = (f.v[i] + ((i & 1) ? 0x7fffffcu : 0xffffffcu)) - g.v[i];
+}
+NW_HD void fe_neg_nc(fe& h, const fe& f) { fe z; fe_0(z); fe_sub_nc(h, z, f); }
+
 // Carry-folded column reduction (fe_mul / fe_sq). Columns 0-4 and 5-9 are accumulated as
 // two interleaved chains (independent v_mad_u64_u32 streams, so no dependent-issue wait
 // states); inside a chain each column's carry is the initial accumulator of the next one,

@@ -34,16 +34,20 @@ NW_HD void ge_to_cached(ge_cached& c, const ge& p, const fe& d2) {
   fe_mul(c.T2d, p.T, d2);
 }
 
+// Uncarried differences (fe_sub_nc) are used only as the FIRST fe_mul operand (the second
+// is multiplied by 19 in 32 bits and must stay carried); tests/test_field_bounds.py checks
+// every (first, second) operand pair below.
+
 // r = p + q (q cached). Computes T3 only when want_t.
 NW_HD void ge_add_cached(ge& r, const ge& p, const ge_cached& q, bool want_t) {
   fe a, b, c, d, e, f, g, h;
-  fe_sub(a, p.Y, p.X);
+  fe_sub_nc(a, p.Y, p.X);
   fe_mul(a, a, q.YmX);
   fe_add(b, p.Y, p.X);
   fe_mul(b, b, q.YpX);
-  fe_mul(c, p.T, q.T2d);
+  fe_mul(c, q.T2d, p.T);
   fe_mul(d, p.Z, q.Z2);
-  fe_sub(e, b, a);
+  fe_sub_nc(e, b, a);
   fe_sub(f, d, c);
   fe_add(g, d, c);
   fe_add(h, b, a);
@@ -56,32 +60,32 @@ NW_HD void ge_add_cached(ge& r, const ge& p, const ge_cached& q, bool want_t) {
 // r = p - q (q cached): swap YpX/YmX and negate 2dT.
 NW_HD void ge_sub_cached(ge& r, const ge& p, const ge_cached& q, bool want_t) {
   fe a, b, c, d, e, f, g, h;
-  fe_sub(a, p.Y, p.X);
+  fe_sub_nc(a, p.Y, p.X);
   fe_mul(a, a, q.YpX);
   fe_add(b, p.Y, p.X);
   fe_mul(b, b, q.YmX);
-  fe_mul(c, p.T, q.T2d);
+  fe_mul(c, q.T2d, p.T);
   fe_mul(d, p.Z, q.Z2);
-  fe_sub(e, b, a);
+  fe_sub_nc(e, b, a);
   fe_add(f, d, c);
-  fe_sub(g, d, c);
+  fe_sub_nc(g, d, c);
   fe_add(h, b, a);
   fe_mul(r.X, e, f);
   fe_mul(r.Y, g, h);
-  fe_mul(r.Z, f, g);
+  fe_mul(r.Z, g, f);
   if (want_t) fe_mul(r.T, e, h);
 }
 
 // r = p + q (q affine niels, Z = 1).
 NW_HD void ge_add_niels(ge& r, const ge& p, const ge_niels& q, bool want_t) {
   fe a, b, c, d, e, f, g, h;
-  fe_sub(a, p.Y, p.X);
+  fe_sub_nc(a, p.Y, p.X);
   fe_mul(a, a, q.ymx);
   fe_add(b, p.Y, p.X);
   fe_mul(b, b, q.ypx);
-  fe_mul(c, p.T, q.xy2d);
+  fe_mul(c, q.xy2d, p.T);
   fe_add(d, p.Z, p.Z);
-  fe_sub(e, b, a);
+  fe_sub_nc(e, b, a);
   fe_sub(f, d, c);
   fe_add(g, d, c);
   fe_add(h, b, a);
@@ -95,14 +99,14 @@ NW_HD void ge_add_niels(ge& r, const ge& p, const ge_niels& q, bool want_t) {
 // in cached form (q.Z2 unused: 2 Z1 Z2 = 2 Z1). One routine for every ladder term.
 NW_HD void ge_add_any(ge& r, const ge& p, const ge_cached& q, bool affine) {
   fe a, b, c, d, e, f, g, h;
-  fe_sub(a, p.Y, p.X);
+  fe_sub_nc(a, p.Y, p.X);
   fe_mul(a, a, q.YmX);
   fe_add(b, p.Y, p.X);
   fe_mul(b, b, q.YpX);
-  fe_mul(c, p.T, q.T2d);
+  fe_mul(c, q.T2d, p.T);
   if (affine) fe_add(d, p.Z, p.Z);
   else fe_mul(d, p.Z, q.Z2);
-  fe_sub(e, b, a);
+  fe_sub_nc(e, b, a);
   fe_sub(f, d, c);
   fe_add(g, d, c);
   fe_add(h, b, a);
@@ -121,7 +125,7 @@ NW_HD void ge_niels_cneg(ge_niels& n, bool neg) {
     n.ypx.v[i] = neg ? b : a;
     n.ymx.v[i] = neg ? a : b;
   }
-  fe_neg(t, n.xy2d);
+  fe_neg_nc(t, n.xy2d);
   fe_cmov(n.xy2d, t, neg);
 }
 NW_HD void ge_cached_cneg(ge_cached& c, bool neg) {
@@ -132,7 +136,7 @@ NW_HD void ge_cached_cneg(ge_cached& c, bool neg) {
     c.YpX.v[i] = neg ? b : a;
     c.YmX.v[i] = neg ? a : b;
   }
-  fe_neg(t, c.T2d);
+  fe_neg_nc(t, c.T2d);
   fe_cmov(c.T2d, t, neg);
 }
 
@@ -148,7 +152,7 @@ NW_HD void ge_dbl(ge& r, const ge& p, bool want_t) {
   fe_add(H, A, B);
   fe_add(t, p.X, p.Y);
   fe_sq(t, t);
-  fe_sub(E, H, t);
+  fe_sub_nc(E, H, t);
   fe_sub(G, A, B);
   fe_add(F, G, C);
   fe_mul(r.X, E, F);
