@@ -4,7 +4,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -Inarwhal_amd/csrc -Wall -Wno-unused-function
 CSRC := narwhal_amd/csrc
-HDRS := $(wildcard $(CSRC)/*.hpp) $(CSRC)/nw_kernels.h include/narwhal_amd.h
+HDRS := $(wildcard $(CSRC)/*.hpp) $(CSRC)/nw_kernels.h $(CSRC)/nw_runtime.h include/narwhal_amd.h
 LIB := narwhal_amd/libnarwhal_amd.so
 BUILD := build
 
@@ -22,11 +22,15 @@ $(BUILD)/nw_cert.o: $(CSRC)/nw_cert.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(BUILD)/nw_jobs.o: $(CSRC)/nw_jobs.cpp $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
 $(BUILD)/nw_api.o: $(CSRC)/nw_api.cpp $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-$(LIB): $(BUILD)/nw_kernels.o $(BUILD)/nw_batch.o $(BUILD)/nw_cert.o $(BUILD)/nw_api.o
+$(LIB): $(BUILD)/nw_kernels.o $(BUILD)/nw_batch.o $(BUILD)/nw_cert.o $(BUILD)/nw_api.o $(BUILD)/nw_jobs.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 oracle:

@@ -69,6 +69,17 @@ SMALL_ORDER = [
 ]
 
 
+def pmc_traffic(kernel: str, units: int):
+    """Per-launch HBM bytes of `kernel` from the committed PMC passes (profiles/traffic.json,
+    written by tools/profile_summary.py from FETCH_SIZE x 2 + WRITE_SIZE of a bench-size
+    launch), scaled to `units` per launch. None when no profile exists for it."""
+    try:
+        e = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))[kernel]
+    except (OSError, KeyError, ValueError):
+        return None, None
+    return e["hbm_bytes"] * units / e["units"], e["source"]
+
+
 def enc_y(y: int, sign: int) -> bytes:
     b = bytearray(y.to_bytes(32, "little"))
     b[31] |= sign << 7
@@ -440,6 +451,7 @@ def main():
         units = r["n"] * world
         value = units / r["elapsed"] * args.steps
         achieved = r["n"] * MAC_PER_STRICT_VERIFY / (r["kernel_ms"] * 1e-3) / 1e12
+        traffic, tsrc = pmc_traffic("k_verify_strict", r["n"])
         result = {
             "metric": METRIC, "value": value, "unit": "verifies/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -450,7 +462,9 @@ def main():
                        "invalid_fraction": 0.1, "semantics": "crypto::Signature::verify (dalek verify_strict)",
                        "parallelism": f"shard{world}"},
             "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_TMAC,
-                         "unit": "TMAC/s", "frac": achieved / PEAK_TMAC, "traffic": None,
+                         "unit": "TMAC/s", "frac": achieved / PEAK_TMAC, "traffic": traffic,
+                         "traffic_unit": "HBM bytes per launch", "traffic_source": tsrc,
+                         "algorithmic_bytes": r["n"] * (32 + 32 + 64 + 4) + r["n"] / 8,
                          "kernel": "k_verify_strict", "kernel_ms": r["kernel_ms"],
                          "work_per_unit": f"{MAC_PER_STRICT_VERIFY} MAC/verify (SURVEY 8d)"},
             "parity": "ok" if r["parity"] else "FAIL",
@@ -464,12 +478,15 @@ def main():
             kgbs = s["bytes"] / (s["kernel_ms"] * 1e-3) / 1e9
             blocks = s["n"] * ((W.BATCH_BYTES + 17 + 127) // 128)
             tops = blocks * SHA_OPS_PER_BLOCK / (s["kernel_ms"] * 1e-3) / 1e12
+            straffic, ssrc = pmc_traffic("k_sha512_digest32", s["n"])
             result["sha512"] = {"workload": "config3_worker_batch_digests",
                                 "batches_per_gpu": s["n"], "batch_bytes": W.BATCH_BYTES,
                                 "GB_per_s": gbs, "kernel_GB_per_s": kgbs,
                                 "hbm_frac": kgbs / PEAK_HBM_GBS,
                                 "valu_Tops": tops, "valu_frac": tops / PEAK_TOPS_FULL,
                                 "kernel_ms": s["kernel_ms"],
+                                "traffic": straffic, "traffic_source": ssrc,
+                                "algorithmic_bytes": s["bytes"] + 32 * s["n"],
                                 "parity": "ok" if s["parity"] else "FAIL"}
             if not s["parity"]:
                 result["parity"] = "FAIL"
@@ -519,6 +536,7 @@ def main():
         s = run_sha(args, dev, stream, rank, world)
         gbs = s["bytes"] * world / (s["elapsed"] / args.steps) / 1e9
         kgbs = s["bytes"] / (s["kernel_ms"] * 1e-3) / 1e9
+        straffic, ssrc = pmc_traffic("k_sha512_digest32", s["n"])
         result = {
             "metric": METRIC, "value": gbs, "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -527,7 +545,8 @@ def main():
             "config": {"workload": "config3_worker_batch_digests", "batches_per_gpu": s["n"],
                        "batch_bytes": W.BATCH_BYTES, "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": kgbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": kgbs / PEAK_HBM_GBS, "traffic": None,
+                         "frac": kgbs / PEAK_HBM_GBS, "traffic": straffic,
+                         "traffic_source": ssrc,
                          "kernel": "k_sha512_digest32", "kernel_ms": s["kernel_ms"]},
             "parity": "ok" if s["parity"] else "FAIL",
         }

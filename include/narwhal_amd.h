@@ -121,6 +121,39 @@ int nw_keypair_from_seed_many(const uint8_t* seeds, size_t n, uint8_t* pks_out);
 int nw_sign_many(const uint8_t* sks, size_t sk_stride, const uint8_t* digests,
                  size_t digest_stride, size_t n, uint8_t* sigs_out);
 
+/* ---- asynchronous host-buffer entry points (submit / poll) ------------------------- */
+/* The non-blocking form of the calls above, for callers that must not block their event
+ * loop (the reference's primary Core and worker Processor are tokio tasks, node/Cargo.toml:8;
+ * crypto::SignatureService, crypto/src/lib.rs:222-250, is its own async-service pattern).
+ * Submit copies the inputs into pinned staging memory (input buffers may be reused as soon
+ * as it returns), queues H2D + kernels + D2H on the job's own stream and returns. The output
+ * buffers must stay valid until nw_job_poll returns 1 or nw_job_wait returns: that is when
+ * the library writes them. A job is used by one thread at a time; jobs are independent.
+ * The blocking calls above are exactly submit + wait + release. */
+typedef struct nw_job nw_job;
+
+/* Signature::verify over n items (as nw_verify_strict_many). */
+int nw_submit_verify_strict(const uint8_t* digests, size_t digest_stride, const uint8_t* pks,
+                            const uint8_t* sigs, size_t n, int32_t* status_out,
+                            uint8_t* bitmap_out, nw_job** job);
+/* Signature::verify_batch per batch (as nw_verify_batch_many; fail_index_out optional). */
+int nw_submit_verify_batch_many(const uint8_t* digests, const uint8_t* pks, const uint8_t* sigs,
+                                const uint64_t* offsets, size_t nbatches, const uint8_t* z16,
+                                int32_t* status_out, uint64_t* fail_index_out, nw_job** job);
+/* Digest(Sha512(m)[..32]) (as nw_sha512_digest32_many). */
+int nw_submit_sha512_digest32_many(const uint8_t* data, const uint64_t* offsets,
+                                   const uint64_t* lengths, size_t n, uint8_t* out32,
+                                   nw_job** job);
+/* 1 = done (outputs written), 0 = still running, < 0 = runtime error. Never blocks. */
+int nw_job_poll(nw_job* job);
+/* Block until done (outputs written): 0 or a runtime error. */
+int nw_job_wait(nw_job* job);
+/* Call fn(arg) from a HIP runtime thread once the job's device work has finished (e.g. to
+ * wake an async task, which then calls nw_job_poll). fn must not call into this library. */
+int nw_job_notify(nw_job* job, void (*fn)(void*), void* arg);
+/* Return the job's buffers to the pool (waits first if it is still running). */
+void nw_job_release(nw_job* job);
+
 /* ---- primary messages: Header / Vote / Certificate verification -------------------- */
 /* config::Committee (config/src/lib.rs:139-173): authorities sorted by public-key bytes
  * (BTreeMap order), their stake (config::Stake = u32) and worker ids (WorkerId = u32). */

@@ -24,6 +24,9 @@ E_NAMES = {-1: "NW_E_INVALID_ARG", -2: "NW_E_NO_DEVICE", -3: "NW_E_DEVICE",
 
 _lib = None
 
+# void (*fn)(void*) for nw_job_notify
+NOTIFY_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+
 
 class EngineError(RuntimeError):
     """A runtime/device failure (negative NW_E_* code) — never an 'invalid signature'."""
@@ -67,6 +70,11 @@ def lib() -> ctypes.CDLL:
         "nw_votes_verify_many": ([P, P, P, P, P, P, S, P], I),
         "nw_dev_certificates_workspace": ([S, S], S),
         "nw_dev_certificates_verify_many": ([P, P, I, P, P, P, P, P, P], I),
+        "nw_submit_verify_strict": ([P, S, P, P, S, P, P, ctypes.POINTER(P)], I),
+        "nw_submit_verify_batch_many": ([P, P, P, P, S, P, P, P, ctypes.POINTER(P)], I),
+        "nw_submit_sha512_digest32_many": ([P, P, P, S, P, ctypes.POINTER(P)], I),
+        "nw_job_poll": ([P], I), "nw_job_wait": ([P], I),
+        "nw_job_notify": ([P, NOTIFY_FN, P], I), "nw_job_release": ([P], None),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

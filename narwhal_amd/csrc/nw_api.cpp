@@ -17,6 +17,7 @@
 
 #include "narwhal_amd.h"
 #include "nw_kernels.h"
+#include "nw_runtime.h"
 
 namespace {
 
@@ -210,48 +211,6 @@ int nw_dev_sha512_digest32_many(const void* data, const uint64_t* offsets,
   return 0;
 }
 
-int nw_sha512_digest32_many(const uint8_t* data, const uint64_t* offsets,
-                            const uint64_t* lengths, size_t n, uint8_t* out32) {
-  DevCtx* c;
-  int rc = begin(&c);
-  if (rc) return rc;
-  if (n == 0) return 0;
-  if (!data || !offsets || !lengths || !out32) return set_err(NW_E_INVALID_ARG, "null pointer");
-  // Pack the referenced bytes contiguously (messages may live anywhere in `data`).
-  uint64_t total = 0;
-  for (size_t i = 0; i < n; ++i) total += lengths[i];
-  std::vector<uint64_t> offs(n);
-  uint64_t pos = 0;
-  for (size_t i = 0; i < n; ++i) { offs[i] = pos; pos += lengths[i]; }
-  const size_t b_data = a256(total ? total : 1), b_off = a256(8 * n), b_len = a256(8 * n),
-               b_out = a256(32 * n);
-  rc = reserve(*c, b_data + b_off + b_len + b_out);
-  if (rc) return rc;
-  char* base = static_cast<char*>(c->dbuf);
-  uint8_t* d_data = reinterpret_cast<uint8_t*>(base);
-  uint64_t* d_off = reinterpret_cast<uint64_t*>(base + b_data);
-  uint64_t* d_len = reinterpret_cast<uint64_t*>(base + b_data + b_off);
-  uint32_t* d_out = reinterpret_cast<uint32_t*>(base + b_data + b_off + b_len);
-  hipStream_t s = c->stream;
-  // contiguous runs are copied in one go
-  size_t i = 0;
-  while (i < n) {
-    size_t j = i + 1;
-    while (j < n && offsets[j] == offsets[j - 1] + lengths[j - 1]) ++j;
-    const uint64_t bytes = offs[j - 1] + lengths[j - 1] - offs[i];
-    if (bytes)
-      NW_HIP(hipMemcpyAsync(d_data + offs[i], data + offsets[i], bytes, hipMemcpyHostToDevice, s),
-             "H2D data");
-    i = j;
-  }
-  NW_HIP(hipMemcpyAsync(d_off, offs.data(), 8 * n, hipMemcpyHostToDevice, s), "H2D offsets");
-  NW_HIP(hipMemcpyAsync(d_len, lengths, 8 * n, hipMemcpyHostToDevice, s), "H2D lengths");
-  NW_HIP(nw::launch_sha512_digest32(d_data, d_off, d_len, n, d_out, s), "k_sha512 launch");
-  NW_HIP(hipMemcpyAsync(out32, d_out, 32 * n, hipMemcpyDeviceToHost, s), "D2H digests");
-  NW_HIP(hipStreamSynchronize(s), "sync");
-  return 0;
-}
-
 // ------------------------------------------------------------------------------------
 int nw_dev_verify_strict_many(const void* digests, size_t digest_stride, const void* pks,
                               const void* sigs, size_t n, int32_t* status_out,
@@ -274,54 +233,6 @@ int nw_dev_verify_strict_many(const void* digests, size_t digest_stride, const v
                                   static_cast<uint64_t*>(bitmap_out), ws, pick_stream(stream, c)),
          "k_verify_strict launch");
   return 0;
-}
-
-int nw_verify_strict_many(const uint8_t* digests, size_t digest_stride, const uint8_t* pks,
-                          const uint8_t* sigs, size_t n, int32_t* status_out,
-                          uint8_t* bitmap_out) {
-  DevCtx* c;
-  int rc = begin(&c);
-  if (rc) return rc;
-  if (n == 0) return 0;
-  if (!digests || !pks || !sigs) return set_err(NW_E_INVALID_ARG, "null pointer");
-  if (digest_stride != 0 && digest_stride != 32)
-    return set_err(NW_E_INVALID_ARG, "digest_stride must be 0 or 32");
-  const size_t nmsg = digest_stride ? n : 1;
-  const size_t words = (n + 63) / 64;
-  const size_t b_m = a256(32 * nmsg), b_pk = a256(32 * n), b_sig = a256(64 * n),
-               b_st = a256(4 * n), b_bm = a256(8 * words);
-  rc = reserve(*c, b_m + b_pk + b_sig + b_st + b_bm);
-  if (rc) return rc;
-  char* base = static_cast<char*>(c->dbuf);
-  uint8_t* d_m = reinterpret_cast<uint8_t*>(base);
-  uint8_t* d_pk = reinterpret_cast<uint8_t*>(base + b_m);
-  uint8_t* d_sig = reinterpret_cast<uint8_t*>(base + b_m + b_pk);
-  int32_t* d_st = reinterpret_cast<int32_t*>(base + b_m + b_pk + b_sig);
-  uint64_t* d_bm = reinterpret_cast<uint64_t*>(base + b_m + b_pk + b_sig + b_st);
-  hipStream_t s = c->stream;
-  NW_HIP(hipMemcpyAsync(d_m, digests, 32 * nmsg, hipMemcpyHostToDevice, s), "H2D digests");
-  NW_HIP(hipMemcpyAsync(d_pk, pks, 32 * n, hipMemcpyHostToDevice, s), "H2D pks");
-  NW_HIP(hipMemcpyAsync(d_sig, sigs, 64 * n, hipMemcpyHostToDevice, s), "H2D sigs");
-  void* ws;
-  rc = strict_ws(*c, &ws);
-  if (rc) return rc;
-  NW_HIP(nw::launch_verify_strict(reinterpret_cast<const uint32_t*>(d_m),
-                                  (uint32_t)(digest_stride / 4),
-                                  reinterpret_cast<const uint32_t*>(d_pk),
-                                  reinterpret_cast<const uint32_t*>(d_sig), n, d_st, d_bm, ws, s),
-         "k_verify_strict launch");
-  if (status_out)
-    NW_HIP(hipMemcpyAsync(status_out, d_st, 4 * n, hipMemcpyDeviceToHost, s), "D2H status");
-  if (bitmap_out)
-    NW_HIP(hipMemcpyAsync(bitmap_out, d_bm, (n + 7) / 8, hipMemcpyDeviceToHost, s), "D2H bitmap");
-  NW_HIP(hipStreamSynchronize(s), "sync");
-  return 0;
-}
-
-int nw_signature_verify(const uint8_t sig[64], const uint8_t digest[32], const uint8_t pk[32]) {
-  int32_t st = 0;
-  int rc = nw_verify_strict_many(digest, 32, pk, sig, 1, &st, nullptr);
-  return rc ? rc : st;
 }
 
 // ------------------------------------------------------------------------------------
@@ -457,83 +368,6 @@ int nw_dev_verify_batch_many(const void* digests, const void* pks, const void* s
                                  fail_index, s),
          "verify_batch launch");
   return 0;
-}
-
-static int batch_host(const uint8_t* digests, size_t ndig_bytes, const uint8_t* pks,
-                      const uint8_t* sigs, const uint64_t* offsets, size_t nbatches,
-                      const uint8_t* z16, int32_t* status_out, uint64_t* fail_out) {
-  DevCtx* c;
-  int rc = begin(&c);
-  if (rc) return rc;
-  if (nbatches == 0) return 0;
-  const size_t nitems = offsets[nbatches];
-  const size_t b_d = a256(ndig_bytes), b_off = a256(8 * (nbatches + 1)),
-               b_pk = a256(32 * (nitems ? nitems : 1)), b_sig = a256(64 * (nitems ? nitems : 1)),
-               b_z = a256(16 * (nitems ? nitems : 1)), b_st = a256(4 * nbatches),
-               b_fi = a256(8 * nbatches), b_ws = a256(nw::batch_workspace_bytes(nbatches, nitems));
-  rc = reserve(*c, b_d + b_off + b_pk + b_sig + b_z + b_st + b_fi + b_ws);
-  if (rc) return rc;
-  char* p = static_cast<char*>(c->dbuf);
-  uint8_t* d_d = reinterpret_cast<uint8_t*>(p); p += b_d;
-  uint64_t* d_off = reinterpret_cast<uint64_t*>(p); p += b_off;
-  uint8_t* d_pk = reinterpret_cast<uint8_t*>(p); p += b_pk;
-  uint8_t* d_sig = reinterpret_cast<uint8_t*>(p); p += b_sig;
-  uint8_t* d_z = reinterpret_cast<uint8_t*>(p); p += b_z;
-  int32_t* d_st = reinterpret_cast<int32_t*>(p); p += b_st;
-  uint64_t* d_fi = reinterpret_cast<uint64_t*>(p); p += b_fi;
-  void* d_ws = p;
-  hipStream_t s = c->stream;
-  NW_HIP(hipMemcpyAsync(d_d, digests, ndig_bytes, hipMemcpyHostToDevice, s), "H2D digests");
-  NW_HIP(hipMemcpyAsync(d_off, offsets, 8 * (nbatches + 1), hipMemcpyHostToDevice, s), "H2D offsets");
-  if (nitems) {
-    NW_HIP(hipMemcpyAsync(d_pk, pks, 32 * nitems, hipMemcpyHostToDevice, s), "H2D pks");
-    NW_HIP(hipMemcpyAsync(d_sig, sigs, 64 * nitems, hipMemcpyHostToDevice, s), "H2D sigs");
-    if (z16) NW_HIP(hipMemcpyAsync(d_z, z16, 16 * nitems, hipMemcpyHostToDevice, s), "H2D z");
-  }
-  nw::z_key_t key;
-  rc = fill_key(key, nullptr);
-  if (rc) return rc;
-  NW_HIP(nw::launch_verify_batch(reinterpret_cast<const uint32_t*>(d_d), d_off, offsets,
-                                 nbatches, reinterpret_cast<const uint32_t*>(d_pk),
-                                 reinterpret_cast<const uint32_t*>(d_sig), nitems,
-                                 z16 ? reinterpret_cast<const uint32_t*>(d_z) : nullptr, key,
-                                 d_ws, d_st, d_fi, s),
-         "verify_batch launch");
-  NW_HIP(hipMemcpyAsync(status_out, d_st, 4 * nbatches, hipMemcpyDeviceToHost, s), "D2H status");
-  if (fail_out)
-    NW_HIP(hipMemcpyAsync(fail_out, d_fi, 8 * nbatches, hipMemcpyDeviceToHost, s), "D2H index");
-  NW_HIP(hipStreamSynchronize(s), "sync");
-  return 0;
-}
-
-int nw_signature_verify_batch(const uint8_t digest[32], const uint8_t* pks, const uint8_t* sigs,
-                              size_t n, const uint8_t* z16, size_t* fail_index) {
-  if (!digest || (n && (!pks || !sigs))) return set_err(NW_E_INVALID_ARG, "null pointer");
-  if (n == 0) {   // crypto::verify_batch over no votes: dalek MSM of [0]B -> Ok
-    int rc = ensure_init();
-    if (rc) return rc;
-    if (fail_index) *fail_index = 0;
-    return NW_OK;
-  }
-  uint64_t offs[2] = {0, n};
-  int32_t st = 0;
-  uint64_t fi = 0;
-  int rc = batch_host(digest, 32, pks, sigs, offs, 1, z16, &st, &fi);
-  if (rc) return rc;
-  if (fail_index) *fail_index = (size_t)fi;
-  return st;
-}
-
-int nw_verify_batch_many(const uint8_t* digests, const uint8_t* pks, const uint8_t* sigs,
-                         const uint64_t* offsets, size_t nbatches, const uint8_t* z16,
-                         int32_t* status_out) {
-  if (nbatches == 0) return ensure_init();
-  if (!digests || !offsets || !status_out) return set_err(NW_E_INVALID_ARG, "null pointer");
-  for (size_t b = 0; b < nbatches; ++b)
-    if (offsets[b + 1] < offsets[b]) return set_err(NW_E_INVALID_ARG, "offsets not monotone");
-  if (offsets[0] != 0) return set_err(NW_E_INVALID_ARG, "offsets[0] must be 0");
-  return batch_host(digests, 32 * nbatches, pks, sigs, offsets, nbatches, z16, status_out,
-                    nullptr);
 }
 
 }  // extern "C"
@@ -830,3 +664,29 @@ int nw_votes_verify_many(const nw_committee* committee, const uint8_t* ids,
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------
+// Internal runtime helpers for nw_jobs.cpp (nw_runtime.h).
+// ------------------------------------------------------------------------------------
+namespace nw {
+namespace rt {
+
+int ensure_init() { return ::ensure_init(); }
+
+int select_device(int* dev_index) {
+  int rc = ::ensure_init();
+  if (rc) return rc;
+  const int dev = t_state.device;
+  if (dev < 0 || dev >= g_ndev) return ::set_err(NW_E_INVALID_ARG, "bad device index");
+  hipError_t e = hipSetDevice(g_dev_ids[dev]);
+  if (e != hipSuccess) return ::set_err(NW_E_DEVICE, "hipSetDevice", e);
+  *dev_index = dev;
+  return 0;
+}
+
+int set_err(int code, const char* what, hipError_t e) { return ::set_err(code, what, e); }
+
+int os_random(void* buf, size_t n) { return ::os_random(buf, n); }
+
+}  // namespace rt
+}  // namespace nw

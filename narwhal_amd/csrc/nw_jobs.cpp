@@ -1,0 +1,432 @@
+// nw_jobs.cpp — asynchronous host-buffer entry points (nw_submit_* / nw_job_*), and the
+// blocking host-buffer calls built on them.
+//
+// A job owns a HIP stream, a completion event, a pinned host staging buffer and a device
+// buffer, all grow-only and recycled through a per-device pool, so the steady state does
+// no allocation. Submit copies the caller's inputs into the pinned buffer (the caller may
+// reuse its input memory as soon as submit returns), queues one H2D copy, the kernels and
+// one D2H copy of the outputs on the job's stream, records the event and returns. Poll /
+// wait deliver the outputs from pinned memory into the caller's output buffers. This is
+// the shape the reference's async callers need: Narwhal's primary and workers run on
+// tokio (node/Cargo.toml:8), and Core / Processor loops must not block on the device
+// (crypto/src/lib.rs:222-250 SignatureService is the reference's own async-service pattern).
+//
+// Strict verification uses one per-device table workspace; launches from different jobs
+// are ordered on it with an event chain (the copies of one job still overlap the kernels
+// of another).
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "narwhal_amd.h"
+#include "nw_kernels.h"
+#include "nw_runtime.h"
+
+struct nw_job {
+  int dev = -1;
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  char* hbuf = nullptr;   // pinned: inputs, then outputs
+  size_t hcap = 0;
+  char* dbuf = nullptr;   // device: same layout (+ workspace)
+  size_t dcap = 0;
+  struct Out {
+    void* dst;
+    size_t off;
+    size_t bytes;
+  } outs[3];
+  int nouts = 0;
+  bool pending = false;   // device work queued, outputs not yet delivered
+};
+
+namespace {
+
+using nw::rt::set_err;
+
+constexpr int kMaxDev = 64;
+
+struct DevPool {
+  std::mutex m;
+  std::vector<nw_job*> free;
+  void* strict_ws = nullptr;
+  hipEvent_t strict_last = nullptr;   // completion of the last launch using strict_ws
+  bool strict_last_valid = false;
+};
+DevPool g_pool[kMaxDev];
+
+inline size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+#define JOB_HIP(call, what)                                      \
+  do {                                                           \
+    hipError_t e_ = (call);                                      \
+    if (e_ != hipSuccess) return set_err(NW_E_DEVICE, what, e_); \
+  } while (0)
+
+int job_acquire(nw_job** out) {
+  int dev = 0;
+  int rc = nw::rt::select_device(&dev);
+  if (rc) return rc;
+  DevPool& p = g_pool[dev];
+  nw_job* j = nullptr;
+  {
+    std::lock_guard<std::mutex> g(p.m);
+    if (!p.free.empty()) {
+      j = p.free.back();
+      p.free.pop_back();
+    }
+  }
+  if (!j) {
+    j = new (std::nothrow) nw_job;
+    if (!j) return set_err(NW_E_OUT_OF_MEMORY, "job allocation");
+    j->dev = dev;
+    hipError_t e = hipStreamCreateWithFlags(&j->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&j->done, hipEventDisableTiming);
+    if (e != hipSuccess) {
+      if (j->stream) (void)hipStreamDestroy(j->stream);
+      delete j;
+      return set_err(NW_E_DEVICE, "job stream/event", e);
+    }
+  }
+  j->nouts = 0;
+  j->pending = false;
+  *out = j;
+  return 0;
+}
+
+void job_recycle(nw_job* j) {
+  if (!j) return;
+  if (j->pending) (void)hipEventSynchronize(j->done);
+  j->pending = false;
+  j->nouts = 0;
+  std::lock_guard<std::mutex> g(g_pool[j->dev].m);
+  g_pool[j->dev].free.push_back(j);
+}
+
+// Fail a submit after work may have been queued: drain the stream, recycle, report.
+int job_abort(nw_job* j, int rc) {
+  (void)hipStreamSynchronize(j->stream);
+  j->pending = false;
+  job_recycle(j);
+  return rc;
+}
+
+int job_reserve(nw_job* j, size_t hbytes, size_t dbytes) {
+  if (hbytes > j->hcap) {
+    if (j->hbuf) (void)hipHostFree(j->hbuf);
+    j->hbuf = nullptr;
+    j->hcap = 0;
+    const size_t cap = hbytes < (1u << 20) ? (1u << 20) : hbytes + hbytes / 4;
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&j->hbuf), cap, hipHostMallocDefault);
+    if (e != hipSuccess) return set_err(NW_E_OUT_OF_MEMORY, "hipHostMalloc (job staging)", e);
+    j->hcap = cap;
+  }
+  if (dbytes > j->dcap) {
+    if (j->dbuf) (void)hipFree(j->dbuf);
+    j->dbuf = nullptr;
+    j->dcap = 0;
+    const size_t cap = dbytes < (1u << 20) ? (1u << 20) : dbytes + dbytes / 4;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&j->dbuf), cap);
+    if (e != hipSuccess) return set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (job buffer)", e);
+    j->dcap = cap;
+  }
+  return 0;
+}
+
+void job_out(nw_job* j, void* dst, size_t off, size_t bytes) {
+  if (dst && bytes) j->outs[j->nouts++] = {dst, off, bytes};
+}
+
+void job_deliver(nw_job* j) {
+  for (int i = 0; i < j->nouts; ++i) memcpy(j->outs[i].dst, j->hbuf + j->outs[i].off, j->outs[i].bytes);
+  j->nouts = 0;
+  j->pending = false;
+}
+
+// Queue: H2D of [0, in_bytes), `launch`, D2H of [out_off, out_off + out_bytes), event.
+template <class Launch>
+int job_run(nw_job* j, size_t in_bytes, size_t out_off, size_t out_bytes, Launch launch) {
+  if (in_bytes)
+    JOB_HIP(hipMemcpyAsync(j->dbuf, j->hbuf, in_bytes, hipMemcpyHostToDevice, j->stream),
+            "H2D (job inputs)");
+  int rc = launch();
+  if (rc) return rc;
+  if (out_bytes)
+    JOB_HIP(hipMemcpyAsync(j->hbuf + out_off, j->dbuf + out_off, out_bytes,
+                           hipMemcpyDeviceToHost, j->stream),
+            "D2H (job outputs)");
+  JOB_HIP(hipEventRecord(j->done, j->stream), "hipEventRecord");
+  j->pending = true;
+  return 0;
+}
+
+int fill_key(nw::z_key_t& k) {
+  int rc = nw::rt::os_random(k.key, 32);
+  k.nonce = 0;
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nw_submit_verify_strict(const uint8_t* digests, size_t digest_stride, const uint8_t* pks,
+                            const uint8_t* sigs, size_t n, int32_t* status_out,
+                            uint8_t* bitmap_out, nw_job** job) {
+  if (!job) return set_err(NW_E_INVALID_ARG, "null job pointer");
+  *job = nullptr;
+  if (n && (!digests || !pks || !sigs)) return set_err(NW_E_INVALID_ARG, "null pointer");
+  if (digest_stride != 0 && digest_stride != 32)
+    return set_err(NW_E_INVALID_ARG, "digest_stride must be 0 or 32");
+  nw_job* j;
+  int rc = job_acquire(&j);
+  if (rc) return rc;
+  if (n == 0) {
+    *job = j;
+    return 0;
+  }
+  const size_t nmsg = digest_stride ? n : 1;
+  const size_t o_m = 0, o_pk = o_m + a256(32 * nmsg), o_sig = o_pk + a256(32 * n),
+               o_st = o_sig + a256(64 * n), o_bm = o_st + a256(4 * n),
+               end = o_bm + a256(8 * ((n + 63) / 64));
+  rc = job_reserve(j, end, end);
+  if (rc) return job_abort(j, rc);
+  memcpy(j->hbuf + o_m, digests, 32 * nmsg);
+  memcpy(j->hbuf + o_pk, pks, 32 * n);
+  memcpy(j->hbuf + o_sig, sigs, 64 * n);
+  DevPool& p = g_pool[j->dev];
+  rc = job_run(j, o_st, o_st, end - o_st, [&]() -> int {
+    std::lock_guard<std::mutex> g(p.m);
+    if (!p.strict_ws) {
+      hipError_t e = hipMalloc(&p.strict_ws, nw::strict_workspace_bytes());
+      if (e != hipSuccess) {
+        p.strict_ws = nullptr;
+        return set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (strict workspace)", e);
+      }
+      e = hipEventCreateWithFlags(&p.strict_last, hipEventDisableTiming);
+      if (e != hipSuccess) return set_err(NW_E_DEVICE, "hipEventCreate", e);
+    }
+    if (p.strict_last_valid)
+      JOB_HIP(hipStreamWaitEvent(j->stream, p.strict_last, 0), "hipStreamWaitEvent");
+    JOB_HIP(nw::launch_verify_strict(reinterpret_cast<const uint32_t*>(j->dbuf + o_m),
+                                     (uint32_t)(digest_stride / 4),
+                                     reinterpret_cast<const uint32_t*>(j->dbuf + o_pk),
+                                     reinterpret_cast<const uint32_t*>(j->dbuf + o_sig), n,
+                                     reinterpret_cast<int32_t*>(j->dbuf + o_st),
+                                     reinterpret_cast<uint64_t*>(j->dbuf + o_bm), p.strict_ws,
+                                     j->stream),
+            "k_verify_strict launch");
+    JOB_HIP(hipEventRecord(p.strict_last, j->stream), "hipEventRecord (strict ws)");
+    p.strict_last_valid = true;
+    return 0;
+  });
+  if (rc) return job_abort(j, rc);
+  job_out(j, status_out, o_st, 4 * n);
+  job_out(j, bitmap_out, o_bm, (n + 7) / 8);
+  *job = j;
+  return 0;
+}
+
+int nw_submit_verify_batch_many(const uint8_t* digests, const uint8_t* pks, const uint8_t* sigs,
+                                const uint64_t* offsets, size_t nbatches, const uint8_t* z16,
+                                int32_t* status_out, uint64_t* fail_index_out, nw_job** job) {
+  if (!job) return set_err(NW_E_INVALID_ARG, "null job pointer");
+  *job = nullptr;
+  if (nbatches && (!digests || !offsets)) return set_err(NW_E_INVALID_ARG, "null pointer");
+  if (nbatches) {
+    if (offsets[0] != 0) return set_err(NW_E_INVALID_ARG, "offsets[0] must be 0");
+    for (size_t b = 0; b < nbatches; ++b)
+      if (offsets[b + 1] < offsets[b]) return set_err(NW_E_INVALID_ARG, "offsets not monotone");
+  }
+  const size_t nitems = nbatches ? offsets[nbatches] : 0;
+  if (nitems && (!pks || !sigs)) return set_err(NW_E_INVALID_ARG, "null pointer");
+  nw_job* j;
+  int rc = job_acquire(&j);
+  if (rc) return rc;
+  if (nbatches == 0) {
+    *job = j;
+    return 0;
+  }
+  const size_t m = nitems ? nitems : 1;
+  const size_t o_d = 0, o_off = o_d + a256(32 * nbatches), o_pk = o_off + a256(8 * (nbatches + 1)),
+               o_sig = o_pk + a256(32 * m), o_z = o_sig + a256(64 * m),
+               o_st = o_z + (z16 ? a256(16 * m) : 0), o_fi = o_st + a256(4 * nbatches),
+               o_ws = o_fi + a256(8 * nbatches),
+               end = o_ws + a256(nw::batch_workspace_bytes(nbatches, nitems));
+  rc = job_reserve(j, o_ws, end);
+  if (rc) return job_abort(j, rc);
+  memcpy(j->hbuf + o_d, digests, 32 * nbatches);
+  memcpy(j->hbuf + o_off, offsets, 8 * (nbatches + 1));
+  if (nitems) {
+    memcpy(j->hbuf + o_pk, pks, 32 * nitems);
+    memcpy(j->hbuf + o_sig, sigs, 64 * nitems);
+    if (z16) memcpy(j->hbuf + o_z, z16, 16 * nitems);
+  }
+  nw::z_key_t key;
+  rc = fill_key(key);
+  if (rc) return job_abort(j, rc);
+  const uint64_t* h_off = reinterpret_cast<const uint64_t*>(j->hbuf + o_off);
+  rc = job_run(j, o_st, o_st, o_ws - o_st, [&]() -> int {
+    JOB_HIP(nw::launch_verify_batch(reinterpret_cast<const uint32_t*>(j->dbuf + o_d),
+                                    reinterpret_cast<const uint64_t*>(j->dbuf + o_off), h_off,
+                                    nbatches, reinterpret_cast<const uint32_t*>(j->dbuf + o_pk),
+                                    reinterpret_cast<const uint32_t*>(j->dbuf + o_sig), nitems,
+                                    z16 ? reinterpret_cast<const uint32_t*>(j->dbuf + o_z)
+                                        : nullptr,
+                                    key, j->dbuf + o_ws,
+                                    reinterpret_cast<int32_t*>(j->dbuf + o_st),
+                                    reinterpret_cast<uint64_t*>(j->dbuf + o_fi), j->stream),
+            "verify_batch launch");
+    return 0;
+  });
+  if (rc) return job_abort(j, rc);
+  job_out(j, status_out, o_st, 4 * nbatches);
+  job_out(j, fail_index_out, o_fi, 8 * nbatches);
+  *job = j;
+  return 0;
+}
+
+int nw_submit_sha512_digest32_many(const uint8_t* data, const uint64_t* offsets,
+                                   const uint64_t* lengths, size_t n, uint8_t* out32,
+                                   nw_job** job) {
+  if (!job) return set_err(NW_E_INVALID_ARG, "null job pointer");
+  *job = nullptr;
+  if (n && (!data || !offsets || !lengths || !out32))
+    return set_err(NW_E_INVALID_ARG, "null pointer");
+  nw_job* j;
+  int rc = job_acquire(&j);
+  if (rc) return rc;
+  if (n == 0) {
+    *job = j;
+    return 0;
+  }
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; ++i) total += lengths[i];
+  const size_t o_data = 0, o_off = a256(total ? total : 1), o_len = o_off + a256(8 * n),
+               o_out = o_len + a256(8 * n), end = o_out + a256(32 * n);
+  rc = job_reserve(j, end, end);
+  if (rc) return job_abort(j, rc);
+  // Pack the referenced bytes contiguously (messages may live anywhere in `data`);
+  // contiguous runs are copied in one go.
+  uint64_t* offs = reinterpret_cast<uint64_t*>(j->hbuf + o_off);
+  uint64_t pos = 0;
+  for (size_t i = 0; i < n; ++i) {
+    offs[i] = pos;
+    pos += lengths[i];
+  }
+  size_t i = 0;
+  while (i < n) {
+    size_t k = i + 1;
+    while (k < n && offsets[k] == offsets[k - 1] + lengths[k - 1]) ++k;
+    const uint64_t bytes = offs[k - 1] + lengths[k - 1] - offs[i];
+    if (bytes) memcpy(j->hbuf + o_data + offs[i], data + offsets[i], bytes);
+    i = k;
+  }
+  memcpy(j->hbuf + o_len, lengths, 8 * n);
+  rc = job_run(j, o_out, o_out, 32 * n, [&]() -> int {
+    JOB_HIP(nw::launch_sha512_digest32(reinterpret_cast<const uint8_t*>(j->dbuf + o_data),
+                                       reinterpret_cast<const uint64_t*>(j->dbuf + o_off),
+                                       reinterpret_cast<const uint64_t*>(j->dbuf + o_len), n,
+                                       reinterpret_cast<uint32_t*>(j->dbuf + o_out), j->stream),
+            "k_sha512_digest32 launch");
+    return 0;
+  });
+  if (rc) return job_abort(j, rc);
+  job_out(j, out32, o_out, 32 * n);
+  *job = j;
+  return 0;
+}
+
+int nw_job_poll(nw_job* job) {
+  if (!job) return set_err(NW_E_INVALID_ARG, "null job");
+  if (!job->pending) return 1;
+  hipError_t e = hipEventQuery(job->done);
+  if (e == hipErrorNotReady) return 0;
+  if (e != hipSuccess) return set_err(NW_E_DEVICE, "hipEventQuery", e);
+  job_deliver(job);
+  return 1;
+}
+
+int nw_job_wait(nw_job* job) {
+  if (!job) return set_err(NW_E_INVALID_ARG, "null job");
+  if (!job->pending) return 0;
+  JOB_HIP(hipEventSynchronize(job->done), "hipEventSynchronize");
+  job_deliver(job);
+  return 0;
+}
+
+int nw_job_notify(nw_job* job, void (*fn)(void*), void* arg) {
+  if (!job || !fn) return set_err(NW_E_INVALID_ARG, "null job or callback");
+  if (!job->pending) {
+    fn(arg);
+    return 0;
+  }
+  JOB_HIP(hipLaunchHostFunc(job->stream, fn, arg), "hipLaunchHostFunc");
+  return 0;
+}
+
+void nw_job_release(nw_job* job) { job_recycle(job); }
+
+// ---- blocking host-buffer entry points = submit + wait ------------------------------
+static int run_blocking(int rc, nw_job* j) {
+  if (rc) return rc;
+  rc = nw_job_wait(j);
+  nw_job_release(j);
+  return rc;
+}
+
+int nw_sha512_digest32_many(const uint8_t* data, const uint64_t* offsets,
+                            const uint64_t* lengths, size_t n, uint8_t* out32) {
+  nw_job* j = nullptr;
+  return run_blocking(nw_submit_sha512_digest32_many(data, offsets, lengths, n, out32, &j), j);
+}
+
+int nw_verify_strict_many(const uint8_t* digests, size_t digest_stride, const uint8_t* pks,
+                          const uint8_t* sigs, size_t n, int32_t* status_out,
+                          uint8_t* bitmap_out) {
+  nw_job* j = nullptr;
+  return run_blocking(nw_submit_verify_strict(digests, digest_stride, pks, sigs, n, status_out,
+                                              bitmap_out, &j),
+                      j);
+}
+
+int nw_signature_verify(const uint8_t sig[64], const uint8_t digest[32], const uint8_t pk[32]) {
+  int32_t st = 0;
+  int rc = nw_verify_strict_many(digest, 32, pk, sig, 1, &st, nullptr);
+  return rc ? rc : st;
+}
+
+int nw_signature_verify_batch(const uint8_t digest[32], const uint8_t* pks, const uint8_t* sigs,
+                              size_t n, const uint8_t* z16, size_t* fail_index) {
+  if (!digest || (n && (!pks || !sigs))) return set_err(NW_E_INVALID_ARG, "null pointer");
+  if (n == 0) {   // crypto::verify_batch over no votes: dalek MSM of [0]B -> Ok
+    int rc = nw::rt::ensure_init();
+    if (rc) return rc;
+    if (fail_index) *fail_index = 0;
+    return NW_OK;
+  }
+  const uint64_t offs[2] = {0, n};
+  int32_t st = 0;
+  uint64_t fi = 0;
+  nw_job* j = nullptr;
+  int rc = run_blocking(nw_submit_verify_batch_many(digest, pks, sigs, offs, 1, z16, &st, &fi, &j),
+                        j);
+  if (rc) return rc;
+  if (fail_index) *fail_index = (size_t)fi;
+  return st;
+}
+
+int nw_verify_batch_many(const uint8_t* digests, const uint8_t* pks, const uint8_t* sigs,
+                         const uint64_t* offsets, size_t nbatches, const uint8_t* z16,
+                         int32_t* status_out) {
+  if (nbatches == 0) return nw::rt::ensure_init();
+  if (!status_out) return set_err(NW_E_INVALID_ARG, "null pointer");
+  nw_job* j = nullptr;
+  return run_blocking(nw_submit_verify_batch_many(digests, pks, sigs, offsets, nbatches, z16,
+                                                  status_out, nullptr, &j),
+                      j);
+}
+
+}  // extern "C"
