@@ -34,6 +34,13 @@ static constexpr uint64_t SHA512_H0[8] = {
   0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
   0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
 
+// (lo, hi) -> u64 as a plain register pair (no shift/or: the compiler would otherwise turn
+// `(hi << 32) | lo` into a half-rate v_lshl_add_u64).
+typedef uint32_t nw_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint64_t pack64(uint32_t lo, uint32_t hi) {
+  return __builtin_bit_cast(uint64_t, nw_u32x2{lo, hi});
+}
+
 __device__ __forceinline__ uint64_t rotr64(uint64_t x, const int n) {
   const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
   uint32_t rlo, rhi;
@@ -44,13 +51,32 @@ __device__ __forceinline__ uint64_t rotr64(uint64_t x, const int n) {
     rlo = __builtin_amdgcn_alignbit(lo, hi, n - 32);
     rhi = __builtin_amdgcn_alignbit(hi, lo, n - 32);
   }
-  return ((uint64_t)rhi << 32) | rlo;
+  return pack64(rlo, rhi);
 }
 __device__ __forceinline__ uint64_t shr64(uint64_t x, const int n) {   // n < 32
   const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-  return ((uint64_t)(hi >> n) << 32) | __builtin_amdgcn_alignbit(hi, lo, n);
+  return pack64(__builtin_amdgcn_alignbit(hi, lo, n), hi >> n);
 }
 __device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
+
+// Three-input bitwise functions as one v_bitop3_b32 per 32-bit half (the compiler does not
+// form them from ^/&/| on its own). LUT index = (x << 2) | (y << 1) | z.
+template <int LUT>
+__device__ __forceinline__ uint64_t bitop3_64(uint64_t x, uint64_t y, uint64_t z) {
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)x, (uint32_t)y, (uint32_t)z, LUT);
+  const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(x >> 32), (uint32_t)(y >> 32),
+                                                  (uint32_t)(z >> 32), LUT);
+  return pack64(lo, hi);
+}
+__device__ __forceinline__ uint64_t xor3_64(uint64_t x, uint64_t y, uint64_t z) {
+  return bitop3_64<0x96>(x, y, z);
+}
+__device__ __forceinline__ uint64_t maj64(uint64_t x, uint64_t y, uint64_t z) {
+  return bitop3_64<0xE8>(x, y, z);
+}
+__device__ __forceinline__ uint64_t ch64(uint64_t x, uint64_t y, uint64_t z) {
+  return bitop3_64<0xCA>(x, y, z);   // x ? y : z
+}
 
 // 16 rounds; FIRST = the block words themselves, else the schedule is advanced in place.
 template <bool FIRST>
@@ -65,16 +91,16 @@ __device__ __forceinline__ void sha512_16rounds(uint64_t& a, uint64_t& b, uint64
       wj = w[j];
     } else {
       const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
-      const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ shr64(w15, 7);
-      const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ shr64(w2, 6);
+      const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), shr64(w15, 7));
+      const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), shr64(w2, 6));
       wj = w[j] + s0 + w[(j + 9) & 15] + s1;
       w[j] = wj;
     }
-    const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
-    const uint64_t ch = (e & f) ^ (~e & g);
+    const uint64_t S1 = xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41));
+    const uint64_t ch = ch64(e, f, g);
     const uint64_t t1 = h + S1 + ch + SHA512_K[r + j] + wj;
-    const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-    const uint64_t maj = (a & b) ^ (a & c) ^ (b & c);
+    const uint64_t S0 = xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39));
+    const uint64_t maj = maj64(a, b, c);
     const uint64_t t2 = S0 + maj;
     h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
   }
