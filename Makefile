@@ -26,11 +26,15 @@ $(BUILD)/nw_jobs.o: $(CSRC)/nw_jobs.cpp $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
+$(BUILD)/nw_wire.o: $(CSRC)/nw_wire.cpp $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
 $(BUILD)/nw_api.o: $(CSRC)/nw_api.cpp $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-$(LIB): $(BUILD)/nw_kernels.o $(BUILD)/nw_batch.o $(BUILD)/nw_cert.o $(BUILD)/nw_api.o $(BUILD)/nw_jobs.o
+$(LIB): $(BUILD)/nw_kernels.o $(BUILD)/nw_batch.o $(BUILD)/nw_cert.o $(BUILD)/nw_api.o $(BUILD)/nw_jobs.o $(BUILD)/nw_wire.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 oracle:

@@ -49,6 +49,8 @@ extern "C" {
 #define NW_DAG_MALFORMED_HEADER 18       /* DagError::MalformedHeader(id): unknown worker id */
 #define NW_DAG_AUTHORITY_REUSE 19        /* DagError::AuthorityReuse(pk)                     */
 #define NW_DAG_REQUIRES_QUORUM 20        /* DagError::CertificateRequiresQuorum              */
+#define NW_DAG_SERIALIZATION 21          /* DagError::SerializationError: the frame does not
+                                            bincode-decode as a PrimaryMessage             */
 /* DagError::InvalidSignature(CryptoError): base + the NW_ERR_* of the first failing check.
  * NW_DAG_INVALID_SIGNATURE: the message's own Signature::verify (header or vote);
  * NW_DAG_INVALID_VOTES: the certificate's Signature::verify_batch over its votes. */
@@ -205,6 +207,32 @@ int nw_votes_verify_many(const nw_committee* committee, const uint8_t* ids,
                          const uint64_t* rounds, const uint8_t* origins,
                          const uint8_t* authors, const uint8_t* sigs, size_t n,
                          int32_t* status_out);
+
+/* ---- wire-format ingest ------------------------------------------------------------- */
+/* primary::PrimaryMessage variants (primary/src/primary.rs:32-38). */
+#define NW_MSG_HEADER 0
+#define NW_MSG_VOTE 1
+#define NW_MSG_CERTIFICATE 2
+#define NW_MSG_CERTIFICATES_REQUEST 3
+
+/* n frames as the primary's receiver gets them (PrimaryReceiverHandler::dispatch,
+ * primary/src/primary.rs:224-240): frame i = frames[offsets[i]..offsets[i+1]), each a
+ * bincode-serialized PrimaryMessage. Decoded natively (bincode 1.3 fixint LE; PublicKey as a
+ * base64 string, crypto/src/lib.rs:94-112; payload/parents re-sorted and de-duplicated as
+ * BTreeMap/BTreeSet deserialisation does) and verified with the check each variant gets:
+ * Header::verify, Vote::verify, Certificate::verify (primary/src/messages.rs). status_out:
+ * n x int32 (0 = Ok, NW_DAG_* as for the calls above, NW_DAG_SERIALIZATION for a frame that
+ * does not decode; CertificatesRequest frames are only decoded, status 0). kind_out
+ * (optional): n x int32 NW_MSG_* or -1. index_out (optional): as nw_certificates_verify_many
+ * (0 for votes). Batch coefficients come from the OS CSPRNG. */
+int nw_primary_messages_verify_wire(const nw_committee* committee, const uint8_t* frames,
+                                    const uint64_t* offsets, size_t n, int32_t* kind_out,
+                                    int32_t* status_out, uint64_t* index_out);
+/* Decode only (host code, no device needed): kind_out n x int32 as above; counts_out
+ * (optional) n x 3 uint64: payload entries and parents after BTreeMap/BTreeSet
+ * de-duplication, and votes (Header/Certificate); digests requested (CertificatesRequest). */
+int nw_primary_messages_scan(const uint8_t* frames, const uint64_t* offsets, size_t n,
+                             int32_t* kind_out, uint64_t* counts_out);
 
 /* ---- device-pointer (asynchronous) entry points ------------------------------------ */
 /* All pointers are device pointers on the current device; work is queued on `stream`

@@ -75,6 +75,8 @@ def lib() -> ctypes.CDLL:
         "nw_submit_sha512_digest32_many": ([P, P, P, S, P, ctypes.POINTER(P)], I),
         "nw_job_poll": ([P], I), "nw_job_wait": ([P], I),
         "nw_job_notify": ([P, NOTIFY_FN, P], I), "nw_job_release": ([P], None),
+        "nw_primary_messages_verify_wire": ([P, P, P, S, P, P, P], I),
+        "nw_primary_messages_scan": ([P, P, S, P, P], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
