@@ -363,6 +363,45 @@ def run_batch10k(args, dev, stream, rank, world):
     return res, (digest, pks, sigs)
 
 
+def run_wire(args, dev, stream, rank, world, N: int = 4):
+    """SURVEY 8(f) rank 2: received bincode PrimaryMessage::Certificate frames -> native
+    decode -> Certificate::verify, through the blocking host entry point
+    (nw_primary_messages_verify_wire). Frames/s includes host decode, H2D, kernels, D2H."""
+    from narwhal_amd import wire as WI
+    L = _lib.lib()
+    n = args.wire_frames
+    keys = [(bytes(pk), bytes(sd) + bytes(pk)) for sd, pk in
+            zip(W.fixture_seeds(N), C.keypair_from_seed_many(W.fixture_seeds(N)))]
+    s = W.certificate_stream(n, keys, lambda sk, m: C.sign_many(sk, m),
+                             lambda d, o: C.sha512_digest32_many(d, o[:-1], np.diff(o)),
+                             seed=100 + rank)
+    data, offs = WI.frames_from_stream(s)
+    com = M.committee_struct(s["committee"])
+    kind = np.zeros(n, np.int32)
+    st = np.zeros(n, np.int32)
+
+    def call():
+        check(L.nw_primary_messages_verify_wire(ctypes.byref(com), M._p(data), M._p(offs), n,
+                                                M._p(kind), M._p(st), None), "wire")
+    call()
+    ok = bool((st == 0).all() and (kind == WI.MSG_CERTIFICATE).all())
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.wire_steps):
+        call()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    sec = el / args.wire_steps
+    return {"committee": N, "frames_per_call": n, "frame_bytes": int(offs[-1]),
+            "certs_per_s": n * world / sec, "ms_per_call": sec * 1e3,
+            "path": "host frames -> nw_primary_messages_verify_wire (decode + H2D + kernels + D2H)",
+            "parity": "ok" if ok else "FAIL"}
+
+
 def cpu_baseline_batch(sample, seconds: float):
     """Oracle verify_batch (the dalek-equivalent restatement, single thread like dalek's
     verify_batch) on the same 10k batch, repeated for about ``seconds``."""
@@ -423,6 +462,9 @@ def main():
     ap.add_argument("--no-cert", action="store_true", help="skip the config-2 certificate leg")
     ap.add_argument("--no-batch", action="store_true", help="skip the config-1 verify_batch leg")
     ap.add_argument("--batch-many", type=int, default=64)
+    ap.add_argument("--no-wire", action="store_true", help="skip the wire-ingest leg")
+    ap.add_argument("--wire-frames", type=int, default=65536)
+    ap.add_argument("--wire-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -504,6 +546,11 @@ def main():
                 result["parity"] = "FAIL"
             if rank == 0 and world == 1 and not args.no_cpu_baseline:
                 r1["cpu_baseline"] = cpu_baseline_batch(bsample, min(5.0, args.cpu_seconds))
+        if not args.no_wire:
+            rw = run_wire(args, dev, stream, rank, world)
+            result["wire_ingest"] = rw
+            if rw["parity"] != "ok":
+                result["parity"] = "FAIL"
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             cb, agree = cpu_baseline_strict(sample, args.cpu_seconds)
             result["cpu_baseline"] = cb

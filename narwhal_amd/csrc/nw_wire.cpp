@@ -25,6 +25,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -81,40 +83,41 @@ int b64_value(uint8_t c) {
   return -1;
 }
 
-// base64 0.13 STANDARD decode of s[0..len) into out (cap bytes at least len * 3 / 4).
-bool b64_decode(const uint8_t* s, size_t len, std::vector<uint8_t>& out) {
+// base64 0.13 STANDARD decode of s[0..len): validates the whole string, keeps the first
+// 32 decoded bytes in out32 and returns the decoded length (-1 if invalid).
+long b64_decode32(const uint8_t* s, size_t len, uint8_t out32[32]) {
   size_t end = len;
   int pad = 0;
   while (end > 0 && s[end - 1] == '=' && pad < 2) {
     --end;
     ++pad;
   }
-  if (pad && (len % 4) != 0) return false;          // padded input comes in whole quads
-  if (end % 4 == 1) return false;                   // a lone trailing symbol
-  if (pad && (end % 4) + pad != 4) return false;    // padding must complete the last quad
-  out.clear();
+  if (pad && (len % 4) != 0) return -1;             // padded input comes in whole quads
+  if (end % 4 == 1) return -1;                      // a lone trailing symbol
+  if (pad && (end % 4) + pad != 4) return -1;       // padding must complete the last quad
   uint32_t acc = 0;
   int bits = 0;
+  long nout = 0;
   for (size_t i = 0; i < end; ++i) {
     const int v = b64_value(s[i]);
-    if (v < 0) return false;
+    if (v < 0) return -1;
     acc = (acc << 6) | (uint32_t)v;
     bits += 6;
     if (bits >= 8) {
       bits -= 8;
-      out.push_back((uint8_t)(acc >> bits));
+      if (nout < 32) out32[nout] = (uint8_t)(acc >> bits);
+      ++nout;
       acc &= (1u << bits) - 1;
     }
   }
-  return acc == 0;                                  // non-zero trailing bits rejected
+  return acc == 0 ? nout : -1;                      // non-zero trailing bits rejected
 }
 
-bool read_pk(Reader& r, uint8_t out[32], std::vector<uint8_t>& tmp) {
+bool read_pk(Reader& r, uint8_t out[32]) {
   const uint64_t L = r.len(1);
   const uint8_t* s = r.take(L);
   if (!r.ok) return false;
-  if (!b64_decode(s, L, tmp) || tmp.size() < 32) return (r.ok = false);
-  memcpy(out, tmp.data(), 32);
+  if (b64_decode32(s, L, out) < 32) return (r.ok = false);
   return true;
 }
 
@@ -132,49 +135,73 @@ struct HeaderSoA {
   size_t n() const { return payload_counts.size(); }
 };
 
-bool read_header(Reader& r, HeaderSoA& h, std::vector<uint8_t>& tmp) {
+// Per-thread scratch, reused across frames (no allocation on the steady path).
+struct Scratch {
+  std::vector<std::pair<Digest32, uint32_t>> pay, upay;
+  std::vector<Digest32> par;
+};
+
+// Appends one header to h only if it decodes completely.
+bool read_header(Reader& r, HeaderSoA& h, Scratch& sc) {
   uint8_t author[32];
-  if (!read_pk(r, author, tmp)) return false;
+  if (!read_pk(r, author)) return false;
   const uint64_t round = r.u64();
   const uint64_t np = r.len(36);
-  std::vector<std::pair<Digest32, uint32_t>> pay;
-  pay.reserve(np);
+  sc.pay.resize(np);
   for (uint64_t i = 0; i < np && r.ok; ++i) {
-    std::pair<Digest32, uint32_t> e;
-    r.raw(e.first.b, 32);
-    e.second = r.u32();
-    pay.push_back(e);
+    r.raw(sc.pay[i].first.b, 32);
+    sc.pay[i].second = r.u32();
   }
   const uint64_t nq = r.len(32);
-  std::vector<Digest32> par(nq);
-  for (uint64_t i = 0; i < nq && r.ok; ++i) r.raw(par[i].b, 32);
+  sc.par.resize(nq);
+  for (uint64_t i = 0; i < nq && r.ok; ++i) r.raw(sc.par[i].b, 32);
   uint8_t id[32], sig[64];
   r.raw(id, 32);
   r.raw(sig, 64);
   if (!r.ok) return false;
   // BTreeMap: sorted, duplicate keys keep the last value; BTreeSet: sorted, unique.
-  std::stable_sort(pay.begin(), pay.end(),
-                   [](const auto& a, const auto& b) { return a.first < b.first; });
-  std::vector<std::pair<Digest32, uint32_t>> upay;
+  auto& pay = sc.pay;
+  auto& upay = sc.upay;
+  auto key_less = [](const auto& x, const auto& y) { return x.first < y.first; };
+  if (!std::is_sorted(pay.begin(), pay.end(), key_less))   // wire order is usually sorted
+    std::stable_sort(pay.begin(), pay.end(), key_less);
+  upay.clear();
   for (size_t i = 0; i < pay.size(); ++i) {
     if (!upay.empty() && upay.back().first == pay[i].first) upay.back().second = pay[i].second;
     else upay.push_back(pay[i]);
   }
-  std::sort(par.begin(), par.end());
+  auto& par = sc.par;
+  if (!std::is_sorted(par.begin(), par.end())) std::sort(par.begin(), par.end());
   par.erase(std::unique(par.begin(), par.end()), par.end());
   auto& B = h.bytes;
-  B.insert(B.end(), author, author + 32);
-  for (int k = 0; k < 8; ++k) B.push_back((uint8_t)(round >> (8 * k)));
+  const size_t at = B.size();
+  B.resize(at + 40 + 36 * upay.size() + 32 * par.size());
+  uint8_t* o = B.data() + at;
+  memcpy(o, author, 32);
+  memcpy(o + 32, &round, 8);
+  o += 40;
   for (const auto& e : upay) {
-    B.insert(B.end(), e.first.b, e.first.b + 32);
-    for (int k = 0; k < 4; ++k) B.push_back((uint8_t)(e.second >> (8 * k)));
+    memcpy(o, e.first.b, 32);
+    memcpy(o + 32, &e.second, 4);
+    o += 36;
   }
-  for (const auto& d : par) B.insert(B.end(), d.b, d.b + 32);
+  for (const auto& d : par) {
+    memcpy(o, d.b, 32);
+    o += 32;
+  }
   h.offsets.push_back(B.size());
   h.payload_counts.push_back((uint32_t)upay.size());
   h.ids.insert(h.ids.end(), id, id + 32);
   h.sigs.insert(h.sigs.end(), sig, sig + 64);
   return true;
+}
+
+void pop_header(HeaderSoA& h) {
+  h.offsets.pop_back();
+  h.bytes.resize(h.offsets.back());
+  h.payload_counts.pop_back();
+  h.ids.resize(h.ids.size() - 32);
+  h.sigs.resize(h.sigs.size() - 64);
 }
 
 nw_certificates view(const HeaderSoA& h, const std::vector<uint64_t>* vote_offsets,
@@ -206,47 +233,44 @@ struct Decoded {
   std::vector<uint64_t> v_rounds;
 };
 
-void append_header(HeaderSoA& dst, const HeaderSoA& one) {
-  dst.bytes.insert(dst.bytes.end(), one.bytes.begin(), one.bytes.end());
-  dst.offsets.push_back(dst.bytes.size());
-  dst.payload_counts.push_back(one.payload_counts[0]);
-  dst.ids.insert(dst.ids.end(), one.ids.begin(), one.ids.end());
-  dst.sigs.insert(dst.sigs.end(), one.sigs.begin(), one.sigs.end());
-}
-
-// Decodes frame i; returns its NW_MSG_* kind or -1. counts (optional, 3 values): payload
-// entries and parents after BTreeMap/BTreeSet de-duplication, votes.
+// Decodes frame i into d; returns its NW_MSG_* kind or -1 (d unchanged then). counts
+// (optional, 3 values): payload entries and parents after BTreeMap/BTreeSet
+// de-duplication, votes.
 int32_t decode_frame(const uint8_t* f, size_t len, uint64_t i, Decoded& d, uint64_t* counts,
-                     std::vector<uint8_t>& tmp) {
+                     Scratch& sc) {
   Reader r{f, len};
   const uint32_t variant = r.u32();
   if (!r.ok || variant > NW_MSG_CERTIFICATES_REQUEST) return -1;
   if (counts) counts[0] = counts[1] = counts[2] = 0;
   if (variant == NW_MSG_HEADER || variant == NW_MSG_CERTIFICATE) {
-    HeaderSoA one;
-    if (!read_header(r, one, tmp)) return -1;
-    const uint64_t hl = one.bytes.size(), np = one.payload_counts[0];
+    HeaderSoA& h = variant == NW_MSG_HEADER ? d.hdr : d.cert;
+    if (!read_header(r, h, sc)) return -1;
+    const uint64_t hl = h.offsets.back() - h.offsets[h.offsets.size() - 2];
+    const uint64_t np = h.payload_counts.back();
     if (counts) {
       counts[0] = np;
       counts[1] = (hl - 40 - 36 * np) / 32;
     }
     if (variant == NW_MSG_HEADER) {
-      append_header(d.hdr, one);
       d.hdr_of.push_back(i);
       return NW_MSG_HEADER;
     }
     const uint64_t nv = r.len(72);   // each vote >= 8-byte length + 64-byte signature
-    if (!r.ok) return -1;
-    std::vector<uint8_t> pk(32 * nv), sg(64 * nv);
-    for (uint64_t v = 0; v < nv; ++v) {
-      if (!read_pk(r, &pk[32 * v], tmp)) return -1;
-      r.raw(&sg[64 * v], 64);
-      if (!r.ok) return -1;
+    const size_t pk0 = d.cvpk.size(), sg0 = d.cvsig.size();
+    if (r.ok) {
+      d.cvpk.resize(pk0 + 32 * nv);
+      d.cvsig.resize(sg0 + 64 * nv);
+      for (uint64_t v = 0; v < nv && r.ok; ++v) {
+        if (read_pk(r, &d.cvpk[pk0 + 32 * v])) r.raw(&d.cvsig[sg0 + 64 * v], 64);
+      }
+    }
+    if (!r.ok) {
+      pop_header(d.cert);
+      d.cvpk.resize(pk0);
+      d.cvsig.resize(sg0);
+      return -1;
     }
     if (counts) counts[2] = nv;
-    append_header(d.cert, one);
-    d.cvpk.insert(d.cvpk.end(), pk.begin(), pk.end());
-    d.cvsig.insert(d.cvsig.end(), sg.begin(), sg.end());
     d.cvo.push_back(d.cvo.back() + nv);
     d.cert_of.push_back(i);
     return NW_MSG_CERTIFICATE;
@@ -255,7 +279,7 @@ int32_t decode_frame(const uint8_t* f, size_t len, uint64_t i, Decoded& d, uint6
     uint8_t id[32], origin[32], author[32], sig[64];
     r.raw(id, 32);
     const uint64_t round = r.u64();
-    if (!r.ok || !read_pk(r, origin, tmp) || !read_pk(r, author, tmp)) return -1;
+    if (!r.ok || !read_pk(r, origin) || !read_pk(r, author)) return -1;
     r.raw(sig, 64);
     if (!r.ok) return -1;
     d.v_ids.insert(d.v_ids.end(), id, id + 32);
@@ -270,9 +294,65 @@ int32_t decode_frame(const uint8_t* f, size_t len, uint64_t i, Decoded& d, uint6
   const uint64_t nd = r.len(32);
   r.take(32 * nd);
   uint8_t pk[32];
-  if (!r.ok || !read_pk(r, pk, tmp)) return -1;
+  if (!r.ok || !read_pk(r, pk)) return -1;
   if (counts) counts[0] = nd;
   return NW_MSG_CERTIFICATES_REQUEST;
+}
+
+void merge_header(HeaderSoA& dst, const HeaderSoA& src) {
+  const uint64_t base = dst.bytes.size();
+  dst.bytes.insert(dst.bytes.end(), src.bytes.begin(), src.bytes.end());
+  for (size_t k = 1; k < src.offsets.size(); ++k) dst.offsets.push_back(base + src.offsets[k]);
+  dst.payload_counts.insert(dst.payload_counts.end(), src.payload_counts.begin(),
+                            src.payload_counts.end());
+  dst.ids.insert(dst.ids.end(), src.ids.begin(), src.ids.end());
+  dst.sigs.insert(dst.sigs.end(), src.sigs.begin(), src.sigs.end());
+}
+
+template <class T>
+void cat(std::vector<T>& dst, const std::vector<T>& src) {
+  dst.insert(dst.end(), src.begin(), src.end());
+}
+
+void merge(Decoded& d, const Decoded& s) {
+  merge_header(d.hdr, s.hdr);
+  merge_header(d.cert, s.cert);
+  cat(d.hdr_of, s.hdr_of);
+  cat(d.cert_of, s.cert_of);
+  cat(d.vote_of, s.vote_of);
+  const uint64_t vb = d.cvo.back();
+  for (size_t k = 1; k < s.cvo.size(); ++k) d.cvo.push_back(vb + s.cvo[k]);
+  cat(d.cvpk, s.cvpk);
+  cat(d.cvsig, s.cvsig);
+  cat(d.v_ids, s.v_ids);
+  cat(d.v_origins, s.v_origins);
+  cat(d.v_authors, s.v_authors);
+  cat(d.v_sigs, s.v_sigs);
+  cat(d.v_rounds, s.v_rounds);
+}
+
+// Decodes all frames, in parallel over contiguous ranges (host threads; the per-range
+// results are concatenated in frame order).
+void decode_all(const uint8_t* frames, const uint64_t* offsets, size_t n, Decoded& d,
+                int32_t* kind_out, uint64_t* counts_out) {
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const size_t T = std::min<size_t>({(size_t)std::min(hw, 16u), (n + 4095) / 4096, 64});
+  auto run = [&](size_t a, size_t b, Decoded& out) {
+    Scratch sc;
+    for (size_t i = a; i < b; ++i)
+      kind_out[i] = decode_frame(frames + offsets[i], (size_t)(offsets[i + 1] - offsets[i]), i,
+                                 out, counts_out ? counts_out + 3 * i : nullptr, sc);
+  };
+  if (T <= 1) {
+    run(0, n, d);
+    return;
+  }
+  std::vector<Decoded> parts(T);
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < T; ++t)
+    th.emplace_back(run, n * t / T, n * (t + 1) / T, std::ref(parts[t]));
+  for (auto& x : th) x.join();
+  for (auto& p : parts) merge(d, p);
 }
 
 int check_frames(const uint8_t* frames, const uint64_t* offsets, size_t n) {
@@ -292,10 +372,7 @@ int nw_primary_messages_scan(const uint8_t* frames, const uint64_t* offsets, siz
   if (rc) return rc;
   if (n && !kind_out) return set_err(NW_E_INVALID_ARG, "null kind_out");
   Decoded d;
-  std::vector<uint8_t> tmp;
-  for (size_t i = 0; i < n; ++i)
-    kind_out[i] = decode_frame(frames + offsets[i], (size_t)(offsets[i + 1] - offsets[i]), i, d,
-                               counts_out ? counts_out + 3 * i : nullptr, tmp);
+  decode_all(frames, offsets, n, d, kind_out, counts_out);
   return 0;
 }
 
@@ -308,13 +385,12 @@ int nw_primary_messages_verify_wire(const nw_committee* committee, const uint8_t
   if (rc) return rc;
   if (n && !status_out) return set_err(NW_E_INVALID_ARG, "null status_out");
   Decoded d;
-  std::vector<uint8_t> tmp;
+  std::vector<int32_t> kinds(n);
+  decode_all(frames, offsets, n, d, kinds.data(), nullptr);
   for (size_t i = 0; i < n; ++i) {
-    const int32_t kind = decode_frame(frames + offsets[i], (size_t)(offsets[i + 1] - offsets[i]),
-                                      i, d, nullptr, tmp);
-    status_out[i] = kind < 0 ? NW_DAG_SERIALIZATION : 0;
+    status_out[i] = kinds[i] < 0 ? NW_DAG_SERIALIZATION : 0;
     if (index_out) index_out[i] = 0;
-    if (kind_out) kind_out[i] = kind;
+    if (kind_out) kind_out[i] = kinds[i];
   }
   std::vector<int32_t> st;
   std::vector<uint64_t> ix;

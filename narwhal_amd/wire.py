@@ -104,3 +104,34 @@ def scan(frames: Sequence[bytes] | tuple) -> tuple[np.ndarray, np.ndarray]:
     if rc < 0:
         raise _lib.EngineError(f"nw_primary_messages_scan: {_lib.E_NAMES.get(rc, rc)}")
     return kind[:n], counts[:n]
+
+
+def frames_from_stream(s: dict) -> tuple[np.ndarray, np.ndarray]:
+    """bincode PrimaryMessage::Certificate frames for an nw_certificates SoA stream (the
+    layout of narwhal_amd.workloads.certificate_stream / messages.pack_certificates)."""
+    hb = s["header_bytes"].tobytes()
+    ho, vo = s["header_offsets"], s["vote_offsets"]
+    pcs = s["payload_counts"]
+    ids, hs = s["ids"], s["header_sigs"]
+    vpk, vsg = s["vote_pks"], s["vote_sigs"]
+    tag = struct.pack("<I", MSG_CERTIFICATE)
+    pk_cache: dict[bytes, bytes] = {}
+
+    def pk(b: bytes) -> bytes:
+        e = pk_cache.get(b)
+        if e is None:
+            e = pk_cache[b] = _pk(PublicKey(b))
+        return e
+
+    frames = []
+    for i in range(len(ho) - 1):
+        h = hb[int(ho[i]):int(ho[i + 1])]
+        np_ = int(pcs[i])
+        parents = h[40 + 36 * np_:]
+        a, b = int(vo[i]), int(vo[i + 1])
+        frames.append(b"".join([
+            tag, pk(h[:32]), h[32:40], struct.pack("<Q", np_), h[40:40 + 36 * np_],
+            struct.pack("<Q", len(parents) // 32), parents, ids[i].tobytes(), hs[i].tobytes(),
+            struct.pack("<Q", b - a)] + [pk(vpk[j].tobytes()) + vsg[j].tobytes()
+                                          for j in range(a, b)]))
+    return frames_soa(frames)

@@ -1,0 +1,86 @@
+"""The worker's batch-digest path on the engine.
+
+``Processor.spawn`` mirrors ``worker::Processor::spawn`` (worker/src/processor.rs:21-57):
+receive a serialized ``WorkerMessage::Batch``, compute ``Digest(Sha512(batch)[..32])``,
+``store.write(digest, batch)``, then send
+``bincode::serialize(&WorkerPrimaryMessage::{OurBatch, OthersBatch}(digest, id))``
+(primary/src/primary.rs:51-56) to the primary. Same names, channel semantics and output
+bytes, so the reference's ``hash_and_store`` test (worker/src/tests/processor_tests.rs)
+reads the same (tests/test_worker.py).
+
+The difference is where the hash runs and how batches overlap: the reference hashes one
+batch at a time on the tokio thread. Here every batch is handed to the aggregating
+``VerificationService`` as soon as it arrives (several batches in flight share one
+SHA-512 device job), while a writer task stores and announces the digests strictly in
+arrival order — the store write of one batch overlaps the hashing of the next.
+"""
+from __future__ import annotations
+
+import asyncio
+import struct
+
+from .service import VerificationService
+
+__all__ = ["Store", "Processor", "our_batch_message", "others_batch_message"]
+
+_OUR_BATCH, _OTHERS_BATCH = 0, 1
+
+
+def our_batch_message(digest: bytes, worker_id: int) -> bytes:
+    """bincode::serialize(&WorkerPrimaryMessage::OurBatch(digest, id))."""
+    return struct.pack("<I", _OUR_BATCH) + bytes(digest) + struct.pack("<I", worker_id)
+
+
+def others_batch_message(digest: bytes, worker_id: int) -> bytes:
+    """bincode::serialize(&WorkerPrimaryMessage::OthersBatch(digest, id))."""
+    return struct.pack("<I", _OTHERS_BATCH) + bytes(digest) + struct.pack("<I", worker_id)
+
+
+class Store:
+    """In-memory stand-in for store::Store (store/src/lib.rs: RocksDB behind a channel;
+    storage is out of scope here): async write / read of byte keys and values."""
+
+    def __init__(self):
+        self._kv: dict[bytes, bytes] = {}
+
+    async def write(self, key: bytes, value: bytes) -> None:
+        self._kv[bytes(key)] = bytes(value)
+
+    async def read(self, key: bytes) -> bytes | None:
+        return self._kv.get(bytes(key))
+
+
+class Processor:
+    """worker::Processor: hashes and stores batches, then outputs the batch's digest."""
+
+    @staticmethod
+    def spawn(worker_id: int, store: Store, rx_batch: asyncio.Queue, tx_digest: asyncio.Queue,
+              own_digest: bool, service: VerificationService) -> asyncio.Task:
+        """Runs until ``rx_batch`` yields None (the reference's closed channel)."""
+        pending: asyncio.Queue = asyncio.Queue()
+
+        async def hash_loop():
+            while True:
+                batch = await rx_batch.get()
+                if batch is None:
+                    await pending.put(None)
+                    return
+                # hashing starts now; results are consumed in arrival order below
+                await pending.put((batch, asyncio.ensure_future(service.digest(batch))))
+
+        async def deliver_loop():
+            while True:
+                item = await pending.get()
+                if item is None:
+                    return
+                batch, fut = item
+                digest = await fut
+                await store.write(digest, batch)
+                msg = (our_batch_message if own_digest else others_batch_message)(digest,
+                                                                                   worker_id)
+                await tx_digest.put(msg)
+
+        async def run():
+            await asyncio.gather(hash_loop(), deliver_loop())
+
+        return asyncio.ensure_future(run())

@@ -265,3 +265,19 @@ def test_verify_wire_vs_oracle():
             exp_st[i] = e
     bad = [(i, int(a), int(b)) for i, (a, b) in enumerate(zip(st, exp_st)) if a != b]
     assert not bad, bad
+
+
+def test_frames_from_stream_round_trip():
+    """The bench's frame builder (wire.frames_from_stream) against the restatement."""
+    from narwhal_amd import workloads as W
+    from cert_cases import oracle_digest_many, oracle_sign_many
+    keys = O.keys(4)
+    s = W.certificate_stream(10, keys, oracle_sign_many, oracle_digest_many, payload=2, seed=1)
+    data, offs = WI.frames_from_stream(s)
+    recs = unpack(s)
+    b = data.tobytes()
+    for i, r in enumerate(recs):
+        k, d = ref_decode(b[int(offs[i]):int(offs[i + 1])])
+        assert k == 2 and d["hb"] == r["hb"] and d["id"] == r["id"] and d["votes"] == r["votes"]
+    kind, counts = WI.scan((data, offs))
+    assert (kind == 2).all() and counts[:, 0].tolist() == [2] * 10

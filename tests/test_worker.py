@@ -1,0 +1,70 @@
+"""worker::Processor on the engine (narwhal_amd/worker.py), read like the reference's
+worker/src/tests/processor_tests.rs::hash_and_store: send WorkerMessage::Batch(batch()),
+expect bincode(WorkerPrimaryMessage::OurBatch(Sha512(serialized)[..32], id)) out and the
+batch in the store under its digest. The reference fixture digest is also SURVEY
+Appendix B's (JNAPdKB2...). CPU: a test-only oracle backend; GPU: the real jobs."""
+import asyncio
+import base64
+import hashlib
+import struct
+
+import pytest
+
+from narwhal_amd import workloads as W
+from narwhal_amd.service import VerificationService
+from narwhal_amd.worker import Processor, Store, our_batch_message
+
+from test_service import _OracleBackend
+
+
+def _run(backend, batches, own=True, worker_id=0):
+    async def main():
+        svc = VerificationService(backend=backend, max_delay=0.001)
+        store = Store()
+        rx, tx = asyncio.Queue(), asyncio.Queue()
+        task = Processor.spawn(worker_id, store, rx, tx, own, svc)
+        for b in batches:
+            await rx.put(b)
+        await rx.put(None)
+        await task
+        out = []
+        while not tx.empty():
+            out.append(tx.get_nowait())
+        stored = [await store.read(hashlib.sha512(b).digest()[:32]) for b in batches]
+        return out, stored, svc.jobs_submitted
+    return asyncio.run(main())
+
+
+def _expect(batches, own=True, worker_id=0):
+    return [struct.pack("<I", 0 if own else 1) + hashlib.sha512(b).digest()[:32]
+            + struct.pack("<I", worker_id) for b in batches]
+
+
+APPENDIX_B_BATCH_DIGEST = "JNAPdKB2fnSAjIVGYwkClyhT+iAOB55YK4t73s1zMdg="
+
+
+def test_hash_and_store_reference_fixture():
+    serialized = W.reference_serialized_batch()
+    out, stored, _ = _run(_OracleBackend(), [serialized])
+    digest = hashlib.sha512(serialized).digest()[:32]
+    assert out == [our_batch_message(digest, 0)]
+    assert stored == [serialized]
+    assert base64.b64encode(digest).decode() == APPENDIX_B_BATCH_DIGEST
+
+
+def test_order_preserved_and_batches_share_jobs():
+    batches = [W.serialize_batch([bytes([i]) * (50 + 13 * j) for j in range(i % 5 + 1)])
+               for i in range(40)]
+    out, stored, jobs = _run(_OracleBackend(), batches, own=False, worker_id=3)
+    assert out == _expect(batches, own=False, worker_id=3)
+    assert stored == batches
+    assert jobs < len(batches)
+
+
+@pytest.mark.gpu
+def test_processor_on_gpu():
+    batches = [W.worker_batch(i, seed=4).tobytes() for i in range(6)] + \
+              [W.reference_serialized_batch()]
+    out, stored, _ = _run(None, batches)
+    assert out == _expect(batches)
+    assert stored == batches
