@@ -33,6 +33,9 @@ struct DevCtx {
   void* dbuf = nullptr;
   size_t dcap = 0;
   void* strict_ws = nullptr;   // per-lane tables of k_verify_strict (fixed size)
+  void* ktabs = nullptr;       // committee key tables (grow-only)
+  uint32_t* kok = nullptr;
+  size_t kcap = 0;             // keys
 };
 
 struct ThreadState {
@@ -45,6 +48,8 @@ struct ThreadState {
         (void)hipSetDevice(g_dev_ids[i]);
         if (ctx[i].dbuf) (void)hipFree(ctx[i].dbuf);
         if (ctx[i].strict_ws) (void)hipFree(ctx[i].strict_ws);
+        if (ctx[i].ktabs) (void)hipFree(ctx[i].ktabs);
+        if (ctx[i].kok) (void)hipFree(ctx[i].kok);
         if (ctx[i].stream) (void)hipStreamDestroy(ctx[i].stream);
       }
     }
@@ -138,6 +143,23 @@ int strict_ws(DevCtx& c, void** out) {
     }
   }
   *out = c.strict_ws;
+  return 0;
+}
+
+// Committee key tables for nkeys keys (grow-only, per thread and device).
+int key_tables(DevCtx& c, size_t nkeys) {
+  if (nkeys <= c.kcap && c.ktabs) return 0;
+  (void)hipStreamSynchronize(c.stream);
+  if (c.ktabs) (void)hipFree(c.ktabs);
+  if (c.kok) (void)hipFree(c.kok);
+  c.ktabs = nullptr;
+  c.kok = nullptr;
+  c.kcap = 0;
+  const size_t cap = nkeys < 256 ? 256 : nkeys;
+  hipError_t e = hipMalloc(&c.ktabs, nw::key_tables_bytes(cap));
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c.kok), 4 * cap);
+  if (e != hipSuccess) return set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (key tables)", e);
+  c.kcap = cap;
   return 0;
 }
 
@@ -383,16 +405,18 @@ struct CertWs {
   int32_t *pre1, *pre2, *hdr_st, *batch_st;
   uint64_t *idx1, *idx2, *batch_idx, *bitmap;
   void* batch_ws;
+  uint32_t* vote_key;
 };
 
 size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
   const size_t m = n ? n : 1;
-  const size_t sizes[12] = {a256(32 * m), a256(32 * m), a256(32 * m), a256(4 * m), a256(4 * m),
+  const size_t sizes[13] = {a256(32 * m), a256(32 * m), a256(32 * m), a256(4 * m), a256(4 * m),
                             a256(4 * m),  a256(4 * m),  a256(8 * m),  a256(8 * m), a256(8 * m),
                             a256(8 * ((m + 63) / 64)),
-                            nvotes ? a256(nw::batch_workspace_bytes(n, nvotes)) : 256};
-  size_t off[12], tot = 0;
-  for (int k = 0; k < 12; ++k) { off[k] = tot; tot += sizes[k]; }
+                            nvotes ? a256(nw::batch_workspace_bytes(n, nvotes)) : 256,
+                            a256(4 * (nvotes ? nvotes : 1))};
+  size_t off[13], tot = 0;
+  for (int k = 0; k < 13; ++k) { off[k] = tot; tot += sizes[k]; }
   if (w) {
     w->hdr_digest = reinterpret_cast<uint32_t*>(base + off[0]);
     w->authors = reinterpret_cast<uint32_t*>(base + off[1]);
@@ -406,6 +430,7 @@ size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
     w->batch_idx = reinterpret_cast<uint64_t*>(base + off[9]);
     w->bitmap = reinterpret_cast<uint64_t*>(base + off[10]);
     w->batch_ws = base + off[11];
+    w->vote_key = reinterpret_cast<uint32_t*>(base + off[12]);
   }
   return tot;
 }
@@ -427,19 +452,30 @@ int cert_pipeline(DevCtx& ctx, const nw_committee& com, const nw_certificates& c
   NW_HIP(nw::launch_sha512_digest32(cs.header_bytes, cs.header_offsets, nullptr, n,
                                     w.hdr_digest, s), "k_sha512 (header digests)");
   NW_HIP(nw::launch_cert_prepare(dc, ds, headers_only, w.hdr_digest, w.authors, w.cert_digest,
-                                 w.pre1, w.pre2, w.idx1, w.idx2, s), "k_cert_prepare");
+                                 w.pre1, w.pre2, w.idx1, w.idx2,
+                                 headers_only ? nullptr : w.vote_key, s), "k_cert_prepare");
   void* sws;
   int rc = strict_ws(ctx, &sws);
   if (rc) return rc;
   NW_HIP(nw::launch_verify_strict(reinterpret_cast<const uint32_t*>(cs.ids), 8, w.authors,
                                   reinterpret_cast<const uint32_t*>(cs.header_sigs), n, w.hdr_st,
                                   w.bitmap, sws, s), "k_verify_strict (headers)");
-  if (!headers_only)
+  if (!headers_only) {
+    // Every vote that can decide a verdict is by a committee member (k_cert_prepare fails
+    // the certificate first otherwise), so the committee's keys are decompressed once per
+    // call and their tables reused by every vote, instead of once per vote.
+    rc = key_tables(ctx, com.nauth);
+    if (rc) return rc;
+    NW_HIP(nw::launch_key_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth,
+                                 static_cast<nw::ge_cached*>(ctx.ktabs), ctx.kok, s),
+           "k_key_tables");
+    const nw::key_tables_t kt{static_cast<const nw::ge_cached*>(ctx.ktabs), ctx.kok, w.vote_key};
     NW_HIP(nw::launch_verify_batch(w.cert_digest, cs.vote_offsets, host_vote_offsets, n,
                                    reinterpret_cast<const uint32_t*>(cs.vote_pks),
                                    reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
                                    static_cast<const uint32_t*>(z16), key, w.batch_ws,
-                                   w.batch_st, w.batch_idx, s), "verify_batch (votes)");
+                                   w.batch_st, w.batch_idx, s, &kt), "verify_batch (votes)");
+  }
   NW_HIP(nw::launch_cert_finalize(n, headers_only, w.pre1, w.pre2, w.idx1, w.idx2, w.hdr_st,
                                   w.batch_st, w.batch_idx, status, index, s), "k_cert_finalize");
   return 0;
@@ -685,6 +721,23 @@ int select_device(int* dev_index) {
 }
 
 int set_err(int code, const char* what, hipError_t e) { return ::set_err(code, what, e); }
+
+// Committee key tables for nkeys keys (grow-only, per thread and device).
+int key_tables(DevCtx& c, size_t nkeys) {
+  if (nkeys <= c.kcap && c.ktabs) return 0;
+  (void)hipStreamSynchronize(c.stream);
+  if (c.ktabs) (void)hipFree(c.ktabs);
+  if (c.kok) (void)hipFree(c.kok);
+  c.ktabs = nullptr;
+  c.kok = nullptr;
+  c.kcap = 0;
+  const size_t cap = nkeys < 256 ? 256 : nkeys;
+  hipError_t e = hipMalloc(&c.ktabs, nw::key_tables_bytes(cap));
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c.kok), 4 * cap);
+  if (e != hipSuccess) return set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (key tables)", e);
+  c.kcap = cap;
+  return 0;
+}
 
 int os_random(void* buf, size_t n) { return ::os_random(buf, n); }
 

@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256) void k_bv_items(
     const uint32_t* __restrict__ digests, const uint64_t* __restrict__ offsets, uint64_t b0,
     uint64_t b1, uint64_t i0, uint64_t i1, const uint32_t* __restrict__ pks,
     const uint32_t* __restrict__ sigs, const uint32_t* __restrict__ z16, z_key_t zkey,
-    bv_item* __restrict__ items, ge_cached* __restrict__ tabs) {
+    bv_item* __restrict__ items, ge_cached* __restrict__ tabs, key_tables_t keys) {
   const uint64_t gi = i0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gi >= i1) return;
   const uint64_t li = gi - i0;
@@ -274,14 +274,22 @@ __global__ __launch_bounds__(256) void k_bv_items(
 
   ge P;
   ge_cached* tA = tabs + 16 * li;
-  if (!ge_frombytes(P, Aw, K)) flags |= BF_A_DECODE;
-  it.flags = flags;   // (R decode flag added below)
-  // tables j*P, j = 1..8 (cached form)
+  // A: the caller's pre-decompressed key table when this vote's key has one, else here
+  const uint32_t kk = keys.vote_key ? keys.vote_key[gi] : kNoKey;
+  if (kk != kNoKey) {
+    if (!keys.ok[kk]) flags |= BF_A_DECODE;
 #pragma unroll 1
-  for (int which = 0; which < 2; ++which) {
+    for (int j = 0; j < 8; ++j) tA[j] = keys.tabs[8 * (uint64_t)kk + j];
+  } else if (!ge_frombytes(P, Aw, K)) {
+    flags |= BF_A_DECODE;
+  }
+  it.flags = flags;   // (R decode flag added below)
+  // tables j*P, j = 1..8 (cached form): A (unless given), then R
+#pragma unroll 1
+  for (int which = kk != kNoKey ? 1 : 0; which < 2; ++which) {
     if (which == 1) {
       if (!ge_frombytes(P, Rw, K)) flags |= BF_R_DECODE;
-      tA += 8;
+      tA = tabs + 16 * li + 8;
     }
     ge_cached c1;
     ge_to_cached(c1, P, K.d2);
@@ -513,11 +521,52 @@ size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems) {
   return bv_layout(std::min<uint64_t>(nitems + nbatches, slice_units()), nullptr, nullptr);
 }
 
+// One lane per key: decompress (dalek semantics) and build j*A, j = 1..8 (cached form).
+__global__ __launch_bounds__(256) void k_key_tables(const uint32_t* __restrict__ pks,
+                                                    uint64_t nkeys, ge_cached* __restrict__ tabs,
+                                                    uint32_t* __restrict__ ok) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nkeys) return;
+  const curve_consts& K = g_bc.k;
+  uint32_t Aw[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) Aw[j] = pks[8 * i + j];
+  ge P;
+  ok[i] = ge_frombytes(P, Aw, K) ? 1u : 0u;
+  ge_cached* t = tabs + 8 * i;
+  ge_cached c1;
+  ge_to_cached(c1, P, K.d2);
+  t[0] = c1;
+  ge acc;
+  ge_dbl(acc, P, true);
+  ge_cached cj;
+  ge_to_cached(cj, acc, K.d2);
+  t[1] = cj;
+#pragma unroll 1
+  for (int j = 3; j <= 8; ++j) {
+    ge_add_cached(acc, acc, c1, true);
+    ge_to_cached(cj, acc, K.d2);
+    t[j - 1] = cj;
+  }
+}
+
+size_t key_tables_bytes(uint64_t nkeys) { return sizeof(ge_cached) * 8 * (nkeys ? nkeys : 1); }
+
+hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, ge_cached* tabs, uint32_t* ok,
+                             hipStream_t stream) {
+  if (nkeys == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_key_tables, dim3((unsigned)((nkeys + 255) / 256)), dim3(256), 0, stream,
+                     pks, nkeys, tabs, ok);
+  return hipGetLastError();
+}
+
 hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                const uint64_t* host_offsets, uint64_t nbatches,
                                const uint32_t* pks, const uint32_t* sigs, uint64_t nitems,
                                const uint32_t* z16, const z_key_t& zkey, void* workspace,
-                               int32_t* status, uint64_t* fail_index, hipStream_t stream) {
+                               int32_t* status, uint64_t* fail_index, hipStream_t stream,
+                               const key_tables_t* keys) {
+  const key_tables_t kt = keys ? *keys : key_tables_t{nullptr, nullptr, nullptr};
   if (nbatches == 0) return hipSuccess;
   const uint64_t cap = std::min<uint64_t>(nitems + nbatches, slice_units());
   bv_ws w;
@@ -550,7 +599,7 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
     if (i1 > i0)
       hipLaunchKernelGGL(k_bv_items, dim3((unsigned)((i1 - i0 + 255) / 256)), dim3(256), 0,
                          stream, digests, offsets, b, e, i0, i1, pks, sigs, z16, zkey, w.items,
-                         w.tabs);
+                         w.tabs, kt);
     if (chunks)
       hipLaunchKernelGGL(k_bv_chunks, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
                          stream, w.chunks, (uint32_t)chunks, offsets, b, i0, w.items, w.tabs,

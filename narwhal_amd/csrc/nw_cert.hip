@@ -83,7 +83,8 @@ __global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com, cert
                                                       int32_t* __restrict__ pre1,
                                                       int32_t* __restrict__ pre2,
                                                       uint64_t* __restrict__ idx1,
-                                                      uint64_t* __restrict__ idx2) {
+                                                      uint64_t* __restrict__ idx2,
+                                                      uint32_t* __restrict__ vote_key) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cs.n) return;
   const uint8_t* h = cs.header_bytes + cs.header_offsets[i];
@@ -133,6 +134,10 @@ __global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com, cert
     for (uint64_t q = 0; q < com.nauth; ++q) total += com.stakes[q];
     const uint32_t quorum = 2u * total / 3u + 1u;
     const uint64_t vb = cs.vote_offsets[i], ve = cs.vote_offsets[i + 1];
+    // committee index of each vote's key (for the batch's pre-decompressed key tables);
+    // votes the loop below does not reach keep kNoKey (decompressed in the batch kernel)
+    if (vote_key)
+      for (uint64_t v = vb; v < ve; ++v) vote_key[v] = kNoKey;
     uint32_t weight = 0;
     for (uint64_t v = vb; v < ve && p2 == 0; ++v) {
       uint32_t pk[8];
@@ -146,7 +151,9 @@ __global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com, cert
         reuse = eq;
       }
       if (reuse) { p2 = NW_DAG_AUTHORITY_REUSE; x2 = v - vb; break; }
-      const uint32_t st = committee_stake(com, committee_find(com, pk));
+      const int av = committee_find(com, pk);
+      if (vote_key && av >= 0) vote_key[v] = (uint32_t)av;
+      const uint32_t st = committee_stake(com, av);
       if (st == 0) { p2 = NW_DAG_UNKNOWN_AUTHORITY; x2 = v - vb; break; }
       weight += st;
     }
@@ -229,10 +236,12 @@ static inline unsigned blocks_for(uint64_t n) { return (unsigned)((n + 255) / 25
 hipError_t launch_cert_prepare(const cert_committee_t& com, const cert_stream_t& cs,
                                int headers_only, const uint32_t* hdr_digest, uint32_t* authors,
                                uint32_t* cert_digest, int32_t* pre1, int32_t* pre2,
-                               uint64_t* idx1, uint64_t* idx2, hipStream_t stream) {
+                               uint64_t* idx1, uint64_t* idx2, uint32_t* vote_key,
+                               hipStream_t stream) {
   if (cs.n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_cert_prepare, dim3(blocks_for(cs.n)), dim3(256), 0, stream, com, cs,
-                     headers_only, hdr_digest, authors, cert_digest, pre1, pre2, idx1, idx2);
+                     headers_only, hdr_digest, authors, cert_digest, pre1, pre2, idx1, idx2,
+                     vote_key);
   return hipGetLastError();
 }
 

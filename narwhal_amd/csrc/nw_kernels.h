@@ -40,12 +40,28 @@ hipError_t launch_sign(const uint32_t* sks, uint32_t sk_stride_words, const uint
 // host_offsets: the same nbatches + 1 values in host memory (used to plan the chunks and
 // the workspace slices).
 hipError_t upload_batch_consts();
+
+// Pre-decompressed public keys (a committee): per key its 8-entry table j*A (j = 1..8,
+// cached form) and whether it decompressed. vote_key[i] = key index of vote i, or
+// kNoKey to decompress that vote's key in the kernel (the verdict semantics are
+// unchanged: a key's decompression is deterministic).
+struct key_tables_t {
+  const struct ge_cached* tabs;   // nkeys x 8
+  const uint32_t* ok;             // nkeys
+  const uint32_t* vote_key;       // nitems (global item index)
+};
+constexpr uint32_t kNoKey = 0xffffffffu;
+size_t key_tables_bytes(uint64_t nkeys);
+// tabs: key_tables_bytes(nkeys) of device memory; ok: nkeys words.
+hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, struct ge_cached* tabs,
+                             uint32_t* ok, hipStream_t stream);
 size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems);
 hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                const uint64_t* host_offsets, uint64_t nbatches,
                                const uint32_t* pks, const uint32_t* sigs, uint64_t nitems,
                                const uint32_t* z16, const z_key_t& zkey, void* workspace,
-                               int32_t* status, uint64_t* fail_index, hipStream_t stream);
+                               int32_t* status, uint64_t* fail_index, hipStream_t stream,
+                               const key_tables_t* keys = nullptr);
 
 // ---- primary messages (nw_cert.hip) ----------------------------------------------------
 struct cert_committee_t {
@@ -69,7 +85,8 @@ struct cert_stream_t {
 hipError_t launch_cert_prepare(const cert_committee_t& com, const cert_stream_t& cs,
                                int headers_only, const uint32_t* hdr_digest, uint32_t* authors,
                                uint32_t* cert_digest, int32_t* pre1, int32_t* pre2,
-                               uint64_t* idx1, uint64_t* idx2, hipStream_t stream);
+                               uint64_t* idx1, uint64_t* idx2, uint32_t* vote_key,
+                               hipStream_t stream);
 hipError_t launch_cert_finalize(uint64_t n, int headers_only, const int32_t* pre1,
                                 const int32_t* pre2, const uint64_t* idx1, const uint64_t* idx2,
                                 const int32_t* hdr_status, const int32_t* batch_status,
