@@ -722,23 +722,6 @@ int select_device(int* dev_index) {
 
 int set_err(int code, const char* what, hipError_t e) { return ::set_err(code, what, e); }
 
-// Committee key tables for nkeys keys (grow-only, per thread and device).
-int key_tables(DevCtx& c, size_t nkeys) {
-  if (nkeys <= c.kcap && c.ktabs) return 0;
-  (void)hipStreamSynchronize(c.stream);
-  if (c.ktabs) (void)hipFree(c.ktabs);
-  if (c.kok) (void)hipFree(c.kok);
-  c.ktabs = nullptr;
-  c.kok = nullptr;
-  c.kcap = 0;
-  const size_t cap = nkeys < 256 ? 256 : nkeys;
-  hipError_t e = hipMalloc(&c.ktabs, nw::key_tables_bytes(cap));
-  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c.kok), 4 * cap);
-  if (e != hipSuccess) return set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (key tables)", e);
-  c.kcap = cap;
-  return 0;
-}
-
 int os_random(void* buf, size_t n) { return ::os_random(buf, n); }
 
 }  // namespace rt

@@ -26,6 +26,7 @@
 #include "nw_sha512.hpp"
 #include "nw_ladder.hpp"
 #include "nw_consts.hpp"
+#include "nw_strict.hpp"
 
 #include <stdlib.h>
 
@@ -39,7 +40,8 @@ namespace {
 
 struct batch_consts {
   curve_consts k;
-  ge_niels btab[129];
+  ge_niels btab[129];   // j * B
+  ge_niels b128[129];   // j * 2^128 B (short ladders of keyed chunks)
 };
 __constant__ batch_consts g_bc;
 
@@ -57,13 +59,16 @@ uint64_t env_u64(const char* name, uint64_t dflt) {
 uint64_t slice_units() { return env_u64("NW_BATCH_SLICE_UNITS", kSliceUnits); }
 constexpr uint32_t kMaxChunk = 128;
 constexpr uint32_t kNone = 0xffffffffu;
+constexpr uint32_t kKeyTab = 258;   // entries per caller key table (j*A, j*2^128 A, j = 0..128)
 
 // Per-vote record written by k_bv_items (96 bytes).
 struct bv_item {
-  uint32_t c[8];     // c_i + 0x88..8: signed 4-bit digits of z_i k_i mod l
+  uint32_t c[8];     // c_i = z_i k_i mod l, recoded: + 0x88..8 (signed 4-bit digits), or
+                     // for a keyed vote + 0x80..80 (signed 8-bit digits, 16 low + 16 high)
   uint32_t z[5];     // z_i + 0x88..8 (33 digits)
   uint32_t flags;    // BF_* (check FAILED)
-  uint32_t pad[2];
+  uint32_t key;      // key-table index of A_i, or kNoKey
+  uint32_t pad;
   uint32_t b[8];     // z_i s_i mod l
 };
 
@@ -263,8 +268,11 @@ __global__ __launch_bounds__(256) void k_bv_items(
     for (int j = 0; j < 8; ++j) s.w[j] = 0;   // verdict is decided by the flags
   }
   sc_mul(b, z, s);
+  const uint32_t kk = keys.vote_key ? keys.vote_key[gi] : kNoKey;
   bv_item it;
-  sc_recode(it.c, c, 0x88888888u);
+  sc_recode(it.c, c, kk != kNoKey ? 0x80808080u : 0x88888888u);
+  it.key = kk;
+  it.pad = 0;
   uint32_t zr[8];
   sc_recode(zr, z, 0x88888888u);
 #pragma unroll
@@ -274,17 +282,15 @@ __global__ __launch_bounds__(256) void k_bv_items(
 
   ge P;
   ge_cached* tA = tabs + 16 * li;
-  // A: the caller's pre-decompressed key table when this vote's key has one, else here
-  const uint32_t kk = keys.vote_key ? keys.vote_key[gi] : kNoKey;
+  // A: the caller's pre-decompressed key tables when this vote's key has them (read by
+  // k_bv_chunks directly), else decompressed and tabulated here
   if (kk != kNoKey) {
     if (!keys.ok[kk]) flags |= BF_A_DECODE;
-#pragma unroll 1
-    for (int j = 0; j < 8; ++j) tA[j] = keys.tabs[8 * (uint64_t)kk + j];
   } else if (!ge_frombytes(P, Aw, K)) {
     flags |= BF_A_DECODE;
   }
   it.flags = flags;   // (R decode flag added below)
-  // tables j*P, j = 1..8 (cached form): A (unless given), then R
+  // tables j*P, j = 1..8 (cached form): A (unless keyed), then R
 #pragma unroll 1
   for (int which = kk != kNoKey ? 1 : 0; which < 2; ++which) {
     if (which == 1) {
@@ -307,7 +313,6 @@ __global__ __launch_bounds__(256) void k_bv_items(
     }
   }
   it.flags = flags;
-  it.pad[0] = it.pad[1] = 0;
   items[li] = it;
 }
 
@@ -339,24 +344,67 @@ __device__ __forceinline__ int batch_status(const uint32_t first[3], uint32_t fl
   return identity ? NW_OK : NW_ERR_EQUATION;
 }
 
+__device__ __forceinline__ int wave_max_int(int w) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int x = __shfl_xor(w, o);
+    w = x > w ? x : w;
+  }
+  return __builtin_amdgcn_readfirstlane(w);
+}
+
+// Signed 8-bit digit m (0..31) of a 256-bit value recoded with + 0x80..80.
+__device__ __forceinline__ int digit8(const uint32_t* w, int m) {
+  return (int)((sel8(w, m >> 2) >> ((m & 3) * 8)) & 255u) - 128;
+}
+
+// Keyed vote: A's digit from its key table (129 entries j*A or j*2^128 A, cached form).
+__device__ __forceinline__ void add_key_entry(ge& acc, const ge_cached* tab129, int d) {
+  if (d != 0) {
+    ge_cached e = tab129[d < 0 ? -d : d];
+    ge_cached_cneg(e, d < 0);
+    ge_add_cached(acc, acc, e, true);
+  }
+}
+
+// One lane per chunk: the Straus ladder shared by the chunk's votes and B.
+//   unkeyed chunk: 64 windows of 4 bits (252 doublings); c_i by 4-bit digits over the vote's
+//     own j*A_i table, z_i by 4-bit digits over j*R_i, -sum b by 8-bit digits over j*B;
+//   keyed chunk (every A_i has caller key tables j*A, j*2^128 A): 33 windows (128
+//     doublings); c_i = c_lo + 2^128 c_hi by 8-bit digits over the two key tables, z_i as
+//     before, -sum b = b_lo + 2^128 b_hi by 8-bit digits over j*B and j*2^128 B.
+// A lane whose chunk is keyed simply has no digits above window 32 when the wave runs the
+// long ladder for another lane (the identity doubles to itself).
 __global__ __launch_bounds__(256) void k_bv_chunks(
     const bv_chunk* __restrict__ chunks, uint32_t nchunks, const uint64_t* __restrict__ offsets,
     uint64_t b0, uint64_t i0, const bv_item* __restrict__ items,
-    const ge_cached* __restrict__ tabs, bv_chunk_out* __restrict__ out,
-    int32_t* __restrict__ status, uint64_t* __restrict__ fail_index) {
+    const ge_cached* __restrict__ tabs, const ge_cached* __restrict__ ktabs,
+    bv_chunk_out* __restrict__ out, int32_t* __restrict__ status,
+    uint64_t* __restrict__ fail_index) {
   __shared__ ge_niels s_btab[129];
-  load_btab(s_btab);
+  __shared__ ge_niels s_b128[129];
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&g_bc.btab[0]);
+    const uint32_t* src2 = reinterpret_cast<const uint32_t*>(&g_bc.b128[0]);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(s_btab);
+    uint32_t* dst2 = reinterpret_cast<uint32_t*>(s_b128);
+    for (int i = threadIdx.x; i < BT_WORDS; i += blockDim.x) {
+      dst[i] = src[i];
+      dst2[i] = src2[i];
+    }
+  }
   __syncthreads();
   const uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ci >= nchunks) return;
-  const bv_chunk ch = chunks[ci];
+  const bool live = ci < nchunks;
+  const bv_chunk ch = chunks[live ? ci : nchunks - 1];
   const uint64_t bidx = b0 + ch.batch;
   const uint64_t bstart = offsets[bidx];
   const uint64_t bn = offsets[bidx + 1] - bstart;
   const uint64_t l0 = ch.start - i0;
-  // first failures and sum of b_i over the chunk
+  // first failures, sum of b_i over the chunk, and whether every vote is keyed
   uint32_t first[3] = {kNone, kNone, kNone};
   uint32_t flags0 = 0;
+  bool keyed = ktabs != nullptr;
   sc bsum;
 #pragma unroll
   for (int j = 0; j < 8; ++j) bsum.w[j] = 0;
@@ -367,6 +415,7 @@ __global__ __launch_bounds__(256) void k_bv_chunks(
     if ((f & (BF_S_HIGH | BF_A_DECODE)) && first[0] == kNone) { first[0] = rel; flags0 = f; }
     if ((f & BF_S_NONCANON) && first[1] == kNone) first[1] = rel;
     if ((f & BF_R_DECODE) && first[2] == kNone) first[2] = rel;
+    keyed &= it->key != kNone;
     sc bi;
 #pragma unroll
     for (int j = 0; j < 8; ++j) bi.w[j] = it->b[j];
@@ -376,28 +425,47 @@ __global__ __launch_bounds__(256) void k_bv_chunks(
   sc_neg(nb, bsum);
   uint32_t bb[8];
   sc_recode(bb, nb, 0x80808080u);
+  // an unkeyed chunk among keyed ones cannot read key tables; a keyed one needs no
+  // 4-bit A digits (its c words hold 8-bit digits)
+  const int W = wave_max_int(live ? (keyed ? 33 : 64) : 0);
 
   ge acc;
   ge_identity(acc);
 #pragma unroll 1
-  for (int j = 63; j >= 0; --j) {
-    if (j != 63) {
+  for (int j = W - 1; j >= 0; --j) {
+    if (j != W - 1) {
 #pragma unroll 1
       for (int t = 0; t < 3; ++t) ge_dbl(acc, acc, false);
       ge_dbl(acc, acc, true);
     }
+    if (!live) continue;
 #pragma unroll 1
     for (uint32_t t = 0; t < ch.count; ++t) {
       const bv_item* it = items + l0 + t;
       const ge_cached* tab = tabs + 16 * (l0 + t);
-      add_entry(acc, tab, digit4(it->c[j >> 3], j));
+      if (keyed) {
+        if ((j & 1) == 0 && j < 32) {
+          const ge_cached* kt = ktabs + kKeyTab * (uint64_t)it->key;
+          add_key_entry(acc, kt, digit8(it->c, j >> 1));
+          add_key_entry(acc, kt + 129, digit8(it->c, 16 + (j >> 1)));
+        }
+      } else {
+        add_entry(acc, tab, digit4(it->c[j >> 3], j));
+      }
       if (j <= 32) add_entry(acc, tab + 8, digit4(it->z[j >> 3], j));
     }
     if ((j & 1) == 0) {
-      const int e = (int)((sel8(bb, j >> 3) >> (((j >> 1) & 3) * 8)) & 255u) - 128;
-      add_digit_niels(acc, s_btab, e, true);
+      if (keyed) {
+        if (j < 32) {
+          add_digit_niels(acc, s_btab, digit8(bb, j >> 1), true);
+          add_digit_niels(acc, s_b128, digit8(bb, 16 + (j >> 1)), true);
+        }
+      } else {
+        add_digit_niels(acc, s_btab, digit8(bb, j >> 1), true);
+      }
     }
   }
+  if (!live) return;
   if (ch.count == bn) {   // the batch is this one chunk: finish it here
     uint64_t idx;
     const int st = batch_status(first, flags0, ge_is_identity(acc), bn, &idx);
@@ -513,7 +581,11 @@ size_t bv_layout(uint64_t units, char* base, bv_ws* w) {
 hipError_t upload_batch_consts() {
   static batch_consts host;
   static std::once_flag once;
-  std::call_once(once, [] { compute_consts(host.k, host.btab); });
+  std::call_once(once, [] {
+    compute_consts(host.k, host.btab);
+    strict_consts sk;
+    compute_strict_consts(sk, host.b128);
+  });
   return hipMemcpyToSymbol(HIP_SYMBOL(g_bc), &host, sizeof(host), 0, hipMemcpyHostToDevice);
 }
 
@@ -521,42 +593,63 @@ size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems) {
   return bv_layout(std::min<uint64_t>(nitems + nbatches, slice_units()), nullptr, nullptr);
 }
 
-// One lane per key: decompress (dalek semantics) and build j*A, j = 1..8 (cached form).
-__global__ __launch_bounds__(256) void k_key_tables(const uint32_t* __restrict__ pks,
-                                                    uint64_t nkeys, ge_cached* __restrict__ tabs,
-                                                    uint32_t* __restrict__ ok) {
+// Caller key tables (a committee's keys, decompressed once per call): per key
+// j*A and j*2^128 A for j = 0..128 in cached form (258 entries, 41 KB), used by keyed
+// chunks' 8-bit windows and short ladders.
+//   k_key_base  one lane per key: decompress (dalek semantics), 2^128 A by 128 doublings.
+//   k_key_tabs  one lane per (key, table, j): j*P by double-and-add over the 8 bits of j.
+__global__ __launch_bounds__(256) void k_key_base(const uint32_t* __restrict__ pks,
+                                                  uint64_t nkeys, ge* __restrict__ base,
+                                                  uint32_t* __restrict__ ok) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nkeys) return;
-  const curve_consts& K = g_bc.k;
   uint32_t Aw[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) Aw[j] = pks[8 * i + j];
   ge P;
-  ok[i] = ge_frombytes(P, Aw, K) ? 1u : 0u;
-  ge_cached* t = tabs + 8 * i;
-  ge_cached c1;
-  ge_to_cached(c1, P, K.d2);
-  t[0] = c1;
-  ge acc;
-  ge_dbl(acc, P, true);
-  ge_cached cj;
-  ge_to_cached(cj, acc, K.d2);
-  t[1] = cj;
+  ok[i] = ge_frombytes(P, Aw, g_bc.k) ? 1u : 0u;
+  base[2 * i] = P;
 #pragma unroll 1
-  for (int j = 3; j <= 8; ++j) {
-    ge_add_cached(acc, acc, c1, true);
-    ge_to_cached(cj, acc, K.d2);
-    t[j - 1] = cj;
-  }
+  for (int t = 0; t < 128; ++t) ge_dbl(P, P, t == 127);
+  base[2 * i + 1] = P;
 }
 
-size_t key_tables_bytes(uint64_t nkeys) { return sizeof(ge_cached) * 8 * (nkeys ? nkeys : 1); }
+__global__ __launch_bounds__(256) void k_key_tabs(uint64_t nkeys, const ge* __restrict__ base,
+                                                  ge_cached* __restrict__ tabs) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nkeys * kKeyTab) return;
+  const uint64_t pt = g / 129;           // 2 * key + table
+  const int j = (int)(g % 129);
+  const ge P = base[pt];
+  ge acc;
+  ge_identity(acc);
+#pragma unroll 1
+  for (int bit = 7; bit >= 0; --bit) {
+    ge_dbl(acc, acc, true);
+    if ((j >> bit) & 1) {
+      ge_cached c;
+      ge_to_cached(c, P, g_bc.k.d2);
+      ge_add_cached(acc, acc, c, true);
+    }
+  }
+  ge_cached out;
+  ge_to_cached(out, acc, g_bc.k.d2);
+  tabs[g] = out;
+}
+
+size_t key_tables_bytes(uint64_t nkeys) {
+  const uint64_t n = nkeys ? nkeys : 1;
+  return sizeof(ge_cached) * kKeyTab * n + sizeof(ge) * 2 * n;
+}
 
 hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, ge_cached* tabs, uint32_t* ok,
                              hipStream_t stream) {
   if (nkeys == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_key_tables, dim3((unsigned)((nkeys + 255) / 256)), dim3(256), 0, stream,
-                     pks, nkeys, tabs, ok);
+  ge* base = reinterpret_cast<ge*>(tabs + kKeyTab * nkeys);
+  hipLaunchKernelGGL(k_key_base, dim3((unsigned)((nkeys + 63) / 64)), dim3(64), 0, stream, pks,
+                     nkeys, base, ok);
+  hipLaunchKernelGGL(k_key_tabs, dim3((unsigned)((nkeys * kKeyTab + 255) / 256)), dim3(256), 0,
+                     stream, nkeys, base, tabs);
   return hipGetLastError();
 }
 
@@ -603,7 +696,7 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
     if (chunks)
       hipLaunchKernelGGL(k_bv_chunks, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
                          stream, w.chunks, (uint32_t)chunks, offsets, b, i0, w.items, w.tabs,
-                         w.outs, status, fail_index);
+                         kt.tabs, w.outs, status, fail_index);
     if (multi)
       hipLaunchKernelGGL(k_bv_combine, dim3((unsigned)multi), dim3(256), 0, stream, w.multi,
                          w.multi_first, (uint32_t)multi, offsets, b, C, w.outs, status,

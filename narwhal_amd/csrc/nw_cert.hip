@@ -139,19 +139,36 @@ __global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com, cert
     if (vote_key)
       for (uint64_t v = vb; v < ve; ++v) vote_key[v] = kNoKey;
     uint32_t weight = 0;
+    // `used` only ever holds names that passed the stake check, i.e. committee members, so
+    // AuthorityReuse is "this committee index was seen before" (a bitmap for committees of
+    // up to 256; pairwise key comparison above that).
+    uint32_t seen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bool small_com = com.nauth <= 256;
     for (uint64_t v = vb; v < ve && p2 == 0; ++v) {
       uint32_t pk[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) pk[j] = cs.vote_pks[8 * v + j];
+      const int av = committee_find(com, pk);
       bool reuse = false;
-      for (uint64_t u = vb; u < v && !reuse; ++u) {
-        bool eq = true;
+      if (small_com) {
+        if (av >= 0) {
+          const uint32_t bit = 1u << (av & 31);
+          uint32_t word = 0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) eq &= cs.vote_pks[8 * u + j] == pk[j];
-        reuse = eq;
+          for (int q = 0; q < 8; ++q) word = (av >> 5) == q ? seen[q] : word;
+          reuse = (word & bit) != 0;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) seen[q] |= (av >> 5) == q ? bit : 0u;
+        }
+      } else {
+        for (uint64_t u = vb; u < v && !reuse; ++u) {
+          bool eq = true;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) eq &= cs.vote_pks[8 * u + j] == pk[j];
+          reuse = eq;
+        }
       }
       if (reuse) { p2 = NW_DAG_AUTHORITY_REUSE; x2 = v - vb; break; }
-      const int av = committee_find(com, pk);
       if (vote_key && av >= 0) vote_key[v] = (uint32_t)av;
       const uint32_t st = committee_stake(com, av);
       if (st == 0) { p2 = NW_DAG_UNKNOWN_AUTHORITY; x2 = v - vb; break; }

@@ -41,10 +41,11 @@ hipError_t launch_sign(const uint32_t* sks, uint32_t sk_stride_words, const uint
 // the workspace slices).
 hipError_t upload_batch_consts();
 
-// Pre-decompressed public keys (a committee): per key its 8-entry table j*A (j = 1..8,
-// cached form) and whether it decompressed. vote_key[i] = key index of vote i, or
-// kNoKey to decompress that vote's key in the kernel (the verdict semantics are
-// unchanged: a key's decompression is deterministic).
+// Pre-decompressed public keys (a committee): per key the tables j*A and j*2^128 A
+// (j = 0..128, cached form) and whether it decompressed. vote_key[i] = key index of vote i,
+// or kNoKey to decompress that vote's key in the kernel (the verdict semantics are
+// unchanged: a key's decompression is deterministic). Chunks whose votes are all keyed
+// run 8-bit A windows and a 128-doubling ladder.
 struct key_tables_t {
   const struct ge_cached* tabs;   // nkeys x 8
   const uint32_t* ok;             // nkeys
