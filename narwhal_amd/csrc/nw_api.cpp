@@ -406,17 +406,18 @@ struct CertWs {
   uint64_t *idx1, *idx2, *batch_idx, *bitmap;
   void* batch_ws;
   uint32_t* vote_key;
+  uint32_t* author_key;
 };
 
 size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
   const size_t m = n ? n : 1;
-  const size_t sizes[13] = {a256(32 * m), a256(32 * m), a256(32 * m), a256(4 * m), a256(4 * m),
+  const size_t sizes[14] = {a256(32 * m), a256(32 * m), a256(32 * m), a256(4 * m), a256(4 * m),
                             a256(4 * m),  a256(4 * m),  a256(8 * m),  a256(8 * m), a256(8 * m),
                             a256(8 * ((m + 63) / 64)),
                             nvotes ? a256(nw::batch_workspace_bytes(n, nvotes)) : 256,
-                            a256(4 * (nvotes ? nvotes : 1))};
-  size_t off[13], tot = 0;
-  for (int k = 0; k < 13; ++k) { off[k] = tot; tot += sizes[k]; }
+                            a256(4 * (nvotes ? nvotes : 1)), a256(4 * m)};
+  size_t off[14], tot = 0;
+  for (int k = 0; k < 14; ++k) { off[k] = tot; tot += sizes[k]; }
   if (w) {
     w->hdr_digest = reinterpret_cast<uint32_t*>(base + off[0]);
     w->authors = reinterpret_cast<uint32_t*>(base + off[1]);
@@ -431,6 +432,7 @@ size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
     w->bitmap = reinterpret_cast<uint64_t*>(base + off[10]);
     w->batch_ws = base + off[11];
     w->vote_key = reinterpret_cast<uint32_t*>(base + off[12]);
+    w->author_key = reinterpret_cast<uint32_t*>(base + off[13]);
   }
   return tot;
 }
@@ -451,24 +453,28 @@ int cert_pipeline(DevCtx& ctx, const nw_committee& com, const nw_certificates& c
                        reinterpret_cast<const uint32_t*>(cs.vote_pks)};
   NW_HIP(nw::launch_sha512_digest32(cs.header_bytes, cs.header_offsets, nullptr, n,
                                     w.hdr_digest, s), "k_sha512 (header digests)");
+  int rc_;
+  // The committee's keys are decompressed once per call (k_key_base / k_key_tabs) and their
+  // tables shared by every header (author) and vote that names a committee member; any
+  // other key cannot decide a verdict (k_cert_prepare fails its message first) and is
+  // decompressed in the kernel as usual.
+  rc_ = key_tables(ctx, com.nauth);
+  if (rc_) return rc_;
+  NW_HIP(nw::launch_key_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth,
+                               static_cast<nw::ge_cached*>(ctx.ktabs), ctx.kok, s),
+         "k_key_tables");
   NW_HIP(nw::launch_cert_prepare(dc, ds, headers_only, w.hdr_digest, w.authors, w.cert_digest,
                                  w.pre1, w.pre2, w.idx1, w.idx2,
-                                 headers_only ? nullptr : w.vote_key, s), "k_cert_prepare");
+                                 headers_only ? nullptr : w.vote_key, w.author_key, s),
+         "k_cert_prepare");
   void* sws;
   int rc = strict_ws(ctx, &sws);
   if (rc) return rc;
+  const nw::key_tables_t hk{static_cast<const nw::ge_cached*>(ctx.ktabs), ctx.kok, w.author_key};
   NW_HIP(nw::launch_verify_strict(reinterpret_cast<const uint32_t*>(cs.ids), 8, w.authors,
                                   reinterpret_cast<const uint32_t*>(cs.header_sigs), n, w.hdr_st,
-                                  w.bitmap, sws, s), "k_verify_strict (headers)");
+                                  w.bitmap, sws, s, &hk), "k_verify_strict (headers)");
   if (!headers_only) {
-    // Every vote that can decide a verdict is by a committee member (k_cert_prepare fails
-    // the certificate first otherwise), so the committee's keys are decompressed once per
-    // call and their tables reused by every vote, instead of once per vote.
-    rc = key_tables(ctx, com.nauth);
-    if (rc) return rc;
-    NW_HIP(nw::launch_key_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth,
-                                 static_cast<nw::ge_cached*>(ctx.ktabs), ctx.kok, s),
-           "k_key_tables");
     const nw::key_tables_t kt{static_cast<const nw::ge_cached*>(ctx.ktabs), ctx.kok, w.vote_key};
     NW_HIP(nw::launch_verify_batch(w.cert_digest, cs.vote_offsets, host_vote_offsets, n,
                                    reinterpret_cast<const uint32_t*>(cs.vote_pks),

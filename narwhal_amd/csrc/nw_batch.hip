@@ -59,7 +59,6 @@ uint64_t env_u64(const char* name, uint64_t dflt) {
 uint64_t slice_units() { return env_u64("NW_BATCH_SLICE_UNITS", kSliceUnits); }
 constexpr uint32_t kMaxChunk = 128;
 constexpr uint32_t kNone = 0xffffffffu;
-constexpr uint32_t kKeyTab = 258;   // entries per caller key table (j*A, j*2^128 A, j = 0..128)
 
 // Per-vote record written by k_bv_items (96 bytes).
 struct bv_item {
@@ -285,7 +284,7 @@ __global__ __launch_bounds__(256) void k_bv_items(
   // A: the caller's pre-decompressed key tables when this vote's key has them (read by
   // k_bv_chunks directly), else decompressed and tabulated here
   if (kk != kNoKey) {
-    if (!keys.ok[kk]) flags |= BF_A_DECODE;
+    if (!(keys.ok[kk] & 1u)) flags |= BF_A_DECODE;
   } else if (!ge_frombytes(P, Aw, K)) {
     flags |= BF_A_DECODE;
   }
@@ -607,7 +606,8 @@ __global__ __launch_bounds__(256) void k_key_base(const uint32_t* __restrict__ p
 #pragma unroll
   for (int j = 0; j < 8; ++j) Aw[j] = pks[8 * i + j];
   ge P;
-  ok[i] = ge_frombytes(P, Aw, g_bc.k) ? 1u : 0u;
+  const bool dec = ge_frombytes(P, Aw, g_bc.k);
+  ok[i] = (dec ? 1u : 0u) | (dec && ge_is_small_order(P) ? 2u : 0u);   // bit 1: 8A == 0
   base[2 * i] = P;
 #pragma unroll 1
   for (int t = 0; t < 128; ++t) ge_dbl(P, P, t == 127);

@@ -84,7 +84,8 @@ __global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com, cert
                                                       int32_t* __restrict__ pre2,
                                                       uint64_t* __restrict__ idx1,
                                                       uint64_t* __restrict__ idx2,
-                                                      uint32_t* __restrict__ vote_key) {
+                                                      uint32_t* __restrict__ vote_key,
+                                                      uint32_t* __restrict__ author_key) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cs.n) return;
   const uint8_t* h = cs.header_bytes + cs.header_offsets[i];
@@ -99,6 +100,7 @@ __global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com, cert
   for (int j = 0; j < 8; ++j) authors[8 * i + j] = author[j];
 
   const int a = committee_find(com, author);
+  if (author_key) author_key[i] = a >= 0 ? (uint32_t)a : kNoKey;
   int32_t p1 = 0, p2 = 0;
   uint64_t x1 = 0, x2 = 0;
   // Certificate::verify: genesis(committee).contains(self) compares (header.id, round,
@@ -254,11 +256,11 @@ hipError_t launch_cert_prepare(const cert_committee_t& com, const cert_stream_t&
                                int headers_only, const uint32_t* hdr_digest, uint32_t* authors,
                                uint32_t* cert_digest, int32_t* pre1, int32_t* pre2,
                                uint64_t* idx1, uint64_t* idx2, uint32_t* vote_key,
-                               hipStream_t stream) {
+                               uint32_t* author_key, hipStream_t stream) {
   if (cs.n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_cert_prepare, dim3(blocks_for(cs.n)), dim3(256), 0, stream, com, cs,
                      headers_only, hdr_digest, authors, cert_digest, pre1, pre2, idx1, idx2,
-                     vote_key);
+                     vote_key, author_key);
   return hipGetLastError();
 }
 

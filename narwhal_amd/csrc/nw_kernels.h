@@ -25,10 +25,11 @@ hipError_t launch_sha512_digest32(const uint8_t* data, const uint64_t* offsets,
 // Strict verification; workspace = strict_workspace_bytes() of device memory (per-lane
 // tables; reusable across launches on one stream).
 size_t strict_workspace_bytes();
+// keys (optional): pre-decompressed key tables with vote_key = per-item key index.
 hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
                                 const uint32_t* pks, const uint32_t* sigs, uint64_t n,
                                 int32_t* status, uint64_t* bitmap, void* workspace,
-                                hipStream_t stream);
+                                hipStream_t stream, const struct key_tables_t* keys = nullptr);
 
 hipError_t launch_keypair(const uint32_t* seeds, uint64_t n, uint32_t* pks, hipStream_t stream);
 
@@ -52,6 +53,8 @@ struct key_tables_t {
   const uint32_t* vote_key;       // nitems (global item index)
 };
 constexpr uint32_t kNoKey = 0xffffffffu;
+constexpr uint32_t kKeyTab = 258;   // entries per key: j*A, then j*2^128 A, j = 0..128
+// ok[key]: bit 0 = decompressed, bit 1 = small order (8A == identity)
 size_t key_tables_bytes(uint64_t nkeys);
 // tabs: key_tables_bytes(nkeys) of device memory; ok: nkeys words.
 hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, struct ge_cached* tabs,
@@ -87,7 +90,7 @@ hipError_t launch_cert_prepare(const cert_committee_t& com, const cert_stream_t&
                                int headers_only, const uint32_t* hdr_digest, uint32_t* authors,
                                uint32_t* cert_digest, int32_t* pre1, int32_t* pre2,
                                uint64_t* idx1, uint64_t* idx2, uint32_t* vote_key,
-                               hipStream_t stream);
+                               uint32_t* author_key, hipStream_t stream);
 hipError_t launch_cert_finalize(uint64_t n, int headers_only, const int32_t* pre1,
                                 const int32_t* pre2, const uint64_t* idx1, const uint64_t* idx2,
                                 const int32_t* hdr_status, const int32_t* batch_status,

@@ -188,7 +188,8 @@ __global__ __launch_bounds__(256, 2) void k_verify_strict(const uint32_t* __rest
                                                        const uint32_t* __restrict__ sigs,
                                                        uint64_t n, int32_t* __restrict__ status,
                                                        uint64_t* __restrict__ bitmap,
-                                                       ge_cached* __restrict__ tabs) {
+                                                       ge_cached* __restrict__ tabs,
+                                                       key_tables_t keys) {
   __shared__ ge_niels s_btab[129];
   __shared__ ge_niels s_b128[129];
   load_table(s_btab, g_consts.btab);
@@ -214,8 +215,10 @@ __global__ __launch_bounds__(256, 2) void k_verify_strict(const uint32_t* __rest
     hram96(hx, Rw, Aw, Mw);
     sc k;
     sc_reduce512(k, hx);
+    const uint32_t kk = keys.vote_key ? keys.vote_key[i] : kNoKey;
+    const ge_cached* keytab = kk != kNoKey ? keys.tabs + kKeyTab * (uint64_t)kk : nullptr;
     const int st = strict_verify_core(Aw, Rw, Sw, k, g_consts.sk, s_btab, s_b128, tabA, tabR,
-                                      WaveMax{});
+                                      WaveMax{}, keytab, kk != kNoKey ? keys.ok[kk] : 0u);
     if (active) status[gi] = st;
     const uint64_t mask = __ballot(active && st == NW_OK);
     if ((threadIdx.x & 63) == 0 && gi < n) bitmap[gi >> 6] = mask;
@@ -396,11 +399,12 @@ size_t strict_workspace_bytes() {
 hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
                                 const uint32_t* pks, const uint32_t* sigs, uint64_t n,
                                 int32_t* status, uint64_t* bitmap, void* workspace,
-                                hipStream_t stream) {
+                                hipStream_t stream, const key_tables_t* keys) {
   if (n == 0) return hipSuccess;
   const unsigned grid = std::min<uint64_t>(strict_grid(), grid_for(n, 256));
+  const key_tables_t kt = keys ? *keys : key_tables_t{nullptr, nullptr, nullptr};
   hipLaunchKernelGGL(k_verify_strict, dim3(grid), dim3(256), 0, stream, msgs, msg_stride_words,
-                     pks, sigs, n, status, bitmap, static_cast<ge_cached*>(workspace));
+                     pks, sigs, n, status, bitmap, static_cast<ge_cached*>(workspace), kt);
   return hipGetLastError();
 }
 

@@ -69,11 +69,15 @@ NW_HD void build_table8(ge_cached tab[8], const ge& P, const fe& d2) {
 // Status of one strict verification. wave_max maps this lane's ladder length (in 4-bit
 // windows) to the wave's maximum (identity on the host). tabA/tabR: 8 entries each of
 // per-lane scratch. s_btab / s_b128: j*B and j*2^128 B, j = 0..128.
+// keytab (optional): A's pre-decompressed key table j*A, j = 0..128 (cached form) with
+// keyflags bit 0 = decoded, bit 1 = small order; then A is neither decompressed nor
+// tabulated here and u is taken in signed 8-bit windows over that table.
 template <class WaveMax>
 NW_HD int strict_verify_core(const uint32_t Aw[8], const uint32_t Rw[8], const uint32_t Sw[8],
                              const sc& k, const strict_consts& K, const ge_niels* s_btab,
                              const ge_niels* s_b128, ge_cached* tabA, ge_cached* tabR,
-                             WaveMax wave_max) {
+                             WaveMax wave_max, const ge_cached* keytab = nullptr,
+                             uint32_t keyflags = 0) {
   const bool s_high = (Sw[7] >> 29) != 0;
   sc s;
 #pragma unroll
@@ -84,9 +88,9 @@ NW_HD int strict_verify_core(const uint32_t Aw[8], const uint32_t Rw[8], const u
   // code object): P, its small-order flag and its 8-entry table.
   sc_half h;
   sc_half_split(h, k);
-  bool okA = false, smallA = false, okR = false, smallR = false;
+  bool okA = (keyflags & 1) != 0, smallA = (keyflags & 2) != 0, okR = false, smallR = false;
 #pragma unroll 1
-  for (int pt = 0; pt < 2; ++pt) {
+  for (int pt = keytab ? 1 : 0; pt < 2; ++pt) {
     uint32_t x[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) x[i] = pt ? Rw[i] : Aw[i];
@@ -113,7 +117,8 @@ NW_HD int strict_verify_core(const uint32_t Aw[8], const uint32_t Rw[8], const u
 #pragma unroll
   for (int j = 0; j < 8; ++j) { ur.w[j] = h.u[j]; vr.w[j] = vm.w[j]; }
   uint32_t ud[8], vd[8], wd[8];
-  sc_recode(ud, ur, 0x88888888u);
+  const uint32_t ubias = keytab ? 0x80808080u : 0x88888888u;
+  sc_recode(ud, ur, ubias);
   sc_recode(vd, vr, 0x88888888u);
   {
     uint64_t c = 0;
@@ -135,7 +140,7 @@ NW_HD int strict_verify_core(const uint32_t Aw[8], const uint32_t Rw[8], const u
   // two 128-bit halves of w
   uint32_t xu[8], xv[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { xu[j] = ud[j] ^ 0x88888888u; xv[j] = vd[j] ^ 0x88888888u; }
+  for (int j = 0; j < 8; ++j) { xu[j] = ud[j] ^ ubias; xv[j] = vd[j] ^ 0x88888888u; }
   const int bu = bn_bits(xu, 8), bv = bn_bits(xv, 5);
   int W = ((bu > bv ? bu : bv) + 3) / 4;
   if (W < 32) W = 32;
@@ -157,7 +162,8 @@ NW_HD int strict_verify_core(const uint32_t Aw[8], const uint32_t Rw[8], const u
     for (int slot = 0; slot < nslots; ++slot) {
       int d;
       if (slot == 0) {
-        d = digit4_of(ud, 8, j);
+        d = !keytab ? digit4_of(ud, 8, j)
+                    : (j & 1) ? 0 : (int)((sel8(ud, j >> 3) >> (((j >> 1) & 3) * 8)) & 255u) - 128;
       } else if (slot == 1) {
         d = j < 40 ? digit4_of(vd, 5, j) : 0;
       } else {
@@ -167,7 +173,9 @@ NW_HD int strict_verify_core(const uint32_t Aw[8], const uint32_t Rw[8], const u
       if (d != 0) {
         const int ad = d < 0 ? -d : d;
         ge_cached e;
-        if (slot < 2) {
+        if (slot == 0 && keytab) {
+          e = keytab[ad];
+        } else if (slot < 2) {
           e = (slot == 0 ? tabA : tabR)[ad - 1];
         } else {
           const ge_niels& nb = (slot == 2 ? s_btab : s_b128)[ad];

@@ -120,3 +120,42 @@ def test_device_entry_point_matches_host(case_host):
     assert L.nw_synchronize() == 0
     assert st.cpu().numpy().tolist() == exp_st.tolist()
     assert ix.cpu().numpy().astype(np.uint64).tolist() == exp_ix.tolist()
+
+
+def test_committee_key_classes_vs_oracle():
+    """Committee members whose keys are small-order / non-decodable: their pre-decompressed
+    key tables must give the same Header::verify and Certificate::verify statuses as
+    per-message decompression (oracle). Header authored by each member, votes by all."""
+    import hashlib
+    import struct
+    keys = O.keys(4)
+    small = bytes.fromhex("01" + "00" * 31)                      # identity: small order
+    undec = (2).to_bytes(32, "little")                          # y = 2: not on the curve
+    members = [pk for pk, _ in keys] + [small, undec]
+    sk_of = dict(keys)
+    com = M.Committee({PublicKey(pk): M.Authority(1) for pk in members})
+    d32 = lambda b: hashlib.sha512(b).digest()[:32]
+    certs = []
+    for author in members:
+        h = M.Header(author=PublicKey(author), round=3)
+        h.id = M.Digest(d32(h.digest_bytes()))
+        signer = sk_of.get(author, keys[0][1])                  # no key for small / undec
+        h.signature = Signature.from_bytes(O.sign(signer, h.id.value))
+        c = M.Certificate(h)
+        cd = c.digest().value
+        c.votes = [(PublicKey(pk), Signature.from_bytes(O.sign(sk_of.get(pk, keys[1][1]), cd)))
+                   for pk in members]
+        certs.append(c)
+        c2 = M.Certificate(h)                                   # honest members only
+        c2.votes = [(PublicKey(pk), Signature.from_bytes(O.sign(sk, cd))) for pk, sk in keys]
+        certs.append(c2)
+    p = M.pack_certificates(certs)
+    z16 = np.random.Generator(np.random.PCG64(1)).integers(0, 256, size=(len(p["vote_pks"]), 16),
+                                                           dtype=np.uint8)
+    st, ix = M.verify_certificates_many(com, p, z16)
+    ost, oix = O.certificates_verify_many(com.packed(), p, z16)
+    assert st.tolist() == ost.tolist() and ix.tolist() == oix.tolist()
+    hst, _ = M.verify_headers_many(com, p)
+    ohst, _ = O.certificates_verify_many(com.packed(), p, headers_only=True)
+    assert hst.tolist() == ohst.tolist()
+    assert {int(x) for x in hst} >= {0, 32 + 5, 32 + 3}         # Ok, A small order, A decode
