@@ -421,26 +421,26 @@ def cpu_baseline_batch(sample, seconds: float):
 
 
 def cpu_baseline_strict(sample, seconds: float):
-    """Oracle ('port', the dalek-equivalent restatement) on the host cores, bounded."""
+    """Oracle ('port', the dalek-equivalent restatement) on the host cores, bounded: passes
+    over the unique corpus until about ``seconds`` of wall time; the first pass's statuses
+    are compared with the GPU's."""
     from oracle import oracle as O
     msgs_u, pks_u, sigs_u, gpu_st = sample
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     m, p, s = (t.cpu().numpy() for t in (msgs_u, pks_u, sigs_u))
-    n = min(len(m), 2048)
+    n = len(m)
     t0 = time.perf_counter()
-    st = O.verify_strict_many(m[:n], p[:n], s[:n], nthreads=threads)
-    dt = time.perf_counter() - t0
-    rate = n / dt
-    n2 = int(min(len(m), max(n, rate * seconds)))
-    if n2 > n:
-        t0 = time.perf_counter()
-        st = O.verify_strict_many(m[:n2], p[:n2], s[:n2], nthreads=threads)
-        dt = time.perf_counter() - t0
-        n = n2
+    st = O.verify_strict_many(m, p, s, nthreads=threads)
     agree = bool(np.array_equal(st, gpu_st[:n]))
-    return dict(value=n / dt, unit="verifies/s", cores=threads, kind="port",
-                sample=f"{n} mixed-corpus items (first {n} of the unique corpus), oracle "
-                       f"verify_strict_many, {threads} threads, {dt:.1f} s"), agree
+    done, passes = n, 1
+    while time.perf_counter() - t0 < seconds:
+        O.verify_strict_many(m, p, s, nthreads=threads)
+        done += n
+        passes += 1
+    dt = time.perf_counter() - t0
+    return dict(value=done / dt, unit="verifies/s", cores=threads, kind="port",
+                sample=f"{passes} passes over the {n}-item unique mixed corpus ({done} verifies), "
+                       f"oracle verify_strict_many, {threads} threads, {dt:.1f} s"), agree
 
 
 def main():
