@@ -6,9 +6,11 @@
 Writes into profiles/TAG/:
   kernel_stats.csv     rocprofv3 --stats summary of the traced bench run (verbatim)
   kernels_by_grid.csv  the same trace grouped by (kernel, grid size): calls and mean/min/max
-                       duration, so the bench-size launches of a kernel are not averaged
-                       with its small parity/corpus launches
-  pmc.json             PMC counters per (kernel, grid) from the one-step bench runs, with
+                       duration, plus the mean over the "large" calls (within 20 % of the
+                       longest) = the bench-size launches, which is what bench.py's
+                       kernel_ms is compared with
+  pmc.json             PMC counters per (kernel, grid), largest dispatch, from the one-step
+                       bench runs, with
                        HBM bytes per dispatch (FETCH_SIZE x 2 per the gfx950 correction in
                        MI355X_MICROARCH.md, WRITE_SIZE as reported; both in KiB)
   bench_traced.json    the bench line printed under the tracer
@@ -55,14 +57,20 @@ def main():
             g[(short(r["Kernel_Name"]), int(r["Grid_Size_X"] if "Grid_Size_X" in r else r["Grid_Size"]))].append(dur)
         with open(os.path.join(dst, "kernels_by_grid.csv"), "w", newline="") as f:
             w = csv.writer(f)
-            w.writerow(["kernel", "grid", "calls", "mean_ms", "min_ms", "max_ms", "total_ms"])
+            w.writerow(["kernel", "grid", "calls", "mean_ms", "min_ms", "max_ms", "total_ms",
+                        "large_calls", "large_mean_ms"])
             for (k, grid), d in sorted(g.items(), key=lambda kv: -sum(kv[1])):
+                # the bench-size launches: calls within 20% of the longest (a persistent
+                # kernel's grid does not change with the item count)
+                big = [x for x in d if x >= 0.8 * max(d)]
                 w.writerow([k, grid, len(d), f"{sum(d) / len(d) / 1e6:.4f}", f"{min(d) / 1e6:.4f}",
-                            f"{max(d) / 1e6:.4f}", f"{sum(d) / 1e6:.3f}"])
+                            f"{max(d) / 1e6:.4f}", f"{sum(d) / 1e6:.3f}", len(big),
+                            f"{sum(big) / len(big) / 1e6:.4f}"])
     bt = os.path.join(src, "bench_traced.json")
     if os.path.exists(bt) and os.path.getsize(bt):
         shutil.copy(bt, os.path.join(dst, "bench_traced.json"))
-    # PMC: per dispatch, then per (kernel, grid) mean over dispatches
+    # PMC: per dispatch, then per (kernel, grid) the LARGEST dispatch (the bench-size launch;
+    # smaller launches of the same kernel and grid, e.g. the wire leg's, are other work)
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(os.path.join(src, "pmc_*", "**", "*counter_collection.csv"), recursive=True):
         acc = collections.defaultdict(float)
@@ -73,7 +81,7 @@ def main():
             per[(k, grid)][cn].append(v)
     pmc = {}
     for (k, grid), cs in sorted(per.items()):
-        e = {cn: sum(v) / len(v) for cn, v in cs.items()}
+        e = {cn: max(v) for cn, v in cs.items()}
         e["dispatches"] = max(len(v) for v in cs.values())
         if "FETCH_SIZE" in e:
             e["hbm_read_bytes"] = 2 * e["FETCH_SIZE"] * 1024
