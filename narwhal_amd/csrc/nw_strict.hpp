@@ -55,14 +55,19 @@ NW_HD void add_table_digit(ge& acc, const ge_cached* tab, int d, bool want_t) {
 }
 
 NW_HD void build_table8(ge_cached tab[8], const ge& P, const fe& d2) {
-  ge_to_cached(tab[0], P, d2);
+  ge_cached c1;                 // 1*P stays in registers (no re-reads of tab[0])
+  ge_to_cached(c1, P, d2);
+  tab[0] = c1;
   ge acc;
   ge_dbl(acc, P, true);
-  ge_to_cached(tab[1], acc, d2);
+  ge_cached cj;
+  ge_to_cached(cj, acc, d2);
+  tab[1] = cj;
 #pragma unroll 1
   for (int j = 3; j <= 8; ++j) {
-    ge_add_cached(acc, acc, tab[0], true);
-    ge_to_cached(tab[j - 1], acc, d2);
+    ge_add_cached(acc, acc, c1, true);
+    ge_to_cached(cj, acc, d2);
+    tab[j - 1] = cj;
   }
 }
 
