@@ -27,6 +27,7 @@
 #include "nw_ladder.hpp"
 #include "nw_consts.hpp"
 #include "nw_strict.hpp"
+#include "nw_quad.hpp"
 
 #include <stdlib.h>
 
@@ -152,42 +153,50 @@ __device__ void chacha20_z(uint32_t z[4], const uint32_t key[8], uint64_t nonce,
 // k_bv_expand: one lane per chunk writes its descriptor (balanced split of the batch).
 __global__ __launch_bounds__(1024) void k_bv_plan(const uint64_t* __restrict__ offsets,
                                                   uint64_t b0, uint64_t b1, uint32_t C,
+                                                  uint32_t pmin,
                                                   uint32_t* __restrict__ chunk_start,
                                                   uint32_t* __restrict__ multi,
-                                                  uint32_t* __restrict__ multi_first) {
-  __shared__ uint32_t s_a[1024], s_b[1024];
-  __shared__ uint32_t s_base_a, s_base_b;
+                                                  uint32_t* __restrict__ multi_first,
+                                                  uint32_t* __restrict__ pip_list) {
+  __shared__ uint32_t s_a[1024], s_b[1024], s_c[1024];
+  __shared__ uint32_t s_base_a, s_base_b, s_base_c;
   const int t = threadIdx.x;
-  if (t == 0) { s_base_a = 0; s_base_b = 0; }
+  if (t == 0) { s_base_a = 0; s_base_b = 0; s_base_c = 0; }
   __syncthreads();
   for (uint64_t base = b0; base < b1; base += 1024) {
     const uint64_t b = base + t;
-    uint32_t kb = 0;
+    uint32_t kb = 0, pflag = 0;
     if (b < b1) {
-      const uint32_t nb = (uint32_t)(offsets[b + 1] - offsets[b]);
-      kb = (nb + C - 1) / C;
+      const uint64_t nb = offsets[b + 1] - offsets[b];
+      pflag = nb >= pmin ? 1u : 0u;   // Pippenger batch: no chunks, no combine
+      kb = pflag ? 0u : (uint32_t)((nb + C - 1) / C);
     }
-    const uint32_t mflag = (b < b1 && kb != 1) ? 1u : 0u;
+    const uint32_t mflag = (b < b1 && !pflag && kb != 1) ? 1u : 0u;
     s_a[t] = kb;
     s_b[t] = mflag;
+    s_c[t] = pflag;
     __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {   // Hillis-Steele inclusive scan of both counters
-      const uint32_t va = t >= d ? s_a[t - d] : 0u, vb = t >= d ? s_b[t - d] : 0u;
+    for (int d = 1; d < 1024; d <<= 1) {   // Hillis-Steele inclusive scan of the counters
+      const uint32_t va = t >= d ? s_a[t - d] : 0u, vb = t >= d ? s_b[t - d] : 0u,
+                     vc = t >= d ? s_c[t - d] : 0u;
       __syncthreads();
       s_a[t] += va;
       s_b[t] += vb;
+      s_c[t] += vc;
       __syncthreads();
     }
-    const uint32_t ca = s_base_a + s_a[t] - kb, cb = s_base_b + s_b[t] - mflag;
+    const uint32_t ca = s_base_a + s_a[t] - kb, cb = s_base_b + s_b[t] - mflag,
+                   cc = s_base_c + s_c[t] - pflag;
     if (b < b1) {
       chunk_start[b - b0] = ca;
       if (mflag) {
         multi[cb] = (uint32_t)(b - b0);
         multi_first[cb] = ca;
       }
+      if (pflag) pip_list[cc] = (uint32_t)(b - b0);
     }
     __syncthreads();
-    if (t == 1023) { s_base_a += s_a[1023]; s_base_b += s_b[1023]; }
+    if (t == 1023) { s_base_a += s_a[1023]; s_base_b += s_b[1023]; s_base_c += s_c[1023]; }
     __syncthreads();
   }
   if (t == 0) chunk_start[b1 - b0] = s_base_a;
@@ -219,7 +228,7 @@ __global__ __launch_bounds__(256) void k_bv_expand(const uint64_t* __restrict__ 
 // ------------------------------------------------------------------------------ items
 __global__ __launch_bounds__(256) void k_bv_items(
     const uint32_t* __restrict__ digests, const uint64_t* __restrict__ offsets, uint64_t b0,
-    uint64_t b1, uint64_t i0, uint64_t i1, const uint32_t* __restrict__ pks,
+    uint64_t b1, uint64_t i0, uint64_t i1, uint32_t pmin, const uint32_t* __restrict__ pks,
     const uint32_t* __restrict__ sigs, const uint32_t* __restrict__ z16, z_key_t zkey,
     bv_item* __restrict__ items, ge_cached* __restrict__ tabs, key_tables_t keys) {
   const uint64_t gi = i0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -232,6 +241,7 @@ __global__ __launch_bounds__(256) void k_bv_items(
     const uint64_t mid = (lo + hi) >> 1;
     if (offsets[mid] <= gi) lo = mid; else hi = mid;
   }
+  if (offsets[lo + 1] - offsets[lo] >= pmin) return;   // k_pip_points
   uint32_t Aw[8], Rw[8], Sw[8], Mw[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -545,6 +555,430 @@ __global__ __launch_bounds__(256) void k_bv_combine(const uint32_t* __restrict__
   }
 }
 
+// ------------------------------------------------------------------------------ Pippenger
+// Large batches (n >= NW_BATCH_PIPPENGER_MIN votes, default kPipMin): a bucket
+// multi-scalar multiplication over all 2n points of the batch, spread over the whole chip
+// instead of one Straus ladder per chunk lane.
+//
+//   sum_i z_i R_i + sum_i c_i A_i = sum_{w<32} 2^(8w) sum_{b=1..128} b S_{w,b}
+//
+// with signed 8-bit digits (c_i: 32 windows, z_i: 17) and S_{w,b} = the sum of the points
+// whose window-w digit is +-b (sign applied to the point). A vote costs two decompressions
+// and <= 49 bucket additions; the per-batch tail (bucket sums, window sums, 248-doubling
+// Horner over the windows with -sum b_i folded in by 8-bit windows over the LDS B table) is
+// shared by the whole batch.
+//
+//   k_pip_points   one lane per point (A lanes also do the vote's scalars and flags),
+//                  decompressed points written in affine niels form
+//   k_pip_sort     one workgroup per (batch, window): counting sort of the window's digits
+//                  into its buckets with LDS histograms and cursors ((point index | sign)
+//                  entries; the order inside a bucket does not matter, addition commutes)
+//   k_pip_buckets  G lanes per bucket: partial sums, combined by a lane-shuffle tree
+//   k_pip_windows  one wave per window: sum_b b S_b by a suffix scan + tree over lanes
+//   k_pip_final    one workgroup per batch: sum b_i, first failures, Horner, identity test
+//
+// Each batch's scratch lives in the per-item table slots of its own items (16 cached
+// entries = 2560 B per item, unused by this path): pip_region() lays it out.
+constexpr uint32_t kPipMin = 512;
+constexpr uint32_t kPipFloor = 400;     // smallest n whose item slots hold the region
+constexpr int kPipWin = 32;             // 8-bit windows of c_i (< 2^253)
+constexpr int kPipZWin = 17;            // 8-bit windows of z_i (< 2^128, recoded)
+// Bins: window w, |digit| b -> w * 128 + b - 1, except the two windows whose digits are
+// structurally skewed, which are spread over sub-bins so no bucket is much longer than the
+// mean (bucket sums are sequential chains):
+//   c_i window 31: c < l gives digit (c >> 248) + carry in [0, 17]; digit d of vote t goes
+//     to 31 * 128 + (d - 1) + 17 (t % 7) (weight (j % 17) + 1 for bucket j of window 31);
+//   z_i window 16: the recoding carry, digit 0 or 1 for every vote (about n/2 ones); vote t
+//     goes to kPipWin * 128 + (t % 64), weight 1 at window 16.
+constexpr int kPipWinCap = 2 * kPipWin;   // entry slots per vote: 2 per window
+constexpr int kPipTopSub = 7, kPipTopStride = 17, kPipCarryBins = 64;
+constexpr int kPipBins = kPipWin * 128 + kPipCarryBins;
+
+struct pip_region {
+  ge_niels* pts;     // 2n: A_t at 2t, R_t at 2t + 1
+  uint32_t* ent;     // window w: entries [2n w, 2n w + 2n), point index | sign << 31
+  uint32_t* cnt;     // kPipBins: entries per bucket
+  uint32_t* off;     // kPipBins: first entry of each bucket
+  ge* S;             // kPipBins bucket sums
+  ge_cached* W;      // kPipWin window sums (cached form, for the Horner)
+};
+
+__host__ __device__ inline size_t pip_region_bytes(uint64_t n) {
+  return 2 * n * sizeof(ge_niels) + 4 * kPipWinCap * n + 8 * kPipBins +
+         sizeof(ge) * (kPipBins + kPipWin);
+}
+
+__device__ __forceinline__ pip_region pip_at(ge_cached* tabs, uint64_t li0, uint64_t n) {
+  char* p = reinterpret_cast<char*>(tabs + 16 * li0);
+  pip_region r;
+  r.pts = reinterpret_cast<ge_niels*>(p); p += 2 * n * sizeof(ge_niels);
+  r.ent = reinterpret_cast<uint32_t*>(p); p += 4 * kPipWinCap * n;
+  r.cnt = reinterpret_cast<uint32_t*>(p); p += 4 * kPipBins;
+  r.off = reinterpret_cast<uint32_t*>(p); p += 4 * kPipBins;
+  r.S = reinterpret_cast<ge*>(p); p += sizeof(ge) * kPipBins;
+  r.W = reinterpret_cast<ge_cached*>(p);
+  return r;
+}
+
+__device__ __forceinline__ uint64_t batch_of(const uint64_t* offsets, uint64_t b0, uint64_t b1,
+                                             uint64_t gi) {
+  uint64_t lo = b0, hi = b1;
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (offsets[mid] <= gi) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ void ge_to_niels_z1(ge_niels& q, const ge& P, const fe& d2) {
+  fe_add(q.ypx, P.Y, P.X); fe_carry(q.ypx);
+  fe_sub(q.ymx, P.Y, P.X);
+  fe_mul(q.xy2d, P.T, d2);
+}
+
+// r = p + q for two extended points (q converted to cached form), with T.
+__device__ __forceinline__ void ge_add_ge(ge& r, const ge& p, const ge& q, const fe& d2) {
+  ge_cached c;
+  ge_to_cached(c, q, d2);
+  ge_add_cached(r, p, c, true);
+}
+
+__device__ __forceinline__ void ge_shfl(ge& r, const ge& p, int src) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    r.X.v[i] = (uint32_t)__shfl((int)p.X.v[i], src);
+    r.Y.v[i] = (uint32_t)__shfl((int)p.Y.v[i], src);
+    r.Z.v[i] = (uint32_t)__shfl((int)p.Z.v[i], src);
+    r.T.v[i] = (uint32_t)__shfl((int)p.T.v[i], src);
+  }
+}
+
+// Lane -> (item, which): waves alternate A and R so a wave never mixes the two.
+__global__ __launch_bounds__(256) void k_pip_points(
+    const uint32_t* __restrict__ digests, const uint64_t* __restrict__ offsets, uint64_t b0,
+    uint64_t b1, uint64_t i0, uint64_t i1, uint32_t pmin, const uint32_t* __restrict__ pks,
+    const uint32_t* __restrict__ sigs, const uint32_t* __restrict__ z16, z_key_t zkey,
+    bv_item* __restrict__ items, ge_cached* __restrict__ tabs) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t wave = g >> 6;
+  const int which = (int)(wave & 1);
+  const uint64_t li = (wave >> 1) * 64 + (g & 63);
+  const uint64_t gi = i0 + li;
+  if (gi >= i1) return;
+  const uint64_t lo = batch_of(offsets, b0, b1, gi);
+  const uint64_t bs = offsets[lo], n = offsets[lo + 1] - bs;
+  if (n < pmin) return;
+  const uint64_t t = gi - bs;
+  const pip_region reg = pip_at(tabs, bs - i0, n);
+  const curve_consts& K = g_bc.k;
+  bv_item* it = items + li;
+  ge P;
+  ge_niels q;
+  if (which == 1) {
+    uint32_t Rw[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Rw[j] = sigs[16 * gi + j];
+    const bool ok = ge_frombytes(P, Rw, K);
+    it->pad = ok ? 0u : (uint32_t)BF_R_DECODE;
+    ge_to_niels_z1(q, P, K.d2);
+    reg.pts[2 * t + 1] = q;
+    return;
+  }
+  uint32_t Aw[8], Rw[8], Sw[8], Mw[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    Aw[j] = pks[8 * gi + j];
+    Rw[j] = sigs[16 * gi + j];
+    Sw[j] = sigs[16 * gi + 8 + j];
+    Mw[j] = digests[8 * lo + j];
+  }
+  uint32_t flags = 0;
+  if ((Sw[7] >> 29) != 0) flags |= BF_S_HIGH;
+  sc s;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s.w[j] = Sw[j];
+  if (!sc_is_canonical(s)) flags |= BF_S_NONCANON;
+  uint32_t hx[16];
+  hram96(hx, Rw, Aw, Mw);
+  sc k;
+  sc_reduce512(k, hx);
+  uint32_t zw[4];
+  if (z16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) zw[j] = z16[4 * gi + j];
+  } else {
+    chacha20_z(zw, zkey.key, zkey.nonce, gi);
+  }
+  sc z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z.w[j] = j < 4 ? zw[j] : 0u;
+  sc c, b;
+  sc_mul(c, z, k);
+  if (flags & (BF_S_HIGH | BF_S_NONCANON)) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s.w[j] = 0;   // verdict is decided by the flags
+  }
+  sc_mul(b, z, s);
+  uint32_t cr[8], zr[8];
+  sc_recode(cr, c, 0x80808080u);
+  sc_recode(zr, z, 0x80808080u);
+  if (!ge_frombytes(P, Aw, K)) flags |= BF_A_DECODE;
+  ge_to_niels_z1(q, P, K.d2);
+  reg.pts[2 * t] = q;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    it->c[j] = cr[j];
+    it->b[j] = b.w[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 5; ++j) it->z[j] = zr[j];
+  it->flags = flags;
+  it->key = kNone;
+}
+
+// The nonzero digits of vote t in window w (c_i and, for w <= 16, z_i) as
+// f(local bin, point index, negative); local bins 0..127 are buckets w * 128 + j, and in
+// window 16 local bins 128..191 are the z-carry sub-bins.
+template <typename F>
+__device__ __forceinline__ void pip_window_digits(const bv_item* it, uint64_t t, int w, F&& f) {
+  const uint32_t cw = it->c[w >> 2];
+  const int dc = (int)((cw >> ((w & 3) * 8)) & 255u) - 128;
+  if (dc != 0) {
+    const uint32_t ad = (uint32_t)(dc < 0 ? -dc : dc);
+    const uint32_t lb = w == kPipWin - 1 ? (uint32_t)(kPipTopStride * (t % kPipTopSub)) + ad - 1
+                                         : ad - 1;
+    f(lb, (uint32_t)(2 * t), dc < 0);
+  }
+  if (w < kPipZWin) {
+    const uint32_t zw = it->z[w >> 2];
+    const int dz = (int)((zw >> ((w & 3) * 8)) & 255u) - 128;
+    if (dz != 0) {
+      const uint32_t ad = (uint32_t)(dz < 0 ? -dz : dz);
+      const uint32_t lb = w == kPipZWin - 1 ? (uint32_t)(128 + (t % kPipCarryBins)) : ad - 1;
+      f(lb, (uint32_t)(2 * t + 1), dz < 0);
+    }
+  }
+}
+
+// grid (kPipWin, npip), 1024 threads: histogram of the window's digits in LDS, scan, then
+// scatter with LDS cursors into the window's entry range (capacity 2n).
+__global__ __launch_bounds__(1024) void k_pip_sort(const uint32_t* __restrict__ pip_list,
+                                                   const uint64_t* __restrict__ offsets,
+                                                   uint64_t b0, uint64_t i0,
+                                                   const bv_item* __restrict__ items,
+                                                   ge_cached* __restrict__ tabs) {
+  constexpr int NL = 128 + kPipCarryBins;
+  __shared__ uint32_t s_h[NL], s_c[NL];
+  const uint64_t bidx = b0 + pip_list[blockIdx.y];
+  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
+  const pip_region reg = pip_at(tabs, bs - i0, n);
+  const int w = blockIdx.x, tid = threadIdx.x;
+  const bv_item* its = items + (bs - i0);
+  if (tid < NL) s_h[tid] = 0;
+  __syncthreads();
+  for (uint64_t t = tid; t < n; t += 1024)
+    pip_window_digits(its + t, t, w, [&](uint32_t lb, uint32_t, bool) { atomicAdd(&s_h[lb], 1u); });
+  __syncthreads();
+  // inclusive Hillis-Steele scan over the NL local bins (threads < NL)
+  uint32_t v = tid < NL ? s_h[tid] : 0u;
+  if (tid < NL) s_c[tid] = v;
+  __syncthreads();
+  for (int d = 1; d < NL; d <<= 1) {
+    const uint32_t x = (tid < NL && tid >= d) ? s_c[tid - d] : 0u;
+    __syncthreads();
+    if (tid < NL) s_c[tid] += x;
+    __syncthreads();
+  }
+  const uint32_t base = (uint32_t)(2 * n * (uint64_t)w);
+  if (tid < NL) {
+    const uint32_t ex = s_c[tid] - v;
+    const bool carry = tid >= 128;
+    if (!carry || w == kPipZWin - 1) {
+      const uint32_t bin = carry ? (uint32_t)(kPipWin * 128 + tid - 128) : (uint32_t)(w * 128 + tid);
+      reg.off[bin] = base + ex;
+      reg.cnt[bin] = v;
+    }
+  }
+  __syncthreads();
+  if (tid < NL) s_c[tid] -= v;   // exclusive: cursors
+  __syncthreads();
+  for (uint64_t t = tid; t < n; t += 1024)
+    pip_window_digits(its + t, t, w, [&](uint32_t lb, uint32_t pt, bool neg) {
+      const uint32_t pos = atomicAdd(&s_c[lb], 1u);
+      reg.ent[base + pos] = pt | (neg ? 0x80000000u : 0u);
+    });
+}
+
+// grid (kPipBins * G / 256, npip): lanes [G bin, G bin + G) share bucket bin.
+__global__ __launch_bounds__(256) void k_pip_buckets(const uint32_t* __restrict__ pip_list,
+                                                     const uint64_t* __restrict__ offsets,
+                                                     uint64_t b0, uint64_t i0, uint32_t lg,
+                                                     ge_cached* __restrict__ tabs) {
+  const uint64_t bidx = b0 + pip_list[blockIdx.y];
+  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
+  const pip_region reg = pip_at(tabs, bs - i0, n);
+  const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t bin = gl >> lg, G = 1u << lg, g = gl & (G - 1);
+  if (bin >= (uint32_t)kPipBins) return;   // whole G-groups (kPipBins is a multiple of 64)
+  const uint32_t e0 = reg.off[bin], ne = reg.cnt[bin];
+  const uint32_t a = e0 + (uint32_t)((uint64_t)ne * g >> lg),
+                 e = e0 + (uint32_t)((uint64_t)ne * (g + 1) >> lg);
+  ge acc;
+  ge_identity(acc);
+#pragma unroll 1
+  for (uint32_t k = a; k < e; ++k) {
+    const uint32_t x = reg.ent[k];
+    ge_niels q = reg.pts[x & 0x7fffffffu];
+    ge_niels_cneg(q, (x >> 31) != 0);
+    ge_add_niels(acc, acc, q, true);
+  }
+  const int lane = (int)(threadIdx.x & 63);
+#pragma unroll 1
+  for (uint32_t o = 1; o < G; o <<= 1) {
+    ge other;
+    ge_shfl(other, acc, lane ^ (int)o);
+    ge_add_ge(acc, acc, other, g_bc.k.d2);
+  }
+  if (g == 0) reg.S[bin] = acc;
+}
+
+// grid (kPipWin, npip), one wave per window: sum_b b S_b as a suffix scan over lanes.
+//   windows 0..30: lane l holds buckets 2l+1 and 2l+2, Q_l = S0 + S1, Suf_l = sum_{m>=l} Q_m:
+//     sum_l (2l+1) S0 + (2l+2) S1 = Suf_0 + 2 sum_{l>=1} Suf_l + sum_l S1;
+//     window 16 also adds the z-carry sub-bins (weight 1, lane l holds sub-bin l);
+//   window 31: lane l < 17 folds the kPipTopSub sub-bins of digit l+1 into Q_l, and
+//     sum_l (l+1) Q_l = sum_l Suf_l.
+// Then a tree over lanes.
+__global__ __launch_bounds__(64) void k_pip_windows(const uint32_t* __restrict__ pip_list,
+                                                    const uint64_t* __restrict__ offsets,
+                                                    uint64_t b0, uint64_t i0,
+                                                    ge_cached* __restrict__ tabs) {
+  const uint64_t bidx = b0 + pip_list[blockIdx.y];
+  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
+  const pip_region reg = pip_at(tabs, bs - i0, n);
+  const int w = blockIdx.x, l = threadIdx.x;
+  const fe& d2 = g_bc.k.d2;
+  const bool top = w == kPipWin - 1;
+  ge suf, t;
+  if (top) {
+    ge_identity(suf);
+    if (l < kPipTopStride) {
+#pragma unroll 1
+      for (int k = 0; k < kPipTopSub; ++k)
+        ge_add_ge(suf, suf, reg.S[w * 128 + kPipTopStride * k + l], d2);
+    }
+  } else {
+    ge_add_ge(suf, reg.S[w * 128 + 2 * l], reg.S[w * 128 + 2 * l + 1], d2);
+  }
+#pragma unroll 1
+  for (int d = 1; d < 64; d <<= 1) {
+    ge_shfl(t, suf, l + d < 64 ? l + d : l);
+    if (l + d < 64) ge_add_ge(suf, suf, t, d2);
+  }
+  ge y;
+  if (top) {
+    y = suf;
+  } else {
+    if (l >= 1) ge_dbl(y, suf, true);
+    else y = suf;
+    ge_add_ge(y, y, reg.S[w * 128 + 2 * l + 1], d2);
+    if (w == kPipZWin - 1) ge_add_ge(y, y, reg.S[kPipWin * 128 + l], d2);
+  }
+#pragma unroll 1
+  for (int o = 32; o > 0; o >>= 1) {
+    ge_shfl(t, y, l ^ o);
+    ge_add_ge(y, y, t, d2);
+  }
+  if (l == 0) {
+    ge_cached c;
+    ge_to_cached(c, y, d2);
+    reg.W[w] = c;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pip_final(const uint32_t* __restrict__ pip_list,
+                                                   const uint64_t* __restrict__ offsets,
+                                                   uint64_t b0, uint64_t i0,
+                                                   const bv_item* __restrict__ items,
+                                                   ge_cached* __restrict__ tabs,
+                                                   int32_t* __restrict__ status,
+                                                   uint64_t* __restrict__ fail_index) {
+  __shared__ ge_niels s_btab[129];
+  __shared__ uint32_t s_b[256][8];
+  __shared__ uint32_t s_f[256][4];
+  load_btab(s_btab);
+  const uint64_t bidx = b0 + pip_list[blockIdx.x];
+  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
+  const pip_region reg = pip_at(tabs, bs - i0, n);
+  const int tid = threadIdx.x;
+  const bv_item* its = items + (bs - i0);
+  sc bsum;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bsum.w[j] = 0;
+  uint32_t f[3] = {kNone, kNone, kNone}, flags0 = 0;
+  for (uint64_t t = tid; t < n; t += 256) {
+    const uint32_t fl = its[t].flags | its[t].pad;
+    if ((fl & (BF_S_HIGH | BF_A_DECODE)) && f[0] == kNone) { f[0] = (uint32_t)t; flags0 = fl; }
+    if ((fl & BF_S_NONCANON) && f[1] == kNone) f[1] = (uint32_t)t;
+    if ((fl & BF_R_DECODE) && f[2] == kNone) f[2] = (uint32_t)t;
+    sc bi;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bi.w[j] = its[t].b[j];
+    sc_add(bsum, bsum, bi);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s_b[tid][j] = bsum.w[j];
+  s_f[tid][0] = f[0]; s_f[tid][1] = f[1]; s_f[tid][2] = f[2]; s_f[tid][3] = flags0;
+  __syncthreads();
+  for (int stride = 128; stride > 0; stride >>= 1) {
+    if (tid < stride) {
+      sc a, c;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { a.w[j] = s_b[tid][j]; c.w[j] = s_b[tid + stride][j]; }
+      sc_add(a, a, c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s_b[tid][j] = a.w[j];
+      if (s_f[tid + stride][0] < s_f[tid][0]) {
+        s_f[tid][0] = s_f[tid + stride][0];
+        s_f[tid][3] = s_f[tid + stride][3];
+      }
+      s_f[tid][1] = min(s_f[tid][1], s_f[tid + stride][1]);
+      s_f[tid][2] = min(s_f[tid][2], s_f[tid + stride][2]);
+    }
+    __syncthreads();
+  }
+  // Horner over the windows on one quad (nw_quad.hpp): wave 0 runs it, every quad the same
+  if (tid >= 64) return;
+  const qmask q = quad_mask(tid & 3);
+  sc tot, nb;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) tot.w[j] = s_b[0][j];
+  sc_neg(nb, tot);
+  uint32_t bb[8];
+  sc_recode(bb, nb, 0x80808080u);
+  fe v, tab;
+  quad_identity(v, q);
+#pragma unroll 1
+  for (int w = kPipWin - 1; w >= 0; --w) {
+    if (w != kPipWin - 1) {
+#pragma unroll 1
+      for (int k = 0; k < 8; ++k) quad_dbl(v, q);
+    }
+    quad_cached_component(tab, q, reg.W[w]);
+    quad_add(v, q, tab);
+    const int e = digit8(bb, w);
+    quad_niels_component(tab, q, s_btab[e < 0 ? -e : e], e < 0);
+    quad_add(v, q, tab);
+  }
+  const bool ident = quad_is_identity(v);
+  if (tid != 0) return;
+  const uint32_t ff[3] = {s_f[0][0], s_f[0][1], s_f[0][2]};
+  uint64_t idx;
+  const int st = batch_status(ff, s_f[0][3], ident, n, &idx);
+  status[bidx] = st;
+  if (fail_index) fail_index[bidx] = idx;
+}
+
 inline size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct bv_ws {
@@ -555,6 +989,7 @@ struct bv_ws {
   uint32_t* multi;
   uint32_t* multi_first;
   uint32_t* chunk_start;
+  uint32_t* pip_list;
 };
 
 size_t bv_layout(uint64_t units, char* base, bv_ws* w) {
@@ -570,9 +1005,10 @@ size_t bv_layout(uint64_t units, char* base, bv_ws* w) {
     w->outs = reinterpret_cast<bv_chunk_out*>(p); p += s_out;
     w->multi = reinterpret_cast<uint32_t*>(p); p += s_m;
     w->multi_first = reinterpret_cast<uint32_t*>(p); p += s_m;
+    w->pip_list = reinterpret_cast<uint32_t*>(p); p += s_m;
     w->chunk_start = reinterpret_cast<uint32_t*>(p);
   }
-  return s_items + s_tabs + s_ch + s_out + 2 * s_m + a256(4 * (u + 1));
+  return s_items + s_tabs + s_ch + s_out + 3 * s_m + a256(4 * (u + 1));
 }
 
 }  // namespace
@@ -669,30 +1105,58 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
   const uint64_t target_lanes = 256ull * 4 * 2 * 64;
   uint32_t C = (uint32_t)std::min<uint64_t>(kMaxChunk, std::max<uint64_t>(1, nitems / target_lanes));
   C = (uint32_t)std::min<uint64_t>(kMaxChunk, env_u64("NW_BATCH_CHUNK", C));
+  // Batches of at least pmin votes take the Pippenger path (NW_BATCH_PIPPENGER_MIN test
+  // hook; never below kPipFloor, whose item slots are the smallest that hold the region).
+  const uint32_t pmin = (uint32_t)std::max<uint64_t>(
+      kPipFloor, std::min<uint64_t>(0xffffffffu, env_u64("NW_BATCH_PIPPENGER_MIN", kPipMin)));
   uint64_t b = 0;
   while (b < nbatches) {
     // slice [b, e): items + batches <= cap
-    uint64_t e = b, items = 0, chunks = 0, multi = 0;
+    uint64_t e = b, items = 0, chunks = 0, multi = 0, npip = 0, pmax = 0;
     while (e < nbatches) {
       const uint64_t n = host_offsets[e + 1] - host_offsets[e];
       if (e > b && items + n + (e - b + 1) > cap) break;
       if (n + 1 > cap) return hipErrorInvalidValue;   // one batch larger than a slice
       items += n;
-      const uint64_t kb = (n + C - 1) / C;
-      chunks += kb;
-      multi += kb != 1;
+      if (n >= pmin) {
+        ++npip;
+        pmax = std::max(pmax, n);
+      } else {
+        const uint64_t kb = (n + C - 1) / C;
+        chunks += kb;
+        multi += kb != 1;
+      }
       ++e;
     }
     const uint64_t i0 = host_offsets[b], i1 = host_offsets[e];
-    hipLaunchKernelGGL(k_bv_plan, dim3(1), dim3(1024), 0, stream, offsets, b, e, C,
-                       w.chunk_start, w.multi, w.multi_first);
+    hipLaunchKernelGGL(k_bv_plan, dim3(1), dim3(1024), 0, stream, offsets, b, e, C, pmin,
+                       w.chunk_start, w.multi, w.multi_first, w.pip_list);
     if (chunks)
       hipLaunchKernelGGL(k_bv_expand, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
                          stream, offsets, b, e - b, (uint32_t)chunks, w.chunk_start, w.chunks);
-    if (i1 > i0)
+    if (i1 > i0 && npip != e - b)
       hipLaunchKernelGGL(k_bv_items, dim3((unsigned)((i1 - i0 + 255) / 256)), dim3(256), 0,
-                         stream, digests, offsets, b, e, i0, i1, pks, sigs, z16, zkey, w.items,
-                         w.tabs, kt);
+                         stream, digests, offsets, b, e, i0, i1, pmin, pks, sigs, z16, zkey,
+                         w.items, w.tabs, kt);
+    if (npip) {
+      hipLaunchKernelGGL(k_pip_points, dim3((unsigned)((i1 - i0 + 63) / 64 * 2 * 64 + 255) / 256),
+                         dim3(256), 0, stream, digests, offsets, b, e, i0, i1, pmin, pks, sigs,
+                         z16, zkey, w.items, w.tabs);
+      hipLaunchKernelGGL(k_pip_sort, dim3(kPipWin, (unsigned)npip), dim3(1024), 0, stream,
+                         w.pip_list, offsets, b, i0, w.items, w.tabs);
+      // G lanes per bucket: about 8 additions each at the largest batch's mean bucket size
+      // (49 digits per vote over kPipBins buckets)
+      uint32_t lg = 0;
+      while (lg < 6 && (49 * pmax) / kPipBins > 8ull << lg) ++lg;
+      // ... but no more lanes than the chip runs at once (the shuffle tree is overhead)
+      while (lg > 0 && ((npip * kPipBins) << lg) > (1ull << 20)) --lg;
+      hipLaunchKernelGGL(k_pip_buckets, dim3(((kPipBins << lg) + 255) / 256, (unsigned)npip), dim3(256),
+                         0, stream, w.pip_list, offsets, b, i0, lg, w.tabs);
+      hipLaunchKernelGGL(k_pip_windows, dim3(kPipWin, (unsigned)npip), dim3(64), 0, stream,
+                         w.pip_list, offsets, b, i0, w.tabs);
+      hipLaunchKernelGGL(k_pip_final, dim3((unsigned)npip), dim3(256), 0, stream, w.pip_list,
+                         offsets, b, i0, w.items, w.tabs, status, fail_index);
+    }
     if (chunks)
       hipLaunchKernelGGL(k_bv_chunks, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
                          stream, w.chunks, (uint32_t)chunks, offsets, b, i0, w.items, w.tabs,

@@ -12,10 +12,25 @@ pytestmark = pytest.mark.gpu
 L_ORDER = 2**252 + 27742317777372353535851937790883648493
 
 
-def _corpus(nb, seed, max_n=40, empty=True):
-    rng = np.random.Generator(np.random.PCG64(seed))
-    sizes = rng.integers(0 if empty else 1, max_n + 1, size=nb)
-    sizes[0] = 0 if empty else sizes[0]
+def _mutate(sigs, pk, i, c):
+    """One vote broken in failure class c (0..5)."""
+    if c == 0:
+        sigs[i, 40] ^= 1                        # equation
+    elif c == 1:
+        sigs[i, 63] |= 0x20                     # s high bits
+    elif c == 2:
+        v = int.from_bytes(sigs[i, 32:].tobytes(), "little") + L_ORDER
+        sigs[i, 32:] = np.frombuffer(v.to_bytes(32, "little"), np.uint8)   # s >= l
+    elif c == 3:
+        sigs[i, :32] = np.frombuffer((2).to_bytes(32, "little"), np.uint8)  # R off-curve
+    elif c == 4:
+        pk[i] = np.frombuffer((7).to_bytes(32, "little"), np.uint8)         # A off-curve
+    else:
+        sigs[i, :32] = 0                        # R = small-order point (y = 0)
+
+
+def _corpus_sizes(sizes, rng, every=4):
+    nb = len(sizes)
     off = np.zeros(nb + 1, np.uint64)
     off[1:] = np.cumsum(sizes)
     n = int(off[-1])
@@ -27,25 +42,20 @@ def _corpus(nb, seed, max_n=40, empty=True):
     bidx = np.repeat(np.arange(nb), sizes)
     sigs = C.sign_many(sks, dig[bidx])
     pk = pks[key].copy()
-    # mutate ~1 in 4 non-empty batches, one vote each, with every failure class
-    for b in np.nonzero(sizes)[0][::4]:
+    # mutate 1 in `every` non-empty batches (none for every=0), one vote each, with every
+    # failure class
+    for b in (np.nonzero(sizes)[0][::every] if every else []):
         i = int(off[b] + rng.integers(0, sizes[b]))
-        c = int(rng.integers(0, 6))
-        if c == 0:
-            sigs[i, 40] ^= 1                        # equation
-        elif c == 1:
-            sigs[i, 63] |= 0x20                     # s high bits
-        elif c == 2:
-            v = int.from_bytes(sigs[i, 32:].tobytes(), "little") + L_ORDER
-            sigs[i, 32:] = np.frombuffer(v.to_bytes(32, "little"), np.uint8)   # s >= l
-        elif c == 3:
-            sigs[i, :32] = np.frombuffer((2).to_bytes(32, "little"), np.uint8)  # R off-curve
-        elif c == 4:
-            pk[i] = np.frombuffer((7).to_bytes(32, "little"), np.uint8)         # A off-curve
-        else:
-            sigs[i, :32] = 0                        # R = small-order point (y = 0)
+        _mutate(sigs, pk, i, int(rng.integers(0, 6)))
     z16 = rng.integers(0, 256, size=(max(n, 1), 16), dtype=np.uint8)
     return dig, pk, sigs, off, z16
+
+
+def _corpus(nb, seed, max_n=40, empty=True):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sizes = rng.integers(0 if empty else 1, max_n + 1, size=nb)
+    sizes[0] = 0 if empty else sizes[0]
+    return _corpus_sizes(sizes, rng)
 
 
 @pytest.mark.parametrize("chunk,slice_units", [("1", ""), ("4", ""), ("128", ""), ("3", "97")])
@@ -97,3 +107,69 @@ def test_large_uniform_batches(monkeypatch, chunk):
     exp = np.zeros(nb, np.int32)
     exp[bad] = 7
     assert np.array_equal(st, exp)
+
+
+# ---- Pippenger path (batches of >= NW_BATCH_PIPPENGER_MIN votes) -------------------------
+@pytest.mark.parametrize("slice_units", ["", "2600"])
+def test_pippenger_mixed_vs_oracle(monkeypatch, slice_units):
+    """Large batches (Pippenger) interleaved with small ones (Straus) in one call, every
+    failure class, several slices: status and first failing index bit-exact."""
+    monkeypatch.setenv("NW_BATCH_PIPPENGER_MIN", "400")
+    monkeypatch.setenv("NW_BATCH_SLICE_UNITS", slice_units)
+    rng = np.random.Generator(np.random.PCG64(11 + len(slice_units)))
+    sizes = np.array([400, 3, 0, 1200, 17, 401, 650, 2, 399, 900, 512, 1000], np.int64)
+    dig, pk, sigs, off, z16 = _corpus_sizes(sizes, rng, every=1)
+    # a second failure later in some large batches: the first one must be reported
+    for b in (3, 6, 9):
+        i = int(off[b + 1]) - 5
+        _mutate(sigs, pk, i, 3)
+    st = C.verify_batch_many(dig, pk, sigs, off, z16)
+    for b in range(len(sizes)):
+        a, e = int(off[b]), int(off[b + 1])
+        ost, oidx = O.verify_batch(dig[b].tobytes(), pk[a:e], sigs[a:e], z16[a:e])
+        assert st[b] == ost, (b, st[b], ost)
+        votes = [(C.PublicKey(pk[i].tobytes()), C.Signature.from_bytes(sigs[i].tobytes()))
+                 for i in range(a, e)]
+        try:
+            C.Signature.verify_batch(C.Digest(dig[b].tobytes()), votes,
+                                     z16=z16[a:e].tobytes())
+            got = (0, None)
+        except C.CryptoError as err:
+            got = (err.code, err.index)
+        assert got[0] == ost, b
+        if ost:
+            assert got[1] == oidx, (b, got, oidx)
+
+
+def test_pippenger_valid_and_equation(monkeypatch):
+    """Honest large batches are Ok with random (device ChaCha20) and with injected z; one
+    bad equation anywhere is Err 7; skewed z (all equal: every vote in the same buckets)."""
+    rng = np.random.Generator(np.random.PCG64(21))
+    sizes = np.array([10000, 4096, 777], np.int64)
+    dig, pk, sigs, off, z16 = _corpus_sizes(sizes, rng, every=0)
+    assert (C.verify_batch_many(dig, pk, sigs, off) == 0).all()
+    assert (C.verify_batch_many(dig, pk, sigs, off, z16) == 0).all()
+    same = np.tile(z16[:1], (len(z16), 1))
+    assert (C.verify_batch_many(dig, pk, sigs, off, same) == 0).all()
+    sigs[int(off[1]) + 4000, 35] ^= 0x10
+    st = C.verify_batch_many(dig, pk, sigs, off, same)
+    assert list(st) == [0, 7, 0]
+    st = C.verify_batch_many(dig, pk, sigs, off)
+    assert list(st) == [0, 7, 0]
+
+
+def test_pippenger_config1_shape():
+    """Config 1: 10k pairs on the reference digest, default threshold; the Err
+    variant has vote 9,999 = Signature::default()."""
+    rng = np.random.Generator(np.random.PCG64(31))
+    dig, pk, sigs, off, _ = _corpus_sizes(np.array([10000]), rng, every=0)
+    d = C.Digest(dig[0].tobytes())
+    votes = [(C.PublicKey(pk[i].tobytes()), C.Signature.from_bytes(sigs[i].tobytes()))
+             for i in range(10000)]
+    C.Signature.verify_batch(d, votes)
+    votes[9999] = (votes[9999][0], C.Signature.from_bytes(bytes(64)))
+    with pytest.raises(C.CryptoError) as e:
+        C.Signature.verify_batch(d, votes)
+    ost, oidx = O.verify_batch(dig[0].tobytes(), pk, np.concatenate(
+        [sigs[:9999], np.zeros((1, 64), np.uint8)]), rng.integers(0, 256, (10000, 16), dtype=np.uint8))
+    assert (e.value.code, e.value.index) == (ost, oidx)
