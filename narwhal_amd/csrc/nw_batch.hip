@@ -597,22 +597,29 @@ constexpr int kPipBins = kPipWin * 128 + kPipCarryBins;
 struct pip_region {
   ge_niels* pts;     // 2n: A_t at 2t, R_t at 2t + 1
   uint32_t* ent;     // window w: entries [2n w, 2n w + 2n), point index | sign << 31
+  uint8_t* cd;       // 32 x n, window-major: byte w of recoded c_t at cd[w n + t]
+  uint8_t* zd;       // 17 x n (+ pad): byte w of recoded z_t at zd[w n + t]
   uint32_t* cnt;     // kPipBins: entries per bucket
   uint32_t* off;     // kPipBins: first entry of each bucket
   ge* S;             // kPipBins bucket sums
   ge_cached* W;      // kPipWin window sums (cached form, for the Horner)
 };
 
-__host__ __device__ inline size_t pip_region_bytes(uint64_t n) {
-  return 2 * n * sizeof(ge_niels) + 4 * kPipWinCap * n + 8 * kPipBins +
-         sizeof(ge) * (kPipBins + kPipWin);
+constexpr size_t pip_region_bytes(uint64_t n) {
+  return 2 * n * sizeof(ge_niels) + 4 * kPipWinCap * n + 52 * n + 8 * kPipBins +
+         sizeof(ge) * kPipBins + sizeof(ge_cached) * kPipWin;
 }
+// per-vote bytes grow slower than the item slots (2560 B), so the floor is the binding n
+static_assert(pip_region_bytes(kPipFloor) <= 16 * sizeof(ge_cached) * kPipFloor,
+              "Pippenger region does not fit its items' table slots");
 
 __device__ __forceinline__ pip_region pip_at(ge_cached* tabs, uint64_t li0, uint64_t n) {
   char* p = reinterpret_cast<char*>(tabs + 16 * li0);
   pip_region r;
   r.pts = reinterpret_cast<ge_niels*>(p); p += 2 * n * sizeof(ge_niels);
   r.ent = reinterpret_cast<uint32_t*>(p); p += 4 * kPipWinCap * n;
+  r.cd = reinterpret_cast<uint8_t*>(p); p += 32 * n;
+  r.zd = reinterpret_cast<uint8_t*>(p); p += 20 * n;
   r.cnt = reinterpret_cast<uint32_t*>(p); p += 4 * kPipBins;
   r.off = reinterpret_cast<uint32_t*>(p); p += 4 * kPipBins;
   r.S = reinterpret_cast<ge*>(p); p += sizeof(ge) * kPipBins;
@@ -726,12 +733,11 @@ __global__ __launch_bounds__(256) void k_pip_points(
   ge_to_niels_z1(q, P, K.d2);
   reg.pts[2 * t] = q;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    it->c[j] = cr[j];
-    it->b[j] = b.w[j];
-  }
+  for (int j = 0; j < 8; ++j) it->b[j] = b.w[j];
 #pragma unroll
-  for (int j = 0; j < 5; ++j) it->z[j] = zr[j];
+  for (int w = 0; w < kPipWin; ++w) reg.cd[w * n + t] = (uint8_t)(cr[w >> 2] >> ((w & 3) * 8));
+#pragma unroll
+  for (int w = 0; w < kPipZWin; ++w) reg.zd[w * n + t] = (uint8_t)(zr[w >> 2] >> ((w & 3) * 8));
   it->flags = flags;
   it->key = kNone;
 }
@@ -740,9 +746,9 @@ __global__ __launch_bounds__(256) void k_pip_points(
 // f(local bin, point index, negative); local bins 0..127 are buckets w * 128 + j, and in
 // window 16 local bins 128..191 are the z-carry sub-bins.
 template <typename F>
-__device__ __forceinline__ void pip_window_digits(const bv_item* it, uint64_t t, int w, F&& f) {
-  const uint32_t cw = it->c[w >> 2];
-  const int dc = (int)((cw >> ((w & 3) * 8)) & 255u) - 128;
+__device__ __forceinline__ void pip_window_digits(const pip_region& reg, uint64_t n, uint64_t t,
+                                                  int w, F&& f) {
+  const int dc = (int)reg.cd[w * n + t] - 128;
   if (dc != 0) {
     const uint32_t ad = (uint32_t)(dc < 0 ? -dc : dc);
     const uint32_t lb = w == kPipWin - 1 ? (uint32_t)(kPipTopStride * (t % kPipTopSub)) + ad - 1
@@ -750,8 +756,7 @@ __device__ __forceinline__ void pip_window_digits(const bv_item* it, uint64_t t,
     f(lb, (uint32_t)(2 * t), dc < 0);
   }
   if (w < kPipZWin) {
-    const uint32_t zw = it->z[w >> 2];
-    const int dz = (int)((zw >> ((w & 3) * 8)) & 255u) - 128;
+    const int dz = (int)reg.zd[w * n + t] - 128;
     if (dz != 0) {
       const uint32_t ad = (uint32_t)(dz < 0 ? -dz : dz);
       const uint32_t lb = w == kPipZWin - 1 ? (uint32_t)(128 + (t % kPipCarryBins)) : ad - 1;
@@ -773,11 +778,10 @@ __global__ __launch_bounds__(1024) void k_pip_sort(const uint32_t* __restrict__ 
   const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
   const pip_region reg = pip_at(tabs, bs - i0, n);
   const int w = blockIdx.x, tid = threadIdx.x;
-  const bv_item* its = items + (bs - i0);
   if (tid < NL) s_h[tid] = 0;
   __syncthreads();
   for (uint64_t t = tid; t < n; t += 1024)
-    pip_window_digits(its + t, t, w, [&](uint32_t lb, uint32_t, bool) { atomicAdd(&s_h[lb], 1u); });
+    pip_window_digits(reg, n, t, w, [&](uint32_t lb, uint32_t, bool) { atomicAdd(&s_h[lb], 1u); });
   __syncthreads();
   // inclusive Hillis-Steele scan over the NL local bins (threads < NL)
   uint32_t v = tid < NL ? s_h[tid] : 0u;
@@ -803,7 +807,7 @@ __global__ __launch_bounds__(1024) void k_pip_sort(const uint32_t* __restrict__ 
   if (tid < NL) s_c[tid] -= v;   // exclusive: cursors
   __syncthreads();
   for (uint64_t t = tid; t < n; t += 1024)
-    pip_window_digits(its + t, t, w, [&](uint32_t lb, uint32_t pt, bool neg) {
+    pip_window_digits(reg, n, t, w, [&](uint32_t lb, uint32_t pt, bool neg) {
       const uint32_t pos = atomicAdd(&s_c[lb], 1u);
       reg.ent[base + pos] = pt | (neg ? 0x80000000u : 0u);
     });
@@ -825,11 +829,19 @@ __global__ __launch_bounds__(256) void k_pip_buckets(const uint32_t* __restrict_
                  e = e0 + (uint32_t)((uint64_t)ne * (g + 1) >> lg);
   ge acc;
   ge_identity(acc);
+  // the next entry's point is fetched while the current one is added
+  uint32_t x = a < e ? reg.ent[a] : 0u;
+  ge_niels nx;
+  if (a < e) nx = reg.pts[x & 0x7fffffffu];
 #pragma unroll 1
   for (uint32_t k = a; k < e; ++k) {
-    const uint32_t x = reg.ent[k];
-    ge_niels q = reg.pts[x & 0x7fffffffu];
-    ge_niels_cneg(q, (x >> 31) != 0);
+    ge_niels q = nx;
+    const bool neg = (x >> 31) != 0;
+    if (k + 1 < e) {
+      x = reg.ent[k + 1];
+      nx = reg.pts[x & 0x7fffffffu];
+    }
+    ge_niels_cneg(q, neg);
     ge_add_niels(acc, acc, q, true);
   }
   const int lane = (int)(threadIdx.x & 63);
