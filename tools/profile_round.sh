@@ -5,7 +5,8 @@
 #   2. PMC passes, one counter group per rocprofv3 run (MI355X_MICROARCH.md: FETCH_SIZE and
 #      WRITE_SIZE cannot share a pass), over one untimed-warmup-free bench step of the
 #      config-4 strict leg and the config-3 SHA-512 leg at their full bench sizes, so the
-#      per-dispatch counters are per bench launch.
+#      per-dispatch counters are per bench launch; then the same over one config-1
+#      verify_batch step (the Pippenger kernels, 64 resident 10k batches).
 # Usage (on the GPU box): bash tools/profile_round.sh TAG   -> gpurun_out/prof_TAG/
 # Summarise here with: python tools/profile_summary.py gpurun_out/prof_TAG profiles/TAG
 set -o pipefail
@@ -36,4 +37,9 @@ pmc fetch FETCH_SIZE && \
 pmc write WRITE_SIZE && \
 pmc sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES \
   SQ_BUSY_CYCLES SQ_WAIT_INST_ANY && \
-pmc grbm GRBM_GUI_ACTIVE GRBM_COUNT
+pmc grbm GRBM_GUI_ACTIVE GRBM_COUNT && \
+PMC_ARGS="--workload batch --steps 1 --warmup 0 --no-cpu-baseline" && \
+pmc batch_fetch FETCH_SIZE && \
+pmc batch_write WRITE_SIZE && \
+pmc batch_sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES \
+  SQ_BUSY_CYCLES SQ_WAIT_INST_ANY
