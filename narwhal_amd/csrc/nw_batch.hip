@@ -813,15 +813,27 @@ __global__ __launch_bounds__(1024) void k_pip_sort(const uint32_t* __restrict__ 
     });
 }
 
-// grid (kPipBins * G / 256, npip): lanes [G bin, G bin + G) share bucket bin.
+// grid (bpb = kPipBins * G / 256 blocks per batch, npip): lanes [G bin, G bin + G) share
+// bucket bin. xcd: 1-D grid of 8 * bpb * ceil(npip / 8) blocks, remapped so that every
+// block of a batch runs on one XCD (workgroups are dealt round-robin over the 8 XCDs) and
+// each XCD walks its batches one after another: the batch's points (2n x 120 B, gathered
+// at random by its buckets) then stay in that XCD's L2 instead of in all eight.
 __global__ __launch_bounds__(256) void k_pip_buckets(const uint32_t* __restrict__ pip_list,
                                                      const uint64_t* __restrict__ offsets,
                                                      uint64_t b0, uint64_t i0, uint32_t lg,
+                                                     uint32_t npip, uint32_t bpb, int xcd,
                                                      ge_cached* __restrict__ tabs) {
-  const uint64_t bidx = b0 + pip_list[blockIdx.y];
+  uint32_t jb = blockIdx.y, xb = blockIdx.x;
+  if (xcd) {
+    const uint32_t k = blockIdx.x >> 3;
+    jb = (blockIdx.x & 7) + 8 * (k / bpb);
+    xb = k % bpb;
+    if (jb >= npip) return;
+  }
+  const uint64_t bidx = b0 + pip_list[jb];
   const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
   const pip_region reg = pip_at(tabs, bs - i0, n);
-  const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t gl = xb * blockDim.x + threadIdx.x;
   const uint32_t bin = gl >> lg, G = 1u << lg, g = gl & (G - 1);
   if (bin >= (uint32_t)kPipBins) return;   // whole G-groups (kPipBins is a multiple of 64)
   const uint32_t e0 = reg.off[bin], ne = reg.cnt[bin];
@@ -1161,9 +1173,12 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
       uint32_t lg = 0;
       while (lg < 6 && (49 * pmax) / kPipBins > 8ull << lg) ++lg;
       // ... but no more lanes than the chip runs at once (the shuffle tree is overhead)
-      while (lg > 0 && ((npip * kPipBins) << lg) > (1ull << 20)) --lg;
-      hipLaunchKernelGGL(k_pip_buckets, dim3(((kPipBins << lg) + 255) / 256, (unsigned)npip), dim3(256),
-                         0, stream, w.pip_list, offsets, b, i0, lg, w.tabs);
+      while (lg > 0 && ((npip * kPipBins) << lg) > (1ull << 21)) --lg;
+      const uint32_t bpb = ((kPipBins << lg) + 255) / 256;
+      const int xcd = npip >= 8;
+      const dim3 gb = xcd ? dim3((unsigned)(8 * bpb * ((npip + 7) / 8))) : dim3(bpb, (unsigned)npip);
+      hipLaunchKernelGGL(k_pip_buckets, gb, dim3(256), 0, stream, w.pip_list, offsets, b, i0, lg,
+                         (uint32_t)npip, bpb, xcd, w.tabs);
       hipLaunchKernelGGL(k_pip_windows, dim3(kPipWin, (unsigned)npip), dim3(64), 0, stream,
                          w.pip_list, offsets, b, i0, w.tabs);
       hipLaunchKernelGGL(k_pip_final, dim3((unsigned)npip), dim3(256), 0, stream, w.pip_list,
