@@ -239,7 +239,44 @@ def run_sha(args, dev, stream, rank, world):
     ok = all(o[i].tobytes() == expect[i % uniq] for i in range(0, nb, max(1, nb // 997)))
     ok &= all(o[i].tobytes() == expect[i % uniq] for i in range(uniq))
     del data, data_u
-    return dict(n=nb, bytes=nb * W.BATCH_BYTES, elapsed=elapsed, kernel_ms=kernel_ms, parity=ok)
+    return dict(n=nb, bytes=nb * W.BATCH_BYTES, elapsed=elapsed, kernel_ms=kernel_ms, parity=ok,
+                sample=(ub, expect))
+
+
+def cpu_baseline_sha(sample, seconds: float):
+    """sha2-equivalent SHA-512 on the host cores: the oracle's C restatement
+    (oracle/nw_oracle.c, 'port') over the unique config-3 worker batches, one batch per
+    thread, passes until about ``seconds``; digests checked against hashlib. OpenSSL's
+    SHA-512 (hashlib, one batch per thread) is timed beside it for context."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle as O
+    ub, expect = sample
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    n = len(ub)
+    data = np.ascontiguousarray(ub).reshape(-1)
+    offs = np.arange(n, dtype=np.uint64) * W.BATCH_BYTES
+    lens = np.full(n, W.BATCH_BYTES, dtype=np.uint64)
+    t0 = time.perf_counter()
+    out = O.sha512_digest32_many(data, offs, lens, nthreads=threads)
+    ok = all(out[i].tobytes() == expect[i] for i in range(n))
+    passes = 1
+    while time.perf_counter() - t0 < seconds:
+        O.sha512_digest32_many(data, offs, lens, nthreads=threads)
+        passes += 1
+    dt = time.perf_counter() - t0
+    msgs = [ub[i].tobytes() for i in range(n)]
+    t1, op = time.perf_counter(), 0
+    with ThreadPoolExecutor(threads) as ex:
+        while time.perf_counter() - t1 < seconds / 2:
+            list(ex.map(lambda b: hashlib.sha512(b).digest(), msgs))
+            op += 1
+    dt1 = time.perf_counter() - t1
+    return dict(value=passes * n * W.BATCH_BYTES / dt / 1e9, unit="GB/s", cores=threads,
+                kind="port", sample=f"{passes} passes over {n} unique {W.BATCH_BYTES}-B worker "
+                                    f"batches, oracle sha512_digest32_many, {threads} threads, "
+                                    f"{dt:.1f} s",
+                openssl_GB_per_s=op * n * W.BATCH_BYTES / dt1 / 1e9,
+                parity="ok" if ok else "FAIL")
 
 
 def run_cert(args, dev, stream, rank, world, N: int):
@@ -530,6 +567,9 @@ def main():
                                 "traffic": straffic, "traffic_source": ssrc,
                                 "algorithmic_bytes": s["bytes"] + 32 * s["n"],
                                 "parity": "ok" if s["parity"] else "FAIL"}
+            if rank == 0 and world == 1 and not args.no_cpu_baseline:
+                result["sha512"]["cpu_baseline"] = cpu_baseline_sha(s["sample"],
+                                                                    min(3.0, args.cpu_seconds))
             if not s["parity"]:
                 result["parity"] = "FAIL"
         if not args.no_cert:
@@ -597,6 +637,8 @@ def main():
                          "kernel": "k_sha512_digest32", "kernel_ms": s["kernel_ms"]},
             "parity": "ok" if s["parity"] else "FAIL",
         }
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline_sha(s["sample"], min(3.0, args.cpu_seconds))
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
