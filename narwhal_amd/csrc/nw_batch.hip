@@ -1,10 +1,11 @@
 // nw_batch.hip — crypto::Signature::verify_batch (crypto/src/lib.rs:206-219 -> dalek
-// verify_batch [ext]) for many independent batches, as a chunked Straus multi-scalar
-// multiplication:
+// verify_batch [ext]) for many independent batches: a chunked Straus multi-scalar
+// multiplication for small batches (certificates), a Pippenger bucket MSM (k_pip_*, below)
+// for batches of at least NW_BATCH_PIPPENGER_MIN votes:
 //
 //   sum_i z_i R_i + sum_i (z_i k_i mod l) A_i - (sum_i z_i s_i mod l) B == identity
 //
-//   k_bv_plan     one workgroup per slice: splits every batch into ceil(n_b / C) balanced
+//   k_bv_plan_*   a block scan per slice: splits every batch into ceil(n_b / C) balanced
 //                 chunks (block-wide scan) and lists the batches that need a combine step.
 //   k_bv_items    one lane per vote: parse/decode flags, k_i = H(R||A||M) mod l, z_i
 //                 (ChaCha20 or injected), c_i = z_i k_i, b_i = z_i s_i, signed 4-bit
@@ -57,7 +58,8 @@ uint64_t env_u64(const char* name, uint64_t dflt) {
   const unsigned long long x = strtoull(v, nullptr, 10);
   return x ? (uint64_t)x : dflt;
 }
-uint64_t slice_units() { return env_u64("NW_BATCH_SLICE_UNITS", kSliceUnits); }
+// (never above kSliceUnits: k_bv_plan_top scans at most 4096 plan blocks)
+uint64_t slice_units() { return std::min(env_u64("NW_BATCH_SLICE_UNITS", kSliceUnits), kSliceUnits); }
 constexpr uint32_t kMaxChunk = 128;
 constexpr uint32_t kNone = 0xffffffffu;
 
@@ -147,59 +149,116 @@ __device__ void chacha20_z(uint32_t z[4], const uint32_t key[8], uint64_t nonce,
 }
 
 // ------------------------------------------------------------------------------ plan
-// k_bv_plan: one workgroup (1024 threads) per slice of batches [b0, b1): chunk counts
-// k_b = ceil(n_b / C) (0 for an empty batch) and their exclusive block scan -> chunk_start
-// (nb + 1 entries), plus the list of batches that need k_bv_combine (k_b != 1).
+// Plan of a slice of batches [b0, b1), three passes of 1024-batch blocks (a decoupled
+// block scan; one workgroup looping over a million batches took 3.3 ms):
+//   k_bv_plan_local  per batch: chunk count k_b = ceil(n_b / C) (0 for an empty or a
+//                    Pippenger batch), whether it needs k_bv_combine (k_b != 1, not
+//                    Pippenger), whether it is a Pippenger batch; per-block totals.
+//   k_bv_plan_top    one workgroup: exclusive scan of the block totals, and the slice's
+//                    chunk total in chunk_start[nb].
+//   k_bv_plan_apply  per batch: chunk_start (nb + 1 entries), the combine list (multi,
+//                    multi_first) and the Pippenger list.
 // k_bv_expand: one lane per chunk writes its descriptor (balanced split of the batch).
-__global__ __launch_bounds__(1024) void k_bv_plan(const uint64_t* __restrict__ offsets,
-                                                  uint64_t b0, uint64_t b1, uint32_t C,
-                                                  uint32_t pmin,
-                                                  uint32_t* __restrict__ chunk_start,
-                                                  uint32_t* __restrict__ multi,
-                                                  uint32_t* __restrict__ multi_first,
-                                                  uint32_t* __restrict__ pip_list) {
-  __shared__ uint32_t s_a[1024], s_b[1024], s_c[1024];
-  __shared__ uint32_t s_base_a, s_base_b, s_base_c;
+__device__ __forceinline__ void plan_counts(const uint64_t* offsets, uint64_t b, uint64_t b1,
+                                            uint32_t C, uint32_t pmin, uint32_t& kb,
+                                            uint32_t& mflag, uint32_t& pflag) {
+  kb = 0;
+  pflag = 0;
+  if (b < b1) {
+    const uint64_t nb = offsets[b + 1] - offsets[b];
+    pflag = nb >= pmin ? 1u : 0u;   // Pippenger batch: no chunks, no combine
+    kb = pflag ? 0u : (uint32_t)((nb + C - 1) / C);
+  }
+  mflag = (b < b1 && !pflag && kb != 1) ? 1u : 0u;
+}
+
+// Inclusive Hillis-Steele scan of three counters over a 1024-thread block.
+__device__ __forceinline__ void block_scan3(uint32_t v[3], uint32_t (*s)[1024]) {
   const int t = threadIdx.x;
-  if (t == 0) { s_base_a = 0; s_base_b = 0; s_base_c = 0; }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s[k][t] = v[k];
   __syncthreads();
-  for (uint64_t base = b0; base < b1; base += 1024) {
-    const uint64_t b = base + t;
-    uint32_t kb = 0, pflag = 0;
-    if (b < b1) {
-      const uint64_t nb = offsets[b + 1] - offsets[b];
-      pflag = nb >= pmin ? 1u : 0u;   // Pippenger batch: no chunks, no combine
-      kb = pflag ? 0u : (uint32_t)((nb + C - 1) / C);
-    }
-    const uint32_t mflag = (b < b1 && !pflag && kb != 1) ? 1u : 0u;
-    s_a[t] = kb;
-    s_b[t] = mflag;
-    s_c[t] = pflag;
+  for (int d = 1; d < 1024; d <<= 1) {
+    uint32_t x[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) x[k] = t >= d ? s[k][t - d] : 0u;
     __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {   // Hillis-Steele inclusive scan of the counters
-      const uint32_t va = t >= d ? s_a[t - d] : 0u, vb = t >= d ? s_b[t - d] : 0u,
-                     vc = t >= d ? s_c[t - d] : 0u;
-      __syncthreads();
-      s_a[t] += va;
-      s_b[t] += vb;
-      s_c[t] += vc;
-      __syncthreads();
-    }
-    const uint32_t ca = s_base_a + s_a[t] - kb, cb = s_base_b + s_b[t] - mflag,
-                   cc = s_base_c + s_c[t] - pflag;
-    if (b < b1) {
-      chunk_start[b - b0] = ca;
-      if (mflag) {
-        multi[cb] = (uint32_t)(b - b0);
-        multi_first[cb] = ca;
-      }
-      if (pflag) pip_list[cc] = (uint32_t)(b - b0);
-    }
-    __syncthreads();
-    if (t == 1023) { s_base_a += s_a[1023]; s_base_b += s_b[1023]; s_base_c += s_c[1023]; }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) s[k][t] += x[k];
     __syncthreads();
   }
-  if (t == 0) chunk_start[b1 - b0] = s_base_a;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) v[k] = s[k][t];
+}
+
+__global__ __launch_bounds__(1024) void k_bv_plan_local(const uint64_t* __restrict__ offsets,
+                                                        uint64_t b0, uint64_t b1, uint32_t C,
+                                                        uint32_t pmin, uint32_t* __restrict__ tot) {
+  __shared__ uint32_t s[3][1024];
+  uint32_t v[3];
+  plan_counts(offsets, b0 + (uint64_t)blockIdx.x * 1024 + threadIdx.x, b1, C, pmin, v[0], v[1],
+              v[2]);
+  block_scan3(v, s);
+  if (threadIdx.x == 1023) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) tot[3 * blockIdx.x + k] = v[k];
+  }
+}
+
+// nblk <= 4096 (a slice has at most 4M batches): 4 blocks per thread.
+__global__ __launch_bounds__(1024) void k_bv_plan_top(uint32_t nblk, uint64_t nb,
+                                                      uint32_t* __restrict__ tot,
+                                                      uint32_t* __restrict__ chunk_start) {
+  __shared__ uint32_t s[3][1024];
+  const uint32_t t = threadIdx.x;
+  uint32_t loc[4][3], v[3] = {0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t blk = 4 * t + j;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      loc[j][k] = blk < nblk ? tot[3 * blk + k] : 0u;
+      v[k] += loc[j][k];
+    }
+  }
+  uint32_t inc[3] = {v[0], v[1], v[2]};
+  block_scan3(inc, s);
+  uint32_t run[3] = {inc[0] - v[0], inc[1] - v[1], inc[2] - v[2]};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t blk = 4 * t + j;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (blk < nblk) tot[3 * blk + k] = run[k];
+      run[k] += loc[j][k];
+    }
+  }
+  if (t == 1023) chunk_start[nb] = run[0];
+}
+
+__global__ __launch_bounds__(1024) void k_bv_plan_apply(const uint64_t* __restrict__ offsets,
+                                                        uint64_t b0, uint64_t b1, uint32_t C,
+                                                        uint32_t pmin,
+                                                        const uint32_t* __restrict__ tot,
+                                                        uint32_t* __restrict__ chunk_start,
+                                                        uint32_t* __restrict__ multi,
+                                                        uint32_t* __restrict__ multi_first,
+                                                        uint32_t* __restrict__ pip_list) {
+  __shared__ uint32_t s[3][1024];
+  const uint64_t b = b0 + (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+  uint32_t kb, mflag, pflag;
+  plan_counts(offsets, b, b1, C, pmin, kb, mflag, pflag);
+  uint32_t v[3] = {kb, mflag, pflag};
+  block_scan3(v, s);
+  if (b >= b1) return;
+  const uint32_t ca = tot[3 * blockIdx.x] + v[0] - kb, cb = tot[3 * blockIdx.x + 1] + v[1] - mflag,
+                 cc = tot[3 * blockIdx.x + 2] + v[2] - pflag;
+  chunk_start[b - b0] = ca;
+  if (mflag) {
+    multi[cb] = (uint32_t)(b - b0);
+    multi_first[cb] = ca;
+  }
+  if (pflag) pip_list[cc] = (uint32_t)(b - b0);
 }
 
 __global__ __launch_bounds__(256) void k_bv_expand(const uint64_t* __restrict__ offsets,
@@ -1014,6 +1073,7 @@ struct bv_ws {
   uint32_t* multi_first;
   uint32_t* chunk_start;
   uint32_t* pip_list;
+  uint32_t* plan_tot;   // 3 per 1024-batch plan block
 };
 
 size_t bv_layout(uint64_t units, char* base, bv_ws* w) {
@@ -1030,9 +1090,10 @@ size_t bv_layout(uint64_t units, char* base, bv_ws* w) {
     w->multi = reinterpret_cast<uint32_t*>(p); p += s_m;
     w->multi_first = reinterpret_cast<uint32_t*>(p); p += s_m;
     w->pip_list = reinterpret_cast<uint32_t*>(p); p += s_m;
+    w->plan_tot = reinterpret_cast<uint32_t*>(p); p += a256(12 * (u / 1024 + 1));
     w->chunk_start = reinterpret_cast<uint32_t*>(p);
   }
-  return s_items + s_tabs + s_ch + s_out + 3 * s_m + a256(4 * (u + 1));
+  return s_items + s_tabs + s_ch + s_out + 3 * s_m + a256(12 * (u / 1024 + 1)) + a256(4 * (u + 1));
 }
 
 }  // namespace
@@ -1153,8 +1214,13 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
       ++e;
     }
     const uint64_t i0 = host_offsets[b], i1 = host_offsets[e];
-    hipLaunchKernelGGL(k_bv_plan, dim3(1), dim3(1024), 0, stream, offsets, b, e, C, pmin,
-                       w.chunk_start, w.multi, w.multi_first, w.pip_list);
+    const unsigned nblk = (unsigned)((e - b + 1023) / 1024);
+    hipLaunchKernelGGL(k_bv_plan_local, dim3(nblk), dim3(1024), 0, stream, offsets, b, e, C, pmin,
+                       w.plan_tot);
+    hipLaunchKernelGGL(k_bv_plan_top, dim3(1), dim3(1024), 0, stream, nblk, e - b, w.plan_tot,
+                       w.chunk_start);
+    hipLaunchKernelGGL(k_bv_plan_apply, dim3(nblk), dim3(1024), 0, stream, offsets, b, e, C, pmin,
+                       w.plan_tot, w.chunk_start, w.multi, w.multi_first, w.pip_list);
     if (chunks)
       hipLaunchKernelGGL(k_bv_expand, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
                          stream, offsets, b, e - b, (uint32_t)chunks, w.chunk_start, w.chunks);
