@@ -407,17 +407,19 @@ struct CertWs {
   void* batch_ws;
   uint32_t* vote_key;
   uint32_t* author_key;
+  void* group_ws;
 };
 
 size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
   const size_t m = n ? n : 1;
-  const size_t sizes[14] = {a256(32 * m), a256(32 * m), a256(32 * m), a256(4 * m), a256(4 * m),
+  const size_t sizes[15] = {a256(32 * m), a256(32 * m), a256(32 * m), a256(4 * m), a256(4 * m),
                             a256(4 * m),  a256(4 * m),  a256(8 * m),  a256(8 * m), a256(8 * m),
                             a256(8 * ((m + 63) / 64)),
                             nvotes ? a256(nw::batch_workspace_bytes(n, nvotes)) : 256,
-                            a256(4 * (nvotes ? nvotes : 1)), a256(4 * m)};
-  size_t off[14], tot = 0;
-  for (int k = 0; k < 14; ++k) { off[k] = tot; tot += sizes[k]; }
+                            a256(4 * (nvotes ? nvotes : 1)), a256(4 * m),
+                            nvotes ? a256(nw::cert_groups_bytes(n)) : 256};
+  size_t off[15], tot = 0;
+  for (int k = 0; k < 15; ++k) { off[k] = tot; tot += sizes[k]; }
   if (w) {
     w->hdr_digest = reinterpret_cast<uint32_t*>(base + off[0]);
     w->authors = reinterpret_cast<uint32_t*>(base + off[1]);
@@ -433,6 +435,7 @@ size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
     w->batch_ws = base + off[11];
     w->vote_key = reinterpret_cast<uint32_t*>(base + off[12]);
     w->author_key = reinterpret_cast<uint32_t*>(base + off[13]);
+    w->group_ws = base + off[14];
   }
   return tot;
 }
@@ -476,11 +479,27 @@ int cert_pipeline(DevCtx& ctx, const nw_committee& com, const nw_certificates& c
                                   w.bitmap, sws, s, &hk), "k_verify_strict (headers)");
   if (!headers_only) {
     const nw::key_tables_t kt{static_cast<const nw::ge_cached*>(ctx.ktabs), ctx.kok, w.vote_key};
+    // With random coefficients the votes of many certificates are checked as one random
+    // linear combination per group (launch_cert_groups); only the certificates of groups
+    // that fail it go through their own verify_batch below.
+    const uint64_t K = nw::cert_group_size(host_vote_offsets, n, com.nauth, z16 != nullptr);
+    uint32_t* group_ok = nullptr;
+    if (K) {
+      const nw::ge_cached* kt_tabs = static_cast<const nw::ge_cached*>(ctx.ktabs);
+      NW_HIP(nw::launch_cert_groups(w.cert_digest, cs.vote_offsets, host_vote_offsets, n,
+                                    reinterpret_cast<const uint32_t*>(cs.vote_pks),
+                                    reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
+                                    key, w.batch_ws, w.group_ws, w.pre1, w.pre2, w.hdr_st, kt,
+                                    nw::key_tables_base(kt_tabs, com.nauth),
+                                    (uint32_t)com.nauth, K, &group_ok, s),
+             "certificate groups (votes)");
+    }
     NW_HIP(nw::launch_verify_batch(w.cert_digest, cs.vote_offsets, host_vote_offsets, n,
                                    reinterpret_cast<const uint32_t*>(cs.vote_pks),
                                    reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
                                    static_cast<const uint32_t*>(z16), key, w.batch_ws,
-                                   w.batch_st, w.batch_idx, s, &kt), "verify_batch (votes)");
+                                   w.batch_st, w.batch_idx, s, &kt, group_ok, K),
+           "verify_batch (votes)");
   }
   NW_HIP(nw::launch_cert_finalize(n, headers_only, w.pre1, w.pre2, w.idx1, w.idx2, w.hdr_st,
                                   w.batch_st, w.batch_idx, status, index, s), "k_cert_finalize");

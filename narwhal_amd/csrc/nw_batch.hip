@@ -159,11 +159,25 @@ __device__ void chacha20_z(uint32_t z[4], const uint32_t key[8], uint64_t nonce,
 //   k_bv_plan_apply  per batch: chunk_start (nb + 1 entries), the combine list (multi,
 //                    multi_first) and the Pippenger list.
 // k_bv_expand: one lane per chunk writes its descriptor (balanced split of the batch).
+// Batches settled elsewhere (skip.group_ok[b / skip.per_group] != 0: their certificate
+// group passed the merged check, launch_cert_groups) get no chunks and status Ok.
+struct batch_skip_t {
+  const uint32_t* group_ok;
+  uint64_t per_group;
+};
+__device__ __forceinline__ bool skipped(const batch_skip_t& sk, uint64_t b) {
+  return sk.group_ok && sk.group_ok[b / sk.per_group] != 0;
+}
+
 __device__ __forceinline__ void plan_counts(const uint64_t* offsets, uint64_t b, uint64_t b1,
-                                            uint32_t C, uint32_t pmin, uint32_t& kb,
-                                            uint32_t& mflag, uint32_t& pflag) {
+                                            uint32_t C, uint32_t pmin, const batch_skip_t& sk,
+                                            uint32_t& kb, uint32_t& mflag, uint32_t& pflag) {
   kb = 0;
   pflag = 0;
+  if (b < b1 && skipped(sk, b)) {
+    mflag = 0;
+    return;
+  }
   if (b < b1) {
     const uint64_t nb = offsets[b + 1] - offsets[b];
     pflag = nb >= pmin ? 1u : 0u;   // Pippenger batch: no chunks, no combine
@@ -193,11 +207,12 @@ __device__ __forceinline__ void block_scan3(uint32_t v[3], uint32_t (*s)[1024]) 
 
 __global__ __launch_bounds__(1024) void k_bv_plan_local(const uint64_t* __restrict__ offsets,
                                                         uint64_t b0, uint64_t b1, uint32_t C,
-                                                        uint32_t pmin, uint32_t* __restrict__ tot) {
+                                                        uint32_t pmin, batch_skip_t sk,
+                                                        uint32_t* __restrict__ tot) {
   __shared__ uint32_t s[3][1024];
   uint32_t v[3];
-  plan_counts(offsets, b0 + (uint64_t)blockIdx.x * 1024 + threadIdx.x, b1, C, pmin, v[0], v[1],
-              v[2]);
+  plan_counts(offsets, b0 + (uint64_t)blockIdx.x * 1024 + threadIdx.x, b1, C, pmin, sk, v[0],
+              v[1], v[2]);
   block_scan3(v, s);
   if (threadIdx.x == 1023) {
 #pragma unroll
@@ -233,24 +248,34 @@ __global__ __launch_bounds__(1024) void k_bv_plan_top(uint32_t nblk, uint64_t nb
       run[k] += loc[j][k];
     }
   }
-  if (t == 1023) chunk_start[nb] = run[0];
+  if (t == 1023) {
+    chunk_start[nb] = run[0];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) tot[3 * nblk + k] = run[k];   // device totals
+  }
 }
 
 __global__ __launch_bounds__(1024) void k_bv_plan_apply(const uint64_t* __restrict__ offsets,
                                                         uint64_t b0, uint64_t b1, uint32_t C,
-                                                        uint32_t pmin,
+                                                        uint32_t pmin, batch_skip_t sk,
                                                         const uint32_t* __restrict__ tot,
                                                         uint32_t* __restrict__ chunk_start,
                                                         uint32_t* __restrict__ multi,
                                                         uint32_t* __restrict__ multi_first,
-                                                        uint32_t* __restrict__ pip_list) {
+                                                        uint32_t* __restrict__ pip_list,
+                                                        int32_t* __restrict__ status,
+                                                        uint64_t* __restrict__ fail_index) {
   __shared__ uint32_t s[3][1024];
   const uint64_t b = b0 + (uint64_t)blockIdx.x * 1024 + threadIdx.x;
   uint32_t kb, mflag, pflag;
-  plan_counts(offsets, b, b1, C, pmin, kb, mflag, pflag);
+  plan_counts(offsets, b, b1, C, pmin, sk, kb, mflag, pflag);
   uint32_t v[3] = {kb, mflag, pflag};
   block_scan3(v, s);
   if (b >= b1) return;
+  if (skipped(sk, b)) {
+    status[b] = NW_OK;
+    if (fail_index) fail_index[b] = offsets[b + 1] - offsets[b];
+  }
   const uint32_t ca = tot[3 * blockIdx.x] + v[0] - kb, cb = tot[3 * blockIdx.x + 1] + v[1] - mflag,
                  cc = tot[3 * blockIdx.x + 2] + v[2] - pflag;
   chunk_start[b - b0] = ca;
@@ -266,7 +291,7 @@ __global__ __launch_bounds__(256) void k_bv_expand(const uint64_t* __restrict__ 
                                                    const uint32_t* __restrict__ chunk_start,
                                                    bv_chunk* __restrict__ chunks) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= nchunks) return;
+  if (c >= nchunks || c >= chunk_start[nb]) return;   // host bound, device total
   // batch: largest lb with chunk_start[lb] <= c (empty batches share a start; the last
   // of them is the one that owns chunk c)
   uint64_t lo = 0, hi = nb;
@@ -289,7 +314,8 @@ __global__ __launch_bounds__(256) void k_bv_items(
     const uint32_t* __restrict__ digests, const uint64_t* __restrict__ offsets, uint64_t b0,
     uint64_t b1, uint64_t i0, uint64_t i1, uint32_t pmin, const uint32_t* __restrict__ pks,
     const uint32_t* __restrict__ sigs, const uint32_t* __restrict__ z16, z_key_t zkey,
-    bv_item* __restrict__ items, ge_cached* __restrict__ tabs, key_tables_t keys) {
+    bv_item* __restrict__ items, ge_cached* __restrict__ tabs, key_tables_t keys,
+    batch_skip_t sk) {
   const uint64_t gi = i0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gi >= i1) return;
   const uint64_t li = gi - i0;
@@ -301,6 +327,7 @@ __global__ __launch_bounds__(256) void k_bv_items(
     if (offsets[mid] <= gi) lo = mid; else hi = mid;
   }
   if (offsets[lo + 1] - offsets[lo] >= pmin) return;   // k_pip_points
+  if (skipped(sk, lo)) return;
   uint32_t Aw[8], Rw[8], Sw[8], Mw[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -448,7 +475,7 @@ __global__ __launch_bounds__(256) void k_bv_chunks(
     uint64_t b0, uint64_t i0, const bv_item* __restrict__ items,
     const ge_cached* __restrict__ tabs, const ge_cached* __restrict__ ktabs,
     bv_chunk_out* __restrict__ out, int32_t* __restrict__ status,
-    uint64_t* __restrict__ fail_index) {
+    uint64_t* __restrict__ fail_index, const uint32_t* __restrict__ ctotal) {
   __shared__ ge_niels s_btab[129];
   __shared__ ge_niels s_b128[129];
   {
@@ -463,8 +490,10 @@ __global__ __launch_bounds__(256) void k_bv_chunks(
   }
   __syncthreads();
   const uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = ci < nchunks;
-  const bv_chunk ch = chunks[live ? ci : nchunks - 1];
+  const uint32_t nch = min(nchunks, *ctotal);   // host bound, device total
+  if (nch == 0) return;
+  const bool live = ci < nch;
+  const bv_chunk ch = chunks[live ? ci : nch - 1];
   const uint64_t bidx = b0 + ch.batch;
   const uint64_t bstart = offsets[bidx];
   const uint64_t bn = offsets[bidx + 1] - bstart;
@@ -559,11 +588,12 @@ __global__ __launch_bounds__(256) void k_bv_combine(const uint32_t* __restrict__
                                                     uint64_t b0, uint32_t C,
                                                     const bv_chunk_out* __restrict__ out,
                                                     int32_t* __restrict__ status,
-                                                    uint64_t* __restrict__ fail_index) {
+                                                    uint64_t* __restrict__ fail_index,
+                                                    const uint32_t* __restrict__ mtotal) {
   __shared__ ge s_p[256];
   __shared__ uint32_t s_f[256][4];
   const uint32_t m = blockIdx.x;
-  if (m >= nmulti) return;
+  if (m >= nmulti || m >= *mtotal) return;   // host bound, device total
   const int tid = threadIdx.x;
   const uint64_t bidx = b0 + multi[m];
   const uint64_t bn = offsets[bidx + 1] - offsets[bidx];
@@ -671,6 +701,27 @@ constexpr size_t pip_region_bytes(uint64_t n) {
 // per-vote bytes grow slower than the item slots (2560 B), so the floor is the binding n
 static_assert(pip_region_bytes(kPipFloor) <= 16 * sizeof(ge_cached) * kPipFloor,
               "Pippenger region does not fit its items' table slots");
+// certificate groups: >= kPipMin votes plus up to 256 committee keys
+static_assert(pip_region_bytes(kPipMin + 256) <= 16 * sizeof(ge_cached) * kPipMin,
+              "certificate-group region does not fit its votes' table slots");
+
+// Certificate-group mode (launch_cert_groups): a "batch" is a group of whole certificates;
+// each vote hashes its own certificate's digest, votes of certificates that already failed
+// (pre-checks, header) contribute nothing, and the A terms are not bucketed per vote: every
+// vote's A is a committee key, so c_i is summed per key (k_grp_keys) and the nkeys keys
+// enter as extra "votes" t = n + j with the digits of their sums only.
+struct pip_group_t {
+  const uint64_t* cert_vote_offsets;   // ncert + 1 (device); null: plain batches
+  uint64_t ncert, certs_per_group;
+  const int32_t* pre1;
+  const int32_t* pre2;
+  const int32_t* hdr_st;
+  const uint32_t* vote_key;
+  const uint32_t* key_ok;
+  const ge* key_base;                  // key j decompressed at key_base[2 j] (Z = 1)
+  uint32_t nkeys;
+  uint32_t* group_ok;                  // 1: the group's merged equation holds, no flags
+};
 
 __device__ __forceinline__ pip_region pip_at(ge_cached* tabs, uint64_t li0, uint64_t n) {
   char* p = reinterpret_cast<char*>(tabs + 16 * li0);
@@ -724,7 +775,7 @@ __global__ __launch_bounds__(256) void k_pip_points(
     const uint32_t* __restrict__ digests, const uint64_t* __restrict__ offsets, uint64_t b0,
     uint64_t b1, uint64_t i0, uint64_t i1, uint32_t pmin, const uint32_t* __restrict__ pks,
     const uint32_t* __restrict__ sigs, const uint32_t* __restrict__ z16, z_key_t zkey,
-    bv_item* __restrict__ items, ge_cached* __restrict__ tabs) {
+    bv_item* __restrict__ items, ge_cached* __restrict__ tabs, pip_group_t grp) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t wave = g >> 6;
   const int which = (int)(wave & 1);
@@ -735,9 +786,33 @@ __global__ __launch_bounds__(256) void k_pip_points(
   const uint64_t bs = offsets[lo], n = offsets[lo + 1] - bs;
   if (n < pmin) return;
   const uint64_t t = gi - bs;
-  const pip_region reg = pip_at(tabs, bs - i0, n);
+  const bool group = grp.cert_vote_offsets != nullptr;
+  const uint64_t nreg = n + (group ? grp.nkeys : 0);
+  const pip_region reg = pip_at(tabs, bs - i0, nreg);
   const curve_consts& K = g_bc.k;
   bv_item* it = items + li;
+  uint64_t dig = lo;   // digest index: the batch, or in group mode the vote's certificate
+  if (group) {
+    const uint64_t c0 = lo * grp.certs_per_group;
+    const uint64_t c1 = c0 + grp.certs_per_group < grp.ncert ? c0 + grp.certs_per_group : grp.ncert;
+    dig = batch_of(grp.cert_vote_offsets, c0, c1, gi);
+    if (grp.pre1[dig] != 0 || grp.hdr_st[dig] != 0 || grp.pre2[dig] != 0) {
+      // decided before the votes: contributes nothing
+      if (which == 1) {
+        it->pad = 0;
+      } else {
+#pragma unroll
+        for (int w = 0; w < kPipWin; ++w) reg.cd[w * nreg + t] = 0x80;
+#pragma unroll
+        for (int w = 0; w < kPipZWin; ++w) reg.zd[w * nreg + t] = 0x80;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) it->b[j] = 0;
+        it->flags = 0;
+        it->key = kNone;
+      }
+      return;
+    }
+  }
   ge P;
   ge_niels q;
   if (which == 1) {
@@ -756,7 +831,7 @@ __global__ __launch_bounds__(256) void k_pip_points(
     Aw[j] = pks[8 * gi + j];
     Rw[j] = sigs[16 * gi + j];
     Sw[j] = sigs[16 * gi + 8 + j];
-    Mw[j] = digests[8 * lo + j];
+    Mw[j] = digests[8 * dig + j];
   }
   uint32_t flags = 0;
   if ((Sw[7] >> 29) != 0) flags |= BF_S_HIGH;
@@ -788,17 +863,85 @@ __global__ __launch_bounds__(256) void k_pip_points(
   uint32_t cr[8], zr[8];
   sc_recode(cr, c, 0x80808080u);
   sc_recode(zr, z, 0x80808080u);
-  if (!ge_frombytes(P, Aw, K)) flags |= BF_A_DECODE;
-  ge_to_niels_z1(q, P, K.d2);
-  reg.pts[2 * t] = q;
+  uint32_t key = kNone;
+  if (group) {
+    // A = committee key: c_i goes to the key's sum (k_grp_keys), no per-vote A digits
+    key = grp.vote_key[gi];
+    if (key == kNone || !(grp.key_ok[key] & 1u)) {
+      flags |= BF_A_DECODE;
+      key = kNone;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      it->c[j] = c.w[j];
+      cr[j] = 0x80808080u;
+    }
+  } else {
+    if (!ge_frombytes(P, Aw, K)) flags |= BF_A_DECODE;
+    ge_to_niels_z1(q, P, K.d2);
+    reg.pts[2 * t] = q;
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) it->b[j] = b.w[j];
 #pragma unroll
-  for (int w = 0; w < kPipWin; ++w) reg.cd[w * n + t] = (uint8_t)(cr[w >> 2] >> ((w & 3) * 8));
+  for (int w = 0; w < kPipWin; ++w) reg.cd[w * nreg + t] = (uint8_t)(cr[w >> 2] >> ((w & 3) * 8));
 #pragma unroll
-  for (int w = 0; w < kPipZWin; ++w) reg.zd[w * n + t] = (uint8_t)(zr[w >> 2] >> ((w & 3) * 8));
+  for (int w = 0; w < kPipZWin; ++w) reg.zd[w * nreg + t] = (uint8_t)(zr[w >> 2] >> ((w & 3) * 8));
   it->flags = flags;
-  it->key = kNone;
+  it->key = key;
+}
+
+// Group mode: per group, sum_i c_i per committee key (LDS, 64-bit limb sums), reduced mod l,
+// as the digits of the key "votes" t = n + j, whose A point is the decompressed key.
+__global__ __launch_bounds__(1024) void k_grp_keys(const uint64_t* __restrict__ offsets,
+                                                   uint64_t b0, uint64_t i0, uint32_t pmin,
+                                                   const bv_item* __restrict__ items,
+                                                   ge_cached* __restrict__ tabs, pip_group_t grp) {
+  __shared__ unsigned long long s_acc[256][8];
+  const uint64_t bidx = b0 + blockIdx.x;
+  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
+  if (n < pmin) return;
+  const uint32_t N = grp.nkeys;
+  const uint64_t nreg = n + N;
+  const pip_region reg = pip_at(tabs, bs - i0, nreg);
+  const int tid = threadIdx.x;
+  for (int k = tid; k < 256 * 8; k += 1024) s_acc[k >> 3][k & 7] = 0;
+  __syncthreads();
+  const bv_item* its = items + (bs - i0);
+  for (uint64_t t = tid; t < n; t += 1024) {
+    const uint32_t key = its[t].key;
+    if (key != kNone) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) atomicAdd(&s_acc[key][j], (unsigned long long)its[t].c[j]);
+    }
+  }
+  __syncthreads();
+  for (uint32_t j = tid; j < N; j += 1024) {
+    uint32_t x[16];
+    unsigned long long carry = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      carry += s_acc[j][w];
+      x[w] = (uint32_t)carry;
+      carry >>= 32;
+    }
+    x[8] = (uint32_t)carry;
+    x[9] = (uint32_t)(carry >> 32);
+#pragma unroll
+    for (int w = 10; w < 16; ++w) x[w] = 0;
+    sc C;
+    sc_reduce512(C, x);
+    uint32_t cr[8];
+    sc_recode(cr, C, 0x80808080u);
+    const uint64_t t = n + j;
+#pragma unroll
+    for (int w = 0; w < kPipWin; ++w) reg.cd[w * nreg + t] = (uint8_t)(cr[w >> 2] >> ((w & 3) * 8));
+#pragma unroll
+    for (int w = 0; w < kPipZWin; ++w) reg.zd[w * nreg + t] = 0x80;
+    ge_niels q;
+    ge_to_niels_z1(q, grp.key_base[2 * j], g_bc.k.d2);
+    reg.pts[2 * t] = q;
+  }
 }
 
 // The nonzero digits of vote t in window w (c_i and, for w <= 16, z_i) as
@@ -828,13 +971,14 @@ __device__ __forceinline__ void pip_window_digits(const pip_region& reg, uint64_
 // scatter with LDS cursors into the window's entry range (capacity 2n).
 __global__ __launch_bounds__(1024) void k_pip_sort(const uint32_t* __restrict__ pip_list,
                                                    const uint64_t* __restrict__ offsets,
-                                                   uint64_t b0, uint64_t i0,
-                                                   const bv_item* __restrict__ items,
-                                                   ge_cached* __restrict__ tabs) {
+                                                   uint64_t b0, uint64_t i0, uint32_t extra,
+                                                   uint32_t pmin, ge_cached* __restrict__ tabs) {
   constexpr int NL = 128 + kPipCarryBins;
   __shared__ uint32_t s_h[NL], s_c[NL];
   const uint64_t bidx = b0 + pip_list[blockIdx.y];
-  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
+  const uint64_t bs = offsets[bidx], n0 = offsets[bidx + 1] - bs;
+  if (n0 < pmin) return;
+  const uint64_t n = n0 + extra;   // votes + (group mode) key sums
   const pip_region reg = pip_at(tabs, bs - i0, n);
   const int w = blockIdx.x, tid = threadIdx.x;
   if (tid < NL) s_h[tid] = 0;
@@ -881,6 +1025,7 @@ __global__ __launch_bounds__(256) void k_pip_buckets(const uint32_t* __restrict_
                                                      const uint64_t* __restrict__ offsets,
                                                      uint64_t b0, uint64_t i0, uint32_t lg,
                                                      uint32_t npip, uint32_t bpb, int xcd,
+                                                     uint32_t extra, uint32_t pmin,
                                                      ge_cached* __restrict__ tabs) {
   uint32_t jb = blockIdx.y, xb = blockIdx.x;
   if (xcd) {
@@ -891,7 +1036,8 @@ __global__ __launch_bounds__(256) void k_pip_buckets(const uint32_t* __restrict_
   }
   const uint64_t bidx = b0 + pip_list[jb];
   const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
-  const pip_region reg = pip_at(tabs, bs - i0, n);
+  if (n < pmin) return;
+  const pip_region reg = pip_at(tabs, bs - i0, n + extra);
   const uint32_t gl = xb * blockDim.x + threadIdx.x;
   const uint32_t bin = gl >> lg, G = 1u << lg, g = gl & (G - 1);
   if (bin >= (uint32_t)kPipBins) return;   // whole G-groups (kPipBins is a multiple of 64)
@@ -934,11 +1080,12 @@ __global__ __launch_bounds__(256) void k_pip_buckets(const uint32_t* __restrict_
 // Then a tree over lanes.
 __global__ __launch_bounds__(64) void k_pip_windows(const uint32_t* __restrict__ pip_list,
                                                     const uint64_t* __restrict__ offsets,
-                                                    uint64_t b0, uint64_t i0,
-                                                    ge_cached* __restrict__ tabs) {
+                                                    uint64_t b0, uint64_t i0, uint32_t extra,
+                                                    uint32_t pmin, ge_cached* __restrict__ tabs) {
   const uint64_t bidx = b0 + pip_list[blockIdx.y];
   const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
-  const pip_region reg = pip_at(tabs, bs - i0, n);
+  if (n < pmin) return;
+  const pip_region reg = pip_at(tabs, bs - i0, n + extra);
   const int w = blockIdx.x, l = threadIdx.x;
   const fe& d2 = g_bc.k.d2;
   const bool top = w == kPipWin - 1;
@@ -985,14 +1132,17 @@ __global__ __launch_bounds__(256) void k_pip_final(const uint32_t* __restrict__ 
                                                    const bv_item* __restrict__ items,
                                                    ge_cached* __restrict__ tabs,
                                                    int32_t* __restrict__ status,
-                                                   uint64_t* __restrict__ fail_index) {
+                                                   uint64_t* __restrict__ fail_index,
+                                                   uint32_t extra, uint32_t pmin,
+                                                   uint32_t* __restrict__ group_ok) {
   __shared__ ge_niels s_btab[129];
   __shared__ uint32_t s_b[256][8];
   __shared__ uint32_t s_f[256][4];
-  load_btab(s_btab);
   const uint64_t bidx = b0 + pip_list[blockIdx.x];
   const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
-  const pip_region reg = pip_at(tabs, bs - i0, n);
+  if (n < pmin) return;
+  load_btab(s_btab);
+  const pip_region reg = pip_at(tabs, bs - i0, n + extra);
   const int tid = threadIdx.x;
   const bv_item* its = items + (bs - i0);
   sc bsum;
@@ -1056,6 +1206,10 @@ __global__ __launch_bounds__(256) void k_pip_final(const uint32_t* __restrict__ 
   const bool ident = quad_is_identity(v);
   if (tid != 0) return;
   const uint32_t ff[3] = {s_f[0][0], s_f[0][1], s_f[0][2]};
+  if (group_ok) {   // group mode: any flag or a nonzero sum sends the group to the fallback
+    group_ok[bidx] = (ff[0] == kNone && ff[1] == kNone && ff[2] == kNone && ident) ? 1u : 0u;
+    return;
+  }
   uint64_t idx;
   const int st = batch_status(ff, s_f[0][3], ident, n, &idx);
   status[bidx] = st;
@@ -1090,10 +1244,10 @@ size_t bv_layout(uint64_t units, char* base, bv_ws* w) {
     w->multi = reinterpret_cast<uint32_t*>(p); p += s_m;
     w->multi_first = reinterpret_cast<uint32_t*>(p); p += s_m;
     w->pip_list = reinterpret_cast<uint32_t*>(p); p += s_m;
-    w->plan_tot = reinterpret_cast<uint32_t*>(p); p += a256(12 * (u / 1024 + 1));
+    w->plan_tot = reinterpret_cast<uint32_t*>(p); p += a256(12 * (u / 1024 + 2));
     w->chunk_start = reinterpret_cast<uint32_t*>(p);
   }
-  return s_items + s_tabs + s_ch + s_out + 3 * s_m + a256(12 * (u / 1024 + 1)) + a256(4 * (u + 1));
+  return s_items + s_tabs + s_ch + s_out + 3 * s_m + a256(12 * (u / 1024 + 2)) + a256(4 * (u + 1));
 }
 
 }  // namespace
@@ -1174,13 +1328,75 @@ hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, ge_cached* tab
   return hipGetLastError();
 }
 
+namespace {
+
+// The Pippenger kernels over the pip_list batches of one slice (plain batches or, with
+// grp.cert_vote_offsets set, certificate groups).
+void launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t b, uint64_t e,
+                uint64_t i0, uint64_t i1, uint32_t pmin, uint64_t npip, uint64_t pmax,
+                const uint32_t* pks, const uint32_t* sigs, const uint32_t* z16,
+                const z_key_t& zkey, const bv_ws& w, int32_t* status, uint64_t* fail_index,
+                const pip_group_t& grp, hipStream_t stream) {
+  const bool group = grp.cert_vote_offsets != nullptr;
+  const uint32_t extra = group ? grp.nkeys : 0;
+  hipLaunchKernelGGL(k_pip_points, dim3((unsigned)((i1 - i0 + 63) / 64 * 2 * 64 + 255) / 256),
+                     dim3(256), 0, stream, digests, offsets, b, e, i0, i1, pmin, pks, sigs, z16,
+                     zkey, w.items, w.tabs, grp);
+  if (group)
+    hipLaunchKernelGGL(k_grp_keys, dim3((unsigned)npip), dim3(1024), 0, stream, offsets, b, i0,
+                       pmin, w.items, w.tabs, grp);
+  hipLaunchKernelGGL(k_pip_sort, dim3(kPipWin, (unsigned)npip), dim3(1024), 0, stream,
+                     w.pip_list, offsets, b, i0, extra, pmin, w.tabs);
+  // G lanes per bucket: about 8 additions each at the largest batch's mean bucket size
+  // (<= 49 digits per vote over kPipBins buckets)
+  uint32_t lg = 0;
+  while (lg < 6 && (49 * (pmax + extra)) / kPipBins > 8ull << lg) ++lg;
+  // ... but no more lanes than the chip runs at once (the shuffle tree is overhead)
+  while (lg > 0 && ((npip * kPipBins) << lg) > (1ull << 21)) --lg;
+  const uint32_t bpb = ((kPipBins << lg) + 255) / 256;
+  const int xcd = npip >= 8;
+  const dim3 gb = xcd ? dim3((unsigned)(8 * bpb * ((npip + 7) / 8))) : dim3(bpb, (unsigned)npip);
+  hipLaunchKernelGGL(k_pip_buckets, gb, dim3(256), 0, stream, w.pip_list, offsets, b, i0, lg,
+                     (uint32_t)npip, bpb, xcd, extra, pmin, w.tabs);
+  hipLaunchKernelGGL(k_pip_windows, dim3(kPipWin, (unsigned)npip), dim3(64), 0, stream,
+                     w.pip_list, offsets, b, i0, extra, pmin, w.tabs);
+  hipLaunchKernelGGL(k_pip_final, dim3((unsigned)npip), dim3(256), 0, stream, w.pip_list,
+                     offsets, b, i0, w.items, w.tabs, status, fail_index, extra, pmin,
+                     grp.group_ok);
+}
+
+uint32_t pip_min() {
+  return (uint32_t)std::max<uint64_t>(
+      kPipFloor, std::min<uint64_t>(0xffffffffu, env_u64("NW_BATCH_PIPPENGER_MIN", kPipMin)));
+}
+
+// Group g = certificates [g K, min(g K + K, ncert)): gofs[g] = its first vote; identity list.
+__global__ __launch_bounds__(256) void k_grp_setup(const uint64_t* __restrict__ cvo,
+                                                   uint64_t ncert, uint64_t K, uint64_t ngroups,
+                                                   uint64_t* __restrict__ gofs,
+                                                   uint32_t* __restrict__ ident,
+                                                   uint32_t* __restrict__ group_ok) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g > ngroups) return;
+  const uint64_t c = g * K < ncert ? g * K : ncert;
+  gofs[g] = cvo[c];
+  if (g < ngroups) {
+    ident[g] = (uint32_t)g;
+    group_ok[g] = 0;
+  }
+}
+
+}  // namespace
+
 hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                const uint64_t* host_offsets, uint64_t nbatches,
                                const uint32_t* pks, const uint32_t* sigs, uint64_t nitems,
                                const uint32_t* z16, const z_key_t& zkey, void* workspace,
                                int32_t* status, uint64_t* fail_index, hipStream_t stream,
-                               const key_tables_t* keys) {
+                               const key_tables_t* keys, const uint32_t* skip_group_ok,
+                               uint64_t skip_per_group) {
   const key_tables_t kt = keys ? *keys : key_tables_t{nullptr, nullptr, nullptr};
+  const batch_skip_t sk{skip_group_ok, skip_per_group ? skip_per_group : 1};
   if (nbatches == 0) return hipSuccess;
   const uint64_t cap = std::min<uint64_t>(nitems + nbatches, slice_units());
   bv_ws w;
@@ -1192,8 +1408,9 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
   C = (uint32_t)std::min<uint64_t>(kMaxChunk, env_u64("NW_BATCH_CHUNK", C));
   // Batches of at least pmin votes take the Pippenger path (NW_BATCH_PIPPENGER_MIN test
   // hook; never below kPipFloor, whose item slots are the smallest that hold the region).
-  const uint32_t pmin = (uint32_t)std::max<uint64_t>(
-      kPipFloor, std::min<uint64_t>(0xffffffffu, env_u64("NW_BATCH_PIPPENGER_MIN", kPipMin)));
+  // With a skip list no batch may (launch_cert_groups only skips below pmin).
+  const uint32_t pmin = skip_group_ok ? 0xffffffffu : pip_min();
+  const pip_group_t nogrp{};
   uint64_t b = 0;
   while (b < nbatches) {
     // slice [b, e): items + batches <= cap
@@ -1216,51 +1433,111 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
     const uint64_t i0 = host_offsets[b], i1 = host_offsets[e];
     const unsigned nblk = (unsigned)((e - b + 1023) / 1024);
     hipLaunchKernelGGL(k_bv_plan_local, dim3(nblk), dim3(1024), 0, stream, offsets, b, e, C, pmin,
-                       w.plan_tot);
+                       sk, w.plan_tot);
     hipLaunchKernelGGL(k_bv_plan_top, dim3(1), dim3(1024), 0, stream, nblk, e - b, w.plan_tot,
                        w.chunk_start);
     hipLaunchKernelGGL(k_bv_plan_apply, dim3(nblk), dim3(1024), 0, stream, offsets, b, e, C, pmin,
-                       w.plan_tot, w.chunk_start, w.multi, w.multi_first, w.pip_list);
+                       sk, w.plan_tot, w.chunk_start, w.multi, w.multi_first, w.pip_list, status,
+                       fail_index);
     if (chunks)
       hipLaunchKernelGGL(k_bv_expand, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
                          stream, offsets, b, e - b, (uint32_t)chunks, w.chunk_start, w.chunks);
     if (i1 > i0 && npip != e - b)
       hipLaunchKernelGGL(k_bv_items, dim3((unsigned)((i1 - i0 + 255) / 256)), dim3(256), 0,
                          stream, digests, offsets, b, e, i0, i1, pmin, pks, sigs, z16, zkey,
-                         w.items, w.tabs, kt);
-    if (npip) {
-      hipLaunchKernelGGL(k_pip_points, dim3((unsigned)((i1 - i0 + 63) / 64 * 2 * 64 + 255) / 256),
-                         dim3(256), 0, stream, digests, offsets, b, e, i0, i1, pmin, pks, sigs,
-                         z16, zkey, w.items, w.tabs);
-      hipLaunchKernelGGL(k_pip_sort, dim3(kPipWin, (unsigned)npip), dim3(1024), 0, stream,
-                         w.pip_list, offsets, b, i0, w.items, w.tabs);
-      // G lanes per bucket: about 8 additions each at the largest batch's mean bucket size
-      // (49 digits per vote over kPipBins buckets)
-      uint32_t lg = 0;
-      while (lg < 6 && (49 * pmax) / kPipBins > 8ull << lg) ++lg;
-      // ... but no more lanes than the chip runs at once (the shuffle tree is overhead)
-      while (lg > 0 && ((npip * kPipBins) << lg) > (1ull << 21)) --lg;
-      const uint32_t bpb = ((kPipBins << lg) + 255) / 256;
-      const int xcd = npip >= 8;
-      const dim3 gb = xcd ? dim3((unsigned)(8 * bpb * ((npip + 7) / 8))) : dim3(bpb, (unsigned)npip);
-      hipLaunchKernelGGL(k_pip_buckets, gb, dim3(256), 0, stream, w.pip_list, offsets, b, i0, lg,
-                         (uint32_t)npip, bpb, xcd, w.tabs);
-      hipLaunchKernelGGL(k_pip_windows, dim3(kPipWin, (unsigned)npip), dim3(64), 0, stream,
-                         w.pip_list, offsets, b, i0, w.tabs);
-      hipLaunchKernelGGL(k_pip_final, dim3((unsigned)npip), dim3(256), 0, stream, w.pip_list,
-                         offsets, b, i0, w.items, w.tabs, status, fail_index);
-    }
+                         w.items, w.tabs, kt, sk);
+    if (npip)
+      launch_pip(digests, offsets, b, e, i0, i1, pmin, npip, pmax, pks, sigs, z16, zkey, w,
+                 status, fail_index, nogrp, stream);
     if (chunks)
       hipLaunchKernelGGL(k_bv_chunks, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
                          stream, w.chunks, (uint32_t)chunks, offsets, b, i0, w.items, w.tabs,
-                         kt.tabs, w.outs, status, fail_index);
+                         kt.tabs, w.outs, status, fail_index, w.chunk_start + (e - b));
     if (multi)
       hipLaunchKernelGGL(k_bv_combine, dim3((unsigned)multi), dim3(256), 0, stream, w.multi,
                          w.multi_first, (uint32_t)multi, offsets, b, C, w.outs, status,
-                         fail_index);
+                         fail_index, w.plan_tot + 3 * nblk + 1);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
     b = e;
+  }
+  return hipSuccess;
+}
+
+const ge* key_tables_base(const ge_cached* tabs, uint64_t nkeys) {
+  return reinterpret_cast<const ge*>(tabs + kKeyTab * nkeys);
+}
+
+// Certificates per merged group, or 0 to verify every certificate's votes on its own:
+// injected coefficients (deterministic tests want each certificate's own combination),
+// NW_CERT_MERGE=0, committees above 256 keys, certificates with Pippenger-size vote sets,
+// or too few votes to fill a group.
+uint64_t cert_group_size(const uint64_t* host_cvo, uint64_t ncert, uint64_t nkeys,
+                         bool injected_z) {
+  const char* m = getenv("NW_CERT_MERGE");
+  if (injected_z || (m && m[0] == '0') || nkeys == 0 || nkeys > 256 || ncert == 0) return 0;
+  const uint64_t nvotes = host_cvo[ncert] - host_cvo[0];
+  uint64_t qmax = 0;
+  for (uint64_t c = 0; c < ncert; ++c) qmax = std::max(qmax, host_cvo[c + 1] - host_cvo[c]);
+  if (qmax == 0 || qmax >= kPipMin) return 0;
+  const uint64_t target = std::min<uint64_t>(env_u64("NW_CERT_GROUP_VOTES", 32768), 1ull << 20);
+  if (nvotes < std::max<uint64_t>(target, kPipMin)) return 0;
+  return std::max<uint64_t>(1, target * ncert / nvotes);
+}
+
+size_t cert_groups_bytes(uint64_t ncert) {
+  const uint64_t m = ncert ? ncert : 1;
+  return a256(8 * (m + 1)) + a256(4 * m) + a256(4 * m);
+}
+
+// Certificate::verify's vote batches merged over groups of certificates:
+// per group one Pippenger MSM of sum_i z_i R_i + sum_keys (sum c_i) A_key - (sum b_i) B over
+// the votes of its certificates that passed every earlier check; group_ok[g] = 1 when it
+// is the identity and no vote has a parse/decode flag. Returns with group_ok in scratch
+// (the caller then runs launch_verify_batch with skip_group_ok for the per-certificate
+// verdicts of the other groups). Random coefficients only.
+hipError_t launch_cert_groups(const uint32_t* cert_digest, const uint64_t* cvo,
+                              const uint64_t* host_cvo, uint64_t ncert, const uint32_t* pks,
+                              const uint32_t* sigs, uint64_t nvotes, const z_key_t& zkey,
+                              void* batch_ws, void* group_ws, const int32_t* pre1,
+                              const int32_t* pre2, const int32_t* hdr_st,
+                              const key_tables_t& keys, const ge* key_base, uint32_t nkeys,
+                              uint64_t K, uint32_t** group_ok_out, hipStream_t stream) {
+  if (ncert == 0 || nkeys > 256) return hipErrorInvalidValue;
+  const uint64_t ngroups = (ncert + K - 1) / K;
+  char* gp = static_cast<char*>(group_ws);
+  uint64_t* gofs = reinterpret_cast<uint64_t*>(gp);
+  uint32_t* ident = reinterpret_cast<uint32_t*>(gp + a256(8 * (ncert + 1)));
+  uint32_t* group_ok = reinterpret_cast<uint32_t*>(gp + a256(8 * (ncert + 1)) + a256(4 * ncert));
+  *group_ok_out = group_ok;
+  hipLaunchKernelGGL(k_grp_setup, dim3((unsigned)((ngroups + 1 + 255) / 256)), dim3(256), 0,
+                     stream, cvo, ncert, K, ngroups, gofs, ident, group_ok);
+  const uint64_t cap = std::min<uint64_t>(nvotes + ncert, slice_units());
+  bv_ws w;
+  bv_layout(cap, static_cast<char*>(batch_ws), &w);
+  w.pip_list = ident;   // every group of a slice, relative index = group - first group
+  pip_group_t grp{cvo, ncert, K, pre1, pre2, hdr_st, keys.vote_key, keys.ok, key_base, nkeys,
+                  group_ok};
+  const uint32_t pmin = kPipMin;   // smaller groups stay with the per-certificate path
+  auto gvotes = [&](uint64_t g) {
+    return host_cvo[std::min((g + 1) * K, ncert)] - host_cvo[std::min(g * K, ncert)];
+  };
+  uint64_t g = 0;
+  while (g < ngroups) {
+    uint64_t e = g, votes = 0, pmax = 0;
+    while (e < ngroups && (e == g || votes + gvotes(e) <= cap)) {
+      votes += gvotes(e);
+      pmax = std::max(pmax, gvotes(e));
+      ++e;
+    }
+    if (votes > cap) return hipErrorInvalidValue;
+    const uint64_t i0 = host_cvo[std::min(g * K, ncert)], i1 = host_cvo[std::min(e * K, ncert)];
+    if (i1 > i0)
+      launch_pip(cert_digest, gofs, g, e, i0, i1, pmin, e - g, pmax, pks, sigs, nullptr, zkey, w,
+                 nullptr, nullptr, grp, stream);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+    g = e;
   }
   return hipSuccess;
 }

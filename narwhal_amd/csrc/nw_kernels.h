@@ -60,12 +60,34 @@ size_t key_tables_bytes(uint64_t nkeys);
 hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, struct ge_cached* tabs,
                              uint32_t* ok, hipStream_t stream);
 size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems);
+// skip_group_ok (optional, device): batch b is settled (status Ok) when
+// skip_group_ok[b / skip_per_group] != 0 (launch_cert_groups).
 hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                const uint64_t* host_offsets, uint64_t nbatches,
                                const uint32_t* pks, const uint32_t* sigs, uint64_t nitems,
                                const uint32_t* z16, const z_key_t& zkey, void* workspace,
                                int32_t* status, uint64_t* fail_index, hipStream_t stream,
-                               const key_tables_t* keys = nullptr);
+                               const key_tables_t* keys = nullptr,
+                               const uint32_t* skip_group_ok = nullptr,
+                               uint64_t skip_per_group = 0);
+
+// Certificate::verify vote batches merged over groups of certificates (nw_batch.hip):
+// cert_group_size() = certificates per group, 0 when the merge does not apply;
+// group scratch = cert_groups_bytes(ncert); the batch workspace is the same as
+// launch_verify_batch's (batch_workspace_bytes(ncert, nvotes)). *group_ok_out points into
+// group_ws (1 per group that passed).
+struct ge;
+uint64_t cert_group_size(const uint64_t* host_cvo, uint64_t ncert, uint64_t nkeys,
+                         bool injected_z);
+size_t cert_groups_bytes(uint64_t ncert);
+const ge* key_tables_base(const ge_cached* tabs, uint64_t nkeys);
+hipError_t launch_cert_groups(const uint32_t* cert_digest, const uint64_t* cvo,
+                              const uint64_t* host_cvo, uint64_t ncert, const uint32_t* pks,
+                              const uint32_t* sigs, uint64_t nvotes, const z_key_t& zkey,
+                              void* batch_ws, void* group_ws, const int32_t* pre1,
+                              const int32_t* pre2, const int32_t* hdr_st,
+                              const key_tables_t& keys, const ge* key_base, uint32_t nkeys,
+                              uint64_t K, uint32_t** group_ok_out, hipStream_t stream);
 
 // ---- primary messages (nw_cert.hip) ----------------------------------------------------
 struct cert_committee_t {

@@ -159,3 +159,53 @@ def test_committee_key_classes_vs_oracle():
     ohst, _ = O.certificates_verify_many(com.packed(), p, headers_only=True)
     assert hst.tolist() == ohst.tolist()
     assert {int(x) for x in hst} >= {0, 32 + 5, 32 + 3}         # Ok, A small order, A decode
+
+
+# ---- merged certificate groups (launch_cert_groups) ------------------------------------
+def test_certificate_groups_vs_per_certificate(monkeypatch):
+    """With random coefficients, Certificate::verify's vote batches are checked as one random
+    linear combination per group of certificates and only failing groups are re-verified per
+    certificate. Honest groups (including certificates that fail before their votes: header
+    or pre-check classes, which contribute nothing) must pass the merged check; groups with a
+    bad vote fall back. Statuses and indices equal the expected per-certificate ones, and the
+    unmerged path (NW_CERT_MERGE=0)."""
+    from cert_cases import pack, unpack
+    from narwhal_amd import crypto as C
+    com, ms, exp_st, exp_ix, cls = mutated_stream(N=4, copies=12, seed=7)
+    honest = W.certificate_stream(3000, O.keys(4), lambda sk, m: C.sign_many(sk, m),
+                                  oracle_digest_many, seed=11, n_votes=4)
+    hrec, mrec = unpack(honest), unpack(ms)
+    early = [i for i, c in enumerate(cls) if c in HEADER_LEVEL or c.startswith("genesis")]
+    recs = hrec[:1500] + [mrec[i] for i in early] + hrec[1500:] + mrec
+    exp = ([0] * 1500 + [int(exp_st[i]) for i in early] + [0] * 1500 + [int(x) for x in exp_st])
+    expi = ([0] * 1500 + [int(exp_ix[i]) for i in early] + [0] * 1500 +
+            [int(x) for x in exp_ix])
+    p = pack(recs)
+    monkeypatch.setenv("NW_CERT_GROUP_VOTES", "1024")
+    st, ix = M.verify_certificates_many(_Com(com), p, None)
+    assert st.tolist() == exp and ix.tolist() == expi
+    monkeypatch.setenv("NW_CERT_MERGE", "0")
+    st0, ix0 = M.verify_certificates_many(_Com(com), p, None)
+    assert st0.tolist() == exp and ix0.tolist() == expi
+
+
+@pytest.mark.parametrize("N", [4, 10, 50])
+def test_certificate_groups_honest_and_one_bad(monkeypatch, N):
+    """Default group size over an honest stream (every group passes the merged check), then
+    one bad vote signature: only that certificate fails (its group falls back)."""
+    from narwhal_amd import crypto as C
+    keys = O.keys(N)
+    n = max(2000, 70000 // (2 * N // 3 + 1))
+    s = W.certificate_stream(n, keys, lambda sk, m: C.sign_many(sk, m), oracle_digest_many,
+                             seed=N, n_votes=None)
+    com = _Com(s["committee"])
+    st, _ = M.verify_certificates_many(com, s, None)
+    assert (st == 0).all()
+    bad = n // 2
+    v = int(s["vote_offsets"][bad]) + 1
+    s["vote_sigs"][v, 7] ^= 0x40
+    st, ix = M.verify_certificates_many(com, s, None)
+    assert st[bad] != 0 and (np.delete(st, bad) == 0).all()
+    monkeypatch.setenv("NW_CERT_MERGE", "0")
+    st0, ix0 = M.verify_certificates_many(com, s, None)
+    assert st0.tolist() == st.tolist() and ix0[bad] == ix[bad]
