@@ -162,6 +162,13 @@ def tile(t: torch.Tensor, total: int) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------------ timing helpers
+def max_over_ranks(x: float) -> float:
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def timed_steps(launch, steps: int, warmup: int, world: int):
     for _ in range(warmup):
         launch()
@@ -183,9 +190,7 @@ def timed_steps(launch, steps: int, warmup: int, world: int):
     elapsed = time.perf_counter() - t0
     kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(elapsed)
     return elapsed, kernel_ms
 
 
@@ -429,9 +434,7 @@ def run_wire(args, dev, stream, rank, world, N: int = 4):
         call()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el = max_over_ranks(el)
     sec = el / args.wire_steps
     return {"committee": N, "frames_per_call": n, "frame_bytes": int(offs[-1]),
             "certs_per_s": n * world / sec, "ms_per_call": sec * 1e3,
@@ -508,10 +511,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # NW_BENCH_BACKEND=gloo rehearses the N > 1 path with several ranks sharing the GPUs
+    # of a smaller box (rank -> device local % device_count); the driver's runs use RCCL.
+    backend = os.environ.get("NW_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     L = _lib.lib()
     ndev = L.nw_init()
     if ndev <= 0:
