@@ -12,6 +12,9 @@ import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libnarwhal_amd.so")
+# NW_LIB: an alternative build of the same library (compiler-flag experiments); the
+# default is always the in-tree build.
+LIB_PATH = os.environ.get("NW_LIB", LIB_PATH)
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "narwhal_amd.h")
 
 NW_OK = 0

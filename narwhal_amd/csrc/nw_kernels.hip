@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256) void k_sha512_digest32(const uint8_t* __restri
 // Persistent: the grid covers the resident waves once and strides over the items, so the
 // per-lane tables j*A, j*R live in a fixed workspace (16 entries x 160 B per lane slot, lane-
 // contiguous: a lookup reads 160 consecutive bytes per lane instead of 40 scattered dwords).
-__global__ __launch_bounds__(256, 2) void k_verify_strict(const uint32_t* __restrict__ msgs,
+__global__ __launch_bounds__(256, 3) void k_verify_strict(const uint32_t* __restrict__ msgs,
                                                        uint32_t msg_stride_words,
                                                        const uint32_t* __restrict__ pks,
                                                        const uint32_t* __restrict__ sigs,
