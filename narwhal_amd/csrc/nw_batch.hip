@@ -771,7 +771,7 @@ __device__ __forceinline__ void ge_shfl(ge& r, const ge& p, int src) {
 }
 
 // Lane -> (item, which): waves alternate A and R so a wave never mixes the two.
-__global__ __launch_bounds__(256) void k_pip_points(
+__global__ __launch_bounds__(256, 3) void k_pip_points(
     const uint32_t* __restrict__ digests, const uint64_t* __restrict__ offsets, uint64_t b0,
     uint64_t b1, uint64_t i0, uint64_t i1, uint32_t pmin, const uint32_t* __restrict__ pks,
     const uint32_t* __restrict__ sigs, const uint32_t* __restrict__ z16, z_key_t zkey,
