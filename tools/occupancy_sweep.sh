@@ -7,7 +7,7 @@ set -o pipefail
 mkdir -p gpurun_out/sw
 C="python bench.py --workload cert --committees 4,100 --no-cpu-baseline"
 B="python bench.py --workload batch --steps 5 --no-cpu-baseline"
-for v in def f g h; do
+for v in ${SWEEP:-def f g h}; do
   if [ $v = def ]; then L=narwhal_amd/libnarwhal_amd.so; else L=exp/$v/libnarwhal_amd.so; fi
   NW_LIB=$L timeout -k 10 200 $C > gpurun_out/sw/c_$v.json 2>/dev/null || exit 1
   NW_LIB=$L timeout -k 10 120 $B > gpurun_out/sw/b_$v.json 2>/dev/null || exit 1
