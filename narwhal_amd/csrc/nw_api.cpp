@@ -32,11 +32,20 @@ struct DevCtx {
   hipStream_t stream = nullptr;
   void* dbuf = nullptr;
   size_t dcap = 0;
+};
+
+// Per-device buffers shared by all threads and streams, ordered by an event chain
+// (nw::rt::Lease, nw_runtime.h).
+struct SharedDev {
+  std::mutex m;
   void* strict_ws = nullptr;   // per-lane tables of k_verify_strict (fixed size)
   void* ktabs = nullptr;       // committee key tables (grow-only)
   uint32_t* kok = nullptr;
   size_t kcap = 0;             // keys
+  hipEvent_t last = nullptr;   // completion of the last leased launch sequence
+  bool last_valid = false;
 };
+SharedDev g_shared[kMaxDevices];
 
 struct ThreadState {
   int device = 0;
@@ -47,9 +56,6 @@ struct ThreadState {
       if (ctx[i].stream || ctx[i].dbuf) {
         (void)hipSetDevice(g_dev_ids[i]);
         if (ctx[i].dbuf) (void)hipFree(ctx[i].dbuf);
-        if (ctx[i].strict_ws) (void)hipFree(ctx[i].strict_ws);
-        if (ctx[i].ktabs) (void)hipFree(ctx[i].ktabs);
-        if (ctx[i].kok) (void)hipFree(ctx[i].kok);
         if (ctx[i].stream) (void)hipStreamDestroy(ctx[i].stream);
       }
     }
@@ -133,36 +139,6 @@ int reserve(DevCtx& c, size_t bytes) {
 
 inline size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// The strict kernel's per-lane table workspace (allocated once per thread and device).
-int strict_ws(DevCtx& c, void** out) {
-  if (!c.strict_ws) {
-    hipError_t e = hipMalloc(&c.strict_ws, nw::strict_workspace_bytes());
-    if (e != hipSuccess) {
-      c.strict_ws = nullptr;
-      return set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (strict workspace)", e);
-    }
-  }
-  *out = c.strict_ws;
-  return 0;
-}
-
-// Committee key tables for nkeys keys (grow-only, per thread and device).
-int key_tables(DevCtx& c, size_t nkeys) {
-  if (nkeys <= c.kcap && c.ktabs) return 0;
-  (void)hipStreamSynchronize(c.stream);
-  if (c.ktabs) (void)hipFree(c.ktabs);
-  if (c.kok) (void)hipFree(c.kok);
-  c.ktabs = nullptr;
-  c.kok = nullptr;
-  c.kcap = 0;
-  const size_t cap = nkeys < 256 ? 256 : nkeys;
-  hipError_t e = hipMalloc(&c.ktabs, nw::key_tables_bytes(cap));
-  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c.kok), 4 * cap);
-  if (e != hipSuccess) return set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (key tables)", e);
-  c.kcap = cap;
-  return 0;
-}
-
 int os_random(void* buf, size_t n) {
   size_t got = 0;
   while (got < n) {
@@ -245,16 +221,19 @@ int nw_dev_verify_strict_many(const void* digests, size_t digest_stride, const v
     return set_err(NW_E_INVALID_ARG, "null pointer (status_out and bitmap_out are required)");
   if (digest_stride != 0 && digest_stride != 32)
     return set_err(NW_E_INVALID_ARG, "digest_stride must be 0 or 32");
+  const hipStream_t s = pick_stream(stream, c);
+  nw::rt::Lease lease;
   void* ws;
-  rc = strict_ws(*c, &ws);
+  rc = lease.acquire(t_state.device, s);
+  if (!rc) rc = lease.strict_ws(&ws);
   if (rc) return rc;
   NW_HIP(nw::launch_verify_strict(static_cast<const uint32_t*>(digests),
                                   (uint32_t)(digest_stride / 4),
                                   static_cast<const uint32_t*>(pks),
                                   static_cast<const uint32_t*>(sigs), n, status_out,
-                                  static_cast<uint64_t*>(bitmap_out), ws, pick_stream(stream, c)),
+                                  static_cast<uint64_t*>(bitmap_out), ws, s),
          "k_verify_strict launch");
-  return 0;
+  return lease.release();
 }
 
 // ------------------------------------------------------------------------------------
@@ -441,7 +420,7 @@ size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
 }
 
 // The whole device pipeline; every pointer is a device pointer.
-int cert_pipeline(DevCtx& ctx, const nw_committee& com, const nw_certificates& cs,
+int cert_pipeline(const nw_committee& com, const nw_certificates& cs,
                   const uint64_t* host_vote_offsets, int headers_only, const void* z16,
                   const nw::z_key_t& key, void* workspace, int32_t* status, uint64_t* index,
                   hipStream_t s) {
@@ -456,41 +435,44 @@ int cert_pipeline(DevCtx& ctx, const nw_committee& com, const nw_certificates& c
                        reinterpret_cast<const uint32_t*>(cs.vote_pks)};
   NW_HIP(nw::launch_sha512_digest32(cs.header_bytes, cs.header_offsets, nullptr, n,
                                     w.hdr_digest, s), "k_sha512 (header digests)");
-  int rc_;
   // The committee's keys are decompressed once per call (k_key_base / k_key_tabs) and their
   // tables shared by every header (author) and vote that names a committee member; any
   // other key cannot decide a verdict (k_cert_prepare fails its message first) and is
-  // decompressed in the kernel as usual.
-  rc_ = key_tables(ctx, com.nauth);
-  if (rc_) return rc_;
-  NW_HIP(nw::launch_key_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth,
-                               static_cast<nw::ge_cached*>(ctx.ktabs), ctx.kok, s),
+  // decompressed in the kernel as usual. Key tables and the strict workspace are the
+  // device's shared buffers: the lease orders this call after every earlier user.
+  nw::rt::Lease lease;
+  void* ktabs_v = nullptr;
+  uint32_t* kok = nullptr;
+  void* sws = nullptr;
+  int rc = lease.acquire(t_state.device, s);
+  if (!rc) rc = lease.key_tables(com.nauth, &ktabs_v, &kok);
+  if (!rc) rc = lease.strict_ws(&sws);
+  if (rc) return rc;
+  nw::ge_cached* ktabs = static_cast<nw::ge_cached*>(ktabs_v);
+  NW_HIP(nw::launch_key_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth, ktabs, kok,
+                               s),
          "k_key_tables");
   NW_HIP(nw::launch_cert_prepare(dc, ds, headers_only, w.hdr_digest, w.authors, w.cert_digest,
                                  w.pre1, w.pre2, w.idx1, w.idx2,
                                  headers_only ? nullptr : w.vote_key, w.author_key, s),
          "k_cert_prepare");
-  void* sws;
-  int rc = strict_ws(ctx, &sws);
-  if (rc) return rc;
-  const nw::key_tables_t hk{static_cast<const nw::ge_cached*>(ctx.ktabs), ctx.kok, w.author_key};
+  const nw::key_tables_t hk{ktabs, kok, w.author_key};
   NW_HIP(nw::launch_verify_strict(reinterpret_cast<const uint32_t*>(cs.ids), 8, w.authors,
                                   reinterpret_cast<const uint32_t*>(cs.header_sigs), n, w.hdr_st,
                                   w.bitmap, sws, s, &hk), "k_verify_strict (headers)");
   if (!headers_only) {
-    const nw::key_tables_t kt{static_cast<const nw::ge_cached*>(ctx.ktabs), ctx.kok, w.vote_key};
+    const nw::key_tables_t kt{ktabs, kok, w.vote_key};
     // With random coefficients the votes of many certificates are checked as one random
     // linear combination per group (launch_cert_groups); only the certificates of groups
     // that fail it go through their own verify_batch below.
     const uint64_t K = nw::cert_group_size(host_vote_offsets, n, com.nauth, z16 != nullptr);
     uint32_t* group_ok = nullptr;
     if (K) {
-      const nw::ge_cached* kt_tabs = static_cast<const nw::ge_cached*>(ctx.ktabs);
       NW_HIP(nw::launch_cert_groups(w.cert_digest, cs.vote_offsets, host_vote_offsets, n,
                                     reinterpret_cast<const uint32_t*>(cs.vote_pks),
                                     reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
                                     key, w.batch_ws, w.group_ws, w.pre1, w.pre2, w.hdr_st, kt,
-                                    nw::key_tables_base(kt_tabs, com.nauth),
+                                    nw::key_tables_base(ktabs, com.nauth),
                                     (uint32_t)com.nauth, K, &group_ok, s),
              "certificate groups (votes)");
     }
@@ -503,7 +485,7 @@ int cert_pipeline(DevCtx& ctx, const nw_committee& com, const nw_certificates& c
   }
   NW_HIP(nw::launch_cert_finalize(n, headers_only, w.pre1, w.pre2, w.idx1, w.idx2, w.hdr_st,
                                   w.batch_st, w.batch_idx, status, index, s), "k_cert_finalize");
-  return 0;
+  return lease.release();
 }
 
 int check_committee_host(const nw_committee* com) {
@@ -622,7 +604,7 @@ int certs_host(const nw_committee* com, const nw_certificates* cs, int headers_o
   nw::z_key_t key;
   rc = fill_key(key, nullptr);
   if (rc) return rc;
-  rc = cert_pipeline(*c, dcom, d, cs->vote_offsets, headers_only, dz, key, dws, dst, dix, s);
+  rc = cert_pipeline(dcom, d, cs->vote_offsets, headers_only, dz, key, dws, dst, dix, s);
   if (rc) return rc;
   NW_HIP(hipMemcpyAsync(status_out, dst, 4 * n, hipMemcpyDeviceToHost, s), "D2H status");
   if (index_out) NW_HIP(hipMemcpyAsync(index_out, dix, 8 * n, hipMemcpyDeviceToHost, s), "D2H index");
@@ -670,7 +652,7 @@ int nw_dev_certificates_verify_many(const nw_committee* committee, const nw_cert
     if (hvo[0] != 0 || hvo[certs->n] != certs->nvotes)
       return set_err(NW_E_INVALID_ARG, "vote_offsets must run from 0 to nvotes");
   }
-  return cert_pipeline(*c, *committee, *certs, hvo, headers_only, z16, key, workspace,
+  return cert_pipeline(*committee, *certs, hvo, headers_only, z16, key, workspace,
                        status_out, index_out, s);
 }
 
@@ -711,13 +693,19 @@ int nw_votes_verify_many(const nw_committee* committee, const uint8_t* ids,
                                  reinterpret_cast<const uint32_t*>(d_org),
                                  reinterpret_cast<const uint32_t*>(d_au), d_dig, d_pre, s),
          "k_vote_prepare");
-  void* sws;
-  rc = strict_ws(*c, &sws);
-  if (rc) return rc;
-  NW_HIP(nw::launch_verify_strict(d_dig, 8, reinterpret_cast<const uint32_t*>(d_au),
-                                  reinterpret_cast<const uint32_t*>(d_sig), n, d_sst, d_bm, sws,
-                                  s),
-         "k_verify_strict (votes)");
+  {
+    nw::rt::Lease lease;
+    void* sws;
+    rc = lease.acquire(t_state.device, s);
+    if (!rc) rc = lease.strict_ws(&sws);
+    if (rc) return rc;
+    NW_HIP(nw::launch_verify_strict(d_dig, 8, reinterpret_cast<const uint32_t*>(d_au),
+                                    reinterpret_cast<const uint32_t*>(d_sig), n, d_sst, d_bm, sws,
+                                    s),
+           "k_verify_strict (votes)");
+    rc = lease.release();
+    if (rc) return rc;
+  }
   NW_HIP(nw::launch_vote_finalize(n, d_pre, d_sst, d_st, s), "k_vote_finalize");
   NW_HIP(hipMemcpyAsync(status_out, d_st, 4 * n, hipMemcpyDeviceToHost, s), "D2H status");
   NW_HIP(hipStreamSynchronize(s), "sync");
@@ -748,6 +736,69 @@ int select_device(int* dev_index) {
 int set_err(int code, const char* what, hipError_t e) { return ::set_err(code, what, e); }
 
 int os_random(void* buf, size_t n) { return ::os_random(buf, n); }
+
+int Lease::acquire(int dev_index, hipStream_t stream) {
+  if (held_) return ::set_err(NW_E_INVALID_ARG, "lease already held");
+  if (dev_index < 0 || dev_index >= kMaxDevices) return ::set_err(NW_E_INVALID_ARG, "bad device");
+  SharedDev& d = g_shared[dev_index];
+  d.m.lock();
+  dev_ = dev_index;
+  stream_ = stream;
+  held_ = true;
+  hipError_t e = hipSuccess;
+  if (!d.last) e = hipEventCreateWithFlags(&d.last, hipEventDisableTiming);
+  if (e == hipSuccess && d.last_valid) e = hipStreamWaitEvent(stream, d.last, 0);
+  if (e != hipSuccess) {
+    held_ = false;
+    d.m.unlock();
+    return ::set_err(NW_E_DEVICE, "lease: event chain", e);
+  }
+  return 0;
+}
+
+int Lease::strict_ws(void** out) {
+  SharedDev& d = g_shared[dev_];
+  if (!d.strict_ws) {
+    hipError_t e = hipMalloc(&d.strict_ws, nw::strict_workspace_bytes());
+    if (e != hipSuccess) {
+      d.strict_ws = nullptr;
+      return ::set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (strict workspace)", e);
+    }
+  }
+  *out = d.strict_ws;
+  return 0;
+}
+
+int Lease::key_tables(size_t nkeys, void** tabs, uint32_t** ok) {
+  SharedDev& d = g_shared[dev_];
+  if (nkeys > d.kcap || !d.ktabs) {
+    // every earlier user of the old tables is ordered before d.last
+    if (d.last_valid) (void)hipEventSynchronize(d.last);
+    if (d.ktabs) (void)hipFree(d.ktabs);
+    if (d.kok) (void)hipFree(d.kok);
+    d.ktabs = nullptr;
+    d.kok = nullptr;
+    d.kcap = 0;
+    const size_t cap = nkeys < 256 ? 256 : nkeys;
+    hipError_t e = hipMalloc(&d.ktabs, nw::key_tables_bytes(cap));
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.kok), 4 * cap);
+    if (e != hipSuccess) return ::set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (key tables)", e);
+    d.kcap = cap;
+  }
+  *tabs = d.ktabs;
+  *ok = d.kok;
+  return 0;
+}
+
+int Lease::release() {
+  if (!held_) return 0;
+  SharedDev& d = g_shared[dev_];
+  hipError_t e = hipEventRecord(d.last, stream_);
+  d.last_valid = d.last_valid || e == hipSuccess;
+  held_ = false;
+  d.m.unlock();
+  return e == hipSuccess ? 0 : ::set_err(NW_E_DEVICE, "lease: hipEventRecord", e);
+}
 
 }  // namespace rt
 }  // namespace nw

@@ -1482,7 +1482,10 @@ uint64_t cert_group_size(const uint64_t* host_cvo, uint64_t ncert, uint64_t nkey
   if (qmax == 0 || qmax >= kPipMin) return 0;
   const uint64_t target = std::min<uint64_t>(env_u64("NW_CERT_GROUP_VOTES", 32768), 1ull << 20);
   if (nvotes < std::max<uint64_t>(target, kPipMin)) return 0;
-  return std::max<uint64_t>(1, target * ncert / nvotes);
+  // K from the mean votes per certificate, capped so that K certificates of the largest
+  // vote count still fit one workspace slice (skewed counts never overflow a slice)
+  const uint64_t K = std::max<uint64_t>(1, target * ncert / nvotes);
+  return std::max<uint64_t>(1, std::min<uint64_t>(K, slice_units() / qmax));
 }
 
 size_t cert_groups_bytes(uint64_t ncert) {

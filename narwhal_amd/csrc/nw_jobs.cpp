@@ -11,9 +11,9 @@
 // tokio (node/Cargo.toml:8), and Core / Processor loops must not block on the device
 // (crypto/src/lib.rs:222-250 SignatureService is the reference's own async-service pattern).
 //
-// Strict verification uses one per-device table workspace; launches from different jobs
-// are ordered on it with an event chain (the copies of one job still overlap the kernels
-// of another).
+// Strict verification uses the device's shared table workspace (nw::rt::Lease): launches
+// from different jobs and streams are ordered on it with an event chain (the copies of one
+// job still overlap the kernels of another).
 #include <hip/hip_runtime.h>
 #include <string.h>
 
@@ -51,9 +51,6 @@ constexpr int kMaxDev = 64;
 struct DevPool {
   std::mutex m;
   std::vector<nw_job*> free;
-  void* strict_ws = nullptr;
-  hipEvent_t strict_last = nullptr;   // completion of the last launch using strict_ws
-  bool strict_last_valid = false;
 };
 DevPool g_pool[kMaxDev];
 
@@ -196,31 +193,22 @@ int nw_submit_verify_strict(const uint8_t* digests, size_t digest_stride, const 
   memcpy(j->hbuf + o_m, digests, 32 * nmsg);
   memcpy(j->hbuf + o_pk, pks, 32 * n);
   memcpy(j->hbuf + o_sig, sigs, 64 * n);
-  DevPool& p = g_pool[j->dev];
   rc = job_run(j, o_st, o_st, end - o_st, [&]() -> int {
-    std::lock_guard<std::mutex> g(p.m);
-    if (!p.strict_ws) {
-      hipError_t e = hipMalloc(&p.strict_ws, nw::strict_workspace_bytes());
-      if (e != hipSuccess) {
-        p.strict_ws = nullptr;
-        return set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (strict workspace)", e);
-      }
-      e = hipEventCreateWithFlags(&p.strict_last, hipEventDisableTiming);
-      if (e != hipSuccess) return set_err(NW_E_DEVICE, "hipEventCreate", e);
-    }
-    if (p.strict_last_valid)
-      JOB_HIP(hipStreamWaitEvent(j->stream, p.strict_last, 0), "hipStreamWaitEvent");
+    // the device's shared strict workspace, ordered after its previous user (nw_runtime.h)
+    nw::rt::Lease lease;
+    void* ws = nullptr;
+    int lrc = lease.acquire(j->dev, j->stream);
+    if (!lrc) lrc = lease.strict_ws(&ws);
+    if (lrc) return lrc;
     JOB_HIP(nw::launch_verify_strict(reinterpret_cast<const uint32_t*>(j->dbuf + o_m),
                                      (uint32_t)(digest_stride / 4),
                                      reinterpret_cast<const uint32_t*>(j->dbuf + o_pk),
                                      reinterpret_cast<const uint32_t*>(j->dbuf + o_sig), n,
                                      reinterpret_cast<int32_t*>(j->dbuf + o_st),
-                                     reinterpret_cast<uint64_t*>(j->dbuf + o_bm), p.strict_ws,
+                                     reinterpret_cast<uint64_t*>(j->dbuf + o_bm), ws,
                                      j->stream),
             "k_verify_strict launch");
-    JOB_HIP(hipEventRecord(p.strict_last, j->stream), "hipEventRecord (strict ws)");
-    p.strict_last_valid = true;
-    return 0;
+    return lease.release();
   });
   if (rc) return job_abort(j, rc);
   job_out(j, status_out, o_st, 4 * n);

@@ -17,6 +17,7 @@
 #include "nw_consts.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 
 namespace nw {
@@ -373,13 +374,13 @@ hipError_t launch_sha512_digest32(const uint8_t* data, const uint64_t* offsets,
 }
 
 // Resident 256-thread blocks of k_verify_strict on the current device (occupancy query,
-// once per device).
+// once per device; concurrent first calls compute the same value).
 static unsigned strict_grid() {
-  static int cached[64] = {0};
+  static std::atomic<int> cached[64];
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (dev < 0 || dev >= 64) dev = 0;
-  if (!cached[dev]) {
+  if (!cached[dev].load(std::memory_order_acquire)) {
     int per_cu = 0, cus = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_verify_strict, 256, 0) !=
             hipSuccess || per_cu <= 0)
@@ -387,9 +388,9 @@ static unsigned strict_grid() {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         cus <= 0)
       cus = 256;
-    cached[dev] = per_cu * cus;
+    cached[dev].store(per_cu * cus, std::memory_order_release);
   }
-  return (unsigned)cached[dev];
+  return (unsigned)cached[dev].load(std::memory_order_acquire);
 }
 
 size_t strict_workspace_bytes() {

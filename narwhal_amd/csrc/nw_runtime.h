@@ -17,5 +17,33 @@ int set_err(int code, const char* what, hipError_t e = hipSuccess);
 // Fill buf from the OS CSPRNG (getrandom).
 int os_random(void* buf, size_t n);
 
+// Per-device buffers shared by every caller of the library (host-buffer jobs, blocking
+// calls and nw_dev_* calls on caller streams): the strict kernel's per-lane table workspace
+// and the committee key tables. A launch sequence that uses them holds a Lease on the
+// device: acquire() locks the device's lease and makes `stream` wait for the previous
+// holder's last launch (an event chain), so launches on different streams never overlap on
+// these buffers; release() (or the destructor) records a new event on `stream` and unlocks.
+// Growing the key tables first waits for that event: every earlier user is ordered before
+// it, so no queued launch still reads the old buffer when it is freed.
+class Lease {
+ public:
+  Lease() = default;
+  Lease(const Lease&) = delete;
+  Lease& operator=(const Lease&) = delete;
+  ~Lease() { (void)release(); }
+  int acquire(int dev_index, hipStream_t stream);
+  // The device's strict workspace (nw::strict_workspace_bytes(), allocated once).
+  int strict_ws(void** out);
+  // Key tables for nkeys keys (grow-only): tabs (nw::key_tables_bytes) and ok words.
+  int key_tables(size_t nkeys, void** tabs, uint32_t** ok);
+  // Record the chain event on the stream and unlock (idempotent). 0 or NW_E_DEVICE.
+  int release();
+
+ private:
+  int dev_ = -1;
+  hipStream_t stream_ = nullptr;
+  bool held_ = false;
+};
+
 }  // namespace rt
 }  // namespace nw

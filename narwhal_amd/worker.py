@@ -53,11 +53,19 @@ class Store:
 class Processor:
     """worker::Processor: hashes and stores batches, then outputs the batch's digest."""
 
+    # Batches hashed ahead of the store write (the reference handles one batch before it
+    # receives the next, so rx_batch's bound pushes back on senders; this keeps that
+    # backpressure with a bounded lookahead instead of an unbounded queue).
+    MAX_IN_FLIGHT = 16
+
     @staticmethod
     def spawn(worker_id: int, store: Store, rx_batch: asyncio.Queue, tx_digest: asyncio.Queue,
-              own_digest: bool, service: VerificationService) -> asyncio.Task:
-        """Runs until ``rx_batch`` yields None (the reference's closed channel)."""
-        pending: asyncio.Queue = asyncio.Queue()
+              own_digest: bool, service: VerificationService,
+              max_in_flight: int = MAX_IN_FLIGHT) -> asyncio.Task:
+        """Runs until ``rx_batch`` yields None (the reference's closed channel). At most
+        ``max_in_flight`` batches are hashed ahead of the store write; beyond that the
+        hash loop stops taking batches from ``rx_batch``."""
+        pending: asyncio.Queue = asyncio.Queue(maxsize=max(1, max_in_flight))
 
         async def hash_loop():
             while True:

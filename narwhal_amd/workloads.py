@@ -134,6 +134,43 @@ def certificate_stream(n_certs: int, keys: list[tuple[bytes, bytes]], sign_many,
     }
 
 
+# Certificate::verify statuses of the vote-level mutations below (include/narwhal_amd.h:
+# NW_DAG_INVALID_VOTES + the first failing check of Signature::verify_batch,
+# crypto/src/lib.rs:206-219): (kind, status, index-or-None for "the equation" = #votes).
+VOTE_MUTATIONS = (("s_low_flip", 48 + 7, None),      # equation fails (s changed, s < l kept)
+                  ("s_high_bits", 48 + 1, "j"),      # ed25519 Signature::from_bytes, fail-fast
+                  ("R_undecodable", 48 + 4, "j"))    # y = 2 is not on the curve
+
+
+def mutate_votes(s: dict, bad_certs: np.ndarray, seed: int = 0) -> tuple[dict, np.ndarray, np.ndarray]:
+    """Copy of certificate stream ``s`` in which one vote of every certificate in
+    ``bad_certs`` is invalid (byte edits only; the mutation kind cycles through
+    VOTE_MUTATIONS, the vote is chosen at random). Returns (stream, expected status[n],
+    expected index[n]) as Certificate::verify (primary/src/messages.rs:189-215) gives them:
+    the header and quorum are intact, so the votes' verify_batch decides."""
+    rng = np.random.Generator(np.random.PCG64([seed, 77]))
+    out = dict(s)
+    out["vote_sigs"] = s["vote_sigs"].copy()
+    n = len(s["header_offsets"]) - 1
+    st = np.zeros(n, np.int32)
+    ix = np.zeros(n, np.uint64)
+    vo = s["vote_offsets"]
+    for k, c in enumerate(np.asarray(bad_certs, np.int64)):
+        a, b = int(vo[c]), int(vo[c + 1])
+        j = int(rng.integers(0, b - a))
+        kind, code, where = VOTE_MUTATIONS[k % len(VOTE_MUTATIONS)]
+        sig = out["vote_sigs"][a + j]
+        if kind == "s_low_flip":
+            sig[32] ^= np.uint8(1 << int(rng.integers(0, 8)))   # s' = s +- 2^i, i < 8: s' < l
+        elif kind == "s_high_bits":
+            sig[63] |= np.uint8(0x80 >> int(rng.integers(0, 3)))
+        else:
+            sig[:32] = np.frombuffer((2).to_bytes(32, "little"), np.uint8)
+        st[c] = code
+        ix[c] = (b - a) if where is None else j
+    return out, st, ix
+
+
 # --------------------------------------------------------------------------------------
 # Fixture keys (BASELINE config 1; SURVEY 8(d)): rand 0.7 StdRng::from_seed([0; 32]) =
 # ChaCha20(key = 0^32, nonce = 0) keystream; seed i = bytes [32 i, 32 i + 32)

@@ -52,7 +52,7 @@ def test_appendix_b_fixture_through_mirror():
         bad.verify(committee)
 
 
-@pytest.mark.parametrize("N,copies", [(4, 3), (10, 2)])
+@pytest.mark.parametrize("N,copies", [(4, 3), (10, 2), (100, 1)])
 def test_certificates_vs_oracle(N, copies):
     com, s, exp_st, exp_ix, cls = mutated_stream(N=N, copies=copies, seed=N)
     z16 = np.random.Generator(np.random.PCG64(N)).integers(0, 256, size=(len(s["vote_pks"]), 16),
@@ -189,7 +189,7 @@ def test_certificate_groups_vs_per_certificate(monkeypatch):
     assert st0.tolist() == exp and ix0.tolist() == expi
 
 
-@pytest.mark.parametrize("N", [4, 10, 50])
+@pytest.mark.parametrize("N", [4, 10, 50, 100])
 def test_certificate_groups_honest_and_one_bad(monkeypatch, N):
     """Default group size over an honest stream (every group passes the merged check), then
     one bad vote signature: only that certificate fails (its group falls back)."""
@@ -209,3 +209,25 @@ def test_certificate_groups_honest_and_one_bad(monkeypatch, N):
     monkeypatch.setenv("NW_CERT_MERGE", "0")
     st0, ix0 = M.verify_certificates_many(com, s, None)
     assert st0.tolist() == st.tolist() and ix0[bad] == ix[bad]
+
+
+@pytest.mark.parametrize("N,n", [(4, 6000), (10, 3000), (100, 600)])
+def test_certificate_groups_mixed_validity(monkeypatch, N, n):
+    """About 1% of the certificates carry one invalid vote (equation, s high bits, R not on
+    the curve: workloads.mutate_votes), spread over many merged groups
+    (NW_CERT_GROUP_VOTES=4096). Every group with a bad certificate falls back; statuses and
+    indices equal the construction (pinned by the oracle in tests/test_messages.py) and
+    the unmerged path, with random coefficients as in the reference."""
+    from narwhal_amd import crypto as C
+    keys = O.keys(N)
+    s = W.certificate_stream(n, keys, lambda sk, m: C.sign_many(sk, m), oracle_digest_many,
+                             seed=100 + N)
+    bad = np.arange(37 % n, n, 100)
+    m, exp_st, exp_ix = W.mutate_votes(s, bad, seed=N)
+    com = _Com(s["committee"])
+    monkeypatch.setenv("NW_CERT_GROUP_VOTES", "4096")
+    st, ix = M.verify_certificates_many(com, m, None)
+    assert st.tolist() == exp_st.tolist() and ix.tolist() == exp_ix.tolist()
+    monkeypatch.setenv("NW_CERT_MERGE", "0")
+    st0, ix0 = M.verify_certificates_many(com, m, None)
+    assert st0.tolist() == exp_st.tolist() and ix0.tolist() == exp_ix.tolist()

@@ -128,3 +128,24 @@ def test_certificate_stream_generator_honest():
     assert bytes(hb[3, :32]) == keys[3][0]
     assert struct.unpack("<Q", bytes(hb[11, 32:40]))[0] == 2
     assert hb.shape[1] == 40 + 36 * 2 + 32 * 7
+
+
+@pytest.mark.parametrize("N", [4, 10, 100])
+def test_mutate_votes_expectations_pinned_by_oracle(N):
+    """workloads.mutate_votes (the bench's invalid-certificate legs) states each mutated
+    certificate's Certificate::verify status and index by construction; the oracle agrees,
+    with injected and with random coefficients (the mutations are all in the
+    deterministic set: no torsion residuals)."""
+    keys = O.keys(N)
+    n = 30 if N < 100 else 9
+    s = W.certificate_stream(n, keys, oracle_sign_many, oracle_digest_many, seed=N)
+    bad = np.arange(1, n, 2)
+    m, exp_st, exp_ix = W.mutate_votes(s, bad, seed=N)
+    assert {int(x) for x in exp_st} == {0, 48 + 7, 48 + 1, 48 + 4}
+    z16 = np.random.Generator(np.random.PCG64(N)).integers(0, 256, size=(len(m["vote_pks"]), 16),
+                                                           dtype=np.uint8)
+    st, ix = O.certificates_verify_many(s["committee"], m, z16)
+    assert st.tolist() == exp_st.tolist() and ix.tolist() == exp_ix.tolist()
+    st, ix = O.certificates_verify_many(s["committee"], m)
+    assert st.tolist() == exp_st.tolist() and ix.tolist() == exp_ix.tolist()
+    assert np.array_equal(s["vote_sigs"][0], m["vote_sigs"][0])   # input stream untouched

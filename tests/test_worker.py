@@ -68,3 +68,31 @@ def test_processor_on_gpu():
     out, stored, _ = _run(None, batches)
     assert out == _expect(batches)
     assert stored == batches
+
+
+def test_backpressure_bounded_in_flight():
+    """rx_batch backpressure is kept (processor.rs:36-54 takes one batch at a time): with a
+    store that never completes a write, the hash loop stops taking batches once
+    max_in_flight are pending, so rx_batch's own bound pushes back on the sender."""
+    class StuckStore(Store):
+        async def write(self, key, value):
+            await asyncio.Event().wait()
+
+    async def main():
+        svc = VerificationService(backend=_OracleBackend(), max_delay=0.001)
+        rx, tx = asyncio.Queue(maxsize=1), asyncio.Queue()
+        task = Processor.spawn(0, StuckStore(), rx, tx, True, svc, max_in_flight=3)
+        sent = 0
+        batches = [W.serialize_batch([bytes([i]) * 64]) for i in range(20)]
+        for b in batches:
+            try:
+                await asyncio.wait_for(rx.put(b), timeout=0.2)
+            except asyncio.TimeoutError:
+                break
+            sent += 1
+        task.cancel()
+        return sent
+
+    sent = asyncio.run(main())
+    # 1 batch in the writer, 3 pending, 1 held by the hash loop waiting for room, 1 in rx
+    assert 3 <= sent <= 7, sent
