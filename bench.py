@@ -50,10 +50,16 @@ P_FIELD = 2**255 - 19
 MAC_PER_STRICT_VERIFY = 3200 * 64          # 204,800 32x32->64 MACs
 MAC_PER_BATCH_ITEM_LARGE = 1000 * 64       # batch item, n >= 10k (64,000 MACs)
 MAC_PER_BATCH_ITEM_SMALL = 2000 * 64       # batch item, small n (certificate votes)
+# Certificate groups: a counted vote costs one R decompression (~265 F_p
+# mults) + <= 17 bucket additions (7 mults each) + its share of the key sums ~ 400 F_p mults;
+# the SURVEY small-n constant above describes per-certificate Straus, not this algorithm.
+MAC_PER_GROUP_VOTE = 400 * 64              # 25,600 MACs
 SHA_OPS_PER_BLOCK = 4800                   # int32 ops per 128-B block
-# Peaks (DESIGN.md "Measurement"): v_mad_u64_u32 issues at half rate on gfx950
-# (profiles/r01_ubench_valu_4wps.txt), so MAC peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz.
-PEAK_TMAC = 256 * 4 * 16 * 2.4e9 / 1e12    # 39.32 TMAC/s
+# Peaks (DESIGN.md "Measurement"): v_mad_u64_u32 issues at half rate on gfx950, so the spec
+# MAC peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz; the measured one is the microbenchmark's
+# v_mad_u64_u32 issue rate at 4 waves/SIMD (profiles/r01_ubench_valu_4wps.txt).
+PEAK_TMAC = 256 * 4 * 16 * 2.4e9 / 1e12    # 39.32 TMAC/s (spec)
+PEAK_TMAC_MEASURED = 32.39                 # TMAC/s (measured, v_mad_u64_u32)
 PEAK_TOPS_FULL = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.64 T int32 lane-ops/s (full-rate ops)
 PEAK_HBM_GBS = 8000.0
 
@@ -88,6 +94,55 @@ def enc_y(y: int, sign: int) -> bytes:
 
 def log(msg: str) -> None:
     print(f"[bench r{os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
+
+
+def host_cores() -> dict:
+    """CPU threads the baselines may use: the affinity mask (what nproc reports), capped by
+    the cgroup CPU quota when one is set (the GPU box grants a CPU share smaller than the
+    machine) and by OMP_NUM_THREADS when the environment sets it."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:                                                    # cgroup v2
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        try:                                                # cgroup v1
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, q // per)
+        except (OSError, ValueError):
+            pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = aff
+    for cap in (quota, int(omp) if omp and omp.isdigit() else None):
+        if cap:
+            threads = min(threads, cap)
+    return {"threads": threads, "affinity_cpus": aff, "cgroup_quota_cpus": quota,
+            "omp_num_threads": omp}
+
+
+def oracle_module():
+    """The CPU oracle (test infrastructure, used only by the cpu_baseline legs), loaded with
+    its OpenMP threads pinned one per core (OMP_PROC_BIND / OMP_PLACES are read when libgomp
+    initialises, i.e. on first load)."""
+    os.environ.setdefault("OMP_PROC_BIND", "close")
+    os.environ.setdefault("OMP_PLACES", "cores")
+    from oracle import oracle as O
+    return O
+
+
+def median_rate(fn, units: int, runs: int = 5) -> tuple[float, list[float]]:
+    """Median over ``runs`` wall-clock runs of fn() (warm: one untimed run first) as
+    units/s; returns (median rate, per-run seconds)."""
+    fn()
+    secs = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        fn()
+        secs.append(time.perf_counter() - t0)
+    return units / float(np.median(secs)), secs
 
 
 def ptr(t: torch.Tensor) -> ctypes.c_void_p:
@@ -196,12 +251,21 @@ def timed_steps(launch, steps: int, warmup: int, world: int):
 
 # ------------------------------------------------------------------------ workloads
 def run_strict(args, dev, stream, rank, world):
+    """Config 4: ONE global corpus of items_per_gpu x world items (the same seeded unique
+    corpus on every rank, item g = unique[g mod U]); rank r verifies its contiguous shard
+    (narwhal_amd.shard.shard_range, 64-item aligned) and the verdict bitmaps are gathered
+    with one all_gather (RCCL) into the global 100M-bit bitmap, which rank 0 compares bit
+    for bit with the construction."""
+    from narwhal_amd.shard import gather_bitmaps, shard_range
     L = _lib.lib()
-    n = args.items_per_gpu
-    log(f"building corpus: {args.unique} unique items, tiled to {n}")
-    msgs_u, pks_u, sigs_u, valid_u = build_strict_corpus(dev, stream, args.unique, 4096,
-                                                        seed=1000 + rank)
-    msgs, pks, sigs = tile(msgs_u, n), tile(pks_u, n), tile(sigs_u, n)
+    n_total = args.items_per_gpu * world
+    s0, e0 = shard_range(n_total, rank, world)
+    n = e0 - s0
+    log(f"building corpus: {args.unique} unique items; global {n_total}, shard [{s0}, {e0})")
+    msgs_u, pks_u, sigs_u, valid_u = build_strict_corpus(dev, stream, args.unique, 4096, seed=1000)
+    idx = torch.arange(s0, e0, dtype=torch.int64, device=dev) % args.unique
+    msgs, pks, sigs = (t.index_select(0, idx).contiguous() for t in (msgs_u, pks_u, sigs_u))
+    del idx
     status = torch.empty(n, dtype=torch.int32, device=dev)
     bitmap = torch.zeros((n + 63) // 64 * 8, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
@@ -211,14 +275,29 @@ def run_strict(args, dev, stream, rank, world):
                                           ptr(bitmap), stream), "verify_strict")
 
     elapsed, kernel_ms = timed_steps(launch, args.steps, args.warmup, world)
-    # full-size parity property: the verdict bitmap equals the construction
-    bits = np.unpackbits(bitmap.cpu().numpy(), bitorder="little")[:n].astype(bool)
-    exp = np.resize(valid_u, n)
-    ok = bool(np.array_equal(bits, exp))
+    # the exchange step: one gather of every shard's verdict bitmap (ceil(n/8) bytes each)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    words = bitmap.view(torch.int64)
+    if world > 1 and dist.get_backend() != "nccl":
+        words = words.cpu()
+    full = gather_bitmaps(words, n_total, world)
+    gather_ms = (time.perf_counter() - t0) * 1e3
+    # parity: local statuses vs the construction, then the global bitmap on rank 0
+    exp_local = np.resize(valid_u, args.unique)[(np.arange(s0, e0) % args.unique)]
     st = status.cpu().numpy()
-    ok &= bool(np.array_equal(st == 0, exp))
-    return dict(n=n, elapsed=elapsed, kernel_ms=kernel_ms, parity=ok,
-                sample=(msgs_u, pks_u, sigs_u, st[: args.unique]))
+    ok = bool(np.array_equal(st == 0, exp_local))
+    if rank == 0:
+        bits = np.unpackbits(full.cpu().numpy(), bitorder="little")[:n_total].astype(bool)
+        ok &= bool(np.array_equal(bits, np.resize(valid_u, n_total)))
+    if world > 1:
+        t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64,
+                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        ok = bool(t.item() == 1.0)
+    del msgs, pks, sigs
+    return dict(n=n, n_total=n_total, elapsed=elapsed, kernel_ms=kernel_ms, parity=ok,
+                gather_ms=gather_ms, sample=(msgs_u, pks_u, sigs_u, st[: args.unique]))
 
 
 def run_sha(args, dev, stream, rank, world):
@@ -254,9 +333,9 @@ def cpu_baseline_sha(sample, seconds: float):
     thread, passes until about ``seconds``; digests checked against hashlib. OpenSSL's
     SHA-512 (hashlib, one batch per thread) is timed beside it for context."""
     from concurrent.futures import ThreadPoolExecutor
-    from oracle import oracle as O
+    O = oracle_module()
     ub, expect = sample
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = host_cores()["threads"]
     n = len(ub)
     data = np.ascontiguousarray(ub).reshape(-1)
     offs = np.arange(n, dtype=np.uint64) * W.BATCH_BYTES
@@ -284,22 +363,31 @@ def cpu_baseline_sha(sample, seconds: float):
                 parity="ok" if ok else "FAIL")
 
 
-def run_cert(args, dev, stream, rank, world, N: int):
+def run_cert(args, dev, stream, rank, world, N: int, invalid: float = 0.0, stream_cache=None):
     """Config 2: Certificate::verify stream, committee N, q = 2N/3 + 1 votes per cert.
-    65,536 unique certificates (signed on the GPU), tiled to --certs; no dedup/caching."""
+    65,536 unique certificates (signed on the GPU), tiled to --certs; no dedup/caching.
+    invalid > 0: that fraction of the unique certificates (evenly spaced, so every merged
+    group holds some) carries one invalid vote (workloads.mutate_votes: equation, s high
+    bits, R not on the curve); statuses AND indices are checked against the construction
+    for every certificate of the tiled stream."""
     L = _lib.lib()
     uniq = min(args.cert_unique, args.certs)
-    keys = [(bytes(pk), bytes(sd) + bytes(pk)) for sd, pk in
-            zip(W.fixture_seeds(N), C.keypair_from_seed_many(W.fixture_seeds(N)))]
-
-    def sign_many(sks, msgs):
-        return C.sign_many(sks, msgs)
-
-    def digest_many(data, offsets):
-        return C.sha512_digest32_many(data, offsets[:-1], np.diff(offsets))
-
-    log(f"cert stream N={N}: building {uniq} unique certificates, tiled to {args.certs}")
-    s = W.certificate_stream(uniq, keys, sign_many, digest_many, seed=rank)
+    if stream_cache is not None and N in stream_cache:
+        s = stream_cache[N]
+    else:
+        keys = [(bytes(pk), bytes(sd) + bytes(pk)) for sd, pk in
+                zip(W.fixture_seeds(N), C.keypair_from_seed_many(W.fixture_seeds(N)))]
+        log(f"cert stream N={N}: building {uniq} unique certificates, tiled to {args.certs}")
+        s = W.certificate_stream(uniq, keys, lambda sk, m: C.sign_many(sk, m),
+                                 lambda d, o: C.sha512_digest32_many(d, o[:-1], np.diff(o)),
+                                 seed=rank)
+        if stream_cache is not None:
+            stream_cache[N] = s
+    exp_st_u = np.zeros(uniq, np.int32)
+    exp_ix_u = np.zeros(uniq, np.uint64)
+    if invalid > 0:
+        step = max(1, int(round(1 / invalid)))
+        s, exp_st_u, exp_ix_u = W.mutate_votes(s, np.arange(step // 2, uniq, step), seed=N)
     q, n = s["q"], args.certs
     Lh = int(s["header_offsets"][1])
     reps = (n + uniq - 1) // uniq
@@ -320,6 +408,7 @@ def run_cert(args, dev, stream, rank, world, N: int):
     host_vo = (np.arange(n + 1, dtype=np.uint64) * q)
     ws = torch.empty(L.nw_dev_certificates_workspace(n, nv), dtype=torch.uint8, device=dev)
     st = torch.empty(n, dtype=torch.int32, device=dev)
+    ix = torch.empty(n, dtype=torch.int64, device=dev)
     P = lambda t: t.data_ptr()
     cc = M._CCommittee(N, P(Cm["pks"]), P(Cm["stakes"]), P(Cm["worker_offsets"]),
                        P(Cm["worker_ids"]))
@@ -331,20 +420,65 @@ def run_cert(args, dev, stream, rank, world, N: int):
 
     def launch():
         check(L.nw_dev_certificates_verify_many(ctypes.byref(cc), ctypes.byref(cs), 0, None, None,
-                                                ptr(ws), ptr(st), None, stream), "certificates")
+                                                ptr(ws), ptr(st), ptr(ix), stream), "certificates")
 
     elapsed, kernel_ms = timed_steps(launch, args.cert_steps, 1, world)
-    ok = bool((st == 0).all().item())
+    exp_st = torch.from_numpy(exp_st_u).to(dev).repeat(reps)[:n]
+    exp_ix = torch.from_numpy(exp_ix_u.astype(np.int64)).to(dev).repeat(reps)[:n]
+    ok = bool(torch.equal(st, exp_st) and torch.equal(ix, exp_ix))
     sec = elapsed / args.cert_steps
-    mac = MAC_PER_STRICT_VERIFY + q * MAC_PER_BATCH_ITEM_SMALL
+    mac_survey = MAC_PER_STRICT_VERIFY + q * MAC_PER_BATCH_ITEM_SMALL
+    mac_group = MAC_PER_STRICT_VERIFY + q * MAC_PER_GROUP_VOTE
+    ach = n * mac_group / (kernel_ms * 1e-3) / 1e12
     res = {"committee": N, "quorum": q, "certs_per_gpu": n, "unique_certs": uniq,
+           "invalid_fraction": float((exp_st_u != 0).mean()),
            "certs_per_s": n * world / sec, "sig_checks_per_s": n * (q + 1) * world / sec,
-           "ms_per_step": sec * 1e3, "achieved_TMAC_s": n * mac / (kernel_ms * 1e-3) / 1e12,
-           "work_per_cert": f"{mac} MAC (SURVEY 8d: strict + q x small-n batch item)",
-           "parity": "ok" if ok else "FAIL"}
-    del T, ws, st
+           "ms_per_step": sec * 1e3,
+           "achieved_TMAC_s": ach, "frac": ach / PEAK_TMAC, "frac_measured": ach / PEAK_TMAC_MEASURED,
+           "work_per_cert": f"{mac_group} MAC (strict header 204,800 + q x {MAC_PER_GROUP_VOTE} "
+                            f"per grouped vote: 1 R decompression + <= 17 bucket additions)",
+           "survey_TMAC_s": n * mac_survey / (kernel_ms * 1e-3) / 1e12,
+           "survey_work_note": "SURVEY 8(d) small-n constant (per-certificate Straus, 128,000 "
+                               "MAC/vote) overstates the grouped algorithm's work; not a roofline",
+           "parity": "ok" if ok else "FAIL",
+           "parity_check": "status and index of every certificate == construction"}
+    del T, ws, st, ix
     torch.cuda.empty_cache()
-    return res
+    return res, (s, exp_st_u, exp_ix_u)
+
+
+def cpu_baseline_cert(sample, N: int, seconds: float):
+    """Config 2 on the host cores (BASELINE.md row 2): the oracle's Certificate::verify
+    restatement (Header::verify strict + Signature::verify_batch per certificate, the
+    reference's per-certificate algorithm, primary/src/messages.rs:189-215) over a bounded
+    prefix of the same unique stream, all threads, pinned, median of 5 runs; statuses and
+    indices compared with the construction (= the GPU's)."""
+    O = oracle_module()
+    s, exp_st, exp_ix = sample
+    cores = host_cores()
+    T = cores["threads"]
+
+    def prefix(m):
+        ho, vo = s["header_offsets"], s["vote_offsets"]
+        return {"header_bytes": s["header_bytes"][: int(ho[m])], "header_offsets": ho[: m + 1],
+                "payload_counts": s["payload_counts"][:m], "ids": s["ids"][:m],
+                "header_sigs": s["header_sigs"][:m], "vote_offsets": vo[: m + 1],
+                "vote_pks": s["vote_pks"][: int(vo[m])], "vote_sigs": s["vote_sigs"][: int(vo[m])]}
+
+    m = min(len(exp_st), 256)
+    t0 = time.perf_counter()
+    O.certificates_verify_many(s["committee"], prefix(m), nthreads=T)
+    per = (time.perf_counter() - t0) / m
+    m = int(min(len(exp_st), max(m, seconds / 6 / max(per, 1e-9))))
+    p = prefix(m)
+    st, ix = O.certificates_verify_many(s["committee"], p, nthreads=T)
+    agree = bool(np.array_equal(st, exp_st[:m]) and np.array_equal(ix, exp_ix[:m]))
+    rate, secs = median_rate(lambda: O.certificates_verify_many(s["committee"], p, nthreads=T), m)
+    return {"value": rate, "unit": "certs/s", "cores": T, "kind": "port",
+            "host": cores, "pinned": os.environ.get("OMP_PROC_BIND"),
+            "sample": f"median of {len(secs)} runs over the first {m} unique N={N} certificates, "
+                      f"oracle certificates_verify_many (per-certificate verify_batch), {T} threads",
+            "run_s": secs, "statuses_match": agree}
 
 
 def run_batch10k(args, dev, stream, rank, world):
@@ -443,44 +577,55 @@ def run_wire(args, dev, stream, rank, world, N: int = 4):
 
 
 def cpu_baseline_batch(sample, seconds: float):
-    """Oracle verify_batch (the dalek-equivalent restatement, single thread like dalek's
-    verify_batch) on the same 10k batch, repeated for about ``seconds``."""
-    from oracle import oracle as O
+    """Config 1 on the host: the oracle's verify_batch (the
+    dalek-equivalent restatement, crypto/src/lib.rs:206-219) on the same 10k batch --
+    1 thread (dalek's verify_batch is single-threaded; one call = one batch) and all threads
+    with one 10k batch per thread concurrently; pinned; median of 5 runs each."""
+    O = oracle_module()
     digest, pks, sigs = sample
-    t0 = time.perf_counter()
-    k = 0
-    while True:
-        st, _ = O.verify_batch(digest.tobytes(), pks, sigs)
-        assert st == 0
-        k += 1
-        if time.perf_counter() - t0 > seconds:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": k * len(pks) / dt, "unit": "verifies/s", "cores": 1, "kind": "port",
-            "sample": f"{k} x verify_batch over the 10k config-1 batch, 1 thread, {dt:.1f} s"}
+    cores = host_cores()
+    T = cores["threads"]
+    st, _ = O.verify_batch(digest.tobytes(), pks, sigs)
+    assert st == 0
+    n = len(pks)
+    r1, s1 = median_rate(lambda: O.verify_batch(digest.tobytes(), pks, sigs), n)
+    dg = np.tile(digest, (T, 1))
+    pk_t, sg_t = np.tile(pks, (T, 1)), np.tile(sigs, (T, 1))
+    off = (np.arange(T + 1) * n).astype(np.uint64)
+    stT = O.verify_batch_many(dg, pk_t, sg_t, off, nthreads=T)
+    assert (stT == 0).all()
+    rT, sT = median_rate(lambda: O.verify_batch_many(dg, pk_t, sg_t, off, nthreads=T), T * n)
+    return {"value": rT, "unit": "verifies/s", "cores": T, "kind": "port", "host": cores,
+            "pinned": os.environ.get("OMP_PROC_BIND"),
+            "sample": f"median of 5 runs: {T} concurrent verify_batch calls over the 10k config-1 "
+                      f"batch (one per thread), oracle verify_batch_many",
+            "run_s": sT, "one_thread": {"value": r1, "unit": "verifies/s", "cores": 1,
+                                        "sample": "median of 5 single verify_batch calls "
+                                                  "(one 10k batch, 1 thread)", "run_s": s1}}
 
 
 def cpu_baseline_strict(sample, seconds: float):
-    """Oracle ('port', the dalek-equivalent restatement) on the host cores, bounded: passes
-    over the unique corpus until about ``seconds`` of wall time; the first pass's statuses
-    are compared with the GPU's."""
-    from oracle import oracle as O
+    """Oracle ('port', the dalek-equivalent restatement) on the host cores, pinned, bounded:
+    a prefix of the unique corpus sized to ~seconds/6 per run, median of 5 runs; the
+    prefix's statuses are compared with the GPU's."""
+    O = oracle_module()
     msgs_u, pks_u, sigs_u, gpu_st = sample
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    cores = host_cores()
+    T = cores["threads"]
     m, p, s = (t.cpu().numpy() for t in (msgs_u, pks_u, sigs_u))
-    n = len(m)
+    k = min(len(m), 4096)
     t0 = time.perf_counter()
-    st = O.verify_strict_many(m, p, s, nthreads=threads)
-    agree = bool(np.array_equal(st, gpu_st[:n]))
-    done, passes = n, 1
-    while time.perf_counter() - t0 < seconds:
-        O.verify_strict_many(m, p, s, nthreads=threads)
-        done += n
-        passes += 1
-    dt = time.perf_counter() - t0
-    return dict(value=done / dt, unit="verifies/s", cores=threads, kind="port",
-                sample=f"{passes} passes over the {n}-item unique mixed corpus ({done} verifies), "
-                       f"oracle verify_strict_many, {threads} threads, {dt:.1f} s"), agree
+    O.verify_strict_many(m[:k], p[:k], s[:k], nthreads=T)
+    per = (time.perf_counter() - t0) / k
+    k = int(min(len(m), max(k, seconds / 6 / max(per, 1e-9))))
+    m, p, s = m[:k], p[:k], s[:k]
+    st = O.verify_strict_many(m, p, s, nthreads=T)
+    agree = bool(np.array_equal(st, gpu_st[:k]))
+    rate, secs = median_rate(lambda: O.verify_strict_many(m, p, s, nthreads=T), k)
+    return dict(value=rate, unit="verifies/s", cores=T, kind="port", host=cores,
+                pinned=os.environ.get("OMP_PROC_BIND"),
+                sample=f"median of {len(secs)} runs over the first {k} items of the unique mixed "
+                       f"corpus, oracle verify_strict_many, {T} threads", run_s=secs), agree
 
 
 def main():
@@ -498,6 +643,9 @@ def main():
     ap.add_argument("--certs", type=int, default=1_000_000)
     ap.add_argument("--cert-unique", type=int, default=65536)
     ap.add_argument("--cert-steps", type=int, default=2)
+    ap.add_argument("--cert-invalid", type=float, default=0.01,
+                    help="extra config-2 leg with this fraction of certificates carrying a bad "
+                         "vote (0 = skip)")
     ap.add_argument("--committees", default="4,10,50,100")
     ap.add_argument("--no-cert", action="store_true", help="skip the config-2 certificate leg")
     ap.add_argument("--no-batch", action="store_true", help="skip the config-1 verify_batch leg")
@@ -538,7 +686,7 @@ def main():
     result = {}
     if args.workload == "strict":
         r = run_strict(args, dev, stream, rank, world)
-        units = r["n"] * world
+        units = r["n_total"]
         value = units / r["elapsed"] * args.steps
         achieved = r["n"] * MAC_PER_STRICT_VERIFY / (r["kernel_ms"] * 1e-3) / 1e12
         traffic, tsrc = pmc_traffic("k_verify_strict", r["n"])
@@ -548,11 +696,19 @@ def main():
             "ms_per_step": r["elapsed"] / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
             "config": {"workload": "config4_mixed_corpus_strict_verify",
-                       "items_per_gpu": r["n"], "unique_items": args.unique,
+                       "items_per_gpu": r["n"], "items_total": r["n_total"],
+                       "unique_items": args.unique,
                        "invalid_fraction": 0.1, "semantics": "crypto::Signature::verify (dalek verify_strict)",
-                       "parallelism": f"shard{world}"},
+                       "parallelism": f"shard{world}",
+                       "exchange": "all_gather of the per-shard verdict bitmaps",
+                       "gather_ms": r["gather_ms"]},
             "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_TMAC,
-                         "unit": "TMAC/s", "frac": achieved / PEAK_TMAC, "traffic": traffic,
+                         "unit": "TMAC/s", "frac": achieved / PEAK_TMAC,
+                         "peak_measured": PEAK_TMAC_MEASURED,
+                         "frac_measured": achieved / PEAK_TMAC_MEASURED,
+                         "peak_source": "spec 256 CU x 4 SIMD x 16 MAC/clk x 2.4 GHz; measured "
+                                        "v_mad_u64_u32 rate, profiles/r01_ubench_valu_4wps.txt",
+                         "traffic": traffic,
                          "traffic_unit": "HBM bytes per launch", "traffic_source": tsrc,
                          "algorithmic_bytes": r["n"] * (32 + 32 + 64 + 4) + r["n"] / 8,
                          "kernel": "k_verify_strict", "kernel_ms": r["kernel_ms"],
@@ -585,11 +741,25 @@ def main():
                 result["parity"] = "FAIL"
         if not args.no_cert:
             result["cert_stream"] = {}
+            result["cert_stream_invalid"] = {}
+            cache = {}
             for N in [int(x) for x in args.committees.split(",") if x]:
-                r2 = run_cert(args, dev, stream, rank, world, N)
+                r2, csample = run_cert(args, dev, stream, rank, world, N, stream_cache=cache)
                 result["cert_stream"][f"N{N}"] = r2
                 if r2["parity"] != "ok":
                     result["parity"] = "FAIL"
+                if rank == 0 and world == 1 and not args.no_cpu_baseline:
+                    r2["cpu_baseline"] = cpu_baseline_cert(csample, N, min(6.0, args.cpu_seconds))
+                    if not r2["cpu_baseline"]["statuses_match"]:
+                        result["parity"] = "FAIL"
+                if args.cert_invalid > 0:
+                    r3, _ = run_cert(args, dev, stream, rank, world, N, invalid=args.cert_invalid,
+                                     stream_cache=cache)
+                    r3["vs_all_valid"] = r3["certs_per_s"] / r2["certs_per_s"]
+                    result["cert_stream_invalid"][f"N{N}"] = r3
+                    if r3["parity"] != "ok":
+                        result["parity"] = "FAIL"
+                cache.pop(N, None)
         if not args.no_batch:
             r1, bsample = run_batch10k(args, dev, stream, rank, world)
             result["verify_batch_10k"] = r1
@@ -609,8 +779,15 @@ def main():
                 result["parity"] = "FAIL"
                 log("oracle disagrees with GPU statuses on the cpu_baseline sample")
     elif args.workload == "cert":
-        res = {f"N{N}": run_cert(args, dev, stream, rank, world, N)
-               for N in [int(x) for x in args.committees.split(",") if x]}
+        res, res_bad, cache = {}, {}, {}
+        for N in [int(x) for x in args.committees.split(",") if x]:
+            res[f"N{N}"] = run_cert(args, dev, stream, rank, world, N, stream_cache=cache)[0]
+            if args.cert_invalid > 0:
+                r3 = run_cert(args, dev, stream, rank, world, N, invalid=args.cert_invalid,
+                              stream_cache=cache)[0]
+                r3["vs_all_valid"] = r3["certs_per_s"] / res[f"N{N}"]["certs_per_s"]
+                res_bad[f"N{N}"] = r3
+            cache.pop(N, None)
         last = list(res.values())[-1]
         result = {"metric": METRIC, "value": last["sig_checks_per_s"], "unit": "verifies/s",
                   "n_gpus": world, "steps": args.cert_steps, "warmup": 1,
@@ -618,8 +795,9 @@ def main():
                   "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
                   "config": {"workload": "config2_certificate_stream",
                              "certs_per_gpu": args.certs, "parallelism": f"shard{world}"},
-                  "cert_stream": res,
-                  "parity": "ok" if all(r["parity"] == "ok" for r in res.values()) else "FAIL"}
+                  "cert_stream": res, "cert_stream_invalid": res_bad,
+                  "parity": "ok" if all(r["parity"] == "ok" for r in
+                                        list(res.values()) + list(res_bad.values())) else "FAIL"}
     elif args.workload == "batch":
         r1, bsample = run_batch10k(args, dev, stream, rank, world)
         result = {"metric": METRIC, "value": r1["verifies_per_s_resident"], "unit": "verifies/s",
