@@ -180,10 +180,58 @@ __global__ __launch_bounds__(256) void k_sha512_digest32(const uint8_t* __restri
 // Strict verification
 // ---------------------------------------------------------------------------------------
 
+// Makes p opaque to the optimiser: a load through the result is not merged with an earlier
+// load of the same address, so inputs are re-fetched where they are needed instead of
+// being kept live (and spilled) across the decompression.
+template <class T>
+__device__ __forceinline__ const T* opaque_ptr(const T* p) {
+  asm volatile("" : "+v"(p));
+  return p;
+}
+
+// strict_verify_core's inputs for item i, fetched from global memory when needed.
+struct strict_src_global {
+  const uint32_t* pk;    // 8 words
+  const uint32_t* sig;   // 16 words: R || s
+  const uint32_t* msg;   // 8 words
+  __device__ void A(uint32_t w[8]) const {
+    const uint32_t* p = opaque_ptr(pk);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = p[j];
+  }
+  __device__ void R(uint32_t w[8]) const {
+    const uint32_t* p = opaque_ptr(sig);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = p[j];
+  }
+  __device__ void S(uint32_t w[8]) const {
+    const uint32_t* p = opaque_ptr(sig);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = p[8 + j];
+  }
+  // k = SHA-512(R || A || M) mod l over the raw bytes
+  __device__ void K(uint32_t kw[8]) const {
+    uint32_t Aw[8], Rw[8], Mw[8], hx[16];
+    A(Aw);
+    R(Rw);
+    const uint32_t* m = opaque_ptr(msg);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Mw[j] = m[j];
+    hram96(hx, Rw, Aw, Mw);
+    sc k;
+    sc_reduce512(k, hx);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) kw[j] = k.w[j];
+  }
+};
+
 // Persistent: the grid covers the resident waves once and strides over the items, so the
 // per-lane tables j*A, j*R live in a fixed workspace (16 entries x 160 B per lane slot, lane-
 // contiguous: a lookup reads 160 consecutive bytes per lane instead of 40 scattered dwords).
-__global__ __launch_bounds__(256, 3) void k_verify_strict(const uint32_t* __restrict__ msgs,
+#ifndef NW_STRICT_WAVES
+#define NW_STRICT_WAVES 3
+#endif
+__global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const uint32_t* __restrict__ msgs,
                                                        uint32_t msg_stride_words,
                                                        const uint32_t* __restrict__ pks,
                                                        const uint32_t* __restrict__ sigs,
@@ -204,22 +252,11 @@ __global__ __launch_bounds__(256, 3) void k_verify_strict(const uint32_t* __rest
     const uint64_t gi = base + threadIdx.x;
     const bool active = gi < n;
     const uint64_t i = active ? gi : n - 1;
-    uint32_t Aw[8], Rw[8], Sw[8], Mw[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      Aw[j] = pks[8 * i + j];
-      Rw[j] = sigs[16 * i + j];
-      Sw[j] = sigs[16 * i + 8 + j];
-      Mw[j] = msgs[(uint64_t)msg_stride_words * i + j];
-    }
-    uint32_t hx[16];
-    hram96(hx, Rw, Aw, Mw);
-    sc k;
-    sc_reduce512(k, hx);
+    const strict_src_global src{pks + 8 * i, sigs + 16 * i, msgs + (uint64_t)msg_stride_words * i};
     const uint32_t kk = keys.vote_key ? keys.vote_key[i] : kNoKey;
     const ge_cached* keytab = kk != kNoKey ? keys.tabs + kKeyTab * (uint64_t)kk : nullptr;
-    const int st = strict_verify_core(Aw, Rw, Sw, k, g_consts.sk, s_btab, s_b128, tabA, tabR,
-                                      WaveMax{}, keytab, kk != kNoKey ? keys.ok[kk] : 0u);
+    const int st = strict_verify_core(src, g_consts.sk, s_btab, s_b128, tabA, tabR, WaveMax{},
+                                      keytab, kk != kNoKey ? keys.ok[kk] : 0u);
     if (active) status[gi] = st;
     const uint64_t mask = __ballot(active && st == NW_OK);
     if ((threadIdx.x & 63) == 0 && gi < n) bitmap[gi >> 6] = mask;

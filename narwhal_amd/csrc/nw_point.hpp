@@ -186,17 +186,28 @@ NW_HD bool ge_eq_affine(const ge& p, const ge& q) {
   return fe_eq(a, p.Y);
 }
 
-// curve25519-dalek FieldElement::sqrt_ratio_i -> (was_nonzero_square, non-negative r).
-NW_HD bool fe_sqrt_ratio_i(fe& r, const fe& u, const fe& v, const curve_consts& k) {
-  fe v3, v7, t, uv3, uv7, check, neg_u, neg_u_i, r_prime;
-  fe_sq(t, v);  fe_mul(v3, t, v);
-  fe_sq(t, v3); fe_mul(v7, t, v);
+// Register barrier: the optimiser may not move computation on f across this point (device
+// only). Used to keep work that follows a long exponentiation from being hoisted above it
+// and held (spilled) across its loop.
+NW_HD void fe_barrier(fe& f) {
+#ifdef __HIP_DEVICE_COMPILE__
+#pragma unroll
+  for (int i = 0; i < 10; ++i) asm volatile("" : "+v"(f.v[i]));
+#else
+  (void)f;
+#endif
+}
+
+// The last step of curve25519-dalek FieldElement::sqrt_ratio_i -> (was_nonzero_square,
+// non-negative r), given t = (u v^7)^((p-5)/8).
+NW_HD bool fe_sqrt_ratio_finish(fe& r, const fe& u, const fe& v, const fe& t,
+                                const curve_consts& k) {
+  fe v3, uv3, check, neg_u, neg_u_i, r_prime, x;
+  fe_sq(x, v);  fe_mul(v3, x, v);
   fe_mul(uv3, u, v3);
-  fe_mul(uv7, u, v7);
-  fe_pow22523(t, uv7);
   fe_mul(r, uv3, t);
-  fe_sq(t, r);
-  fe_mul(check, v, t);
+  fe_sq(x, r);
+  fe_mul(check, v, x);
   fe_neg(neg_u, u);
   fe_mul(neg_u_i, neg_u, k.sqrtm1);
   bool correct = fe_eq(check, u);
@@ -204,23 +215,50 @@ NW_HD bool fe_sqrt_ratio_i(fe& r, const fe& u, const fe& v, const curve_consts& 
   bool flipped_i = fe_eq(check, neg_u_i);
   fe_mul(r_prime, k.sqrtm1, r);
   fe_cmov(r, r_prime, flipped || flipped_i);
-  fe_neg(t, r);
-  fe_cmov(r, t, fe_isnegative(r) != 0);
+  fe_neg(x, r);
+  fe_cmov(r, x, fe_isnegative(r) != 0);
   return correct || flipped;
+}
+
+// curve25519-dalek FieldElement::sqrt_ratio_i -> (was_nonzero_square, non-negative r).
+NW_HD bool fe_sqrt_ratio_i(fe& r, const fe& u, const fe& v, const curve_consts& k) {
+  fe v3, v7, t, uv7;
+  fe_sq(t, v);  fe_mul(v3, t, v);
+  fe_sq(t, v3); fe_mul(v7, t, v);
+  fe_mul(uv7, u, v7);
+  fe_pow22523(t, uv7);
+  return fe_sqrt_ratio_finish(r, u, v, t, k);
+}
+
+// u = y^2 - 1, v = d y^2 + 1 (the decompression ratio).
+NW_HD void ge_decomp_uv(fe& u, fe& v, const fe& y, const curve_consts& k) {
+  fe yy, one;
+  fe_1(one);
+  fe_sq(yy, y);
+  fe_sub(u, yy, one);
+  fe_mul(v, yy, k.d);
+  v.v[0] += 1;
 }
 
 // curve25519-dalek CompressedEdwardsY::decompress. w = 8 LE words of the encoding.
 // Returns success; p gets (X, Y, 1, XY) with Y as loaded (possibly >= p).
+// Only y (and the power's own chain) is live across the (p-5)/8 power: u, v and u v^3 are
+// recomputed after it (2 squarings + 3 multiplications) instead of being held in registers.
 NW_HD bool ge_frombytes(ge& p, const uint32_t w[8], const curve_consts& k) {
-  fe yy, u, v, one;
+  fe u, v, t;
   fe_frombytes(p.Y, w);
-  fe_1(one);
-  fe_sq(yy, p.Y);
-  fe_sub(u, yy, one);
-  fe_mul(v, yy, k.d);
-  v.v[0] += 1;
-  bool ok = fe_sqrt_ratio_i(p.X, u, v, k);
-  fe t;
+  {
+    fe v3, v7, uv7;
+    ge_decomp_uv(u, v, p.Y, k);
+    fe_sq(t, v);  fe_mul(v3, t, v);
+    fe_sq(t, v3); fe_mul(v7, t, v);
+    fe_mul(uv7, u, v7);
+    fe_pow22523(t, uv7);
+  }
+  fe_barrier(t);
+  fe_barrier(p.Y);
+  ge_decomp_uv(u, v, p.Y, k);
+  bool ok = fe_sqrt_ratio_finish(p.X, u, v, t, k);
   fe_neg(t, p.X);
   fe_cmov(p.X, t, (w[7] >> 31) != 0);
   fe_1(p.Z);

@@ -10,10 +10,18 @@
 //   3. Half-size scalars (nw_scalar.hpp sc_half_split): u = v k (mod 8l), v odd, and
 //      w = -v s mod l; then  R + [k]A - [s]B == 0  <=>  [v]R + [u]A + [w]B == 0.
 //   4. One ladder of ~128 doublings: signed 4-bit windows over u (table j*A) and |v|
-//      (table j*(+-R)), per-lane tables in private memory; w = w0 + 2^128 w1 by signed
-//      8-bit windows over two affine tables (j*B and j*2^128 B, LDS).
+//      (table j*R, digits negated when v < 0), per-lane tables in private memory;
+//      w = w0 + 2^128 w1 by signed 8-bit windows over two affine tables (j*B and
+//      j*2^128 B, LDS).
 #pragma once
 #include "narwhal_amd.h"
+
+#ifndef NW_TAB_RELOAD
+#define NW_TAB_RELOAD 0
+#endif
+#ifndef NW_DBL_UNROLL
+#define NW_DBL_UNROLL 0
+#endif
 #include "nw_ladder.hpp"
 
 namespace nw {
@@ -55,7 +63,7 @@ NW_HD void add_table_digit(ge& acc, const ge_cached* tab, int d, bool want_t) {
 }
 
 NW_HD void build_table8(ge_cached tab[8], const ge& P, const fe& d2) {
-  ge_cached c1;                 // 1*P stays in registers (no re-reads of tab[0])
+  ge_cached c1;
   ge_to_cached(c1, P, d2);
   tab[0] = c1;
   ge acc;
@@ -65,11 +73,36 @@ NW_HD void build_table8(ge_cached tab[8], const ge& P, const fe& d2) {
   tab[1] = cj;
 #pragma unroll 1
   for (int j = 3; j <= 8; ++j) {
+#if NW_TAB_RELOAD
+    // 1*P re-read from the lane's own table slot instead of held in 40 registers
+    const ge_cached* t0 = tab;
+#ifdef __HIP_DEVICE_COMPILE__
+    asm volatile("" : "+v"(t0));   // a fresh load each iteration, not hoisted
+#endif
+    ge_cached c = *t0;
+    ge_add_cached(acc, acc, c, true);
+#else
     ge_add_cached(acc, acc, c1, true);
+#endif
     ge_to_cached(cj, acc, d2);
     tab[j - 1] = cj;
   }
 }
+
+// Inputs of one strict verification, fetched when needed (so nothing but the decompression
+// is live across the decompression): A(w) / R(w) / S(w) give the 8 LE words of the public
+// key, of R and of s; k(x) gives k = H(R || A || M) mod l. The kernel's source reloads
+// from global memory; the host self-check's returns copies of its arrays.
+struct strict_src_arrays {
+  const uint32_t* a;
+  const uint32_t* r;
+  const uint32_t* s;
+  const uint32_t* k;
+  NW_HD void A(uint32_t w[8]) const { for (int i = 0; i < 8; ++i) w[i] = a[i]; }
+  NW_HD void R(uint32_t w[8]) const { for (int i = 0; i < 8; ++i) w[i] = r[i]; }
+  NW_HD void S(uint32_t w[8]) const { for (int i = 0; i < 8; ++i) w[i] = s[i]; }
+  NW_HD void K(uint32_t w[8]) const { for (int i = 0; i < 8; ++i) w[i] = k[i]; }
+};
 
 // Status of one strict verification. wave_max maps this lane's ladder length (in 4-bit
 // windows) to the wave's maximum (identity on the host). tabA/tabR: 8 entries each of
@@ -77,35 +110,37 @@ NW_HD void build_table8(ge_cached tab[8], const ge& P, const fe& d2) {
 // keytab (optional): A's pre-decompressed key table j*A, j = 0..128 (cached form) with
 // keyflags bit 0 = decoded, bit 1 = small order; then A is neither decompressed nor
 // tabulated here and u is taken in signed 8-bit windows over that table.
-template <class WaveMax>
-NW_HD int strict_verify_core(const uint32_t Aw[8], const uint32_t Rw[8], const uint32_t Sw[8],
-                             const sc& k, const strict_consts& K, const ge_niels* s_btab,
+template <class Src, class WaveMax>
+NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const ge_niels* s_btab,
                              const ge_niels* s_b128, ge_cached* tabA, ge_cached* tabR,
                              WaveMax wave_max, const ge_cached* keytab = nullptr,
                              uint32_t keyflags = 0) {
-  const bool s_high = (Sw[7] >> 29) != 0;
-  sc s;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s.w[j] = Sw[j];
-  const bool s_canon = sc_is_canonical(s);
-
   // Decompress A, then R, in one rolled loop (one copy of the sqrt_ratio_i chain in the
-  // code object): P, its small-order flag and its 8-entry table.
-  sc_half h;
-  sc_half_split(h, k);
+  // code object): P, its small-order flag and its 8-entry table j * P. Only the point is
+  // live here: the scalars are computed afterwards (register pressure).
   bool okA = (keyflags & 1) != 0, smallA = (keyflags & 2) != 0, okR = false, smallR = false;
 #pragma unroll 1
   for (int pt = keytab ? 1 : 0; pt < 2; ++pt) {
     uint32_t x[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) x[i] = pt ? Rw[i] : Aw[i];
+    if (pt) src.R(x); else src.A(x);
     ge P;
     const bool ok = ge_frombytes(P, x, K.k);
     const bool small = small_order_by_y(P.Y, K.small_y);
     if (pt == 0) { okA = ok; smallA = small; } else { okR = ok; smallR = small; }
-    if (pt == 1 && h.vneg) ge_neg(P, P);
     build_table8(pt ? tabR : tabA, P, K.k.d2);
   }
+
+  uint32_t Sw[8], kw[8];
+  src.S(Sw);
+  src.K(kw);
+  const bool s_high = (Sw[7] >> 29) != 0;
+  sc s, k;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s.w[j] = Sw[j]; k.w[j] = kw[j]; }
+  const bool s_canon = sc_is_canonical(s);
+  // v < 0: [v]R = [|v|](-R), taken as negated R digits (the table holds j * R)
+  sc_half h;
+  sc_half_split(h, k);
 
   // w = -v s mod l (s zeroed when invalid: the verdict is already decided)
   sc vm, w;
@@ -159,7 +194,11 @@ NW_HD int strict_verify_core(const uint32_t Aw[8], const uint32_t Rw[8], const u
 #pragma unroll 1
   for (int j = W - 1; j >= 0; --j) {
     if (j != W - 1) {
+#if NW_DBL_UNROLL
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
       for (int t = 0; t < 4; ++t) ge_dbl(acc, acc, t == 3);
     }
     const int nslots = ((j & 1) == 0 && j < 32) ? 4 : 2;
@@ -171,6 +210,7 @@ NW_HD int strict_verify_core(const uint32_t Aw[8], const uint32_t Rw[8], const u
                     : (j & 1) ? 0 : (int)((sel8(ud, j >> 3) >> (((j >> 1) & 3) * 8)) & 255u) - 128;
       } else if (slot == 1) {
         d = j < 40 ? digit4_of(vd, 5, j) : 0;
+        if (h.vneg) d = -d;
       } else {
         const int m = j >> 1;   // 8-bit window m of w0 (word m / 4) and of w1 (word 4 + m / 4)
         d = (int)((sel8(wd, (slot == 2 ? 0 : 4) + (m >> 2)) >> ((m & 3) * 8)) & 255u) - 128;

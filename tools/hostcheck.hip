@@ -120,9 +120,10 @@ int hc_verify_strict_half(const uint8_t pk[32], const uint8_t sig[64], const uin
   init();
   uint32_t Aw[8], Rw[8], Sw[8];
   load8(Aw, pk); load8(Rw, sig); load8(Sw, sig + 32);
-  sc k; load8(k.w, k32);
+  uint32_t kw[8]; load8(kw, k32);
   ge_cached ta[8], tr[8];
-  return strict_verify_core(Aw, Rw, Sw, k, SK, BT, B128, ta, tr, [](int w) { return w; });
+  const strict_src_arrays src{Aw, Rw, Sw, kw};
+  return strict_verify_core(src, SK, BT, B128, ta, tr, [](int w) { return w; });
 }
 
 }
