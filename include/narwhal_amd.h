@@ -69,7 +69,13 @@ extern "C" {
 int nw_init(void);
 /* Number of usable devices (0 if none). */
 int nw_device_count(void);
-/* Device used by the calling thread's host-buffer calls (default 0). */
+/* Device used by the calling thread's calls (default 0). NW_ALL_DEVICES: the calling
+ * thread's host-buffer calls (nw_submit_*, the blocking calls built on them, and the
+ * Header / Vote / Certificate host calls) split their items into contiguous parts, one per
+ * device, run them concurrently on per-device streams and merge the outputs in order, so
+ * one process (Narwhal's single Core task, primary/src/core.rs:338-346) drives every GPU;
+ * the nw_dev_* calls (device pointers) then fail with NW_E_INVALID_ARG. */
+#define NW_ALL_DEVICES (-1)
 int nw_set_device(int device);
 int nw_get_device(void);
 /* Human-readable description of the calling thread's last error ("" if none). */

@@ -7,12 +7,17 @@
 // There is no CPU fallback: without a gfx950 device every call fails with NW_E_NO_DEVICE.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/random.h>
 
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "narwhal_amd.h"
@@ -110,6 +115,9 @@ int begin(DevCtx** out) {
   int rc = ensure_init();
   if (rc) return rc;
   int dev = t_state.device;
+  if (dev == NW_ALL_DEVICES)
+    return set_err(NW_E_INVALID_ARG, "this entry point runs on one device: nw_set_device(d), "
+                                     "d >= 0 (NW_ALL_DEVICES fans out host-buffer calls only)");
   if (dev < 0 || dev >= g_ndev) return set_err(NW_E_INVALID_ARG, "bad device index");
   hipError_t e = hipSetDevice(g_dev_ids[dev]);
   if (e != hipSuccess) return set_err(NW_E_DEVICE, "hipSetDevice", e);
@@ -176,7 +184,8 @@ int nw_device_count(void) {
 int nw_set_device(int device) {
   int rc = ensure_init();
   if (rc) return rc;
-  if (device < 0 || device >= g_ndev) return set_err(NW_E_INVALID_ARG, "bad device index");
+  if (device != NW_ALL_DEVICES && (device < 0 || device >= g_ndev))
+    return set_err(NW_E_INVALID_ARG, "bad device index");
   t_state.device = device;
   return 0;
 }
@@ -612,17 +621,139 @@ int certs_host(const nw_committee* com, const nw_certificates* cs, int headers_o
   return 0;
 }
 
+// ---- fan-out of the blocking message calls (nw_set_device(NW_ALL_DEVICES)) ----------
+// One persistent host worker thread per part (its thread-local stream and staging buffers
+// persist across calls); a call splits its messages into contiguous parts, runs part p on
+// worker p with device devs[p], waits for all and returns the first failure.
+class PartWorker {
+ public:
+  PartWorker() : th_([this] { loop(); }) { th_.detach(); }
+  void post(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_one();
+  }
+
+ private:
+  void loop() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [this] { return !q_.empty(); });
+        f = std::move(q_.front());
+        q_.pop_front();
+      }
+      f();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  std::thread th_;
+};
+
+PartWorker* part_worker(size_t p) {
+  static std::mutex m;
+  static PartWorker* w[kMaxDevices] = {};   // never destroyed (detached threads)
+  std::lock_guard<std::mutex> g(m);
+  if (!w[p]) w[p] = new PartWorker;
+  return w[p];
+}
+
+// fn(begin, end) for every non-empty part [b[p], b[p+1]) on its worker, the worker's
+// nw_set_device set to devs[p]; blocks until all parts are done.
+template <class Fn>
+int fan_out_blocking(const std::vector<int>& devs, const std::vector<size_t>& b, Fn fn) {
+  const size_t P = devs.size();
+  std::vector<int> rc(P, 0);
+  std::vector<std::string> err(P);
+  std::mutex m;
+  std::condition_variable cv;
+  size_t left = 0;
+  for (size_t p = 0; p < P; ++p) left += b[p + 1] > b[p];
+  for (size_t p = 0; p < P; ++p) {
+    if (b[p + 1] == b[p]) continue;
+    part_worker(p)->post([&, p] {
+      t_state.device = devs[p];
+      const int r = fn(b[p], b[p + 1]);
+      std::lock_guard<std::mutex> g(m);
+      rc[p] = r;
+      if (r < 0) err[p] = t_state.err;
+      if (--left == 0) cv.notify_all();
+    });
+  }
+  {
+    std::unique_lock<std::mutex> g(m);
+    cv.wait(g, [&] { return left == 0; });
+  }
+  for (size_t p = 0; p < P; ++p)
+    if (rc[p] < 0) return set_err(rc[p], err[p].c_str());
+  return 0;
+}
+
+// Contiguous parts of n messages with about equal weight (prefix sums w[0..n]).
+std::vector<size_t> parts_by_weight(size_t n, size_t P, const std::vector<uint64_t>& w) {
+  std::vector<size_t> b(P + 1, 0);
+  size_t i = 0;
+  for (size_t p = 1; p < P; ++p) {
+    const uint64_t target = w[n] * p / P;
+    while (i < n && w[i] < target) ++i;
+    b[p] = i;
+  }
+  b[P] = n;
+  return b;
+}
+
+int certs_fanout(const std::vector<int>& devs, const nw_committee* com, const nw_certificates* cs,
+                 int headers_only, const uint8_t* z16, int32_t* status_out, uint64_t* index_out) {
+  if (!cs || !status_out) return set_err(NW_E_INVALID_ARG, "null pointer");
+  const size_t n = cs->n;
+  if (!headers_only && n && !cs->vote_offsets)
+    return set_err(NW_E_INVALID_ARG, "vote_offsets is NULL");
+  std::vector<uint64_t> w(n + 1, 0);
+  for (size_t i = 0; i < n; ++i)
+    w[i + 1] = w[i] + 1 + (headers_only ? 0 : cs->vote_offsets[i + 1] - cs->vote_offsets[i]);
+  return fan_out_blocking(devs, parts_by_weight(n, devs.size(), w), [&](size_t a, size_t e) {
+    nw_certificates part = *cs;
+    part.n = e - a;
+    part.header_offsets = cs->header_offsets + a;   // absolute: certs_host rebases
+    part.payload_counts = cs->payload_counts + a;
+    part.ids = cs->ids + 32 * a;
+    part.header_sigs = cs->header_sigs + 64 * a;
+    std::vector<uint64_t> vo;
+    const uint8_t* pz = z16;
+    if (!headers_only) {
+      const uint64_t v0 = cs->vote_offsets[a];
+      vo.resize(e - a + 1);
+      for (size_t i = a; i <= e; ++i) vo[i - a] = cs->vote_offsets[i] - v0;
+      part.vote_offsets = vo.data();
+      part.vote_pks = cs->vote_pks ? cs->vote_pks + 32 * v0 : nullptr;
+      part.vote_sigs = cs->vote_sigs ? cs->vote_sigs + 64 * v0 : nullptr;
+      if (z16) pz = z16 + 16 * v0;
+    }
+    return certs_host(com, &part, headers_only, pz, status_out + a,
+                      index_out ? index_out + a : nullptr);
+  });
+}
+
 }  // namespace
 
 extern "C" {
 
 int nw_certificates_verify_many(const nw_committee* committee, const nw_certificates* certs,
                                 const uint8_t* z16, int32_t* status_out, uint64_t* index_out) {
+  const std::vector<int> devs = nw::rt::fanout_devices();
+  if (!devs.empty()) return certs_fanout(devs, committee, certs, 0, z16, status_out, index_out);
   return certs_host(committee, certs, 0, z16, status_out, index_out);
 }
 
 int nw_headers_verify_many(const nw_committee* committee, const nw_certificates* headers,
                            int32_t* status_out, uint64_t* index_out) {
+  const std::vector<int> devs = nw::rt::fanout_devices();
+  if (!devs.empty()) return certs_fanout(devs, committee, headers, 1, nullptr, status_out, index_out);
   return certs_host(committee, headers, 1, nullptr, status_out, index_out);
 }
 
@@ -660,6 +791,17 @@ int nw_votes_verify_many(const nw_committee* committee, const uint8_t* ids,
                          const uint64_t* rounds, const uint8_t* origins,
                          const uint8_t* authors, const uint8_t* sigs, size_t n,
                          int32_t* status_out) {
+  const std::vector<int> devs = nw::rt::fanout_devices();
+  if (!devs.empty()) {
+    if (n && (!ids || !rounds || !origins || !authors || !sigs || !status_out))
+      return set_err(NW_E_INVALID_ARG, "null pointer");
+    std::vector<uint64_t> w(n + 1);
+    for (size_t i = 0; i <= n; ++i) w[i] = i;
+    return fan_out_blocking(devs, parts_by_weight(n, devs.size(), w), [&](size_t a, size_t e) {
+      return nw_votes_verify_many(committee, ids + 32 * a, rounds + a, origins + 32 * a,
+                                  authors + 32 * a, sigs + 64 * a, e - a, status_out + a);
+    });
+  }
   DevCtx* c;
   int rc = begin(&c);
   if (rc) return rc;
@@ -731,6 +873,35 @@ int select_device(int* dev_index) {
   if (e != hipSuccess) return ::set_err(NW_E_DEVICE, "hipSetDevice", e);
   *dev_index = dev;
   return 0;
+}
+
+int use_device(int dev_index) {
+  int rc = ::ensure_init();
+  if (rc) return rc;
+  if (dev_index < 0 || dev_index >= g_ndev) return ::set_err(NW_E_INVALID_ARG, "bad device index");
+  hipError_t e = hipSetDevice(g_dev_ids[dev_index]);
+  if (e != hipSuccess) return ::set_err(NW_E_DEVICE, "hipSetDevice", e);
+  return 0;
+}
+
+int thread_device() { return t_state.device; }
+
+void set_thread_device(int dev_index) { t_state.device = dev_index; }
+
+int device_count() { return g_init_status > 0 ? g_ndev : 0; }
+
+std::vector<int> fanout_devices() {
+  std::vector<int> out;
+  if (t_state.device != NW_ALL_DEVICES || ::ensure_init()) return out;
+  // NW_FANOUT_PARTS=k (test hook): k parts dealt round-robin over the devices, so the
+  // split/merge logic runs on a one-GPU machine too
+  int parts = g_ndev;
+  if (const char* e = getenv("NW_FANOUT_PARTS")) {
+    const int k = atoi(e);
+    if (k > 0 && k <= 64) parts = k;
+  }
+  for (int p = 0; p < parts; ++p) out.push_back(p % g_ndev);
+  return out;
 }
 
 int set_err(int code, const char* what, hipError_t e) { return ::set_err(code, what, e); }

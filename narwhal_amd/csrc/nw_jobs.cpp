@@ -14,9 +14,18 @@
 // Strict verification uses the device's shared table workspace (nw::rt::Lease): launches
 // from different jobs and streams are ordered on it with an event chain (the copies of one
 // job still overlap the kernels of another).
+//
+// Fan-out (nw_set_device(NW_ALL_DEVICES)): a submit splits its items into contiguous parts,
+// one per device (strict: 64-item aligned so bitmap bytes concatenate; verify_batch: whole
+// batches, about equal votes per part; SHA-512: whole messages, about equal bytes), submits
+// each part as an ordinary job on its device and returns a parent job over them; poll /
+// wait / notify / release act on every part, and each part delivers straight into its slice
+// of the caller's outputs.
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -40,6 +49,7 @@ struct nw_job {
   } outs[3];
   int nouts = 0;
   bool pending = false;   // device work queued, outputs not yet delivered
+  std::vector<nw_job*> parts;   // fan-out parent (dev = -1): one ordinary job per part
 };
 
 namespace {
@@ -62,9 +72,8 @@ inline size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
     if (e_ != hipSuccess) return set_err(NW_E_DEVICE, what, e_); \
   } while (0)
 
-int job_acquire(nw_job** out) {
-  int dev = 0;
-  int rc = nw::rt::select_device(&dev);
+int job_acquire(int dev, nw_job** out) {
+  int rc = nw::rt::use_device(dev);
   if (rc) return rc;
   DevPool& p = g_pool[dev];
   nw_job* j = nullptr;
@@ -95,6 +104,11 @@ int job_acquire(nw_job** out) {
 
 void job_recycle(nw_job* j) {
   if (!j) return;
+  if (!j->parts.empty() || j->dev < 0) {   // fan-out parent: recycle the parts
+    for (nw_job* x : j->parts) job_recycle(x);
+    delete j;
+    return;
+  }
   if (j->pending) (void)hipEventSynchronize(j->done);
   j->pending = false;
   j->nouts = 0;
@@ -165,20 +179,12 @@ int fill_key(nw::z_key_t& k) {
   return rc;
 }
 
-}  // namespace
-
-extern "C" {
-
-int nw_submit_verify_strict(const uint8_t* digests, size_t digest_stride, const uint8_t* pks,
-                            const uint8_t* sigs, size_t n, int32_t* status_out,
-                            uint8_t* bitmap_out, nw_job** job) {
-  if (!job) return set_err(NW_E_INVALID_ARG, "null job pointer");
-  *job = nullptr;
-  if (n && (!digests || !pks || !sigs)) return set_err(NW_E_INVALID_ARG, "null pointer");
-  if (digest_stride != 0 && digest_stride != 32)
-    return set_err(NW_E_INVALID_ARG, "digest_stride must be 0 or 32");
+// ---- one device --------------------------------------------------------------------
+int submit_strict(int dev, const uint8_t* digests, size_t digest_stride, const uint8_t* pks,
+                  const uint8_t* sigs, size_t n, int32_t* status_out, uint8_t* bitmap_out,
+                  nw_job** job) {
   nw_job* j;
-  int rc = job_acquire(&j);
+  int rc = job_acquire(dev, &j);
   if (rc) return rc;
   if (n == 0) {
     *job = j;
@@ -217,21 +223,13 @@ int nw_submit_verify_strict(const uint8_t* digests, size_t digest_stride, const 
   return 0;
 }
 
-int nw_submit_verify_batch_many(const uint8_t* digests, const uint8_t* pks, const uint8_t* sigs,
-                                const uint64_t* offsets, size_t nbatches, const uint8_t* z16,
-                                int32_t* status_out, uint64_t* fail_index_out, nw_job** job) {
-  if (!job) return set_err(NW_E_INVALID_ARG, "null job pointer");
-  *job = nullptr;
-  if (nbatches && (!digests || !offsets)) return set_err(NW_E_INVALID_ARG, "null pointer");
-  if (nbatches) {
-    if (offsets[0] != 0) return set_err(NW_E_INVALID_ARG, "offsets[0] must be 0");
-    for (size_t b = 0; b < nbatches; ++b)
-      if (offsets[b + 1] < offsets[b]) return set_err(NW_E_INVALID_ARG, "offsets not monotone");
-  }
+// offsets: nbatches + 1 host values from 0
+int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint8_t* sigs,
+                 const uint64_t* offsets, size_t nbatches, const uint8_t* z16,
+                 int32_t* status_out, uint64_t* fail_index_out, nw_job** job) {
   const size_t nitems = nbatches ? offsets[nbatches] : 0;
-  if (nitems && (!pks || !sigs)) return set_err(NW_E_INVALID_ARG, "null pointer");
   nw_job* j;
-  int rc = job_acquire(&j);
+  int rc = job_acquire(dev, &j);
   if (rc) return rc;
   if (nbatches == 0) {
     *job = j;
@@ -276,15 +274,10 @@ int nw_submit_verify_batch_many(const uint8_t* digests, const uint8_t* pks, cons
   return 0;
 }
 
-int nw_submit_sha512_digest32_many(const uint8_t* data, const uint64_t* offsets,
-                                   const uint64_t* lengths, size_t n, uint8_t* out32,
-                                   nw_job** job) {
-  if (!job) return set_err(NW_E_INVALID_ARG, "null job pointer");
-  *job = nullptr;
-  if (n && (!data || !offsets || !lengths || !out32))
-    return set_err(NW_E_INVALID_ARG, "null pointer");
+int submit_sha(int dev, const uint8_t* data, const uint64_t* offsets, const uint64_t* lengths,
+               size_t n, uint8_t* out32, nw_job** job) {
   nw_job* j;
-  int rc = job_acquire(&j);
+  int rc = job_acquire(dev, &j);
   if (rc) return rc;
   if (n == 0) {
     *job = j;
@@ -327,8 +320,150 @@ int nw_submit_sha512_digest32_many(const uint8_t* data, const uint64_t* offsets,
   return 0;
 }
 
+// ---- fan-out --------------------------------------------------------------------------
+// Runs submit(device, begin, end, &job) for each non-empty part [b[p], b[p+1]) and returns a
+// parent over the parts (or, for a single device without NW_ALL_DEVICES, the job itself).
+template <class Submit>
+int fan_out(const std::vector<int>& devs, const std::vector<size_t>& b, Submit submit,
+            nw_job** job) {
+  nw_job* parent = new (std::nothrow) nw_job;
+  if (!parent) return set_err(NW_E_OUT_OF_MEMORY, "job allocation");
+  for (size_t p = 0; p + 1 < b.size(); ++p) {
+    if (b[p + 1] == b[p] && !(p == 0 && b.back() == 0)) continue;
+    nw_job* sub = nullptr;
+    const int rc = submit(devs[p], b[p], b[p + 1], &sub);
+    if (rc) {
+      job_recycle(parent);
+      return rc;
+    }
+    parent->parts.push_back(sub);
+  }
+  *job = parent;
+  return 0;
+}
+
+// Part p of n items over P parts, boundaries rounded down to a multiple of `align`.
+std::vector<size_t> even_bounds(size_t n, size_t P, size_t align) {
+  std::vector<size_t> b(P + 1);
+  for (size_t p = 0; p <= P; ++p) b[p] = p == P ? n : std::min(n, n * p / P / align * align);
+  return b;
+}
+
+// Boundaries (indices into n units) with about equal weight prefix[i] per part.
+std::vector<size_t> weighted_bounds(size_t n, size_t P, const std::vector<uint64_t>& prefix) {
+  std::vector<size_t> b(P + 1, 0);
+  const uint64_t tot = prefix[n];
+  size_t i = 0;
+  for (size_t p = 1; p < P; ++p) {
+    const uint64_t target = tot * p / P;
+    while (i < n && prefix[i] < target) ++i;
+    b[p] = i;
+  }
+  b[P] = n;
+  return b;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nw_submit_verify_strict(const uint8_t* digests, size_t digest_stride, const uint8_t* pks,
+                            const uint8_t* sigs, size_t n, int32_t* status_out,
+                            uint8_t* bitmap_out, nw_job** job) {
+  if (!job) return set_err(NW_E_INVALID_ARG, "null job pointer");
+  *job = nullptr;
+  if (n && (!digests || !pks || !sigs)) return set_err(NW_E_INVALID_ARG, "null pointer");
+  if (digest_stride != 0 && digest_stride != 32)
+    return set_err(NW_E_INVALID_ARG, "digest_stride must be 0 or 32");
+  const std::vector<int> devs = nw::rt::fanout_devices();
+  if (devs.empty()) {
+    int dev = 0;
+    int rc = nw::rt::select_device(&dev);
+    return rc ? rc : submit_strict(dev, digests, digest_stride, pks, sigs, n, status_out,
+                                   bitmap_out, job);
+  }
+  return fan_out(devs, even_bounds(n, devs.size(), 64),
+                 [&](int dev, size_t a, size_t e, nw_job** sub) {
+                   return submit_strict(dev, digests + (digest_stride ? 32 * a : 0),
+                                        digest_stride, pks + 32 * a, sigs + 64 * a, e - a,
+                                        status_out ? status_out + a : nullptr,
+                                        bitmap_out ? bitmap_out + a / 8 : nullptr, sub);
+                 },
+                 job);
+}
+
+int nw_submit_verify_batch_many(const uint8_t* digests, const uint8_t* pks, const uint8_t* sigs,
+                                const uint64_t* offsets, size_t nbatches, const uint8_t* z16,
+                                int32_t* status_out, uint64_t* fail_index_out, nw_job** job) {
+  if (!job) return set_err(NW_E_INVALID_ARG, "null job pointer");
+  *job = nullptr;
+  if (nbatches && (!digests || !offsets)) return set_err(NW_E_INVALID_ARG, "null pointer");
+  if (nbatches) {
+    if (offsets[0] != 0) return set_err(NW_E_INVALID_ARG, "offsets[0] must be 0");
+    for (size_t b = 0; b < nbatches; ++b)
+      if (offsets[b + 1] < offsets[b]) return set_err(NW_E_INVALID_ARG, "offsets not monotone");
+  }
+  const size_t nitems = nbatches ? offsets[nbatches] : 0;
+  if (nitems && (!pks || !sigs)) return set_err(NW_E_INVALID_ARG, "null pointer");
+  const std::vector<int> devs = nw::rt::fanout_devices();
+  if (devs.empty()) {
+    int dev = 0;
+    int rc = nw::rt::select_device(&dev);
+    return rc ? rc : submit_batch(dev, digests, pks, sigs, offsets, nbatches, z16, status_out,
+                                  fail_index_out, job);
+  }
+  // whole batches per part, about equal votes (+1 per batch for its fixed tail)
+  std::vector<uint64_t> w(nbatches + 1);
+  for (size_t b = 0; b <= nbatches; ++b) w[b] = offsets[b] + b;
+  return fan_out(devs, weighted_bounds(nbatches, devs.size(), w),
+                 [&](int dev, size_t a, size_t e, nw_job** sub) {
+                   std::vector<uint64_t> off(e - a + 1);
+                   for (size_t b = a; b <= e; ++b) off[b - a] = offsets[b] - offsets[a];
+                   const uint64_t v0 = offsets[a];
+                   return submit_batch(dev, digests + 32 * a, pks ? pks + 32 * v0 : nullptr,
+                                       sigs ? sigs + 64 * v0 : nullptr, off.data(), e - a,
+                                       z16 ? z16 + 16 * v0 : nullptr,
+                                       status_out ? status_out + a : nullptr,
+                                       fail_index_out ? fail_index_out + a : nullptr, sub);
+                 },
+                 job);
+}
+
+int nw_submit_sha512_digest32_many(const uint8_t* data, const uint64_t* offsets,
+                                   const uint64_t* lengths, size_t n, uint8_t* out32,
+                                   nw_job** job) {
+  if (!job) return set_err(NW_E_INVALID_ARG, "null job pointer");
+  *job = nullptr;
+  if (n && (!data || !offsets || !lengths || !out32))
+    return set_err(NW_E_INVALID_ARG, "null pointer");
+  const std::vector<int> devs = nw::rt::fanout_devices();
+  if (devs.empty()) {
+    int dev = 0;
+    int rc = nw::rt::select_device(&dev);
+    return rc ? rc : submit_sha(dev, data, offsets, lengths, n, out32, job);
+  }
+  // whole messages per part, about equal bytes (+1 per message)
+  std::vector<uint64_t> w(n + 1, 0);
+  for (size_t i = 0; i < n; ++i) w[i + 1] = w[i] + lengths[i] + 1;
+  return fan_out(devs, weighted_bounds(n, devs.size(), w),
+                 [&](int dev, size_t a, size_t e, nw_job** sub) {
+                   return submit_sha(dev, data, offsets + a, lengths + a, e - a, out32 + 32 * a,
+                                     sub);
+                 },
+                 job);
+}
+
 int nw_job_poll(nw_job* job) {
   if (!job) return set_err(NW_E_INVALID_ARG, "null job");
+  if (!job->parts.empty()) {
+    int done = 1;
+    for (nw_job* x : job->parts) {
+      const int rc = nw_job_poll(x);
+      if (rc < 0) return rc;
+      done &= rc;
+    }
+    return done;
+  }
   if (!job->pending) return 1;
   hipError_t e = hipEventQuery(job->done);
   if (e == hipErrorNotReady) return 0;
@@ -339,14 +474,55 @@ int nw_job_poll(nw_job* job) {
 
 int nw_job_wait(nw_job* job) {
   if (!job) return set_err(NW_E_INVALID_ARG, "null job");
+  if (!job->parts.empty()) {
+    int first = 0;
+    for (nw_job* x : job->parts) {
+      const int rc = nw_job_wait(x);
+      if (rc && !first) first = rc;
+    }
+    return first;
+  }
   if (!job->pending) return 0;
   JOB_HIP(hipEventSynchronize(job->done), "hipEventSynchronize");
   job_deliver(job);
   return 0;
 }
 
+namespace {
+// fn(arg) once every part of a fan-out job has finished (from the last part's callback)
+struct Countdown {
+  std::atomic<int> left;
+  void (*fn)(void*);
+  void* arg;
+};
+void countdown_tick(void* p) {
+  Countdown* c = static_cast<Countdown*>(p);
+  if (c->left.fetch_sub(1) == 1) {
+    c->fn(c->arg);
+    delete c;
+  }
+}
+}  // namespace
+
 int nw_job_notify(nw_job* job, void (*fn)(void*), void* arg) {
   if (!job || !fn) return set_err(NW_E_INVALID_ARG, "null job or callback");
+  if (!job->parts.empty()) {
+    Countdown* c = new (std::nothrow) Countdown;
+    if (!c) return set_err(NW_E_OUT_OF_MEMORY, "notify");
+    c->left = (int)job->parts.size() + 1;   // +1: released below, after every part is armed
+    c->fn = fn;
+    c->arg = arg;
+    int first = 0;
+    for (nw_job* x : job->parts) {
+      const int rc = nw_job_notify(x, countdown_tick, c);
+      if (rc && !first) {
+        first = rc;
+        countdown_tick(c);   // this part will never tick: count it now
+      }
+    }
+    countdown_tick(c);
+    return first;
+  }
   if (!job->pending) {
     fn(arg);
     return 0;

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 
+#include <vector>
+
 namespace nw {
 namespace rt {
 
@@ -12,6 +14,15 @@ int ensure_init();
 // Make the calling thread's selected device (nw_set_device) current for HIP; returns 0 and
 // the library device index, or a negative NW_E_*.
 int select_device(int* dev_index);
+// Make library device dev_index current for HIP on this thread (0 or NW_E_*).
+int use_device(int dev_index);
+// The calling thread's nw_set_device value (NW_ALL_DEVICES = fan out), and setting it.
+int thread_device();
+void set_thread_device(int dev_index);
+int device_count();
+// With nw_set_device(NW_ALL_DEVICES): the device index of every part a host-buffer call is
+// split into (one per device, or NW_FANOUT_PARTS parts round-robin); empty otherwise.
+std::vector<int> fanout_devices();
 // Record the calling thread's last error (nw_last_error) and return `code`.
 int set_err(int code, const char* what, hipError_t e = hipSuccess);
 // Fill buf from the OS CSPRNG (getrandom).

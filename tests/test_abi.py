@@ -36,6 +36,10 @@ def test_no_device_fails_loudly():
     assert L.nw_verify_strict_many(b"\0" * 32, 32, b"\0" * 32, b"\0" * 64, 1,
                                    ctypes.byref(st), None) == -2
     assert b"gfx950" in L.nw_last_error()
+    # the fan-out mode fails the same way (no silent CPU path behind NW_ALL_DEVICES)
+    assert L.nw_set_device(-1) == -2
+    assert L.nw_submit_verify_strict(b"\0" * 32, 32, b"\0" * 32, b"\0" * 64, 1, None, None,
+                                     ctypes.byref(ctypes.c_void_p())) == -2
 
 
 def test_header_status_codes_match_oracle():
