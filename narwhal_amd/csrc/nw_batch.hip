@@ -28,7 +28,7 @@
 #include "nw_ladder.hpp"
 #include "nw_consts.hpp"
 #include "nw_strict.hpp"
-#include "nw_quad.hpp"
+#include "nw_lp.hpp"
 
 #include <stdlib.h>
 
@@ -664,7 +664,10 @@ __global__ __launch_bounds__(256) void k_bv_combine(const uint32_t* __restrict__
 //                  entries; the order inside a bucket does not matter, addition commutes)
 //   k_pip_buckets  G lanes per bucket: partial sums, combined by a lane-shuffle tree
 //   k_pip_windows  one wave per window: sum_b b S_b by a suffix scan + tree over lanes
-//   k_pip_final    one workgroup per batch: sum b_i, first failures, Horner, identity test
+//   k_pip_bsum     one workgroup per batch: sum b_i and first failures; -sum b_i becomes
+//                  the batch's last bucketed point (B), so the Horner adds no B terms
+//   k_pip_final    one wave per batch: the 248-doubling Horner over the window sums,
+//                  limb-parallel (nw_lp.hpp), identity test, status
 //
 // Each batch's scratch lives in the per-item table slots of its own items (16 cached
 // entries = 2560 B per item, unused by this path): pip_region() lays it out.
@@ -692,17 +695,18 @@ struct pip_region {
   uint32_t* off;     // kPipBins: first entry of each bucket
   ge* S;             // kPipBins bucket sums
   ge_cached* W;      // kPipWin window sums (cached form, for the Horner)
+  uint32_t* hdr;     // k_pip_bsum -> k_pip_final: first failures (3) and their flags
 };
 
 constexpr size_t pip_region_bytes(uint64_t n) {
   return 2 * n * sizeof(ge_niels) + 4 * kPipWinCap * n + 52 * n + 8 * kPipBins +
-         sizeof(ge) * kPipBins + sizeof(ge_cached) * kPipWin;
+         sizeof(ge) * kPipBins + sizeof(ge_cached) * kPipWin + 16;
 }
 // per-vote bytes grow slower than the item slots (2560 B), so the floor is the binding n
-static_assert(pip_region_bytes(kPipFloor) <= 16 * sizeof(ge_cached) * kPipFloor,
+static_assert(pip_region_bytes(kPipFloor + 1) <= 16 * sizeof(ge_cached) * kPipFloor,
               "Pippenger region does not fit its items' table slots");
 // certificate groups: >= kPipMin votes plus up to 256 committee keys
-static_assert(pip_region_bytes(kPipMin + 256) <= 16 * sizeof(ge_cached) * kPipMin,
+static_assert(pip_region_bytes(kPipMin + 256 + 1) <= 16 * sizeof(ge_cached) * kPipMin,
               "certificate-group region does not fit its votes' table slots");
 
 // Certificate-group mode (launch_cert_groups): a "batch" is a group of whole certificates;
@@ -733,7 +737,8 @@ __device__ __forceinline__ pip_region pip_at(ge_cached* tabs, uint64_t li0, uint
   r.cnt = reinterpret_cast<uint32_t*>(p); p += 4 * kPipBins;
   r.off = reinterpret_cast<uint32_t*>(p); p += 4 * kPipBins;
   r.S = reinterpret_cast<ge*>(p); p += sizeof(ge) * kPipBins;
-  r.W = reinterpret_cast<ge_cached*>(p);
+  r.W = reinterpret_cast<ge_cached*>(p); p += sizeof(ge_cached) * kPipWin;
+  r.hdr = reinterpret_cast<uint32_t*>(p);
   return r;
 }
 
@@ -770,16 +775,22 @@ __device__ __forceinline__ void ge_shfl(ge& r, const ge& p, int src) {
   }
 }
 
-// Lane -> (item, which): waves alternate A and R so a wave never mixes the two.
+// Lane -> (item, role): consecutive waves take the roles of 64 votes in turn, so a wave
+// never mixes two: role 0 = the vote's scalars (SHA-512 k, z, c, b, digits, parse flags;
+// in group mode also the committee-key lookup), role 1 = decompress R, role 2 (plain
+// batches only: in group mode A is a committee key) = decompress A. Three short chains
+// instead of one lane doing the scalars and A's decompression in series (the one-call
+// latency of config 1 is this kernel's longest lane).
 __global__ __launch_bounds__(256, 3) void k_pip_points(
     const uint32_t* __restrict__ digests, const uint64_t* __restrict__ offsets, uint64_t b0,
     uint64_t b1, uint64_t i0, uint64_t i1, uint32_t pmin, const uint32_t* __restrict__ pks,
     const uint32_t* __restrict__ sigs, const uint32_t* __restrict__ z16, z_key_t zkey,
-    bv_item* __restrict__ items, ge_cached* __restrict__ tabs, pip_group_t grp) {
+    bv_item* __restrict__ items, ge_cached* __restrict__ tabs, pip_group_t grp,
+    uint32_t roles) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t wave = g >> 6;
-  const int which = (int)(wave & 1);
-  const uint64_t li = (wave >> 1) * 64 + (g & 63);
+  const int which = (int)(wave % roles);
+  const uint64_t li = (wave / roles) * 64 + (g & 63);
   const uint64_t gi = i0 + li;
   if (gi >= i1) return;
   const uint64_t lo = batch_of(offsets, b0, b1, gi);
@@ -787,7 +798,7 @@ __global__ __launch_bounds__(256, 3) void k_pip_points(
   if (n < pmin) return;
   const uint64_t t = gi - bs;
   const bool group = grp.cert_vote_offsets != nullptr;
-  const uint64_t nreg = n + (group ? grp.nkeys : 0);
+  const uint64_t nreg = n + (group ? grp.nkeys : 0) + 1;   // + key sums + the B term
   const pip_region reg = pip_at(tabs, bs - i0, nreg);
   const curve_consts& K = g_bc.k;
   bv_item* it = items + li;
@@ -800,7 +811,8 @@ __global__ __launch_bounds__(256, 3) void k_pip_points(
       // decided before the votes: contributes nothing
       if (which == 1) {
         it->pad = 0;
-      } else {
+      } else if (which == 0) {
+        it->z[0] = 0;
 #pragma unroll
         for (int w = 0; w < kPipWin; ++w) reg.cd[w * nreg + t] = 0x80;
 #pragma unroll
@@ -813,16 +825,22 @@ __global__ __launch_bounds__(256, 3) void k_pip_points(
       return;
     }
   }
-  ge P;
-  ge_niels q;
-  if (which == 1) {
-    uint32_t Rw[8];
+  if (which != 0) {   // decompress R (role 1) or A (role 2) into the region
+    uint32_t w8[8];
+    const uint32_t* src = which == 1 ? sigs + 16 * gi : pks + 8 * gi;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) Rw[j] = sigs[16 * gi + j];
-    const bool ok = ge_frombytes(P, Rw, K);
-    it->pad = ok ? 0u : (uint32_t)BF_R_DECODE;
+    for (int j = 0; j < 8; ++j) w8[j] = src[j];
+    ge P;
+    ge_niels q;
+    const bool ok = ge_frombytes(P, w8, K);
     ge_to_niels_z1(q, P, K.d2);
-    reg.pts[2 * t + 1] = q;
+    if (which == 1) {
+      it->pad = ok ? 0u : (uint32_t)BF_R_DECODE;
+      reg.pts[2 * t + 1] = q;
+    } else {
+      it->z[0] = ok ? 0u : (uint32_t)BF_A_DECODE;   // Pippenger batches: z[] is unused
+      reg.pts[2 * t] = q;
+    }
     return;
   }
   uint32_t Aw[8], Rw[8], Sw[8], Mw[8];
@@ -876,10 +894,7 @@ __global__ __launch_bounds__(256, 3) void k_pip_points(
       it->c[j] = c.w[j];
       cr[j] = 0x80808080u;
     }
-  } else {
-    if (!ge_frombytes(P, Aw, K)) flags |= BF_A_DECODE;
-    ge_to_niels_z1(q, P, K.d2);
-    reg.pts[2 * t] = q;
+    it->z[0] = 0;   // no A lane in group mode
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) it->b[j] = b.w[j];
@@ -902,7 +917,7 @@ __global__ __launch_bounds__(1024) void k_grp_keys(const uint64_t* __restrict__ 
   const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
   if (n < pmin) return;
   const uint32_t N = grp.nkeys;
-  const uint64_t nreg = n + N;
+  const uint64_t nreg = n + N + 1;   // votes, key sums, the B term
   const pip_region reg = pip_at(tabs, bs - i0, nreg);
   const int tid = threadIdx.x;
   for (int k = tid; k < 256 * 8; k += 1024) s_acc[k >> 3][k & 7] = 0;
@@ -978,7 +993,7 @@ __global__ __launch_bounds__(1024) void k_pip_sort(const uint32_t* __restrict__ 
   const uint64_t bidx = b0 + pip_list[blockIdx.y];
   const uint64_t bs = offsets[bidx], n0 = offsets[bidx + 1] - bs;
   if (n0 < pmin) return;
-  const uint64_t n = n0 + extra;   // votes + (group mode) key sums
+  const uint64_t n = n0 + extra;   // votes + (group mode) key sums + the B term
   const pip_region reg = pip_at(tabs, bs - i0, n);
   const int w = blockIdx.x, tid = threadIdx.x;
   if (tid < NL) s_h[tid] = 0;
@@ -1126,32 +1141,45 @@ __global__ __launch_bounds__(64) void k_pip_windows(const uint32_t* __restrict__
   }
 }
 
-__global__ __launch_bounds__(256) void k_pip_final(const uint32_t* __restrict__ pip_list,
+// One workgroup per batch, before the sort: sum_i b_i and the first failures (in the
+// reference's order) over the batch's votes; -sum b_i enters the bucket MSM as one more
+// point (B, the last "vote" of the region: t = n + extra - 1, c digits only), so the
+// Horner in k_pip_final has no B additions.
+// Scalar sum a += b mod l and first-failure merge across lanes (xor shuffles).
+__device__ __forceinline__ void bsum_merge(sc& a, uint32_t f[4], int o) {
+  sc b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b.w[j] = (uint32_t)__shfl_xor((int)a.w[j], o);
+  sc_add(a, a, b);
+  const uint32_t g0 = (uint32_t)__shfl_xor((int)f[0], o), g3 = (uint32_t)__shfl_xor((int)f[3], o);
+  const uint32_t g1 = (uint32_t)__shfl_xor((int)f[1], o), g2 = (uint32_t)__shfl_xor((int)f[2], o);
+  if (g0 < f[0]) { f[0] = g0; f[3] = g3; }
+  f[1] = min(f[1], g1);
+  f[2] = min(f[2], g2);
+}
+
+__global__ __launch_bounds__(1024) void k_pip_bsum(const uint32_t* __restrict__ pip_list,
                                                    const uint64_t* __restrict__ offsets,
                                                    uint64_t b0, uint64_t i0,
                                                    const bv_item* __restrict__ items,
-                                                   ge_cached* __restrict__ tabs,
-                                                   int32_t* __restrict__ status,
-                                                   uint64_t* __restrict__ fail_index,
-                                                   uint32_t extra, uint32_t pmin,
-                                                   uint32_t* __restrict__ group_ok) {
-  __shared__ ge_niels s_btab[129];
-  __shared__ uint32_t s_b[256][8];
-  __shared__ uint32_t s_f[256][4];
+                                                   ge_cached* __restrict__ tabs, uint32_t extra,
+                                                   uint32_t pmin) {
+  __shared__ uint32_t s_b[16][8];
+  __shared__ uint32_t s_f[16][4];
   const uint64_t bidx = b0 + pip_list[blockIdx.x];
   const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
   if (n < pmin) return;
-  load_btab(s_btab);
-  const pip_region reg = pip_at(tabs, bs - i0, n + extra);
-  const int tid = threadIdx.x;
+  const uint64_t nreg = n + extra;
+  const pip_region reg = pip_at(tabs, bs - i0, nreg);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const bv_item* its = items + (bs - i0);
   sc bsum;
 #pragma unroll
   for (int j = 0; j < 8; ++j) bsum.w[j] = 0;
-  uint32_t f[3] = {kNone, kNone, kNone}, flags0 = 0;
-  for (uint64_t t = tid; t < n; t += 256) {
-    const uint32_t fl = its[t].flags | its[t].pad;
-    if ((fl & (BF_S_HIGH | BF_A_DECODE)) && f[0] == kNone) { f[0] = (uint32_t)t; flags0 = fl; }
+  uint32_t f[4] = {kNone, kNone, kNone, 0};
+  for (uint64_t t = tid; t < n; t += 1024) {
+    const uint32_t fl = its[t].flags | its[t].pad | its[t].z[0];   // scalar, R and A lanes
+    if ((fl & (BF_S_HIGH | BF_A_DECODE)) && f[0] == kNone) { f[0] = (uint32_t)t; f[3] = fl; }
     if ((fl & BF_S_NONCANON) && f[1] == kNone) f[1] = (uint32_t)t;
     if ((fl & BF_R_DECODE) && f[2] == kNone) f[2] = (uint32_t)t;
     sc bi;
@@ -1159,59 +1187,72 @@ __global__ __launch_bounds__(256) void k_pip_final(const uint32_t* __restrict__ 
     for (int j = 0; j < 8; ++j) bi.w[j] = its[t].b[j];
     sc_add(bsum, bsum, bi);
   }
+#pragma unroll 1
+  for (int o = 32; o > 0; o >>= 1) bsum_merge(bsum, f, o);
+  if (lane == 0) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) s_b[tid][j] = bsum.w[j];
-  s_f[tid][0] = f[0]; s_f[tid][1] = f[1]; s_f[tid][2] = f[2]; s_f[tid][3] = flags0;
-  __syncthreads();
-  for (int stride = 128; stride > 0; stride >>= 1) {
-    if (tid < stride) {
-      sc a, c;
+    for (int j = 0; j < 8; ++j) s_b[wv][j] = bsum.w[j];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { a.w[j] = s_b[tid][j]; c.w[j] = s_b[tid + stride][j]; }
-      sc_add(a, a, c);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s_b[tid][j] = a.w[j];
-      if (s_f[tid + stride][0] < s_f[tid][0]) {
-        s_f[tid][0] = s_f[tid + stride][0];
-        s_f[tid][3] = s_f[tid + stride][3];
-      }
-      s_f[tid][1] = min(s_f[tid][1], s_f[tid + stride][1]);
-      s_f[tid][2] = min(s_f[tid][2], s_f[tid + stride][2]);
-    }
-    __syncthreads();
+    for (int j = 0; j < 4; ++j) s_f[wv][j] = f[j];
   }
-  // Horner over the windows on one quad (nw_quad.hpp): wave 0 runs it, every quad the same
-  if (tid >= 64) return;
-  const qmask q = quad_mask(tid & 3);
-  sc tot, nb;
+  __syncthreads();
+  if (wv != 0) return;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) tot.w[j] = s_b[0][j];
-  sc_neg(nb, tot);
+  for (int j = 0; j < 8; ++j) bsum.w[j] = lane < 16 ? s_b[lane][j] : 0u;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) f[j] = lane < 16 ? s_f[lane][j] : (j < 3 ? kNone : 0u);
+#pragma unroll 1
+  for (int o = 8; o > 0; o >>= 1) bsum_merge(bsum, f, o);
+  if (lane != 0) return;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) reg.hdr[j] = f[j];
+  sc nb;
+  sc_neg(nb, bsum);
   uint32_t bb[8];
   sc_recode(bb, nb, 0x80808080u);
-  fe v, tab;
-  quad_identity(v, q);
+  const uint64_t t = nreg - 1;
+#pragma unroll
+  for (int w = 0; w < kPipWin; ++w) reg.cd[w * nreg + t] = (uint8_t)(bb[w >> 2] >> ((w & 3) * 8));
+#pragma unroll
+  for (int w = 0; w < kPipZWin; ++w) reg.zd[w * nreg + t] = 0x80;
+  reg.pts[2 * t] = g_bc.btab[1];   // 1 * B, affine niels
+}
+
+__global__ __launch_bounds__(64) void k_pip_final(const uint32_t* __restrict__ pip_list,
+                                                  const uint64_t* __restrict__ offsets,
+                                                  uint64_t b0, uint64_t i0,
+                                                  ge_cached* __restrict__ tabs,
+                                                  int32_t* __restrict__ status,
+                                                  uint64_t* __restrict__ fail_index,
+                                                  uint32_t extra, uint32_t pmin,
+                                                  uint32_t* __restrict__ group_ok) {
+  __shared__ uint32_t s_tmp[40];
+  const uint64_t bidx = b0 + pip_list[blockIdx.x];
+  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
+  if (n < pmin) return;
+  const pip_region reg = pip_at(tabs, bs - i0, n + extra);
+  const int tid = threadIdx.x;
+  // Horner over the windows (the B term is one of the bucketed points), the point spread
+  // limb-parallel over the wave (nw_lp.hpp)
+  const lp_ctx L = lp_init((uint32_t)tid);
+  uint32_t v = lp_identity(L);
 #pragma unroll 1
   for (int w = kPipWin - 1; w >= 0; --w) {
     if (w != kPipWin - 1) {
 #pragma unroll 1
-      for (int k = 0; k < 8; ++k) quad_dbl(v, q);
+      for (int k = 0; k < 8; ++k) v = lp_dbl(L, v);
     }
-    quad_cached_component(tab, q, reg.W[w]);
-    quad_add(v, q, tab);
-    const int e = digit8(bb, w);
-    quad_niels_component(tab, q, s_btab[e < 0 ? -e : e], e < 0);
-    quad_add(v, q, tab);
+    v = lp_add(L, v, lp_cached_component(L, reg.W[w]));
   }
-  const bool ident = quad_is_identity(v);
+  const bool ident = lp_is_identity(L, v, s_tmp);
   if (tid != 0) return;
-  const uint32_t ff[3] = {s_f[0][0], s_f[0][1], s_f[0][2]};
+  const uint32_t ff[3] = {reg.hdr[0], reg.hdr[1], reg.hdr[2]};
   if (group_ok) {   // group mode: any flag or a nonzero sum sends the group to the fallback
     group_ok[bidx] = (ff[0] == kNone && ff[1] == kNone && ff[2] == kNone && ident) ? 1u : 0u;
     return;
   }
   uint64_t idx;
-  const int st = batch_status(ff, s_f[0][3], ident, n, &idx);
+  const int st = batch_status(ff, reg.hdr[3], ident, n, &idx);
   status[bidx] = st;
   if (fail_index) fail_index[bidx] = idx;
 }
@@ -1338,17 +1379,23 @@ void launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t b, ui
                 const z_key_t& zkey, const bv_ws& w, int32_t* status, uint64_t* fail_index,
                 const pip_group_t& grp, hipStream_t stream) {
   const bool group = grp.cert_vote_offsets != nullptr;
-  const uint32_t extra = group ? grp.nkeys : 0;
-  hipLaunchKernelGGL(k_pip_points, dim3((unsigned)((i1 - i0 + 63) / 64 * 2 * 64 + 255) / 256),
+  const uint32_t extra = (group ? grp.nkeys : 0) + 1;   // key sums, the B term
+  const uint32_t roles = group ? 2 : 3;
+  hipLaunchKernelGGL(k_pip_points,
+                     dim3((unsigned)((i1 - i0 + 63) / 64 * roles * 64 + 255) / 256),
                      dim3(256), 0, stream, digests, offsets, b, e, i0, i1, pmin, pks, sigs, z16,
-                     zkey, w.items, w.tabs, grp);
+                     zkey, w.items, w.tabs, grp, roles);
   if (group)
     hipLaunchKernelGGL(k_grp_keys, dim3((unsigned)npip), dim3(1024), 0, stream, offsets, b, i0,
                        pmin, w.items, w.tabs, grp);
+  hipLaunchKernelGGL(k_pip_bsum, dim3((unsigned)npip), dim3(1024), 0, stream, w.pip_list, offsets,
+                     b, i0, w.items, w.tabs, extra, pmin);
   hipLaunchKernelGGL(k_pip_sort, dim3(kPipWin, (unsigned)npip), dim3(1024), 0, stream,
                      w.pip_list, offsets, b, i0, extra, pmin, w.tabs);
   // G lanes per bucket: about 8 additions each at the largest batch's mean bucket size
-  // (<= 49 digits per vote over kPipBins buckets)
+  // (<= 49 digits per vote over kPipBins buckets); more lanes measured slower (the shuffle
+  // tree's full additions cost more than the niels additions they replace: 10k batch,
+  // G = 64 122 us vs G = 16 68 us)
   uint32_t lg = 0;
   while (lg < 6 && (49 * (pmax + extra)) / kPipBins > 8ull << lg) ++lg;
   // ... but no more lanes than the chip runs at once (the shuffle tree is overhead)
@@ -1360,14 +1407,18 @@ void launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t b, ui
                      (uint32_t)npip, bpb, xcd, extra, pmin, w.tabs);
   hipLaunchKernelGGL(k_pip_windows, dim3(kPipWin, (unsigned)npip), dim3(64), 0, stream,
                      w.pip_list, offsets, b, i0, extra, pmin, w.tabs);
-  hipLaunchKernelGGL(k_pip_final, dim3((unsigned)npip), dim3(256), 0, stream, w.pip_list,
-                     offsets, b, i0, w.items, w.tabs, status, fail_index, extra, pmin,
-                     grp.group_ok);
+  hipLaunchKernelGGL(k_pip_final, dim3((unsigned)npip), dim3(64), 0, stream, w.pip_list,
+                     offsets, b, i0, w.tabs, status, fail_index, extra, pmin, grp.group_ok);
 }
 
 uint32_t pip_min() {
   return (uint32_t)std::max<uint64_t>(
       kPipFloor, std::min<uint64_t>(0xffffffffu, env_u64("NW_BATCH_PIPPENGER_MIN", kPipMin)));
+}
+
+__global__ __launch_bounds__(256) void k_iota(uint32_t* __restrict__ list, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) list[i] = i;
 }
 
 // Group g = certificates [g K, min(g K + K, ncert)): gofs[g] = its first vote; identity list.
@@ -1432,13 +1483,20 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
     }
     const uint64_t i0 = host_offsets[b], i1 = host_offsets[e];
     const unsigned nblk = (unsigned)((e - b + 1023) / 1024);
-    hipLaunchKernelGGL(k_bv_plan_local, dim3(nblk), dim3(1024), 0, stream, offsets, b, e, C, pmin,
-                       sk, w.plan_tot);
-    hipLaunchKernelGGL(k_bv_plan_top, dim3(1), dim3(1024), 0, stream, nblk, e - b, w.plan_tot,
-                       w.chunk_start);
-    hipLaunchKernelGGL(k_bv_plan_apply, dim3(nblk), dim3(1024), 0, stream, offsets, b, e, C, pmin,
-                       sk, w.plan_tot, w.chunk_start, w.multi, w.multi_first, w.pip_list, status,
-                       fail_index);
+    if (npip == e - b) {
+      // every batch of the slice takes the Pippenger path (config 1's one 10k batch): no
+      // chunk plan, the Pippenger list is the slice's batches in order
+      hipLaunchKernelGGL(k_iota, dim3((unsigned)((npip + 255) / 256)), dim3(256), 0, stream,
+                         w.pip_list, (uint32_t)npip);
+    } else {
+      hipLaunchKernelGGL(k_bv_plan_local, dim3(nblk), dim3(1024), 0, stream, offsets, b, e, C,
+                         pmin, sk, w.plan_tot);
+      hipLaunchKernelGGL(k_bv_plan_top, dim3(1), dim3(1024), 0, stream, nblk, e - b, w.plan_tot,
+                         w.chunk_start);
+      hipLaunchKernelGGL(k_bv_plan_apply, dim3(nblk), dim3(1024), 0, stream, offsets, b, e, C,
+                         pmin, sk, w.plan_tot, w.chunk_start, w.multi, w.multi_first, w.pip_list,
+                         status, fail_index);
+    }
     if (chunks)
       hipLaunchKernelGGL(k_bv_expand, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
                          stream, offsets, b, e - b, (uint32_t)chunks, w.chunk_start, w.chunks);

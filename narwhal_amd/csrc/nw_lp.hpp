@@ -1,0 +1,204 @@
+// nw_lp.hpp — limb-parallel GF(2^255 - 19) and edwards25519 point arithmetic for ONE
+// latency-bound chain per wave: the 248-doubling Horner over the Pippenger windows in
+// k_pip_final (crypto::Signature::verify_batch, crypto/src/lib.rs:206-219; config 1).
+//
+// A lone wave is issue-bound: every VALU instruction costs its full issue whatever its
+// active lanes, so the chain's time is its instruction count. Here one wave holds one point:
+// row r (lanes 16r .. 16r+15) holds coordinate r of (X, Y, Z, T) and lane k < 10 of a row
+// holds limb k (radix 2^25.5, the same limbs as nw_field.hpp; lanes 10..15 hold 0). Limb-
+// wise additions are then ONE instruction, and a product is 10 multiply-accumulates per
+// lane: lane k accumulates column k = sum_j f_j g_{(k - j) mod 10} (x19 when wrapped, x2
+// for odd j with even k), with f_j broadcast by DPP row_newbcast and g rotated by
+// ds_bpermute. The four independent products of each formula stage run in the four rows.
+//
+// Operand discipline is nw_point.hpp's (same products, same first/second operand roles:
+// the second operand is the one scaled by 19, the first by 2); lp_carry64 leaves limbs in
+// the T_LP bound, for which tests/test_field_bounds.py checks every operand pair.
+#pragma once
+#include "nw_point.hpp"
+
+namespace nw {
+
+struct lp_ctx {
+  uint32_t k;          // limb index (lane & 15)
+  uint32_t row;        // coordinate (lane >> 4)
+  uint32_t mask;       // M26 / M25 for limbs 0..9, 0 above
+  uint32_t sh;         // 26 / 25
+  uint32_t c0;         // incoming-carry factor: 19 in limb 0 (wrapped from limb 9), 1 in
+                       // limbs 1..9, 0 above (lanes 10..15 stay 0)
+  uint32_t p4;         // limb k of 4p (0 above limb 9)
+  uint32_t rot[10];    // ds_bpermute address of limb (k - j) mod 10 of this row
+  uint32_t c19[10];    // 19 where column k wraps past limb 9 (k < j), else 1
+  uint32_t s2[10];     // 1 for odd j with even k (the x2 of odd x odd limbs), else 0
+};
+
+__device__ __forceinline__ lp_ctx lp_init(uint32_t lane) {
+  lp_ctx c;
+  c.k = lane & 15;
+  c.row = (lane >> 4) & 3;
+  const bool live = c.k < 10;
+  c.mask = !live ? 0u : (c.k & 1) ? M25 : M26;
+  c.sh = (c.k & 1) ? 25u : 26u;
+  c.c0 = c.k == 0 ? 19u : live ? 1u : 0u;
+  c.p4 = !live ? 0u : c.k == 0 ? 0xfffffb4u : (c.k & 1) ? 0x7fffffcu : 0xffffffcu;
+  const uint32_t base = 16 * c.row;
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    const uint32_t src = live ? (c.k + 10 - j) % 10 : 15u;   // lane 15 of a row holds 0
+    c.rot[j] = 4 * (base + src);
+    c.c19[j] = (live && (int)c.k < j) ? 19u : 1u;
+    c.s2[j] = ((j & 1) && !(c.k & 1)) ? 1u : 0u;
+  }
+  return c;
+}
+
+// DPP move; lanes whose source is outside the row read 0 (bound_ctrl).
+template <int CTRL>
+__device__ __forceinline__ uint32_t lp_dpp(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, true);
+}
+__device__ __forceinline__ uint32_t lp_perm(uint32_t addr, uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)addr, (int)x);
+}
+
+// Carry of value x (64-bit) of limb k into limb k+1 (limb 9's times 19 into limb 0):
+// the incoming carry of this lane.
+__device__ __forceinline__ uint64_t lp_carry_in64(const lp_ctx& c, uint64_t carry) {
+  const uint32_t lo = (uint32_t)carry, hi = (uint32_t)(carry >> 32);
+  // row_shr:1 (lane k <- lane k-1) for k >= 1; row_ror:7 (lane 0 <- lane 9) for k = 0
+  const uint32_t lo1 = lp_dpp<0x111>(lo), hi1 = lp_dpp<0x111>(hi);
+  const uint32_t lo9 = lp_dpp<0x127>(lo), hi9 = lp_dpp<0x127>(hi);
+  const uint32_t l = c.k == 0 ? lo9 : lo1, h = c.k == 0 ? hi9 : hi1;
+  return (uint64_t)l * c.c0 + ((uint64_t)(h * c.c0) << 32);
+}
+__device__ __forceinline__ uint32_t lp_carry_in32(const lp_ctx& c, uint32_t carry) {
+  const uint32_t x1 = lp_dpp<0x111>(carry), x9 = lp_dpp<0x127>(carry);
+  return (c.k == 0 ? x9 : x1) * c.c0;
+}
+
+// 64-bit columns (< 2^64) -> limbs in two parallel carry passes: after the first, limb k
+// holds < 2^26 + 19 * 2^39 (limb 0) / < 2^26 + 2^39; after the second, limb 0 < 2^26 +
+// 2^18.3, limb 1 < 2^25 + 2^17.3, the others < 2^26 / 2^25 + 2^14 -- the "T_LP" bound,
+// checked with every operand pair of the point formulas in tests/test_field_bounds.py.
+// (Lanes 10..15 hold 0 and receive no carry, so they stay 0.)
+__device__ __forceinline__ uint32_t lp_carry64(const lp_ctx& c, uint64_t col) {
+  const uint64_t t = (col & c.mask) + lp_carry_in64(c, col >> c.sh);
+  return (uint32_t)(t & c.mask) + lp_carry_in32(c, (uint32_t)(t >> c.sh));
+}
+// 32-bit limbs below 2^29 (a difference a + 4p - b) -> one pass: carries < 2^4 (x19 into
+// limb 0), inside T_LP.
+__device__ __forceinline__ uint32_t lp_carry32(const lp_ctx& c, uint32_t x) {
+  return (x & c.mask) + lp_carry_in32(c, x >> c.sh);
+}
+
+template <int J>
+__device__ __forceinline__ uint64_t lp_mac(const lp_ctx& c, uint64_t acc, uint32_t f,
+                                           uint32_t gj) {
+  const uint32_t fj = lp_dpp<0x150 + J>(f) << c.s2[J];   // row_newbcast:J, x2 odd x odd
+  return acc + (uint64_t)fj * (gj * c.c19[J]);
+}
+
+// h = f g (fe_mul's operand roles: f first, g second).
+__device__ __forceinline__ uint32_t lp_mul(const lp_ctx& c, uint32_t f, uint32_t g) {
+  uint32_t gr[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) gr[j] = lp_perm(c.rot[j], g);
+  uint64_t a = 0, b = 0;   // two chains
+  a = lp_mac<0>(c, a, f, gr[0]); b = lp_mac<1>(c, b, f, gr[1]);
+  a = lp_mac<2>(c, a, f, gr[2]); b = lp_mac<3>(c, b, f, gr[3]);
+  a = lp_mac<4>(c, a, f, gr[4]); b = lp_mac<5>(c, b, f, gr[5]);
+  a = lp_mac<6>(c, a, f, gr[6]); b = lp_mac<7>(c, b, f, gr[7]);
+  a = lp_mac<8>(c, a, f, gr[8]); b = lp_mac<9>(c, b, f, gr[9]);
+  return lp_carry64(c, a + b);
+}
+
+// Limb k of row q, in every row.
+__device__ __forceinline__ uint32_t lp_row(const lp_ctx& c, uint32_t q, uint32_t x) {
+  return lp_perm(4 * (16 * q + c.k), x);
+}
+__device__ __forceinline__ uint32_t lp_sel(const lp_ctx& c, uint32_t a0, uint32_t a1,
+                                           uint32_t a2, uint32_t a3) {
+  return c.row == 0 ? a0 : c.row == 1 ? a1 : c.row == 2 ? a2 : a3;
+}
+// a + 4p - b uncarried (fe_sub_nc) and carried (fe_sub).
+__device__ __forceinline__ uint32_t lp_sub_nc(const lp_ctx& c, uint32_t a, uint32_t b) {
+  return a + c.p4 - b;
+}
+__device__ __forceinline__ uint32_t lp_sub(const lp_ctx& c, uint32_t a, uint32_t b) {
+  return lp_carry32(c, a + c.p4 - b);
+}
+
+// Stage 2 shared by doubling and addition: X3 = E F, Y3 = G H, Z3 = F G, T3 = E H.
+__device__ __forceinline__ uint32_t lp_stage2(const lp_ctx& c, uint32_t E, uint32_t F,
+                                              uint32_t G, uint32_t H) {
+  return lp_mul(c, lp_sel(c, E, G, F, E), lp_sel(c, F, H, G, H));
+}
+
+// 2P (ge_dbl with T): A = X^2, B = Y^2, C = Z^2, t = (X + Y)^2 in rows 0..3, then stage 2.
+__device__ __forceinline__ uint32_t lp_dbl(const lp_ctx& c, uint32_t v) {
+  const uint32_t X = lp_row(c, 0, v), Y = lp_row(c, 1, v);
+  const uint32_t in = c.row == 3 ? X + Y : v;
+  const uint32_t s = lp_mul(c, in, in);
+  const uint32_t A = lp_row(c, 0, s), B = lp_row(c, 1, s), C = lp_row(c, 2, s),
+                 t = lp_row(c, 3, s);
+  const uint32_t H = A + B;
+  const uint32_t E = lp_sub_nc(c, H, t);
+  const uint32_t G = lp_sub(c, A, B);
+  const uint32_t F = G + C + C;
+  return lp_stage2(c, E, F, G, H);
+}
+
+// P + Q, row q of tab holding component q of Q in the order (YmX, YpX, T2d, Z2)
+// (ge_add_cached with T; an affine niels Q has Z2 = 2).
+__device__ __forceinline__ uint32_t lp_add(const lp_ctx& c, uint32_t v, uint32_t tab) {
+  const uint32_t X = lp_row(c, 0, v), Y = lp_row(c, 1, v);
+  const uint32_t sw = lp_row(c, c.row ^ (c.row >> 1), v);   // rows 2 and 3 swapped: T, Z
+  const uint32_t ymx = lp_sub_nc(c, Y, X), ypx = Y + X;
+  // a = (Y - X) YmX, b = (Y + X) YpX, c = T2d T, d = Z Z2 (operand order as ge_add_cached)
+  const uint32_t m = lp_mul(c, lp_sel(c, ymx, ypx, tab, sw), lp_sel(c, tab, tab, sw, tab));
+  const uint32_t A = lp_row(c, 0, m), B = lp_row(c, 1, m), C = lp_row(c, 2, m),
+                 D = lp_row(c, 3, m);
+  return lp_stage2(c, lp_sub_nc(c, B, A), lp_sub(c, D, C), D + C, B + A);
+}
+
+__device__ __forceinline__ uint32_t lp_identity(const lp_ctx& c) {
+  return (c.k == 0 && (c.row == 1 || c.row == 2)) ? 1u : 0u;
+}
+
+// Component (row) of a cached point in memory, in lp_add's order.
+__device__ __forceinline__ uint32_t lp_cached_component(const lp_ctx& c, const ge_cached& p) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&p);   // YpX, YmX, Z2, T2d
+  const uint32_t field = c.row == 0 ? 1u : c.row == 1 ? 0u : c.row == 2 ? 3u : 2u;
+  return c.k < 10 ? w[10 * field + c.k] : 0u;
+}
+
+// Component of sign * n for an affine niels point n (Z2 = 2), in lp_add's order.
+__device__ __forceinline__ uint32_t lp_niels_component(const lp_ctx& c, const ge_niels& n,
+                                                       bool neg) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&n);   // ypx, ymx, xy2d
+  const uint32_t kk = c.k < 10 ? c.k : 0u;
+  // rows 0/1: ymx/ypx of sign * n (swapped when negative); row 2: +-xy2d; row 3: 2
+  const uint32_t field = c.row == 2 ? 2u : (((c.row == 1) != neg) ? 0u : 1u);
+  const uint32_t x = w[10 * field + kk];
+  const uint32_t t = (c.row == 2 && neg) ? c.p4 - x : x;   // fe_neg_nc
+  const uint32_t r = c.row == 3 ? (c.k == 0 ? 2u : 0u) : t;
+  return c.k < 10 ? r : 0u;
+}
+
+// Every lane: is the point the identity (X == 0 and Y == Z, curve25519-dalek is_identity)?
+// s_tmp: 40 words of LDS.
+__device__ __forceinline__ bool lp_is_identity(const lp_ctx& c, uint32_t v, uint32_t* s_tmp) {
+  if (c.k < 10) s_tmp[10 * c.row + c.k] = v;
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  fe X, Y, Z;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    X.v[i] = s_tmp[i];
+    Y.v[i] = s_tmp[10 + i];
+    Z.v[i] = s_tmp[20 + i];
+  }
+  return fe_iszero(X) && fe_eq(Y, Z);
+}
+
+}  // namespace nw

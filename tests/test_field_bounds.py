@@ -71,3 +71,32 @@ def test_sq_columns_and_32bit_scalings():
 def test_uncarried_operand_needs_first_slot():
     # why fe_sub_nc results may not be fe_mul's second operand
     assert max(S_T) * 19 >= 2**32
+
+
+# Limb-parallel arithmetic (narwhal_amd/csrc/nw_lp.hpp, the Horner of k_pip_final): products
+# are carried in two parallel passes, so limb 0 may hold up to 2^26 + 2^18.3 (19 x the
+# second-pass carry from limb 9), limb 1 up to 2^25 + 2^17.3 and the rest up to
+# 2^26 / 2^25 + 2^14; one-pass carried differences stay inside that.
+T_LP = [2**26 + 2**18.3 if i == 0 else 2**25 + 2**17.3 if i == 1 else
+        (2**26 if i % 2 == 0 else 2**25) + 2**14 for i in range(10)]
+T_LP = [int(x) + 1 for x in T_LP]
+
+
+def test_limb_parallel_bounds():
+    L_ = [2 * x for x in T_LP]
+    P15_ = [a + b for a, b in zip(T_LP, L_)]
+    S_T_ = [a + b for a, b in zip(T_LP, P4)]
+    S_L_ = [a + b for a, b in zip(L_, P4)]
+    pairs = [(S_T_, T_LP), (S_T_, L_), (T_LP, P15_), (P15_, L_), (S_L_, P15_), (S_L_, L_),
+             (P15_, T_LP), (T_LP, T_LP), (T_LP, T_LP), (L_, L_)]
+    for F, G in pairs:
+        c = colmax(F, G)
+        assert c < 2**64
+        assert max(G) * 19 < 2**32 and max(F[1::2]) * 2 < 2**32
+    # first pass: carries < 2^39 (x19 < 2^43.3 into limb 0); second: < 2^18.3 into limb 0
+    assert (2**64 >> 25) * 19 < 2**44
+    assert 19 * (((2**25 + 2**39) >> 25) + 1) < 2**18.3
+    assert ((2**26 + 19 * 2**39) >> 26) < 2**17.3
+    # one-pass lp_sub: a + 4p - b < 2^29, carry < 2^4, x19 into limb 0 < 2^9
+    assert max(a + b for a, b in zip(P15_, P4)) < 2**29
+    assert 19 * (2**29 >> 25) < 2**18.3
