@@ -46,6 +46,8 @@ struct batch_consts {
   ge_niels b128[129];   // j * 2^128 B (short ladders of keyed chunks)
 };
 __constant__ batch_consts g_bc;
+// j * 2^(8 w) * B (nw_consts.hpp compute_comb): [-sum b_i]B in 32 additions, no doublings
+__device__ ge_niels g_comb[32 * 129];
 
 constexpr int BT_WORDS = 129 * 30;
 constexpr uint64_t kSliceUnits = 4ull << 20;   // items + batches per slice (workspace bound)
@@ -661,11 +663,11 @@ __global__ __launch_bounds__(256) void k_bv_combine(const uint32_t* __restrict__
 //                  decompressed points written in affine niels form
 //   k_pip_sort     one workgroup per (batch, window): counting sort of the window's digits
 //                  into its buckets with LDS histograms and cursors ((point index | sign)
-//                  entries; the order inside a bucket does not matter, addition commutes)
+//                  entries; the order inside a bucket does not matter, addition commutes);
+//                  one more workgroup per batch: sum b_i and the first failures
 //   k_pip_buckets  G lanes per bucket: partial sums, combined by a lane-shuffle tree
-//   k_pip_windows  one wave per window: sum_b b S_b by a suffix scan + tree over lanes
-//   k_pip_bsum     one workgroup per batch: sum b_i and first failures; -sum b_i becomes
-//                  the batch's last bucketed point (B), so the Horner adds no B terms
+//   k_pip_windows  one wave per window: sum_b b S_b by a suffix scan + tree over lanes;
+//                  one more wave per batch: [-sum b_i]B from the comb tables (no doublings)
 //   k_pip_final    one wave per batch: the 248-doubling Horner over the window sums,
 //                  limb-parallel (nw_lp.hpp), identity test, status
 //
@@ -695,18 +697,20 @@ struct pip_region {
   uint32_t* off;     // kPipBins: first entry of each bucket
   ge* S;             // kPipBins bucket sums
   ge_cached* W;      // kPipWin window sums (cached form, for the Horner)
-  uint32_t* hdr;     // k_pip_bsum -> k_pip_final: first failures (3) and their flags
+  uint32_t* hdr;     // first failures (3) and their flags (k_pip_sort's extra block)
+  uint32_t* bb;      // -sum b_i, recoded to signed 8-bit digits (k_pip_sort's extra block)
+  ge_cached* Bc;     // [-sum b_i]B (k_pip_windows' extra block), added after the Horner
 };
 
 constexpr size_t pip_region_bytes(uint64_t n) {
   return 2 * n * sizeof(ge_niels) + 4 * kPipWinCap * n + 52 * n + 8 * kPipBins +
-         sizeof(ge) * kPipBins + sizeof(ge_cached) * kPipWin + 16;
+         sizeof(ge) * kPipBins + sizeof(ge_cached) * kPipWin + 16 + 32 + sizeof(ge_cached);
 }
 // per-vote bytes grow slower than the item slots (2560 B), so the floor is the binding n
-static_assert(pip_region_bytes(kPipFloor + 1) <= 16 * sizeof(ge_cached) * kPipFloor,
+static_assert(pip_region_bytes(kPipFloor) <= 16 * sizeof(ge_cached) * kPipFloor,
               "Pippenger region does not fit its items' table slots");
 // certificate groups: >= kPipMin votes plus up to 256 committee keys
-static_assert(pip_region_bytes(kPipMin + 256 + 1) <= 16 * sizeof(ge_cached) * kPipMin,
+static_assert(pip_region_bytes(kPipMin + 256) <= 16 * sizeof(ge_cached) * kPipMin,
               "certificate-group region does not fit its votes' table slots");
 
 // Certificate-group mode (launch_cert_groups): a "batch" is a group of whole certificates;
@@ -738,7 +742,9 @@ __device__ __forceinline__ pip_region pip_at(ge_cached* tabs, uint64_t li0, uint
   r.off = reinterpret_cast<uint32_t*>(p); p += 4 * kPipBins;
   r.S = reinterpret_cast<ge*>(p); p += sizeof(ge) * kPipBins;
   r.W = reinterpret_cast<ge_cached*>(p); p += sizeof(ge_cached) * kPipWin;
-  r.hdr = reinterpret_cast<uint32_t*>(p);
+  r.Bc = reinterpret_cast<ge_cached*>(p); p += sizeof(ge_cached);
+  r.hdr = reinterpret_cast<uint32_t*>(p); p += 16;
+  r.bb = reinterpret_cast<uint32_t*>(p);
   return r;
 }
 
@@ -798,7 +804,7 @@ __global__ __launch_bounds__(256, 3) void k_pip_points(
   if (n < pmin) return;
   const uint64_t t = gi - bs;
   const bool group = grp.cert_vote_offsets != nullptr;
-  const uint64_t nreg = n + (group ? grp.nkeys : 0) + 1;   // + key sums + the B term
+  const uint64_t nreg = n + (group ? grp.nkeys : 0);   // + key sums
   const pip_region reg = pip_at(tabs, bs - i0, nreg);
   const curve_consts& K = g_bc.k;
   bv_item* it = items + li;
@@ -917,7 +923,7 @@ __global__ __launch_bounds__(1024) void k_grp_keys(const uint64_t* __restrict__ 
   const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
   if (n < pmin) return;
   const uint32_t N = grp.nkeys;
-  const uint64_t nreg = n + N + 1;   // votes, key sums, the B term
+  const uint64_t nreg = n + N;   // votes, key sums
   const pip_region reg = pip_at(tabs, bs - i0, nreg);
   const int tid = threadIdx.x;
   for (int k = tid; k < 256 * 8; k += 1024) s_acc[k >> 3][k & 7] = 0;
@@ -982,19 +988,87 @@ __device__ __forceinline__ void pip_window_digits(const pip_region& reg, uint64_
   }
 }
 
+// The extra block of k_pip_sort (1024 threads): sum_i b_i and the first failures (in the
+// reference's order) over the batch's votes; -sum b_i recoded into reg.bb for the comb in
+// k_pip_windows' extra block (off the Horner's critical path).
+// Scalar sum a += b mod l and first-failure merge across lanes (xor shuffles).
+__device__ __forceinline__ void bsum_merge(sc& a, uint32_t f[4], int o) {
+  sc b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b.w[j] = (uint32_t)__shfl_xor((int)a.w[j], o);
+  sc_add(a, a, b);
+  const uint32_t g0 = (uint32_t)__shfl_xor((int)f[0], o), g3 = (uint32_t)__shfl_xor((int)f[3], o);
+  const uint32_t g1 = (uint32_t)__shfl_xor((int)f[1], o), g2 = (uint32_t)__shfl_xor((int)f[2], o);
+  if (g0 < f[0]) { f[0] = g0; f[3] = g3; }
+  f[1] = min(f[1], g1);
+  f[2] = min(f[2], g2);
+}
+
+__device__ __forceinline__ void pip_bsum_block(const pip_region& reg, uint64_t n,
+                                               const bv_item* __restrict__ its,
+                                               uint32_t (*s_b)[8], uint32_t (*s_f)[4]) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  sc bsum;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bsum.w[j] = 0;
+  uint32_t f[4] = {kNone, kNone, kNone, 0};
+  for (uint64_t t = tid; t < n; t += 1024) {
+    const uint32_t fl = its[t].flags | its[t].pad | its[t].z[0];   // scalar, R and A lanes
+    if ((fl & (BF_S_HIGH | BF_A_DECODE)) && f[0] == kNone) { f[0] = (uint32_t)t; f[3] = fl; }
+    if ((fl & BF_S_NONCANON) && f[1] == kNone) f[1] = (uint32_t)t;
+    if ((fl & BF_R_DECODE) && f[2] == kNone) f[2] = (uint32_t)t;
+    sc bi;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bi.w[j] = its[t].b[j];
+    sc_add(bsum, bsum, bi);
+  }
+#pragma unroll 1
+  for (int o = 32; o > 0; o >>= 1) bsum_merge(bsum, f, o);
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s_b[wv][j] = bsum.w[j];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s_f[wv][j] = f[j];
+  }
+  __syncthreads();
+  if (wv != 0) return;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bsum.w[j] = lane < 16 ? s_b[lane][j] : 0u;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) f[j] = lane < 16 ? s_f[lane][j] : (j < 3 ? kNone : 0u);
+#pragma unroll 1
+  for (int o = 8; o > 0; o >>= 1) bsum_merge(bsum, f, o);
+  if (lane != 0) return;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) reg.hdr[j] = f[j];
+  sc nb;
+  sc_neg(nb, bsum);
+  uint32_t bb[8];
+  sc_recode(bb, nb, 0x80808080u);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) reg.bb[j] = bb[j];
+}
+
 // grid (kPipWin, npip), 1024 threads: histogram of the window's digits in LDS, scan, then
 // scatter with LDS cursors into the window's entry range (capacity 2n).
 __global__ __launch_bounds__(1024) void k_pip_sort(const uint32_t* __restrict__ pip_list,
                                                    const uint64_t* __restrict__ offsets,
                                                    uint64_t b0, uint64_t i0, uint32_t extra,
-                                                   uint32_t pmin, ge_cached* __restrict__ tabs) {
+                                                   uint32_t pmin, ge_cached* __restrict__ tabs,
+                                                   const bv_item* __restrict__ items) {
   constexpr int NL = 128 + kPipCarryBins;
   __shared__ uint32_t s_h[NL], s_c[NL];
+  __shared__ uint32_t s_b[16][8];
+  __shared__ uint32_t s_f[16][4];
   const uint64_t bidx = b0 + pip_list[blockIdx.y];
   const uint64_t bs = offsets[bidx], n0 = offsets[bidx + 1] - bs;
   if (n0 < pmin) return;
-  const uint64_t n = n0 + extra;   // votes + (group mode) key sums + the B term
+  const uint64_t n = n0 + extra;   // votes + (group mode) key sums
   const pip_region reg = pip_at(tabs, bs - i0, n);
+  if (blockIdx.x == kPipWin) {     // the batch's b sum and first failures
+    pip_bsum_block(reg, n0, items + (bs - i0), s_b, s_f);
+    return;
+  }
   const int w = blockIdx.x, tid = threadIdx.x;
   if (tid < NL) s_h[tid] = 0;
   __syncthreads();
@@ -1103,6 +1177,24 @@ __global__ __launch_bounds__(64) void k_pip_windows(const uint32_t* __restrict__
   const pip_region reg = pip_at(tabs, bs - i0, n + extra);
   const int w = blockIdx.x, l = threadIdx.x;
   const fe& d2 = g_bc.k.d2;
+  if (w == kPipWin) {
+    // [-sum b_i]B = sum_w comb[w][digit w] (32 additions, no doublings), limb-parallel,
+    // stored in cached form for the last addition of k_pip_final's Horner
+    const lp_ctx L = lp_init((uint32_t)l);
+    uint32_t bb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bb[j] = reg.bb[j];
+    uint32_t v = lp_identity(L);
+#pragma unroll 1
+    for (int m = 0; m < kPipWin; ++m) {
+      const int e = digit8(bb, m);
+      v = lp_add(L, v, lp_niels_component(L, g_comb[129 * m + (e < 0 ? -e : e)], e < 0));
+    }
+    const uint32_t c = lp_to_cached(L, v, L.k < 10 ? d2.v[L.k] : 0u);
+    const uint32_t field = L.row == 0 ? 1u : L.row == 1 ? 0u : L.row == 2 ? 3u : 2u;
+    if (L.k < 10) reinterpret_cast<uint32_t*>(reg.Bc)[10 * field + L.k] = c;
+    return;
+  }
   const bool top = w == kPipWin - 1;
   ge suf, t;
   if (top) {
@@ -1141,83 +1233,6 @@ __global__ __launch_bounds__(64) void k_pip_windows(const uint32_t* __restrict__
   }
 }
 
-// One workgroup per batch, before the sort: sum_i b_i and the first failures (in the
-// reference's order) over the batch's votes; -sum b_i enters the bucket MSM as one more
-// point (B, the last "vote" of the region: t = n + extra - 1, c digits only), so the
-// Horner in k_pip_final has no B additions.
-// Scalar sum a += b mod l and first-failure merge across lanes (xor shuffles).
-__device__ __forceinline__ void bsum_merge(sc& a, uint32_t f[4], int o) {
-  sc b;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) b.w[j] = (uint32_t)__shfl_xor((int)a.w[j], o);
-  sc_add(a, a, b);
-  const uint32_t g0 = (uint32_t)__shfl_xor((int)f[0], o), g3 = (uint32_t)__shfl_xor((int)f[3], o);
-  const uint32_t g1 = (uint32_t)__shfl_xor((int)f[1], o), g2 = (uint32_t)__shfl_xor((int)f[2], o);
-  if (g0 < f[0]) { f[0] = g0; f[3] = g3; }
-  f[1] = min(f[1], g1);
-  f[2] = min(f[2], g2);
-}
-
-__global__ __launch_bounds__(1024) void k_pip_bsum(const uint32_t* __restrict__ pip_list,
-                                                   const uint64_t* __restrict__ offsets,
-                                                   uint64_t b0, uint64_t i0,
-                                                   const bv_item* __restrict__ items,
-                                                   ge_cached* __restrict__ tabs, uint32_t extra,
-                                                   uint32_t pmin) {
-  __shared__ uint32_t s_b[16][8];
-  __shared__ uint32_t s_f[16][4];
-  const uint64_t bidx = b0 + pip_list[blockIdx.x];
-  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
-  if (n < pmin) return;
-  const uint64_t nreg = n + extra;
-  const pip_region reg = pip_at(tabs, bs - i0, nreg);
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const bv_item* its = items + (bs - i0);
-  sc bsum;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bsum.w[j] = 0;
-  uint32_t f[4] = {kNone, kNone, kNone, 0};
-  for (uint64_t t = tid; t < n; t += 1024) {
-    const uint32_t fl = its[t].flags | its[t].pad | its[t].z[0];   // scalar, R and A lanes
-    if ((fl & (BF_S_HIGH | BF_A_DECODE)) && f[0] == kNone) { f[0] = (uint32_t)t; f[3] = fl; }
-    if ((fl & BF_S_NONCANON) && f[1] == kNone) f[1] = (uint32_t)t;
-    if ((fl & BF_R_DECODE) && f[2] == kNone) f[2] = (uint32_t)t;
-    sc bi;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bi.w[j] = its[t].b[j];
-    sc_add(bsum, bsum, bi);
-  }
-#pragma unroll 1
-  for (int o = 32; o > 0; o >>= 1) bsum_merge(bsum, f, o);
-  if (lane == 0) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s_b[wv][j] = bsum.w[j];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) s_f[wv][j] = f[j];
-  }
-  __syncthreads();
-  if (wv != 0) return;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bsum.w[j] = lane < 16 ? s_b[lane][j] : 0u;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) f[j] = lane < 16 ? s_f[lane][j] : (j < 3 ? kNone : 0u);
-#pragma unroll 1
-  for (int o = 8; o > 0; o >>= 1) bsum_merge(bsum, f, o);
-  if (lane != 0) return;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) reg.hdr[j] = f[j];
-  sc nb;
-  sc_neg(nb, bsum);
-  uint32_t bb[8];
-  sc_recode(bb, nb, 0x80808080u);
-  const uint64_t t = nreg - 1;
-#pragma unroll
-  for (int w = 0; w < kPipWin; ++w) reg.cd[w * nreg + t] = (uint8_t)(bb[w >> 2] >> ((w & 3) * 8));
-#pragma unroll
-  for (int w = 0; w < kPipZWin; ++w) reg.zd[w * nreg + t] = 0x80;
-  reg.pts[2 * t] = g_bc.btab[1];   // 1 * B, affine niels
-}
-
 __global__ __launch_bounds__(64) void k_pip_final(const uint32_t* __restrict__ pip_list,
                                                   const uint64_t* __restrict__ offsets,
                                                   uint64_t b0, uint64_t i0,
@@ -1232,8 +1247,7 @@ __global__ __launch_bounds__(64) void k_pip_final(const uint32_t* __restrict__ p
   if (n < pmin) return;
   const pip_region reg = pip_at(tabs, bs - i0, n + extra);
   const int tid = threadIdx.x;
-  // Horner over the windows (the B term is one of the bucketed points), the point spread
-  // limb-parallel over the wave (nw_lp.hpp)
+  // Horner over the windows, the point spread limb-parallel over the wave (nw_lp.hpp)
   const lp_ctx L = lp_init((uint32_t)tid);
   uint32_t v = lp_identity(L);
 #pragma unroll 1
@@ -1244,6 +1258,7 @@ __global__ __launch_bounds__(64) void k_pip_final(const uint32_t* __restrict__ p
     }
     v = lp_add(L, v, lp_cached_component(L, reg.W[w]));
   }
+  v = lp_add(L, v, lp_cached_component(L, *reg.Bc));   // + [-sum b_i]B
   const bool ident = lp_is_identity(L, v, s_tmp);
   if (tid != 0) return;
   const uint32_t ff[3] = {reg.hdr[0], reg.hdr[1], reg.hdr[2]};
@@ -1301,7 +1316,13 @@ hipError_t upload_batch_consts() {
     strict_consts sk;
     compute_strict_consts(sk, host.b128);
   });
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_bc), &host, sizeof(host), 0, hipMemcpyHostToDevice);
+  static std::vector<ge_niels> comb(32 * 129);
+  static std::once_flag once_comb;
+  std::call_once(once_comb, [] { compute_comb(comb.data()); });
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_bc), &host, sizeof(host), 0, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return e;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_comb), comb.data(), sizeof(ge_niels) * comb.size(), 0,
+                           hipMemcpyHostToDevice);
 }
 
 size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems) {
@@ -1379,7 +1400,7 @@ void launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t b, ui
                 const z_key_t& zkey, const bv_ws& w, int32_t* status, uint64_t* fail_index,
                 const pip_group_t& grp, hipStream_t stream) {
   const bool group = grp.cert_vote_offsets != nullptr;
-  const uint32_t extra = (group ? grp.nkeys : 0) + 1;   // key sums, the B term
+  const uint32_t extra = group ? grp.nkeys : 0;   // key sums
   const uint32_t roles = group ? 2 : 3;
   hipLaunchKernelGGL(k_pip_points,
                      dim3((unsigned)((i1 - i0 + 63) / 64 * roles * 64 + 255) / 256),
@@ -1388,10 +1409,8 @@ void launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t b, ui
   if (group)
     hipLaunchKernelGGL(k_grp_keys, dim3((unsigned)npip), dim3(1024), 0, stream, offsets, b, i0,
                        pmin, w.items, w.tabs, grp);
-  hipLaunchKernelGGL(k_pip_bsum, dim3((unsigned)npip), dim3(1024), 0, stream, w.pip_list, offsets,
-                     b, i0, w.items, w.tabs, extra, pmin);
-  hipLaunchKernelGGL(k_pip_sort, dim3(kPipWin, (unsigned)npip), dim3(1024), 0, stream,
-                     w.pip_list, offsets, b, i0, extra, pmin, w.tabs);
+  hipLaunchKernelGGL(k_pip_sort, dim3(kPipWin + 1, (unsigned)npip), dim3(1024), 0, stream,
+                     w.pip_list, offsets, b, i0, extra, pmin, w.tabs, w.items);
   // G lanes per bucket: about 8 additions each at the largest batch's mean bucket size
   // (<= 49 digits per vote over kPipBins buckets); more lanes measured slower (the shuffle
   // tree's full additions cost more than the niels additions they replace: 10k batch,
@@ -1405,7 +1424,7 @@ void launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t b, ui
   const dim3 gb = xcd ? dim3((unsigned)(8 * bpb * ((npip + 7) / 8))) : dim3(bpb, (unsigned)npip);
   hipLaunchKernelGGL(k_pip_buckets, gb, dim3(256), 0, stream, w.pip_list, offsets, b, i0, lg,
                      (uint32_t)npip, bpb, xcd, extra, pmin, w.tabs);
-  hipLaunchKernelGGL(k_pip_windows, dim3(kPipWin, (unsigned)npip), dim3(64), 0, stream,
+  hipLaunchKernelGGL(k_pip_windows, dim3(kPipWin + 1, (unsigned)npip), dim3(64), 0, stream,
                      w.pip_list, offsets, b, i0, extra, pmin, w.tabs);
   hipLaunchKernelGGL(k_pip_final, dim3((unsigned)npip), dim3(64), 0, stream, w.pip_list,
                      offsets, b, i0, w.tabs, status, fail_index, extra, pmin, grp.group_ok);

@@ -103,3 +103,35 @@ inline void compute_strict_consts(strict_consts& sk, ge_niels b128[129]) {
 }
 
 }  // namespace nw
+
+namespace nw {
+// Fixed-base comb for [b]B with signed 8-bit digits and no doublings:
+// comb[w * 129 + j] = j * 2^(8 w) * B, w = 0..31, j = 0..128 (affine niels), 495 KB.
+inline void compute_comb(ge_niels* comb) {
+  curve_consts k;
+  ge_niels btab[129];
+  compute_consts(k, btab);
+  fe a, b, t;
+  fe_from_u32(a, 4);
+  fe_from_u32(b, 5);
+  fe_invert(t, b);
+  fe_mul(a, a, t);
+  uint32_t yw[8];
+  fe_tobytes(yw, a);
+  ge base;
+  ge_frombytes(base, yw, k);   // B
+  for (int w = 0; w < 32; ++w) {
+    ge_niels_identity(comb[w * 129]);
+    ge_cached cb;
+    ge_to_cached(cb, base, k.d2);
+    ge acc = base;
+    for (int j = 1; j <= 128; ++j) {
+      ge_to_niels(comb[w * 129 + j], acc, k.d2);
+      ge nxt;
+      ge_add_cached(nxt, acc, cb, true);
+      acc = nxt;
+    }
+    for (int d = 0; d < 8; ++d) ge_dbl(base, base, d == 7);   // 2^(8(w+1)) B
+  }
+}
+}  // namespace nw

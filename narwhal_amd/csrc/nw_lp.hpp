@@ -161,6 +161,16 @@ __device__ __forceinline__ uint32_t lp_add(const lp_ctx& c, uint32_t v, uint32_t
   return lp_stage2(c, lp_sub_nc(c, B, A), lp_sub(c, D, C), D + C, B + A);
 }
 
+// Cached form (YpX, YmX, Z2, T2d; carried) of the point, row r producing the component
+// that lp_cached_component reads back for row r: YmX, YpX, T2d, Z2. d2l: limb k of 2d.
+__device__ __forceinline__ uint32_t lp_to_cached(const lp_ctx& c, uint32_t v, uint32_t d2l) {
+  const uint32_t X = lp_row(c, 0, v), Y = lp_row(c, 1, v), Z = lp_row(c, 2, v),
+                 T = lp_row(c, 3, v);
+  const uint32_t prod = lp_mul(c, T, d2l);                       // T 2d (row 2 keeps it)
+  const uint32_t sum = lp_carry32(c, c.row == 0 ? Y + c.p4 - X : c.row == 1 ? Y + X : Z + Z);
+  return c.row == 2 ? prod : sum;
+}
+
 __device__ __forceinline__ uint32_t lp_identity(const lp_ctx& c) {
   return (c.k == 0 && (c.row == 1 || c.row == 2)) ? 1u : 0u;
 }
