@@ -1550,19 +1550,53 @@ const ge* key_tables_base(const ge_cached* tabs, uint64_t nkeys) {
 // NW_CERT_MERGE=0, committees above 256 keys, certificates with Pippenger-size vote sets,
 // or too few votes to fill a group.
 uint64_t cert_group_size(const uint64_t* host_cvo, uint64_t ncert, uint64_t nkeys,
-                         bool injected_z) {
+                         bool injected_z, uint64_t target_votes) {
   const char* m = getenv("NW_CERT_MERGE");
-  if (injected_z || (m && m[0] == '0') || nkeys == 0 || nkeys > 256 || ncert == 0) return 0;
+  if (injected_z || (m && m[0] == '0') || nkeys == 0 || nkeys > 256 || ncert == 0 ||
+      target_votes == 0)
+    return 0;
   const uint64_t nvotes = host_cvo[ncert] - host_cvo[0];
   uint64_t qmax = 0;
   for (uint64_t c = 0; c < ncert; ++c) qmax = std::max(qmax, host_cvo[c + 1] - host_cvo[c]);
   if (qmax == 0 || qmax >= kPipMin) return 0;
-  const uint64_t target = std::min<uint64_t>(env_u64("NW_CERT_GROUP_VOTES", 32768), 1ull << 20);
+  const uint64_t target =
+      std::min<uint64_t>(env_u64("NW_CERT_GROUP_VOTES", target_votes), 1ull << 20);
   if (nvotes < std::max<uint64_t>(target, kPipMin)) return 0;
   // K from the mean votes per certificate, capped so that K certificates of the largest
   // vote count still fit one workspace slice (skewed counts never overflow a slice)
   const uint64_t K = std::max<uint64_t>(1, target * ncert / nvotes);
   return std::max<uint64_t>(1, std::min<uint64_t>(K, slice_units() / qmax));
+}
+
+bool cert_group_env_fixed() { return getenv("NW_CERT_GROUP_VOTES") != nullptr; }
+
+// One thread: how many of the call's groups failed the merged check (group_ok == 0), for
+// the host's adaptive group size (written to host-mapped memory, read by a later call).
+__global__ __launch_bounds__(256) void k_grp_feedback(const uint32_t* __restrict__ group_ok,
+                                                      uint32_t ngroups, uint32_t target,
+                                                      uint32_t* __restrict__ fb) {
+  __shared__ uint32_t s_fail;
+  if (threadIdx.x == 0) s_fail = 0;
+  __syncthreads();
+  uint32_t fail = 0;
+  for (uint32_t g = threadIdx.x; g < ngroups; g += 256) fail += group_ok[g] == 0;
+  atomicAdd(&s_fail, fail);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    fb[1] = ngroups;
+    fb[2] = s_fail;
+    fb[3] = target;
+    __threadfence_system();
+    fb[0] = fb[0] + 1;   // sequence number, written last
+  }
+}
+
+hipError_t launch_group_feedback(const uint32_t* group_ok, uint64_t ncert, uint64_t K,
+                                 uint32_t target, uint32_t* fb, hipStream_t stream) {
+  const uint64_t ngroups = (ncert + K - 1) / K;
+  hipLaunchKernelGGL(k_grp_feedback, dim3(1), dim3(256), 0, stream, group_ok, (uint32_t)ngroups,
+                     target, fb);
+  return hipGetLastError();
 }
 
 size_t cert_groups_bytes(uint64_t ncert) {

@@ -77,8 +77,13 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
 // launch_verify_batch's (batch_workspace_bytes(ncert, nvotes)). *group_ok_out points into
 // group_ws (1 per group that passed).
 struct ge;
+// target_votes: votes per merged group (0 = do not merge); NW_CERT_GROUP_VOTES overrides.
 uint64_t cert_group_size(const uint64_t* host_cvo, uint64_t ncert, uint64_t nkeys,
-                         bool injected_z);
+                         bool injected_z, uint64_t target_votes);
+bool cert_group_env_fixed();
+// fb (host-mapped, 4 words): [0] sequence, [1] groups, [2] groups that failed, [3] target
+hipError_t launch_group_feedback(const uint32_t* group_ok, uint64_t ncert, uint64_t K,
+                                 uint32_t target, uint32_t* fb, hipStream_t stream);
 size_t cert_groups_bytes(uint64_t ncert);
 const ge* key_tables_base(const ge_cached* tabs, uint64_t nkeys);
 hipError_t launch_cert_groups(const uint32_t* cert_digest, const uint64_t* cvo,

@@ -231,3 +231,20 @@ def test_certificate_groups_mixed_validity(monkeypatch, N, n):
     monkeypatch.setenv("NW_CERT_MERGE", "0")
     st0, ix0 = M.verify_certificates_many(com, m, None)
     assert st0.tolist() == exp_st.tolist() and ix0.tolist() == exp_ix.tolist()
+
+
+def test_certificate_groups_adaptive_repeated_calls():
+    """Adaptive merging (nw_api.cpp group_target): a stream whose groups keep failing is
+    verified per certificate from the next call on, with a merged probe every 8th call; every
+    call's statuses and indices equal the construction, whichever path ran."""
+    from narwhal_amd import crypto as C
+    N, n = 10, 5200
+    s = W.certificate_stream(n, O.keys(N), lambda sk, m: C.sign_many(sk, m), oracle_digest_many,
+                             seed=77)
+    m, exp_st, exp_ix = W.mutate_votes(s, np.arange(13, n, 100), seed=5)
+    com = _Com(s["committee"])
+    for _ in range(10):
+        st, ix = M.verify_certificates_many(com, m, None)
+        assert st.tolist() == exp_st.tolist() and ix.tolist() == exp_ix.tolist()
+    st, ix = M.verify_certificates_many(com, s, None)     # honest again
+    assert (st == 0).all()
