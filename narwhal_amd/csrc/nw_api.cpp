@@ -433,23 +433,24 @@ size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
 // Adaptive certificate grouping. A merged group whose random linear
 // combination fails sends every certificate of the group through its own verify_batch, so
 // when invalid certificates are spread through the stream (say 1%: every 32k-vote group
-// holds some) merging costs the merged check AND the per-certificate path. Each call's
-// groups report how many failed (k_grp_feedback, into host-mapped memory); a later call
-// with the same committee size verifies per certificate while more than a quarter of the
-// groups failed, probing the merged check again every kProbe-th call. Smaller groups do not
-// help: a group's Pippenger tail (4,160 buckets, 32 window sums, the Horner) is paid per
-// group, and at ~500 votes per group the merged path measured no faster than the
-// per-certificate one (N = 100, 1% invalid: 2.36 vs 2.41 M certs/s). Verdicts do not depend
-// on the choice; NW_CERT_GROUP_VOTES fixes the group size, NW_CERT_MERGE=0
-// turns merging off.
-constexpr uint32_t kGroupDefault = 32768, kProbe = 8;
+// holds some) merging costs the merged check AND the per-certificate path. Every call
+// reports the fraction p of its counted certificates whose vote batch failed (k_grp_count /
+// k_grp_publish, into host-mapped memory); a later call with the same committee size merges
+// only while at most a quarter of its groups would fail at that p, 1 - (1 - p)^K <= 1/4,
+// and otherwise verifies every certificate on its own. Smaller groups do not help: a
+// group's Pippenger tail (4,160 buckets, 33 window sums, the Horner) is paid per group (at
+// 1,024 votes per group N = 100 ran 3.2 M certs/s all-valid against 5.7 M with 32k-vote
+// groups), and K-certificate keyed Straus groups measured slower than the per-certificate
+// path. Verdicts do not depend on the choice;
+// NW_CERT_GROUP_VOTES fixes the group size, NW_CERT_MERGE=0 turns merging off.
+constexpr uint32_t kGroupDefault = 32768;
 
 struct GroupPolicy {
-  uint32_t* fb = nullptr;       // host-mapped: seq, groups, failed, target
+  uint32_t* fb = nullptr;       // host-mapped: seq, groups, failed, tag, counted, bad
   uint32_t* fb_dev = nullptr;
+  uint32_t* cnt = nullptr;      // device: k_grp_count's sums (zero between calls)
   uint32_t seen = 0;
-  bool merge = true;
-  uint32_t off_calls = 0;
+  double p = 0.0;               // fraction of counted certificates whose votes failed
 };
 struct DevPolicies {
   std::mutex m;
@@ -457,32 +458,39 @@ struct DevPolicies {
 };
 DevPolicies g_policies[kMaxDevices];
 
-// Votes per merged group for this call (0: per certificate), and where its report goes.
-uint32_t group_target(int dev, uint64_t nkeys, uint32_t** fb_dev) {
+// The latest failure-rate report for this committee size, and where this call's goes.
+double group_failure_rate(int dev, uint64_t nkeys, hipStream_t s, uint32_t** fb_dev,
+                          uint32_t** cnt) {
   DevPolicies& d = g_policies[dev];
   std::lock_guard<std::mutex> g(d.m);
   GroupPolicy& p = d.by_committee[nkeys];
   *fb_dev = nullptr;
+  *cnt = nullptr;
   if (!p.fb) {
     void* h = nullptr;
-    if (hipHostMalloc(&h, 16, hipHostMallocMapped) != hipSuccess) return kGroupDefault;
-    memset(h, 0, 16);
+    if (hipHostMalloc(&h, 32, hipHostMallocMapped) != hipSuccess) return p.p;
+    memset(h, 0, 32);
     void* dp = nullptr;
-    if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess) return kGroupDefault;
+    void* c = nullptr;
+    if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess || hipMalloc(&c, 16) != hipSuccess ||
+        hipMemsetAsync(c, 0, 16, s) != hipSuccess) {   // ordered before this call's count
+      (void)hipHostFree(h);
+      return p.p;
+    }
     p.fb = static_cast<uint32_t*>(h);
     p.fb_dev = static_cast<uint32_t*>(dp);
+    p.cnt = static_cast<uint32_t*>(c);
   }
   volatile uint32_t* fb = p.fb;
   const uint32_t seq = fb[0];
   if (seq != p.seen) {          // a report from a call that has finished since
     p.seen = seq;
-    const uint32_t ng = fb[1], nf = fb[2];
-    p.merge = ng == 0 || 4ull * nf <= ng;
-    p.off_calls = 0;
+    const uint32_t counted = fb[4], bad = fb[5];
+    if (counted) p.p = (double)bad / (double)counted;
   }
   *fb_dev = p.fb_dev;
-  if (p.merge) return kGroupDefault;
-  return ++p.off_calls % kProbe == 0 ? kGroupDefault : 0u;
+  *cnt = p.cnt;
+  return p.p;
 }
 
 // The whole device pipeline; every pointer is a device pointer.
@@ -532,31 +540,36 @@ int cert_pipeline(const nw_committee& com, const nw_certificates& cs,
     // linear combination per group (launch_cert_groups); only the certificates of groups
     // that fail it go through their own verify_batch below.
     uint32_t* fb_dev = nullptr;
-    const bool fixed = nw::cert_group_env_fixed();
-    const uint32_t target =
-        fixed || z16 ? kGroupDefault : group_target(t_state.device, com.nauth, &fb_dev);
-    const uint64_t K = nw::cert_group_size(host_vote_offsets, n, com.nauth, z16 != nullptr, target);
+    uint32_t* fb_cnt = nullptr;
+    double p_cert = 0.0;
+    uint64_t K = nw::cert_group_size(host_vote_offsets, n, com.nauth, z16 != nullptr, kGroupDefault);
+    if (K && !nw::cert_group_env_fixed()) {
+      p_cert = group_failure_rate(t_state.device, com.nauth, s, &fb_dev, &fb_cnt);
+      if (1.0 - std::pow(1.0 - p_cert, (double)K) > 0.25) K = 0;
+    }
     if (getenv("NW_DEBUG_GROUPS"))
-      fprintf(stderr, "[narwhal_amd] certificates: n=%zu keys=%zu group target=%u votes, K=%llu\n",
-              (size_t)n, (size_t)com.nauth, target, (unsigned long long)K);
+      fprintf(stderr, "[narwhal_amd] certificates: n=%zu keys=%zu K=%llu p=%.4g\n", (size_t)n,
+              (size_t)com.nauth, (unsigned long long)K, p_cert);
     uint32_t* group_ok = nullptr;
-    if (K) {
+    if (K)
       NW_HIP(nw::launch_cert_groups(w.cert_digest, cs.vote_offsets, host_vote_offsets, n,
                                     reinterpret_cast<const uint32_t*>(cs.vote_pks),
                                     reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
                                     key, w.batch_ws, w.group_ws, w.pre1, w.pre2, w.hdr_st, kt,
-                                    nw::key_tables_base(ktabs, com.nauth),
-                                    (uint32_t)com.nauth, K, &group_ok, s),
+                                    nw::key_tables_base(ktabs, com.nauth), (uint32_t)com.nauth,
+                                    K, &group_ok, s),
              "certificate groups (votes)");
-      if (fb_dev)
-        NW_HIP(nw::launch_group_feedback(group_ok, n, K, target, fb_dev, s), "group feedback");
-    }
     NW_HIP(nw::launch_verify_batch(w.cert_digest, cs.vote_offsets, host_vote_offsets, n,
                                    reinterpret_cast<const uint32_t*>(cs.vote_pks),
                                    reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
                                    static_cast<const uint32_t*>(z16), key, w.batch_ws,
                                    w.batch_st, w.batch_idx, s, &kt, group_ok, K),
            "verify_batch (votes)");
+    if (fb_dev)
+      NW_HIP(nw::launch_group_feedback(group_ok, n, K, (uint32_t)K,
+                                       w.batch_st, w.pre1, w.pre2, w.hdr_st, fb_cnt, fb_dev,
+                                       s),
+             "group feedback");
   }
   NW_HIP(nw::launch_cert_finalize(n, headers_only, w.pre1, w.pre2, w.idx1, w.idx2, w.hdr_st,
                                   w.batch_st, w.batch_idx, status, index, s), "k_cert_finalize");

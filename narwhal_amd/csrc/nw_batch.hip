@@ -1570,32 +1570,58 @@ uint64_t cert_group_size(const uint64_t* host_cvo, uint64_t ncert, uint64_t nkey
 
 bool cert_group_env_fixed() { return getenv("NW_CERT_GROUP_VOTES") != nullptr; }
 
-// One thread: how many of the call's groups failed the merged check (group_ok == 0), for
-// the host's adaptive group size (written to host-mapped memory, read by a later call).
-__global__ __launch_bounds__(256) void k_grp_feedback(const uint32_t* __restrict__ group_ok,
-                                                      uint32_t ngroups, uint32_t target,
-                                                      uint32_t* __restrict__ fb) {
-  __shared__ uint32_t s_fail;
-  if (threadIdx.x == 0) s_fail = 0;
-  __syncthreads();
-  uint32_t fail = 0;
-  for (uint32_t g = threadIdx.x; g < ngroups; g += 256) fail += group_ok[g] == 0;
-  atomicAdd(&s_fail, fail);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    fb[1] = ngroups;
-    fb[2] = s_fail;
-    fb[3] = target;
-    __threadfence_system();
-    fb[0] = fb[0] + 1;   // sequence number, written last
+// How many of the call's groups failed the merged check (group_ok == 0) and how many of its
+// counted certificates (no pre-check or header failure) have a failing vote batch, for the
+// host's adaptive grouping: k_grp_count sums into cnt (3 device words, zero between calls)
+// over the whole grid, k_grp_publish copies the sums to host-mapped memory (read by a later
+// call) and clears cnt. Launched after the per-certificate verify_batch (batch_st final).
+__global__ __launch_bounds__(256) void k_grp_count(
+    const uint32_t* __restrict__ group_ok, uint64_t ngroups, uint64_t ncert,
+    const int32_t* __restrict__ batch_st, const int32_t* __restrict__ pre1,
+    const int32_t* __restrict__ pre2, const int32_t* __restrict__ hdr_st,
+    uint32_t* __restrict__ cnt) {
+  uint32_t v[3] = {0, 0, 0};   // failed groups, counted certificates, failing ones
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint64_t g = t0; g < ngroups; g += stride) v[0] += group_ok[g] == 0;
+  for (uint64_t c = t0; c < ncert; c += stride) {
+    if (pre1[c] != 0 || hdr_st[c] != 0 || pre2[c] != 0) continue;
+    ++v[1];
+    v[2] += batch_st[c] != 0;
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[k] += (uint32_t)__shfl_xor((int)v[k], o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) atomicAdd(&cnt[k], v[k]);
   }
 }
 
+__global__ void k_grp_publish(uint32_t ngroups, uint32_t tag, uint32_t* __restrict__ cnt,
+                              uint32_t* __restrict__ fb) {
+  fb[1] = ngroups;
+  fb[2] = cnt[0];
+  fb[3] = tag;
+  fb[4] = cnt[1];
+  fb[5] = cnt[2];
+  cnt[0] = cnt[1] = cnt[2] = 0;
+  __threadfence_system();
+  fb[0] = fb[0] + 1;   // sequence number, written last
+}
+
 hipError_t launch_group_feedback(const uint32_t* group_ok, uint64_t ncert, uint64_t K,
-                                 uint32_t target, uint32_t* fb, hipStream_t stream) {
-  const uint64_t ngroups = (ncert + K - 1) / K;
-  hipLaunchKernelGGL(k_grp_feedback, dim3(1), dim3(256), 0, stream, group_ok, (uint32_t)ngroups,
-                     target, fb);
+                                 uint32_t tag, const int32_t* batch_st, const int32_t* pre1,
+                                 const int32_t* pre2, const int32_t* hdr_st, uint32_t* cnt,
+                                 uint32_t* fb, hipStream_t stream) {
+  const uint64_t ngroups = K && group_ok ? (ncert + K - 1) / K : 0;
+  const uint64_t work = std::max(ngroups, ncert);
+  const unsigned blocks = (unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, (work + 2047) / 2048));
+  hipLaunchKernelGGL(k_grp_count, dim3(blocks), dim3(256), 0, stream, group_ok, ngroups, ncert,
+                     batch_st, pre1, pre2, hdr_st, cnt);
+  hipLaunchKernelGGL(k_grp_publish, dim3(1), dim3(1), 0, stream, (uint32_t)ngroups, tag, cnt, fb);
   return hipGetLastError();
 }
 

@@ -81,9 +81,14 @@ struct ge;
 uint64_t cert_group_size(const uint64_t* host_cvo, uint64_t ncert, uint64_t nkeys,
                          bool injected_z, uint64_t target_votes);
 bool cert_group_env_fixed();
-// fb (host-mapped, 4 words): [0] sequence, [1] groups, [2] groups that failed, [3] target
+// fb (host-mapped, 8 words): [0] sequence, [1] groups, [2] groups that failed, [3] tag,
+// [4] counted certificates, [5] counted certificates whose vote batch failed. cnt: 3 device
+// words, zero before the first call (left zero). Launch after the per-certificate
+// verify_batch (batch_st final); group_ok may be null (K = 0).
 hipError_t launch_group_feedback(const uint32_t* group_ok, uint64_t ncert, uint64_t K,
-                                 uint32_t target, uint32_t* fb, hipStream_t stream);
+                                 uint32_t tag, const int32_t* batch_st, const int32_t* pre1,
+                                 const int32_t* pre2, const int32_t* hdr_st, uint32_t* cnt,
+                                 uint32_t* fb, hipStream_t stream);
 size_t cert_groups_bytes(uint64_t ncert);
 const ge* key_tables_base(const ge_cached* tabs, uint64_t nkeys);
 hipError_t launch_cert_groups(const uint32_t* cert_digest, const uint64_t* cvo,

@@ -10,8 +10,13 @@ import math
 
 P4 = [4 * (2**26 - 19)] + [4 * (2**26 - 1) if i % 2 == 0 else 4 * (2**25 - 1) for i in range(1, 10)]
 T = [2**26 if i % 2 == 0 else 2**25 for i in range(10)]
-T[1] += 2**17          # fe_join / fold_top: limb 1 receives the wrapped carry (< 2^17)
-T[6] += 2**13          # fe_join: limb 6 receives the column-4 carry (< 2^13)
+# fe_join5 (five two-column chains): chain c's final carry (< 2^64 >> 25 = 2^39) enters limb
+# 2c + 2 (x 19 into limb 0), which is re-split once, so limb 2c + 3 receives < 2^13 + 1
+# (limb 1: < 2^17.25 + 1); the old two-chain fe_join fed limbs 1 and 6 the same way.
+T[1] += (19 * 2**39 + 2**26) >> 26
+for i in (3, 5, 7, 9):
+    T[i] += (2**39 + 2**26) >> 26
+T[6] += (2**39 + 2**26) >> 26   # fe_join (NW_MAC_CHAINS=2)
 L = [2 * x for x in T]
 P15 = [a + b for a, b in zip(T, L)]
 S_T = [a + b for a, b in zip(T, P4)]      # fe_sub_nc(T, T)

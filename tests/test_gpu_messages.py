@@ -234,9 +234,10 @@ def test_certificate_groups_mixed_validity(monkeypatch, N, n):
 
 
 def test_certificate_groups_adaptive_repeated_calls():
-    """Adaptive merging (nw_api.cpp group_target): a stream whose groups keep failing is
-    verified per certificate from the next call on, with a merged probe every 8th call; every
-    call's statuses and indices equal the construction, whichever path ran."""
+    """Adaptive merging (nw_api.cpp group_failure_rate): a stream with ~1% failing
+    certificates is verified per certificate from the next call on (the measured rate makes
+    most merged groups fail), and merged again once an honest stream reports no failures;
+    every call's statuses and indices equal the construction, whichever path ran."""
     from narwhal_amd import crypto as C
     N, n = 10, 5200
     s = W.certificate_stream(n, O.keys(N), lambda sk, m: C.sign_many(sk, m), oracle_digest_many,
@@ -246,5 +247,6 @@ def test_certificate_groups_adaptive_repeated_calls():
     for _ in range(10):
         st, ix = M.verify_certificates_many(com, m, None)
         assert st.tolist() == exp_st.tolist() and ix.tolist() == exp_ix.tolist()
-    st, ix = M.verify_certificates_many(com, s, None)     # honest again
-    assert (st == 0).all()
+    for _ in range(3):
+        st, ix = M.verify_certificates_many(com, s, None)     # honest again
+        assert (st == 0).all()
