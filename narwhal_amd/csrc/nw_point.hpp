@@ -95,9 +95,10 @@ NW_HD void ge_add_niels(ge& r, const ge& p, const ge_niels& q, bool want_t) {
   if (want_t) fe_mul(r.T, e, h);
 }
 
-// r = p + q with T, q either cached or (affine, wave-uniform) an affine niels point held
-// in cached form (q.Z2 unused: 2 Z1 Z2 = 2 Z1). One routine for every ladder term.
-NW_HD void ge_add_any(ge& r, const ge& p, const ge_cached& q, bool affine) {
+// r = p + q, q either cached or (affine, wave-uniform) an affine niels point held in cached
+// form (q.Z2 unused: 2 Z1 Z2 = 2 Z1). One routine for every ladder term. T3 only when
+// want_t (wave-uniform): the doublings that follow a window's last addition never read T.
+NW_HD void ge_add_any(ge& r, const ge& p, const ge_cached& q, bool affine, bool want_t = true) {
   fe a, b, c, d, e, f, g, h;
   fe_sub_nc(a, p.Y, p.X);
   fe_mul(a, a, q.YmX);
@@ -113,7 +114,7 @@ NW_HD void ge_add_any(ge& r, const ge& p, const ge_cached& q, bool affine) {
   fe_mul(r.X, e, f);
   fe_mul(r.Y, g, h);
   fe_mul(r.Z, f, g);
-  fe_mul(r.T, e, h);
+  if (want_t) fe_mul(r.T, e, h);
 }
 
 // Conditionally negate a niels point: -(x, y) = (-x, y) -> swap y+x / y-x, negate 2dxy.

@@ -22,6 +22,9 @@
 #ifndef NW_DBL_UNROLL
 #define NW_DBL_UNROLL 0
 #endif
+#ifndef NW_LAST_T
+#define NW_LAST_T 0   // 1: T3 also for a window's last addition (A/B variant)
+#endif
 #include "nw_ladder.hpp"
 
 namespace nw {
@@ -185,6 +188,9 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const ge_ni
   int W = ((bu > bv ? bu : bv) + 3) / 4;
   if (W < 32) W = 32;
   W = wave_max(W);
+#ifdef NW_EXP_NO_LADDER
+  W = 0;   // timing experiment only (tools/strict_variants.py): the cost without the ladder
+#endif
 
   // One rolled doubling and one addition routine serve every term (code size: the ladder
   // body stays inside the instruction cache). Per 4-bit window j: 4 doublings, then the
@@ -229,7 +235,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const ge_ni
           fe_copy(e.T2d, nb.xy2d);
         }
         ge_cached_cneg(e, d < 0);
-        ge_add_any(acc, acc, e, slot >= 2);
+        ge_add_any(acc, acc, e, slot >= 2, NW_LAST_T || slot != nslots - 1);
       }
     }
   }
