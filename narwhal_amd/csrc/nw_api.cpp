@@ -433,16 +433,21 @@ size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
 // Adaptive certificate grouping. A merged group whose random linear
 // combination fails sends every certificate of the group through its own verify_batch, so
 // when invalid certificates are spread through the stream (say 1%: every 32k-vote group
-// holds some) merging costs the merged check AND the per-certificate path. Every call
+// holds some) big groups cost the merged check AND the per-certificate path. Every call
 // reports the fraction p of its counted certificates whose vote batch failed (k_grp_count /
-// k_grp_publish, into host-mapped memory); a later call with the same committee size merges
-// only while at most a quarter of its groups would fail at that p, 1 - (1 - p)^K <= 1/4,
-// and otherwise verifies every certificate on its own. Smaller groups do not help: a
-// group's Pippenger tail (4,160 buckets, 33 window sums, the Horner) is paid per group (at
-// 1,024 votes per group N = 100 ran 3.2 M certs/s all-valid against 5.7 M with 32k-vote
-// groups), and K-certificate keyed Straus groups measured slower than the per-certificate
-// path. Verdicts do not depend on the choice;
-// NW_CERT_GROUP_VOTES fixes the group size, NW_CERT_MERGE=0 turns merging off.
+// k_grp_publish, into host-mapped memory after the per-certificate pass); a later call with
+// the same committee size then picks:
+//   big    Pippenger groups of ~32k votes (launch_cert_groups) while at most a quarter of
+//          them would fail at that p, 1 - (1 - p)^K <= 1/4;
+//   small  K-certificate keyed Straus groups with the fallback ladders run from the same
+//          per-vote items (launch_cert_sgroups), K cost-optimal at that p
+//          (cert_sgroup_size), when they beat every certificate's own ladder;
+//   per-certificate otherwise.
+// Mid-size Pippenger groups do not help: a group's Pippenger tail (4,160 buckets, 33 window
+// sums, the Horner) is paid per group (at 1,024 votes per group N = 100 ran 3.2 M certs/s
+// all-valid against 5.7 M with 32k-vote groups). Verdicts do not depend on the choice
+// (DESIGN.md 2); NW_CERT_GROUP_VOTES fixes big groups of that size, NW_CERT_SMALL_K small
+// groups of K certificates, NW_CERT_MERGE=0 turns merging off.
 constexpr uint32_t kGroupDefault = 32768;
 
 struct GroupPolicy {
@@ -543,15 +548,21 @@ int cert_pipeline(const nw_committee& com, const nw_certificates& cs,
     uint32_t* fb_cnt = nullptr;
     double p_cert = 0.0;
     uint64_t K = nw::cert_group_size(host_vote_offsets, n, com.nauth, z16 != nullptr, kGroupDefault);
-    if (K && !nw::cert_group_env_fixed()) {
+    bool small = getenv("NW_CERT_SMALL_K") != nullptr;
+    if (!z16 && !small && !nw::cert_group_env_fixed()) {
       p_cert = group_failure_rate(t_state.device, com.nauth, s, &fb_dev, &fb_cnt);
-      if (1.0 - std::pow(1.0 - p_cert, (double)K) > 0.25) K = 0;
+      if (!K || 1.0 - std::pow(1.0 - p_cert, (double)K) > 0.25) small = true;
+    }
+    if (small) {
+      bool wins = false;
+      K = nw::cert_sgroup_size(host_vote_offsets, n, com.nauth, z16 != nullptr, p_cert, &wins);
+      if (!wins) K = 0;
     }
     if (getenv("NW_DEBUG_GROUPS"))
-      fprintf(stderr, "[narwhal_amd] certificates: n=%zu keys=%zu K=%llu p=%.4g\n", (size_t)n,
-              (size_t)com.nauth, (unsigned long long)K, p_cert);
+      fprintf(stderr, "[narwhal_amd] certificates: n=%zu keys=%zu %s K=%llu p=%.4g\n", (size_t)n,
+              (size_t)com.nauth, small ? "small" : "big", (unsigned long long)K, p_cert);
     uint32_t* group_ok = nullptr;
-    if (K)
+    if (K && !small)
       NW_HIP(nw::launch_cert_groups(w.cert_digest, cs.vote_offsets, host_vote_offsets, n,
                                     reinterpret_cast<const uint32_t*>(cs.vote_pks),
                                     reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
@@ -559,14 +570,23 @@ int cert_pipeline(const nw_committee& com, const nw_certificates& cs,
                                     nw::key_tables_base(ktabs, com.nauth), (uint32_t)com.nauth,
                                     K, &group_ok, s),
              "certificate groups (votes)");
-    NW_HIP(nw::launch_verify_batch(w.cert_digest, cs.vote_offsets, host_vote_offsets, n,
-                                   reinterpret_cast<const uint32_t*>(cs.vote_pks),
-                                   reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
-                                   static_cast<const uint32_t*>(z16), key, w.batch_ws,
-                                   w.batch_st, w.batch_idx, s, &kt, group_ok, K),
-           "verify_batch (votes)");
+    if (K && small)
+      NW_HIP(nw::launch_cert_sgroups(w.cert_digest, cs.vote_offsets, host_vote_offsets, n,
+                                     reinterpret_cast<const uint32_t*>(cs.vote_pks),
+                                     reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
+                                     key, w.batch_ws, w.group_ws, w.pre1, w.pre2, w.hdr_st, kt,
+                                     (uint32_t)com.nauth, K, p_cert, w.batch_st, w.batch_idx,
+                                     &group_ok, s),
+             "small certificate groups (votes)");
+    else
+      NW_HIP(nw::launch_verify_batch(w.cert_digest, cs.vote_offsets, host_vote_offsets, n,
+                                     reinterpret_cast<const uint32_t*>(cs.vote_pks),
+                                     reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
+                                     static_cast<const uint32_t*>(z16), key, w.batch_ws,
+                                     w.batch_st, w.batch_idx, s, &kt, group_ok, K),
+             "verify_batch (votes)");
     if (fb_dev)
-      NW_HIP(nw::launch_group_feedback(group_ok, n, K, (uint32_t)K,
+      NW_HIP(nw::launch_group_feedback(group_ok, n, K, ((small ? 1u : 0u) << 24) | (uint32_t)K,
                                        w.batch_st, w.pre1, w.pre2, w.hdr_st, fb_cnt, fb_dev,
                                        s),
              "group feedback");

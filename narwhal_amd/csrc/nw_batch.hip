@@ -33,6 +33,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <cmath>
 #include <mutex>
 #include <vector>
 
@@ -1675,6 +1676,378 @@ hipError_t launch_cert_groups(const uint32_t* cert_digest, const uint64_t* cvo,
     if (i1 > i0)
       launch_pip(cert_digest, gofs, g, e, i0, i1, pmin, e - g, pmax, pks, sigs, nullptr, zkey, w,
                  nullptr, nullptr, grp, stream);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+    g = e;
+  }
+  return hipSuccess;
+}
+
+
+// ------------------------------------------------------------------ small certificate groups
+// For streams whose big merged groups keep failing (invalid certificates spread through the
+// stream: at 1 % every ~32k-vote group holds some), the adaptive policy (nw_api.cpp) checks
+// the votes in groups of K certificates (a handful) with one keyed Straus MSM each and runs
+// the per-certificate ladders only for the certificates of groups that fail — from the SAME
+// per-vote items, so a failing group's fallback costs its ladders only:
+//
+//   sum_votes z_i R_i + sum_keys (sum c_i) A_key - (sum b_i) B == identity
+//
+// per slice of whole groups:
+//   k_bv_items      (keyed) per vote: flags, k_i, z_i, c_i, b_i and the R table j*R_i
+//   k_sgrp_keys     one wave per group: c_i summed per committee key (LDS), sum b_i, the
+//                   group's flags; the used keys compacted into a list; counted votes marked
+//   k_sgrp_ladder   one lane per (group, chunk): the 132-doubling keyed ladder over the
+//                   chunk's counted votes (z_i by 4-bit windows over their R tables), its share
+//                   of the key list (8-bit windows over the two key tables) and, chunk 0, -sum b
+//   k_sgrp_combine  one lane per group: sum of its chunks, identity test -> group_ok
+//   k_bv_plan_* / k_bv_expand / k_bv_chunks / k_bv_combine  the per-certificate verify_batch
+//                   of every certificate in a failed group (settled ones get status Ok)
+//
+// A counted vote costs 33 additions here instead of 65 in its own certificate's ladder (the
+// A term is paid per distinct key of the group, the doublings and B per group). Counted
+// votes are those of certificates that passed every earlier check (as in
+// launch_cert_groups); group_ok[g] = 1 when the sum is the identity and no counted vote has
+// a flag. Every counted vote is keyed, so its A-table slots (0..7) are free: the key list
+// lives in slot 0 of the group's votes 0..M-1 (M <= counted votes), the header in slot 1 of
+// vote 0 (the fallback ladders read only R tables and the committee key tables).
+namespace {
+
+struct sgrp_hdr {
+  uint32_t nkeys;    // M: distinct keys among the counted votes
+  uint32_t flagged;  // OR of the counted votes' BF_* flags
+  uint32_t bb[8];    // -sum b_i mod l, recoded to signed 8-bit digits
+};
+struct sgrp_key {
+  uint32_t key;
+  uint32_t c[8];     // sum of the key's c_i mod l, recoded to signed 8-bit digits
+};
+static_assert(sizeof(sgrp_hdr) <= sizeof(ge_cached) && sizeof(sgrp_key) <= sizeof(ge_cached),
+              "small-group records must fit a table slot");
+
+constexpr uint64_t kSgrpMaxCerts = 32;
+
+__device__ __forceinline__ bool cert_decided(const int32_t* pre1, const int32_t* pre2,
+                                             const int32_t* hdr_st, uint64_t c) {
+  return pre1[c] != 0 || hdr_st[c] != 0 || pre2[c] != 0;
+}
+
+__global__ __launch_bounds__(64) void k_sgrp_keys(
+    const uint64_t* __restrict__ cvo, uint64_t g0, uint64_t ncert, uint64_t K, uint64_t i0,
+    uint32_t nkeys, const int32_t* __restrict__ pre1, const int32_t* __restrict__ pre2,
+    const int32_t* __restrict__ hdr_st, bv_item* __restrict__ items,
+    ge_cached* __restrict__ tabs) {
+  __shared__ unsigned long long s_acc[256][8];
+  __shared__ uint32_t s_cnt[256];
+  const int tid = threadIdx.x;
+  const uint64_t g = g0 + blockIdx.x;
+  const uint64_t c0 = g * K, c1 = c0 + K < ncert ? c0 + K : ncert;
+  const uint64_t v0 = cvo[c0], v1 = cvo[c1];
+  if (v1 == v0) return;   // no votes: k_sgrp_combine settles the group
+  for (uint32_t j = tid; j < nkeys; j += 64) {
+    s_cnt[j] = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) s_acc[j][w] = 0;
+  }
+  __syncthreads();
+  sc bsum;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bsum.w[j] = 0;
+  uint32_t flagged = 0;
+  for (uint64_t v = v0 + tid; v < v1; v += 64) {
+    const uint64_t c = batch_of(cvo, c0, c1, v);
+    const bool counted = !cert_decided(pre1, pre2, hdr_st, c);
+    items[v - i0].pad = counted ? 1u : 0u;   // k_sgrp_ladder adds counted votes only
+    if (!counted) continue;
+    const bv_item& it = items[v - i0];
+    flagged |= it.flags;
+    const uint32_t key = it.key;
+    if (key == kNone || key >= nkeys) {   // cannot happen for a counted vote (k_cert_prepare)
+      flagged |= BF_A_DECODE;
+      continue;
+    }
+    // c_i from its signed-digit recoding (c + 0x80..80, no final carry since c < l)
+    uint64_t borrow = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      const uint64_t d = (uint64_t)it.c[w] - 0x80808080u - borrow;
+      borrow = (d >> 63) & 1;
+      atomicAdd(&s_acc[key][w], (unsigned long long)(uint32_t)d);
+    }
+    atomicAdd(&s_cnt[key], 1u);
+    sc bi;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bi.w[j] = it.b[j];
+    sc_add(bsum, bsum, bi);
+  }
+#pragma unroll 1
+  for (int o = 32; o > 0; o >>= 1) {
+    sc b;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b.w[j] = (uint32_t)__shfl_xor((int)bsum.w[j], o);
+    sc_add(bsum, bsum, b);
+    flagged |= (uint32_t)__shfl_xor((int)flagged, o);
+  }
+  __syncthreads();
+  ge_cached* slots = tabs + 16 * (v0 - i0);
+  uint32_t base = 0;
+  for (uint32_t j0 = 0; j0 < nkeys; j0 += 64) {
+    const uint32_t j = j0 + tid;
+    const bool used = j < nkeys && s_cnt[j] != 0;
+    const uint64_t mask = __ballot(used);
+    if (used) {
+      const uint32_t pos = base + (uint32_t)__popcll(mask & ((1ull << tid) - 1));
+      uint32_t x[16];
+      unsigned long long carry = 0;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        carry += s_acc[j][w];
+        x[w] = (uint32_t)carry;
+        carry >>= 32;
+      }
+      x[8] = (uint32_t)carry;
+      x[9] = (uint32_t)(carry >> 32);
+#pragma unroll
+      for (int w = 10; w < 16; ++w) x[w] = 0;
+      sc s;
+      sc_reduce512(s, x);
+      sgrp_key e;
+      e.key = j;
+      sc_recode(e.c, s, 0x80808080u);
+      *reinterpret_cast<sgrp_key*>(slots + 16 * (uint64_t)pos) = e;
+    }
+    base += (uint32_t)__popcll(mask);
+  }
+  if (tid == 0) {
+    sgrp_hdr h;
+    h.nkeys = base;
+    h.flagged = flagged;
+    sc nb;
+    sc_neg(nb, bsum);
+    sc_recode(h.bb, nb, 0x80808080u);
+    *reinterpret_cast<sgrp_hdr*>(slots + 1) = h;
+  }
+}
+
+// One lane per (group, chunk), nch chunks per group. Chunk k takes the group's votes
+// [V k / nch, V (k + 1) / nch) (counted ones only), its keys m = k, k + nch, ... and (k = 0)
+// the B term; its partial sum goes to out[(g - g0) nch + k] for k_sgrp_combine.
+__global__ __launch_bounds__(256) void k_sgrp_ladder(
+    const uint64_t* __restrict__ cvo, uint64_t g0, uint64_t g1, uint64_t ncert, uint64_t K,
+    uint32_t nch, uint64_t i0, const bv_item* __restrict__ items,
+    const ge_cached* __restrict__ tabs, const ge_cached* __restrict__ ktabs,
+    bv_chunk_out* __restrict__ out) {
+  __shared__ ge_niels s_btab[129];
+  __shared__ ge_niels s_b128[129];
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&g_bc.btab[0]);
+    const uint32_t* src2 = reinterpret_cast<const uint32_t*>(&g_bc.b128[0]);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(s_btab);
+    uint32_t* dst2 = reinterpret_cast<uint32_t*>(s_b128);
+    for (int i = threadIdx.x; i < BT_WORDS; i += blockDim.x) {
+      dst[i] = src[i];
+      dst2[i] = src2[i];
+    }
+  }
+  __syncthreads();
+  const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nl = (g1 - g0) * nch;
+  if ((uint64_t)blockIdx.x * blockDim.x >= nl) return;   // whole block past the end
+  const bool inrange = lane < nl;
+  const uint64_t gl = inrange ? lane : nl - 1;
+  const uint64_t g = g0 + gl / nch;
+  const uint32_t k = (uint32_t)(gl % nch);
+  const uint64_t c0 = g * K, c1 = c0 + K < ncert ? c0 + K : ncert;
+  const uint64_t v0 = cvo[c0], V = cvo[c1] - v0;
+  const uint64_t t0 = v0 + V * k / nch, t1 = v0 + V * (k + 1) / nch;
+  const bool live = inrange && V > 0;
+  sgrp_hdr h{};
+  if (live) h = *reinterpret_cast<const sgrp_hdr*>(tabs + 16 * (v0 - i0) + 1);
+  const ge_cached* slots = tabs + 16 * (v0 - i0);
+  ge acc;
+  ge_identity(acc);
+  const int W = wave_max_int(live ? 33 : 0);
+#pragma unroll 1
+  for (int j = W - 1; j >= 0; --j) {
+    if (j != W - 1) {
+#pragma unroll 1
+      for (int t = 0; t < 3; ++t) ge_dbl(acc, acc, false);
+      ge_dbl(acc, acc, true);
+    }
+    if (!live) continue;
+#pragma unroll 1
+    for (uint64_t t = t0; t < t1; ++t) {
+      const bv_item* it = items + (t - i0);
+      if (it->pad) add_entry(acc, tabs + 16 * (t - i0) + 8, digit4(it->z[j >> 3], j));
+    }
+    if ((j & 1) == 0 && j < 32) {
+#pragma unroll 1
+      for (uint32_t m = k; m < h.nkeys; m += nch) {
+        const sgrp_key& e = *reinterpret_cast<const sgrp_key*>(slots + 16 * (uint64_t)m);
+        const ge_cached* kt = ktabs + kKeyTab * (uint64_t)e.key;
+        add_key_entry(acc, kt, digit8(e.c, j >> 1));
+        add_key_entry(acc, kt + 129, digit8(e.c, 16 + (j >> 1)));
+      }
+      if (k == 0) {
+        add_digit_niels(acc, s_btab, digit8(h.bb, j >> 1), true);
+        add_digit_niels(acc, s_b128, digit8(h.bb, 16 + (j >> 1)), true);
+      }
+    }
+  }
+  if (!inrange) return;
+  out[gl].P = acc;
+}
+
+// One lane per group: the sum of its chunks' points; group_ok = identity and no flags.
+__global__ __launch_bounds__(256) void k_sgrp_combine(
+    const uint64_t* __restrict__ cvo, uint64_t g0, uint64_t g1, uint64_t ncert, uint64_t K,
+    uint32_t nch, uint64_t i0, const ge_cached* __restrict__ tabs,
+    const bv_chunk_out* __restrict__ out, uint32_t* __restrict__ group_ok) {
+  const uint64_t gl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g0 + gl >= g1) return;
+  const uint64_t g = g0 + gl;
+  const uint64_t c0 = g * K, c1 = c0 + K < ncert ? c0 + K : ncert;
+  const uint64_t v0 = cvo[c0];
+  if (cvo[c1] == v0) {   // no votes: nothing to check
+    group_ok[g] = 1;
+    return;
+  }
+  const sgrp_hdr& h = *reinterpret_cast<const sgrp_hdr*>(tabs + 16 * (v0 - i0) + 1);
+  ge acc = out[gl * nch].P;
+#pragma unroll 1
+  for (uint32_t k = 1; k < nch; ++k) {
+    ge_cached c;
+    ge_to_cached(c, out[gl * nch + k].P, g_bc.k.d2);
+    ge_add_cached(acc, acc, c, true);
+  }
+  group_ok[g] = (h.flagged == 0 && ge_is_identity(acc)) ? 1u : 0u;
+}
+
+}  // namespace
+
+// Cost model (point additions per certificate), the per-vote items being
+// common to both paths: a certificate's own keyed ladder costs q (33 + 32) + 151 (132
+// doublings and 32 B additions); in a group of K it costs 33 per vote, its share of
+// 32 per distinct key and 151 per group, plus, when the group fails (probability
+// 1 - (1 - p)^K), its own ladder. K minimises that; *beats_per_cert says whether the best K
+// is cheaper than the certificate's own ladder.
+uint64_t cert_sgroup_size(const uint64_t* host_cvo, uint64_t ncert, uint64_t nkeys,
+                          bool injected_z, double p_cert, bool* beats_per_cert) {
+  if (beats_per_cert) *beats_per_cert = false;
+  const char* m = getenv("NW_CERT_MERGE");
+  if (injected_z || (m && m[0] == '0') || nkeys == 0 || nkeys > 256 || ncert == 0) return 0;
+  const uint64_t nvotes = host_cvo[ncert] - host_cvo[0];
+  uint64_t qmax = 0;
+  for (uint64_t c = 0; c < ncert; ++c) qmax = std::max(qmax, host_cvo[c + 1] - host_cvo[c]);
+  if (qmax == 0 || qmax >= kPipMin || nvotes == 0) return 0;
+  const uint64_t kcap = std::max<uint64_t>(
+      1, std::min<uint64_t>(kSgrpMaxCerts, slice_units() / (2 * (qmax + 1))));
+  const uint64_t forced = env_u64("NW_CERT_SMALL_K", 0);
+  if (forced) {
+    if (beats_per_cert) *beats_per_cert = true;
+    return std::min(forced, kcap);
+  }
+  const double q = (double)nvotes / (double)ncert;
+  const double p = std::min(0.5, std::max(1e-5, p_cert));
+  const double own = q * 65.0 + 151.0;
+  uint64_t best = 1;
+  double best_cost = 1e300;
+  for (uint64_t K = 1; K <= kcap; ++K) {
+    const double keys = std::min((double)nkeys, (double)K * q);
+    const double fail = 1.0 - std::pow(1.0 - p, (double)K);
+    const double cost = q * 33.0 + (32.0 * keys + 151.0) / (double)K + fail * own;
+    if (cost < best_cost) { best_cost = cost; best = K; }
+  }
+  if (beats_per_cert) *beats_per_cert = best_cost < own;
+  return best;
+}
+
+hipError_t launch_cert_sgroups(const uint32_t* cert_digest, const uint64_t* cvo,
+                               const uint64_t* host_cvo, uint64_t ncert, const uint32_t* pks,
+                               const uint32_t* sigs, uint64_t nvotes, const z_key_t& zkey,
+                               void* batch_ws, void* group_ws, const int32_t* pre1,
+                               const int32_t* pre2, const int32_t* hdr_st,
+                               const key_tables_t& keys, uint32_t nkeys, uint64_t K,
+                               double p_cert, int32_t* status, uint64_t* fail_index,
+                               uint32_t** group_ok_out, hipStream_t stream) {
+  if (ncert == 0 || nkeys > 256 || K == 0 || K > kSgrpMaxCerts || !keys.tabs || !keys.vote_key)
+    return hipErrorInvalidValue;
+  const uint64_t ngroups = (ncert + K - 1) / K;
+  char* gp = static_cast<char*>(group_ws);
+  uint32_t* group_ok = reinterpret_cast<uint32_t*>(gp + a256(8 * (ncert + 1)) + a256(4 * ncert));
+  *group_ok_out = group_ok;
+  const uint64_t cap = std::min<uint64_t>(nvotes + ncert, slice_units());
+  bv_ws w;
+  bv_layout(cap, static_cast<char*>(batch_ws), &w);
+  const batch_skip_t nosk{nullptr, 1}, sk{group_ok, K};
+  uint64_t qmax = 0;
+  for (uint64_t c = 0; c < ncert; ++c) qmax = std::max(qmax, host_cvo[c + 1] - host_cvo[c]);
+  // group chunks: about Cg votes each, so that they fill the chip (~2 waves per SIMD) while
+  // the 132 doublings are shared by as many votes as possible (balanced split per group);
+  // fallback chunks as in launch_verify_batch
+  const uint64_t target_lanes = 256ull * 4 * 2 * 64;
+  const uint64_t Cg = std::min<uint64_t>(32, std::max<uint64_t>(4, nvotes / target_lanes));
+  const uint64_t kq = std::min(K, ncert) * qmax;
+  const uint32_t nch = (uint32_t)std::min<uint64_t>(cap, std::max<uint64_t>(1, (kq + Cg - 1) / Cg));
+  // Fallback chunks: only the failed groups' certificates run (about a fraction
+  // 1 - (1 - p)^K of a slice's votes), so they are cut small enough to fill the chip on
+  // their own: a certificate of q votes split over several chunks costs a few more doublings,
+  // one chunk per certificate leaves most SIMDs idle at N = 100 (67-vote ladders).
+  const double fail = 1.0 - std::pow(1.0 - std::min(0.5, std::max(0.0, p_cert)), (double)K);
+  const uint64_t fb_votes = (uint64_t)(fail * (double)std::min(nvotes, cap));
+  uint32_t C = (uint32_t)std::min<uint64_t>(kMaxChunk, std::max<uint64_t>(4, fb_votes / target_lanes));
+  C = (uint32_t)std::min<uint64_t>(kMaxChunk, env_u64("NW_BATCH_CHUNK", C));
+  auto cert_at = [&](uint64_t g) { return std::min(g * K, ncert); };
+  uint64_t g = 0;
+  while (g < ngroups) {
+    // slice [g, e) of whole groups: votes + certificates and the group chunks fit the workspace
+    uint64_t e = g;
+    while (e < ngroups) {
+      const uint64_t b = cert_at(g), be = cert_at(e + 1);
+      if (e > g && ((host_cvo[be] - host_cvo[b]) + (be - b) > cap || (e + 1 - g) * nch > cap))
+        break;
+      ++e;
+    }
+    const uint64_t b = cert_at(g), be = cert_at(e);
+    const uint64_t i0 = host_cvo[b], i1 = host_cvo[be];
+    if ((i1 - i0) + (be - b) > cap || (e - g) * nch > cap) return hipErrorInvalidValue;
+    uint64_t chunks = 0, multi = 0;   // host upper bounds for the fallback (every certificate)
+    for (uint64_t c = b; c < be; ++c) {
+      const uint64_t kb = (host_cvo[c + 1] - host_cvo[c] + C - 1) / C;
+      chunks += kb;
+      multi += kb != 1;
+    }
+    if (i1 > i0)
+      hipLaunchKernelGGL(k_bv_items, dim3((unsigned)((i1 - i0 + 255) / 256)), dim3(256), 0,
+                         stream, cert_digest, cvo, b, be, i0, i1, kPipMin, pks, sigs, nullptr,
+                         zkey, w.items, w.tabs, keys, nosk);
+    hipLaunchKernelGGL(k_sgrp_keys, dim3((unsigned)(e - g)), dim3(64), 0, stream, cvo, g, ncert,
+                       K, i0, nkeys, pre1, pre2, hdr_st, w.items, w.tabs);
+    hipLaunchKernelGGL(k_sgrp_ladder, dim3((unsigned)(((e - g) * nch + 255) / 256)), dim3(256),
+                       0, stream, cvo, g, e, ncert, K, nch, i0, w.items, w.tabs, keys.tabs,
+                       w.outs);
+    hipLaunchKernelGGL(k_sgrp_combine, dim3((unsigned)((e - g + 255) / 256)), dim3(256), 0,
+                       stream, cvo, g, e, ncert, K, nch, i0, w.tabs, w.outs, group_ok);
+    // the certificates of failed groups: their own verify_batch from the same items
+    const unsigned nblk = (unsigned)((be - b + 1023) / 1024);
+    hipLaunchKernelGGL(k_bv_plan_local, dim3(nblk), dim3(1024), 0, stream, cvo, b, be, C,
+                       kPipMin, sk, w.plan_tot);
+    hipLaunchKernelGGL(k_bv_plan_top, dim3(1), dim3(1024), 0, stream, nblk, be - b, w.plan_tot,
+                       w.chunk_start);
+    hipLaunchKernelGGL(k_bv_plan_apply, dim3(nblk), dim3(1024), 0, stream, cvo, b, be, C, kPipMin,
+                       sk, w.plan_tot, w.chunk_start, w.multi, w.multi_first, w.pip_list, status,
+                       fail_index);
+    if (chunks) {
+      hipLaunchKernelGGL(k_bv_expand, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
+                         stream, cvo, b, be - b, (uint32_t)chunks, w.chunk_start, w.chunks);
+      hipLaunchKernelGGL(k_bv_chunks, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
+                         stream, w.chunks, (uint32_t)chunks, cvo, b, i0, w.items, w.tabs,
+                         keys.tabs, w.outs, status, fail_index, w.chunk_start + (be - b));
+    }
+    if (multi)
+      hipLaunchKernelGGL(k_bv_combine, dim3((unsigned)multi), dim3(256), 0, stream, w.multi,
+                         w.multi_first, (uint32_t)multi, cvo, b, C, w.outs, status, fail_index,
+                         w.plan_tot + 3 * nblk + 1);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
     g = e;

@@ -98,6 +98,22 @@ hipError_t launch_cert_groups(const uint32_t* cert_digest, const uint64_t* cvo,
                               const int32_t* pre2, const int32_t* hdr_st,
                               const key_tables_t& keys, const ge* key_base, uint32_t nkeys,
                               uint64_t K, uint32_t** group_ok_out, hipStream_t stream);
+// Small groups: K certificates per keyed Straus check, then the per-certificate
+// verify_batch of the certificates of failed groups from the same per-vote items. Writes
+// status / fail_index for every certificate (in place of launch_verify_batch);
+// cert_sgroup_size() picks K for an estimated fraction p_cert of certificates whose votes
+// fail (NW_CERT_SMALL_K fixes it), 0 when merging does not apply; *beats_per_cert: the
+// cost model prefers these groups to every certificate's own ladder. keys.vote_key required.
+uint64_t cert_sgroup_size(const uint64_t* host_cvo, uint64_t ncert, uint64_t nkeys,
+                          bool injected_z, double p_cert, bool* beats_per_cert);
+hipError_t launch_cert_sgroups(const uint32_t* cert_digest, const uint64_t* cvo,
+                               const uint64_t* host_cvo, uint64_t ncert, const uint32_t* pks,
+                               const uint32_t* sigs, uint64_t nvotes, const z_key_t& zkey,
+                               void* batch_ws, void* group_ws, const int32_t* pre1,
+                               const int32_t* pre2, const int32_t* hdr_st,
+                               const key_tables_t& keys, uint32_t nkeys, uint64_t K,
+                               double p_cert, int32_t* status, uint64_t* fail_index,
+                               uint32_t** group_ok_out, hipStream_t stream);
 
 // ---- primary messages (nw_cert.hip) ----------------------------------------------------
 struct cert_committee_t {

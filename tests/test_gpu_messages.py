@@ -233,11 +233,59 @@ def test_certificate_groups_mixed_validity(monkeypatch, N, n):
     assert st0.tolist() == exp_st.tolist() and ix0.tolist() == exp_ix.tolist()
 
 
+@pytest.mark.parametrize("N,n,K", [(4, 6000, 1), (4, 6000, 8), (10, 3000, 5), (100, 600, 3),
+                                   (100, 600, 32)])
+def test_certificate_small_groups_mixed_validity(monkeypatch, N, n, K):
+    """Small groups (launch_cert_sgroups, NW_CERT_SMALL_K = K certificates per keyed Straus
+    check, then the per-certificate ladders of failed groups from the same items): about 1%
+    of the certificates carry one invalid vote of every class (workloads.mutate_votes);
+    statuses and indices equal the construction and the unmerged path."""
+    from narwhal_amd import crypto as C
+    keys = O.keys(N)
+    s = W.certificate_stream(n, keys, lambda sk, m: C.sign_many(sk, m), oracle_digest_many,
+                             seed=200 + N)
+    bad = np.arange(11 % n, n, 97)
+    m, exp_st, exp_ix = W.mutate_votes(s, bad, seed=N + K)
+    com = _Com(s["committee"])
+    monkeypatch.setenv("NW_CERT_SMALL_K", str(K))
+    st, ix = M.verify_certificates_many(com, m, None)
+    assert st.tolist() == exp_st.tolist() and ix.tolist() == exp_ix.tolist()
+    st, _ = M.verify_certificates_many(com, s, None)      # honest: every group passes
+    assert (st == 0).all()
+    monkeypatch.setenv("NW_BATCH_SLICE_UNITS", "20000")   # several slices of whole groups
+    st, ix = M.verify_certificates_many(com, m, None)
+    assert st.tolist() == exp_st.tolist() and ix.tolist() == exp_ix.tolist()
+    monkeypatch.delenv("NW_BATCH_SLICE_UNITS")
+    monkeypatch.setenv("NW_CERT_MERGE", "0")
+    st0, ix0 = M.verify_certificates_many(com, m, None)
+    assert st0.tolist() == exp_st.tolist() and ix0.tolist() == exp_ix.tolist()
+
+
+def test_certificate_small_groups_early_failures(monkeypatch):
+    """Small groups mixing honest certificates with every header-level and pre-check failure
+    class (they contribute no votes) and every vote-level class: statuses and indices equal
+    the expected per-certificate ones."""
+    from cert_cases import pack, unpack
+    from narwhal_amd import crypto as C
+    com, ms, exp_st, exp_ix, cls = mutated_stream(N=4, copies=12, seed=9)
+    honest = W.certificate_stream(600, O.keys(4), lambda sk, m: C.sign_many(sk, m),
+                                  oracle_digest_many, seed=13, n_votes=4)
+    hrec, mrec = unpack(honest), unpack(ms)
+    recs = hrec[:300] + mrec + hrec[300:]
+    exp = [0] * 300 + [int(x) for x in exp_st] + [0] * 300
+    expi = [0] * 300 + [int(x) for x in exp_ix] + [0] * 300
+    p = pack(recs)
+    for K in (2, 7, 32):
+        monkeypatch.setenv("NW_CERT_SMALL_K", str(K))
+        st, ix = M.verify_certificates_many(_Com(com), p, None)
+        assert st.tolist() == exp and ix.tolist() == expi, K
+
+
 def test_certificate_groups_adaptive_repeated_calls():
     """Adaptive merging (nw_api.cpp group_failure_rate): a stream with ~1% failing
-    certificates is verified per certificate from the next call on (the measured rate makes
-    most merged groups fail), and merged again once an honest stream reports no failures;
-    every call's statuses and indices equal the construction, whichever path ran."""
+    certificates moves from the big merged groups to small groups from the next call on (the
+    measured rate makes most big groups fail), and back once an honest stream reports no
+    failures; every call's statuses and indices equal the construction, whichever path ran."""
     from narwhal_amd import crypto as C
     N, n = 10, 5200
     s = W.certificate_stream(n, O.keys(N), lambda sk, m: C.sign_many(sk, m), oracle_digest_many,
