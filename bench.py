@@ -86,6 +86,19 @@ def pmc_traffic(kernel: str, units: int):
     return e["hbm_bytes"] * units / e["units"], e["source"]
 
 
+def pmc_issue_peak():
+    """Issue-bound peak of k_verify_strict (verifies/s) from its committed PMC instruction mix
+    (profiles/r02a/pmc_mix.json, tools/pmc_mix.sh): per-verify 64-bit / 32-bit integer and
+    other VALU lane-ops, each priced at its microbenchmarked issue rate
+    (profiles/r01_ubench_valu_4wps.txt; 32-bit integer ops at the half rate, an upper bound
+    on their cost). None when the profile is absent."""
+    try:
+        m = json.load(open(os.path.join(ROOT, "profiles", "r02a", "pmc_mix.json")))
+    except (OSError, ValueError):
+        return None, None
+    return m["issue_peak_verifies_per_s"], "profiles/r02a/pmc_mix.json"
+
+
 def enc_y(y: int, sign: int) -> bytes:
     b = bytearray(y.to_bytes(32, "little"))
     b[31] |= sign << 7
@@ -690,6 +703,7 @@ def main():
         value = units / r["elapsed"] * args.steps
         achieved = r["n"] * MAC_PER_STRICT_VERIFY / (r["kernel_ms"] * 1e-3) / 1e12
         traffic, tsrc = pmc_traffic("k_verify_strict", r["n"])
+        issue_peak, issue_src = pmc_issue_peak()
         result = {
             "metric": METRIC, "value": value, "unit": "verifies/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -712,7 +726,11 @@ def main():
                          "traffic_unit": "HBM bytes per launch", "traffic_source": tsrc,
                          "algorithmic_bytes": r["n"] * (32 + 32 + 64 + 4) + r["n"] / 8,
                          "kernel": "k_verify_strict", "kernel_ms": r["kernel_ms"],
-                         "work_per_unit": f"{MAC_PER_STRICT_VERIFY} MAC/verify (SURVEY 8d)"},
+                         "work_per_unit": f"{MAC_PER_STRICT_VERIFY} MAC/verify (SURVEY 8d)",
+                         "issue_peak": issue_peak, "issue_unit": "verifies/s",
+                         "issue_frac": (r["n"] / (r["kernel_ms"] * 1e-3) / issue_peak
+                                        if issue_peak else None),
+                         "issue_source": issue_src},
             "parity": "ok" if r["parity"] else "FAIL",
         }
         sample = r["sample"]
