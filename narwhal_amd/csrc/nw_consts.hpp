@@ -105,6 +105,63 @@ inline void compute_strict_consts(strict_consts& sk, ge_niels b128[129]) {
 }  // namespace nw
 
 namespace nw {
+// Affine niels form of p given zi = 1/Z.
+inline void ge_to_niels_zi(ge_niels& n, const ge& p, const fe& zi, const fe& d2) {
+  fe x, y;
+  fe_mul(x, p.X, zi);
+  fe_mul(y, p.Y, zi);
+  fe_add(n.ypx, y, x); fe_carry(n.ypx);
+  fe_sub(n.ymx, y, x);
+  fe_mul(n.xy2d, x, y);
+  fe_mul(n.xy2d, n.xy2d, d2);
+}
+
+// The strict kernel's wide B tables (nw_strict.hpp, signed bw-bit windows of w = w0 +
+// 2^128 w1): out[h * n + j] = j * 2^(128 h) * B, j = 0..n-1, n = 2^(bw-1) + 1, h = 0, 1,
+// in padded affine niels form (128 B entries). j * P by repeated addition, the 2n
+// inversions batched into one (Montgomery's trick). bw = 16: 2 x 32,769 entries, 8.4 MB.
+inline void compute_wide_btab(ge_niels_pad* out, int bw) {
+  const uint32_t n = (1u << (bw - 1)) + 1;
+  strict_consts sk;
+  ge_niels b128[129];
+  compute_strict_consts(sk, b128);
+  fe a, b, t;
+  fe_from_u32(a, 4);
+  fe_from_u32(b, 5);
+  fe_invert(t, b);
+  fe_mul(a, a, t);
+  uint32_t yw[8];
+  fe_tobytes(yw, a);
+  ge P;
+  ge_frombytes(P, yw, sk.k);   // B
+  ge* pts = new ge[n];
+  fe* pre = new fe[n];
+  for (int h = 0; h < 2; ++h) {
+    if (h == 1)
+      for (int i = 0; i < 128; ++i) { ge d; ge_dbl(d, P, true); P = d; }   // 2^128 B
+    ge_cached cP;
+    ge_to_cached(cP, P, sk.k.d2);
+    pts[1] = P;
+    for (uint32_t j = 2; j < n; ++j) ge_add_cached(pts[j], pts[j - 1], cP, true);
+    fe_1(pre[0]);
+    for (uint32_t j = 1; j < n; ++j) fe_mul(pre[j], pre[j - 1], pts[j].Z);
+    fe inv;
+    fe_invert(inv, pre[n - 1]);
+    ge_niels_pad* o = out + (size_t)h * n;
+    for (uint32_t j = n - 1; j >= 1; --j) {
+      fe zi;
+      fe_mul(zi, inv, pre[j - 1]);   // 1 / Z_j
+      fe_mul(inv, inv, pts[j].Z);    // 1 / (Z_1 ... Z_{j-1})
+      ge_to_niels_zi(o[j].n, pts[j], zi, sk.k.d2);
+      o[j].pad[0] = o[j].pad[1] = 0;
+    }
+    ge_niels_identity(o[0].n);
+    o[0].pad[0] = o[0].pad[1] = 0;
+  }
+  delete[] pts;
+  delete[] pre;
+}
+
 // Fixed-base comb for [b]B with signed 8-bit digits and no doublings:
 // comb[w * 129 + j] = j * 2^(8 w) * B, w = 0..31, j = 0..128 (affine niels), 495 KB.
 inline void compute_comb(ge_niels* comb) {

@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <atomic>
 #include <mutex>
+#include <vector>
 
 namespace nw {
 
@@ -238,12 +239,19 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
                                                        uint64_t n, int32_t* __restrict__ status,
                                                        uint64_t* __restrict__ bitmap,
                                                        ge_cached* __restrict__ tabs,
-                                                       key_tables_t keys) {
+                                                       key_tables_t keys,
+                                                       const ge_niels_pad* __restrict__ btw) {
+#if NW_BWIN == 8
   __shared__ ge_niels s_btab[129];
   __shared__ ge_niels s_b128[129];
   load_table(s_btab, g_consts.btab);
   load_table(s_b128, g_consts.b128);
   __syncthreads();
+  const btab_pair bt{s_btab, s_b128};
+  (void)btw;
+#else
+  const btab_wide bt{btw, (1u << (NW_BWIN - 1)) + 1};
+#endif
   ge_cached* tabA = tabs + 16 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
   ge_cached* tabR = tabA + 8;
 #pragma unroll 1
@@ -255,8 +263,8 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
     const strict_src_global src{pks + 8 * i, sigs + 16 * i, msgs + (uint64_t)msg_stride_words * i};
     const uint32_t kk = keys.vote_key ? keys.vote_key[i] : kNoKey;
     const ge_cached* keytab = kk != kNoKey ? keys.tabs + kKeyTab * (uint64_t)kk : nullptr;
-    const int st = strict_verify_core(src, g_consts.sk, s_btab, s_b128, tabA, tabR, WaveMax{},
-                                      keytab, kk != kNoKey ? keys.ok[kk] : 0u);
+    const int st = strict_verify_core<NW_BWIN>(src, g_consts.sk, bt, tabA, tabR, WaveMax{},
+                                               keytab, kk != kNoKey ? keys.ok[kk] : 0u);
     if (active) status[gi] = st;
     const uint64_t mask = __ballot(active && st == NW_OK);
     if ((threadIdx.x & 63) == 0 && gi < n) bitmap[gi >> 6] = mask;
@@ -385,16 +393,48 @@ __global__ __launch_bounds__(256) void k_sign(const uint32_t* __restrict__ sks,
 // ---------------------------------------------------------------------------------------
 namespace nw {
 
+// The strict kernel's wide B tables (nw_consts.hpp compute_wide_btab), one copy per device,
+// indexed by HIP device id; built on the host once per process, uploaded by upload_consts.
+static constexpr int kMaxDevIds = 64;
+static ge_niels_pad* g_btw[kMaxDevIds];
+static constexpr size_t kBtwEntries = 2 * ((size_t(1) << (NW_BWIN - 1)) + 1);
+
+static const ge_niels_pad* btw_for_current_device() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  return dev >= 0 && dev < kMaxDevIds ? g_btw[dev] : nullptr;
+}
+
 hipError_t upload_consts() {
   static dev_consts host;
+  static std::vector<ge_niels_pad> btw;
   static std::once_flag once;
   std::call_once(once, [] {
     compute_consts(host.k, host.btab);
     compute_strict_consts(host.sk, host.b128);
+#if NW_BWIN != 8
+    btw.resize(kBtwEntries);
+    compute_wide_btab(btw.data(), NW_BWIN);
+#endif
   });
   hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_consts), &host, sizeof(host), 0,
                                    hipMemcpyHostToDevice);
-  return e != hipSuccess ? e : upload_batch_consts();
+  if (e != hipSuccess) return e;
+#if NW_BWIN != 8
+  int dev = 0;
+  e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= kMaxDevIds) return hipErrorInvalidDevice;
+  if (!g_btw[dev]) {
+    void* p = nullptr;
+    e = hipMalloc(&p, kBtwEntries * sizeof(ge_niels_pad));
+    if (e != hipSuccess) return e;
+    e = hipMemcpy(p, btw.data(), kBtwEntries * sizeof(ge_niels_pad), hipMemcpyHostToDevice);
+    if (e != hipSuccess) { (void)hipFree(p); return e; }
+    g_btw[dev] = static_cast<ge_niels_pad*>(p);
+  }
+#endif
+  return upload_batch_consts();
 }
 
 static inline unsigned grid_for(uint64_t n, unsigned block) {
@@ -441,8 +481,10 @@ hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
   if (n == 0) return hipSuccess;
   const unsigned grid = std::min<uint64_t>(strict_grid(), grid_for(n, 256));
   const key_tables_t kt = keys ? *keys : key_tables_t{nullptr, nullptr, nullptr};
+  const ge_niels_pad* btw = btw_for_current_device();
+  if (NW_BWIN != 8 && !btw) return hipErrorNotInitialized;
   hipLaunchKernelGGL(k_verify_strict, dim3(grid), dim3(256), 0, stream, msgs, msg_stride_words,
-                     pks, sigs, n, status, bitmap, static_cast<ge_cached*>(workspace), kt);
+                     pks, sigs, n, status, bitmap, static_cast<ge_cached*>(workspace), kt, btw);
   return hipGetLastError();
 }
 

@@ -13,6 +13,8 @@ namespace nw {
 struct ge { fe X, Y, Z, T; };
 struct ge_cached { fe YpX, YmX, Z2, T2d; };
 struct ge_niels { fe ypx, ymx, xy2d; };
+// 128-byte entry of a large table in global memory (eight aligned 16-byte loads).
+struct alignas(16) ge_niels_pad { ge_niels n; uint32_t pad[2]; };
 
 // Field constants (derived on the host at init from their definitions; see nw_api.cpp).
 struct curve_consts {
@@ -36,7 +38,9 @@ NW_HD void ge_to_cached(ge_cached& c, const ge& p, const fe& d2) {
 
 // Uncarried differences (fe_sub_nc) are used only as the FIRST fe_mul operand (the second
 // is multiplied by 19 in 32 bits and must stay carried); tests/test_field_bounds.py checks
-// every (first, second) operand pair below.
+// every (first, second) operand pair below. The output products are ordered so that two
+// share each second operand (f, h) and two each first one (e, g): the inlined multiplies
+// then compute each operand's x19 / x2 limb scalings once (CSE), not twice.
 
 // r = p + q (q cached). Computes T3 only when want_t.
 NW_HD void ge_add_cached(ge& r, const ge& p, const ge_cached& q, bool want_t) {
@@ -52,8 +56,8 @@ NW_HD void ge_add_cached(ge& r, const ge& p, const ge_cached& q, bool want_t) {
   fe_add(g, d, c);
   fe_add(h, b, a);
   fe_mul(r.X, e, f);
+  fe_mul(r.Z, g, f);
   fe_mul(r.Y, g, h);
-  fe_mul(r.Z, f, g);
   if (want_t) fe_mul(r.T, e, h);
 }
 
@@ -71,8 +75,8 @@ NW_HD void ge_sub_cached(ge& r, const ge& p, const ge_cached& q, bool want_t) {
   fe_sub_nc(g, d, c);
   fe_add(h, b, a);
   fe_mul(r.X, e, f);
-  fe_mul(r.Y, g, h);
   fe_mul(r.Z, g, f);
+  fe_mul(r.Y, g, h);
   if (want_t) fe_mul(r.T, e, h);
 }
 
@@ -90,8 +94,8 @@ NW_HD void ge_add_niels(ge& r, const ge& p, const ge_niels& q, bool want_t) {
   fe_add(g, d, c);
   fe_add(h, b, a);
   fe_mul(r.X, e, f);
+  fe_mul(r.Z, g, f);
   fe_mul(r.Y, g, h);
-  fe_mul(r.Z, f, g);
   if (want_t) fe_mul(r.T, e, h);
 }
 
@@ -112,8 +116,8 @@ NW_HD void ge_add_any(ge& r, const ge& p, const ge_cached& q, bool affine, bool 
   fe_add(g, d, c);
   fe_add(h, b, a);
   fe_mul(r.X, e, f);
+  fe_mul(r.Z, g, f);
   fe_mul(r.Y, g, h);
-  fe_mul(r.Z, f, g);
   if (want_t) fe_mul(r.T, e, h);
 }
 
@@ -143,7 +147,7 @@ NW_HD void ge_cached_cneg(ge_cached& c, bool neg) {
 
 // r = 2p (dbl-2008-hwcd, a = -1, with E, G, H negated so every operand stays non-negative:
 // E' = (A+B) - (X+Y)^2, G' = A - B, F' = G' + 2Z^2, H' = A + B; X3 = E'F', Y3 = G'H',
-// Z3 = F'G', T3 = E'H').
+// Z3 = G'F', T3 = E'H').
 NW_HD void ge_dbl(ge& r, const ge& p, bool want_t) {
   fe A, B, C, E, F, G, H, t;
   fe_sq(A, p.X);
@@ -157,8 +161,8 @@ NW_HD void ge_dbl(ge& r, const ge& p, bool want_t) {
   fe_sub(G, A, B);
   fe_add(F, G, C);
   fe_mul(r.X, E, F);
+  fe_mul(r.Z, G, F);
   fe_mul(r.Y, G, H);
-  fe_mul(r.Z, F, G);
   if (want_t) fe_mul(r.T, E, H);
 }
 

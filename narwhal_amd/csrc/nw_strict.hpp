@@ -11,10 +11,16 @@
 //      w = -v s mod l; then  R + [k]A - [s]B == 0  <=>  [v]R + [u]A + [w]B == 0.
 //   4. One ladder of ~128 doublings: signed 4-bit windows over u (table j*A) and |v|
 //      (table j*R, digits negated when v < 0), per-lane tables in private memory;
-//      w = w0 + 2^128 w1 by signed 8-bit windows over two affine tables (j*B and
-//      j*2^128 B, LDS).
+//      w = w0 + 2^128 w1 by signed NW_BWIN-bit windows over two affine tables (j*B and
+//      j*2^128 B): 16-bit windows over 2 x 32,769 entries in global memory (8.4 MB, L2 /
+//      MALL resident; 16 B additions per verify), or 8-bit windows over 2 x 129 entries
+//      in LDS (32 B additions; NW_BWIN=8).
 #pragma once
 #include "narwhal_amd.h"
+
+#ifndef NW_BWIN
+#define NW_BWIN 16
+#endif
 
 #ifndef NW_TAB_RELOAD
 #define NW_TAB_RELOAD 0
@@ -107,17 +113,47 @@ struct strict_src_arrays {
   NW_HD void K(uint32_t w[8]) const { for (int i = 0; i < 8; ++i) w[i] = k[i]; }
 };
 
+// The B term's tables: entry ad of j * 2^(128 h) * B (h = 0, 1) into e's YpX / YmX / T2d.
+// btab_pair: two 129-entry arrays (8-bit windows, LDS); btab_wide: one array of 2 x n
+// padded entries (16-bit windows, global memory, nw_consts.hpp compute_wide_btab).
+struct btab_pair {
+  const ge_niels* t0;
+  const ge_niels* t1;
+  NW_HD void operator()(int h, int ad, ge_cached& e) const {
+    const ge_niels& nb = (h == 0 ? t0 : t1)[ad];
+    fe_copy(e.YpX, nb.ypx);
+    fe_copy(e.YmX, nb.ymx);
+    fe_copy(e.T2d, nb.xy2d);
+  }
+};
+struct btab_wide {
+  const ge_niels_pad* t;
+  uint32_t n;   // entries per half: 2^(bw-1) + 1
+  NW_HD void operator()(int h, int ad, ge_cached& e) const {
+    const ge_niels& nb = t[(h ? n : 0u) + (uint32_t)ad].n;
+    fe_copy(e.YpX, nb.ypx);
+    fe_copy(e.YmX, nb.ymx);
+    fe_copy(e.T2d, nb.xy2d);
+  }
+};
+
 // Status of one strict verification. wave_max maps this lane's ladder length (in 4-bit
 // windows) to the wave's maximum (identity on the host). tabA/tabR: 8 entries each of
-// per-lane scratch. s_btab / s_b128: j*B and j*2^128 B, j = 0..128.
+// per-lane scratch. bt: j*B and j*2^128 B, j = 0..2^(BW-1) (btab_pair / btab_wide).
 // keytab (optional): A's pre-decompressed key table j*A, j = 0..128 (cached form) with
 // keyflags bit 0 = decoded, bit 1 = small order; then A is neither decompressed nor
 // tabulated here and u is taken in signed 8-bit windows over that table.
-template <class Src, class WaveMax>
-NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const ge_niels* s_btab,
-                             const ge_niels* s_b128, ge_cached* tabA, ge_cached* tabR,
+template <int BW, class BTab, class Src, class WaveMax>
+NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab& bt,
+                             ge_cached* tabA, ge_cached* tabR,
                              WaveMax wave_max, const ge_cached* keytab = nullptr,
                              uint32_t keyflags = 0) {
+  static_assert(BW == 8 || BW == 16, "B windows of 8 or 16 bits");
+  constexpr int WPB = BW / 4;          // 4-bit ladder windows per B window
+  constexpr int DPW = 32 / BW;         // B digits per 32-bit word
+  constexpr uint32_t BBIAS = BW == 8 ? 0x80808080u : 0x80008000u;
+  constexpr uint32_t BMASK = (1u << BW) - 1;
+  constexpr int BHALF = 1 << (BW - 1);
   // Decompress A, then R, in one rolled loop (one copy of the sqrt_ratio_i chain in the
   // code object): P, its small-order flag and its 8-entry table j * P. Only the point is
   // live here: the scalars are computed afterwards (register pressure).
@@ -155,7 +191,9 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const ge_ni
   }
   sc_mul(w, vm, s);
   if (!h.vneg) sc_neg(w, w);
-  // signed digits: u, |v| in 4-bit windows; w0 = w mod 2^128, w1 = w >> 128 in 8-bit windows
+  // signed digits: u, |v| in 4-bit windows; w0 = w mod 2^128, w1 = w >> 128 in BW-bit
+  // windows (one signed recoding of the whole w: digit m of w1 is digit m + 128 / BW of w,
+  // the carry out of w0's top digit flows into w1's bottom one)
   sc ur, vr;
 #pragma unroll
   for (int j = 0; j < 8; ++j) { ur.w[j] = h.u[j]; vr.w[j] = vm.w[j]; }
@@ -163,21 +201,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const ge_ni
   const uint32_t ubias = keytab ? 0x80808080u : 0x88888888u;
   sc_recode(ud, ur, ubias);
   sc_recode(vd, vr, 0x88888888u);
-  {
-    uint64_t c = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      c += (uint64_t)w.w[i] + 0x80808080u;
-      wd[i] = (uint32_t)c;
-      c >>= 32;
-    }
-#pragma unroll
-    for (int i = 4; i < 8; ++i) {
-      c += (uint64_t)w.w[i] + 0x80808080u;
-      wd[i] = (uint32_t)c;
-      c >>= 32;
-    }
-  }
+  sc_recode(wd, w, BBIAS);
   // ladder length in 4-bit windows: up to the highest nonzero signed digit of u and |v|
   // (digit j is nonzero iff nibble j of the recoded word is not 8), at least 32 for the
   // two 128-bit halves of w
@@ -194,7 +218,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const ge_ni
 
   // One rolled doubling and one addition routine serve every term (code size: the ladder
   // body stays inside the instruction cache). Per 4-bit window j: 4 doublings, then the
-  // A digit, the R digit and, on even j < 32, the two 8-bit B digits.
+  // A digit, the R digit and, on j < 32 with j % (BW / 4) == 0, the two BW-bit B digits.
   ge acc;
   ge_identity(acc);
 #pragma unroll 1
@@ -207,7 +231,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const ge_ni
 #endif
       for (int t = 0; t < 4; ++t) ge_dbl(acc, acc, t == 3);
     }
-    const int nslots = ((j & 1) == 0 && j < 32) ? 4 : 2;
+    const int nslots = (j % WPB == 0 && j < 32) ? 4 : 2;
 #pragma unroll 1
     for (int slot = 0; slot < nslots; ++slot) {
       int d;
@@ -218,8 +242,10 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const ge_ni
         d = j < 40 ? digit4_of(vd, 5, j) : 0;
         if (h.vneg) d = -d;
       } else {
-        const int m = j >> 1;   // 8-bit window m of w0 (word m / 4) and of w1 (word 4 + m / 4)
-        d = (int)((sel8(wd, (slot == 2 ? 0 : 4) + (m >> 2)) >> ((m & 3) * 8)) & 255u) - 128;
+        // BW-bit window m of w0 (word m / DPW) and of w1 (word 4 + m / DPW)
+        const int m = j / WPB;
+        d = (int)((sel8(wd, (slot == 2 ? 0 : 4) + m / DPW) >> ((m % DPW) * BW)) & BMASK) -
+            BHALF;
       }
       if (d != 0) {
         const int ad = d < 0 ? -d : d;
@@ -229,10 +255,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const ge_ni
         } else if (slot < 2) {
           e = (slot == 0 ? tabA : tabR)[ad - 1];
         } else {
-          const ge_niels& nb = (slot == 2 ? s_btab : s_b128)[ad];
-          fe_copy(e.YpX, nb.ypx);
-          fe_copy(e.YmX, nb.ymx);
-          fe_copy(e.T2d, nb.xy2d);
+          bt(slot - 2, ad, e);
         }
         ge_cached_cneg(e, d < 0);
         ge_add_any(acc, acc, e, slot >= 2, NW_LAST_T || slot != nslots - 1);

@@ -50,6 +50,8 @@ MUL_PAIRS = {
     "dbl X3 = E*F": (S_L, P15),
     "dbl T3 = E*H": (S_L, L),
     "dbl Z3 = F*G": (P15, T),
+    "dbl Z3 = G*F (shared second operand F)": (T, P15),
+    "add Z3 = g*f (shared second operand f)": (L, T),
     "generic": (T, T),
 }
 SQ_INPUTS = {"X, Y, Z": T, "X+Y": L}

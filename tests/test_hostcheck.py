@@ -141,11 +141,38 @@ def test_half_split_lattice(hc):
         assert (u - v * k) % n == 0 and v % 2 == 1 and 0 <= u < 2**253, k
 
 
-def test_strict_half_edge_corpus(hc, golden):
+@pytest.mark.parametrize("bw", [16, 8])
+def test_strict_half_edge_corpus(hc, golden, bw):
     for it in golden["edge_corpus"]["items"]:
         m, pk, sig = (bytes.fromhex(it[k]) for k in ("msg", "pk", "sig"))
         k = O.hram(sig[:32], pk, m)
-        assert hc.hc_verify_strict_half(_b(pk), _b(sig), _b(k)) == it["status"], it["class"]
+        assert hc.hc_verify_strict_half(_b(pk), _b(sig), _b(k), bw) == it["status"], it["class"]
+
+
+P25519 = 2**255 - 19
+
+
+def _limbs_to_int(limbs):
+    """Value of 10 radix-2^25.5 limbs (limb i at bit ceil(25.5 i))."""
+    return sum(int(x) << ((51 * i + 1) // 2) for i, x in enumerate(limbs))
+
+
+def test_wide_btab_entries(hc):
+    """The strict kernel's wide B tables (nw_consts.hpp compute_wide_btab, 16-bit windows):
+    entry j of half h is j * 2^(128 h) * B in affine niels form, against the oracle."""
+    rng = np.random.Generator(np.random.PCG64(13))
+    js = [0, 1, 2, 3, 127, 128, 129, 32767, 32768] + [int(x) for x in rng.integers(0, 32769, 24)]
+    out = (ctypes.c_uint32 * 30)()
+    inv2 = pow(2, P25519 - 2, P25519)
+    for h in (0, 1):
+        for j in js:
+            hc.hc_wide_btab_entry(h, j, out)
+            ypx, ymx, xy2d = (_limbs_to_int(out[10 * c:10 * c + 10]) % P25519 for c in range(3))
+            y = (ypx + ymx) * inv2 % P25519
+            x = (ypx - ymx) * inv2 % P25519
+            enc = (y | ((x & 1) << 255)).to_bytes(32, "little")
+            s = (j << (128 * h)) % L
+            assert enc == O.scalarmult_base(s.to_bytes(32, "little")), (h, j)
 
 
 def test_strict_half_random_and_tampered(hc):
@@ -160,5 +187,6 @@ def test_strict_half_random_and_tampered(hc):
         elif i % 3 == 2:
             sig[int(rng.integers(0, 32))] ^= 1 << int(rng.integers(0, 8))
         k = O.hram(bytes(sig[:32]), pk, m)
-        assert hc.hc_verify_strict_half(_b(pk), _b(bytes(sig)), _b(k)) == \
-            O.verify_strict(m, pk, bytes(sig))
+        want = O.verify_strict(m, pk, bytes(sig))
+        for bw in (16, 8):
+            assert hc.hc_verify_strict_half(_b(pk), _b(bytes(sig)), _b(k), bw) == want

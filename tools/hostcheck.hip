@@ -12,11 +12,15 @@ static curve_consts K;
 static ge_niels BT[129];
 static strict_consts SK;
 static ge_niels B128[129];
+static ge_niels_pad* BTW = nullptr;   // 16-bit-window tables (the kernel's default)
+static const uint32_t BTW_N = (1u << 15) + 1;
 static bool ready = false;
 static void init() {
   if (!ready) {
     compute_consts(K, BT);
     compute_strict_consts(SK, B128);
+    BTW = new ge_niels_pad[2 * BTW_N];
+    compute_wide_btab(BTW, 16);
     ready = true;
   }
 }
@@ -115,15 +119,25 @@ int hc_half_split(const uint8_t k32[32], uint8_t u32[32], uint8_t v20[20]) {
   return h.vneg ? 1 : 0;
 }
 
-// The kernel's strict verification (nw_strict.hpp), k supplied (device-only SHA).
-int hc_verify_strict_half(const uint8_t pk[32], const uint8_t sig[64], const uint8_t k32[32]) {
+// The kernel's strict verification (nw_strict.hpp), k supplied (device-only SHA), with
+// B windows of bw = 16 bits (wide global tables, the default build) or 8 bits (LDS tables).
+int hc_verify_strict_half(const uint8_t pk[32], const uint8_t sig[64], const uint8_t k32[32],
+                          int bw) {
   init();
   uint32_t Aw[8], Rw[8], Sw[8];
   load8(Aw, pk); load8(Rw, sig); load8(Sw, sig + 32);
   uint32_t kw[8]; load8(kw, k32);
   ge_cached ta[8], tr[8];
   const strict_src_arrays src{Aw, Rw, Sw, kw};
-  return strict_verify_core(src, SK, BT, B128, ta, tr, [](int w) { return w; });
+  auto id = [](int w) { return w; };
+  if (bw == 8) return strict_verify_core<8>(src, SK, btab_pair{BT, B128}, ta, tr, id);
+  return strict_verify_core<16>(src, SK, btab_wide{BTW, BTW_N}, ta, tr, id);
+}
+
+// Entry j of the wide B table half h (ypx || ymx || xy2d as 30 limbs), for the table test.
+void hc_wide_btab_entry(int h, uint32_t j, uint32_t out[30]) {
+  init();
+  memcpy(out, &BTW[(h ? BTW_N : 0u) + j].n, 120);
 }
 
 }
