@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--unique", type=int, default=1 << 18)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--all-valid", action="store_true",
+                    help="tile only the corpus's valid items (no early-decided statuses)")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -55,7 +57,12 @@ def main():
     assert _lib.lib().nw_init() > 0
     m_u, p_u, s_u, valid = bench.build_strict_corpus(dev, stream, a.unique, 4096, seed=1000)
     n = a.items
-    idx = torch.arange(n, dtype=torch.int64, device=dev) % a.unique
+    if a.all_valid:
+        good = torch.from_numpy(np.nonzero(valid)[0]).to(dev)
+        idx = good[torch.arange(n, dtype=torch.int64, device=dev) % good.numel()]
+        valid = np.ones(good.numel(), dtype=bool)
+    else:
+        idx = torch.arange(n, dtype=torch.int64, device=dev) % a.unique
     m, p, s = (t.index_select(0, idx).contiguous() for t in (m_u, p_u, s_u))
     del idx
     exp = np.resize(valid, n)
