@@ -251,6 +251,81 @@ NW_HD void bn_addmul(uint32_t* r, const uint32_t* a, const uint32_t* b, uint32_t
   }
 }
 
+// floor(x / 2^s) mod 2^52 for a 256-bit x (8 LE words), 0 <= s <= 204, as an exact double.
+NW_HD double bn8_bits52(const uint32_t x[8], int s) {
+  const int wi = s >> 5, b = s & 31;
+  uint32_t w0 = 0, w1 = 0, w2 = 0;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    w0 = t == wi ? x[t] : w0;
+    w1 = t == wi + 1 ? x[t] : w1;
+    w2 = t == wi + 2 ? x[t] : w2;
+  }
+  const uint64_t lo = (((uint64_t)w1 << 32) | w0) >> b;
+  const uint64_t hi = b ? ((uint64_t)w2 << (64 - b)) : 0ull;
+  return (double)((lo | hi) & ((1ull << 52) - 1));
+}
+
+// floor(a / b) for integers 0 <= a < 2^53, 0 < b < 2^53 held exactly in doubles.
+NW_HD double f64_floor_div(double a, double b) {
+  double q = floor(a / b);
+  if (fma(-q, b, a) < 0.0) q -= 1.0;   // a / b rounded up to an integer
+  return q;
+}
+
+// r = |pa x - pb y| for 8-word x, y and 32-bit pa, pb (the true difference fits 256 bits).
+NW_HD void bn8_absdiff_mul(uint32_t r[8], const uint32_t x[8], uint32_t pa, const uint32_t y[8],
+                           uint32_t pb) {
+  uint64_t c1 = 0, c2 = 0, borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint64_t p1 = (uint64_t)pa * x[i] + c1;
+    const uint64_t p2 = (uint64_t)pb * y[i] + c2;
+    c1 = p1 >> 32;
+    c2 = p2 >> 32;
+    const uint64_t d = (uint64_t)(uint32_t)p1 - (uint32_t)p2 - borrow;
+    r[i] = (uint32_t)d;
+    borrow = (d >> 63) & 1;
+  }
+  // sign of the 9-word difference: (c1 - c2 - borrow) < 0
+  if ((int64_t)(c1 - c2 - borrow) < 0) {   // negative: two's-complement negation
+    uint64_t c = 1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      c += (uint64_t)(uint32_t)~r[i];
+      r[i] = (uint32_t)c;
+      c >>= 32;
+    }
+  }
+}
+
+// r = pa x + pb y for 5-word x, y (the sum fits 160 bits).
+NW_HD void bn5_addmul2(uint32_t r[5], const uint32_t x[5], uint32_t pa, const uint32_t y[5],
+                       uint32_t pb) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const uint64_t p1 = (uint64_t)pa * x[i];
+    const uint64_t p2 = (uint64_t)pb * y[i];
+    const uint64_t s = (p1 & 0xffffffffull) + (p2 & 0xffffffffull) + (c & 0xffffffffull);
+    r[i] = (uint32_t)s;
+    c = (p1 >> 32) + (p2 >> 32) + (c >> 32) + (s >> 32);
+  }
+}
+
+#ifndef NW_SPLIT_LEHMER
+#define NW_SPLIT_LEHMER 1
+#endif
+
+// Any lane of the wave (device) / this thread (host).
+NW_HD bool nw_any(bool p) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __ballot(p) != 0;
+#else
+  return p;
+#endif
+}
+
 NW_HD void sc_half_split(sc_half& out, const sc& k) {
   uint32_t xr[8], yr[8], xt[5], yt[5];
 #pragma unroll
@@ -262,6 +337,54 @@ NW_HD void sc_half_split(sc_half& out, const sc& k) {
   for (int it = 0; it < 400; ++it) {
     done = (yr[4] | yr[5] | yr[6] | yr[7]) == 0;
     if (done) break;
+#if NW_SPLIT_LEHMER
+    // Lehmer round (Knuth, TAOCP 4.5.2 Algorithm L): Euclid on the leading 52 bits of
+    // (xr, yr) in exact double arithmetic with cofactors A B / C D, each quotient accepted
+    // only when both bracketing quotients agree (so it equals the full numbers' quotient),
+    // and only while the remainder stays above 2^129 (the loop must stop at the FIRST
+    // remainder below 2^128, as the one-step loop does); then one multi-word update
+    // (xr, yr) <- (|A xr - B yr|, |C xr - D yr|), (xt, yt) <- (|A| xt + |B| yt, ...).
+    {
+      const int bx = bn_bits(xr, 8);   // > 128 here
+      const int sh = bx - 52;
+      double x = bn8_bits52(xr, sh), y = bn8_bits52(yr, sh);
+      const int le = 130 - sh > 28 ? 130 - sh : 28;
+      const double lim = ldexp(1.0, le);
+      double A = 1.0, B = 0.0, C = 0.0, D = 1.0;
+      int j = 0;
+#pragma unroll 1
+      for (int st = 0; st < 64; ++st) {
+        const double yc = y + C, yd = y + D;
+        if (!(yc > 0.0) || !(yd > 0.0)) break;
+        const double q = f64_floor_div(x + A, yc);
+        if (q != f64_floor_div(x + B, yd)) break;
+        const double r = fma(-q, y, x);
+        const double nC = fma(-q, C, A), nD = fma(-q, D, B);
+        if (r < lim || fabs(nC) >= 2147483648.0 || fabs(nD) >= 2147483648.0) break;
+        A = C; B = D; C = nC; D = nD; x = y; y = r;
+        ++j;
+      }
+      // Lanes that made Lehmer progress update; the one-step code below runs only in an
+      // iteration where no lane of the wave could (SIMT: the wave would execute both).
+      const bool any_progress = nw_any(j > 0);
+      if (any_progress) {
+        if (j == 0) continue;
+        const uint32_t a = (uint32_t)fabs(A), b = (uint32_t)fabs(B);
+        const uint32_t c = (uint32_t)fabs(C), d = (uint32_t)fabs(D);
+        uint32_t nx[8], ny[8], nxt[5], nyt[5];
+        bn8_absdiff_mul(nx, xr, a, yr, b);
+        bn8_absdiff_mul(ny, xr, c, yr, d);
+        bn5_addmul2(nxt, xt, a, yt, b);
+        bn5_addmul2(nyt, xt, c, yt, d);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { xr[i] = nx[i]; yr[i] = ny[i]; }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) { xt[i] = nxt[i]; yt[i] = nyt[i]; }
+        yneg = (j & 1) ? !yneg : yneg;
+        continue;
+      }
+    }
+#endif
     // q <= floor(xr / yr): relative error of the f64 quotient < 2^-49.
     const double qd = floor(bn8_to_f64(xr) / bn8_to_f64(yr) * (1.0 - 0x1p-46));
     const uint32_t q = qd >= 4294967295.0 ? 0xffffffffu : (qd < 1.0 ? 1u : (uint32_t)qd);
