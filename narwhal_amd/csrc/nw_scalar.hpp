@@ -326,6 +326,7 @@ NW_HD bool nw_any(bool p) {
 #endif
 }
 
+template <bool LEHMER = NW_SPLIT_LEHMER != 0>
 NW_HD void sc_half_split(sc_half& out, const sc& k) {
   uint32_t xr[8], yr[8], xt[5], yt[5];
 #pragma unroll
@@ -337,7 +338,7 @@ NW_HD void sc_half_split(sc_half& out, const sc& k) {
   for (int it = 0; it < 400; ++it) {
     done = (yr[4] | yr[5] | yr[6] | yr[7]) == 0;
     if (done) break;
-#if NW_SPLIT_LEHMER
+    if (LEHMER) {
     // Lehmer round (Knuth, TAOCP 4.5.2 Algorithm L): Euclid on the leading 52 bits of
     // (xr, yr) in exact double arithmetic with cofactors A B / C D, each quotient accepted
     // only when both bracketing quotients agree (so it equals the full numbers' quotient),
@@ -384,7 +385,7 @@ NW_HD void sc_half_split(sc_half& out, const sc& k) {
         continue;
       }
     }
-#endif
+    }
     // q <= floor(xr / yr): relative error of the f64 quotient < 2^-49.
     const double qd = floor(bn8_to_f64(xr) / bn8_to_f64(yr) * (1.0 - 0x1p-46));
     const uint32_t q = qd >= 4294967295.0 ? 0xffffffffu : (qd < 1.0 ? 1u : (uint32_t)qd);

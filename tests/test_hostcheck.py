@@ -141,6 +141,20 @@ def test_half_split_lattice(hc):
         assert (u - v * k) % n == 0 and v % 2 == 1 and 0 <= u < 2**253, k
 
 
+def test_half_split_lehmer_equals_one_step(hc):
+    """The Lehmer rounds (Knuth Algorithm L, nw_scalar.hpp) only batch exact Euclid steps:
+    the split equals the one-step loop's on random and adversarial k."""
+    rng = np.random.Generator(np.random.PCG64(14))
+    ks = [int.from_bytes(rng.bytes(32), "little") % L_ORDER for _ in range(4000)]
+    ks += _adversarial_k() + [2**129 + 5, 3 * 2**127, 2**200 + 1, (8 * L_ORDER) // 3 % L_ORDER]
+    for k in ks:
+        outs = []
+        for f in (hc.hc_half_split, hc.hc_half_split_onestep):
+            u, v = _out(32), _out(20)
+            outs.append((f(_b(k.to_bytes(32, "little")), u, v), u.raw, v.raw))
+        assert outs[0] == outs[1], k
+
+
 @pytest.mark.parametrize("bw", [16, 8])
 def test_strict_half_edge_corpus(hc, golden, bw):
     for it in golden["edge_corpus"]["items"]:

@@ -119,6 +119,14 @@ int hc_half_split(const uint8_t k32[32], uint8_t u32[32], uint8_t v20[20]) {
   return h.vneg ? 1 : 0;
 }
 
+// The same split by single Euclid steps only (the reference for the Lehmer rounds).
+int hc_half_split_onestep(const uint8_t k32[32], uint8_t u32[32], uint8_t v20[20]) {
+  sc k; load8(k.w, k32);
+  sc_half h; sc_half_split<false>(h, k);
+  memcpy(u32, h.u, 32); memcpy(v20, h.v, 20);
+  return h.vneg ? 1 : 0;
+}
+
 // The kernel's strict verification (nw_strict.hpp), k supplied (device-only SHA), with
 // B windows of bw = 16 bits (wide global tables, the default build) or 8 bits (LDS tables).
 int hc_verify_strict_half(const uint8_t pk[32], const uint8_t sig[64], const uint8_t k32[32],
