@@ -88,15 +88,15 @@ def pmc_traffic(kernel: str, units: int):
 
 def pmc_issue_peak():
     """Issue-bound peak of k_verify_strict (verifies/s) from its committed PMC instruction mix
-    (profiles/r02a/pmc_mix.json, tools/pmc_mix.sh): per-verify 64-bit / 32-bit integer and
+    (profiles/r02c/pmc_mix.json, tools/pmc_mix.sh): per-verify 64-bit / 32-bit integer and
     other VALU lane-ops, each priced at its microbenchmarked issue rate
     (profiles/r01_ubench_valu_4wps.txt; 32-bit integer ops at the half rate, an upper bound
     on their cost). None when the profile is absent."""
     try:
-        m = json.load(open(os.path.join(ROOT, "profiles", "r02a", "pmc_mix.json")))
+        m = json.load(open(os.path.join(ROOT, "profiles", "r02c", "pmc_mix.json")))
     except (OSError, ValueError):
         return None, None
-    return m["issue_peak_verifies_per_s"], "profiles/r02a/pmc_mix.json"
+    return m["issue_peak_verifies_per_s"], "profiles/r02c/pmc_mix.json"
 
 
 def enc_y(y: int, sign: int) -> bytes:
@@ -530,20 +530,40 @@ def run_batch10k(args, dev, stream, rank, world):
     d_dig = torch.from_numpy(digest).to(dev).repeat(nb).contiguous()
     d_off = torch.arange(nb + 1, dtype=torch.int64, device=dev) * n
     host_off = np.arange(nb + 1, dtype=np.uint64) * n
+    # a quarter of the resident batches carry one bad vote: every 8th (from 3) a flipped bit in
+    # s (equation failure: status 7, index n), every 8th (from 6) s with a high bit set
+    # (Signature::from_bytes failure: status 1 at that vote's index)
+    exp_st = np.zeros(nb, np.int32)
+    exp_ix = np.zeros(nb, np.int64)
+    for b in range(nb):
+        if b % 8 == 3:
+            j = (b * 997) % n
+            d_sig[b * n + j, 32] ^= 1
+            exp_st[b], exp_ix[b] = 7, n
+        elif b % 8 == 6:
+            j = (b * 1237) % n
+            d_sig[b * n + j, 63] |= 0x80
+            exp_st[b], exp_ix[b] = 1, j
     ws = torch.empty(L.nw_dev_verify_batch_workspace(nb, nb * n), dtype=torch.uint8, device=dev)
     d_st = torch.empty(nb, dtype=torch.int32, device=dev)
+    d_fi = torch.empty(nb, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
 
     def launch():
         check(L.nw_dev_verify_batch_many(ptr(d_dig), ptr(d_pk), ptr(d_sig), ptr(d_off),
                                          host_off.ctypes.data_as(ctypes.c_void_p), nb,
-                                         nb * n, None, None, ptr(ws), ptr(d_st), None, stream),
+                                         nb * n, None, None, ptr(ws), ptr(d_st), ptr(d_fi),
+                                         stream),
               "verify_batch_many")
     elapsed, kernel_ms = timed_steps(launch, args.steps, 1, world)
-    ok &= bool((d_st == 0).all().item())
+    ok &= bool(np.array_equal(d_st.cpu().numpy(), exp_st) and
+               np.array_equal(d_fi.cpu().numpy()[exp_st != 0], exp_ix[exp_st != 0]))
     sec = elapsed / args.steps
     res = {"items": n, "latency_ms": lat * 1e3, "verifies_per_s_one_call": n / lat,
            "batches_resident": nb, "verifies_per_s_resident": nb * n * world / sec,
+           "resident_invalid_batches": int((exp_st != 0).sum()),
+           "parity_check": "one-call: valid Ok, Signature::default() Err; resident: status of "
+                           "every batch and index of every failing one == construction",
            "achieved_TMAC_s": nb * n * MAC_PER_BATCH_ITEM_LARGE / (kernel_ms * 1e-3) / 1e12,
            "work_per_item": f"{MAC_PER_BATCH_ITEM_LARGE} MAC (SURVEY 8d, n >= 10k)",
            "parity": "ok" if ok else "FAIL"}
@@ -564,16 +584,20 @@ def run_wire(args, dev, stream, rank, world, N: int = 4):
     s = W.certificate_stream(n, keys, lambda sk, m: C.sign_many(sk, m),
                              lambda d, o: C.sha512_digest32_many(d, o[:-1], np.diff(o)),
                              seed=100 + rank)
+    # 1 % of the certificates carry one invalid vote (as the config-2 invalid leg)
+    s, exp_st, exp_ix = W.mutate_votes(s, np.arange(50, n, 100), seed=N + 7)
     data, offs = WI.frames_from_stream(s)
     com = M.committee_struct(s["committee"])
     kind = np.zeros(n, np.int32)
     st = np.zeros(n, np.int32)
+    ix = np.zeros(n, np.uint64)
 
     def call():
         check(L.nw_primary_messages_verify_wire(ctypes.byref(com), M._p(data), M._p(offs), n,
-                                                M._p(kind), M._p(st), None), "wire")
+                                                M._p(kind), M._p(st), M._p(ix)), "wire")
     call()
-    ok = bool((st == 0).all() and (kind == WI.MSG_CERTIFICATE).all())
+    ok = bool(np.array_equal(st, exp_st) and np.array_equal(ix, exp_ix) and
+              (kind == WI.MSG_CERTIFICATE).all())
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -586,7 +610,9 @@ def run_wire(args, dev, stream, rank, world, N: int = 4):
     return {"committee": N, "frames_per_call": n, "frame_bytes": int(offs[-1]),
             "certs_per_s": n * world / sec, "ms_per_call": sec * 1e3,
             "path": "host frames -> nw_primary_messages_verify_wire (decode + H2D + kernels + D2H)",
-            "parity": "ok" if ok else "FAIL"}
+            "invalid_fraction": float((exp_st != 0).mean()),
+            "parity": "ok" if ok else "FAIL",
+            "parity_check": "status and index of every frame's certificate == construction"}
 
 
 def cpu_baseline_batch(sample, seconds: float):
