@@ -99,6 +99,29 @@ def pmc_issue_peak():
     return m["issue_peak_verifies_per_s"], "profiles/r02c/pmc_mix.json"
 
 
+# One wave per SIMD (config 3: 65,536 messages = 1,024 waves): a lone wave issues one VALU
+# instruction per 4 cycles whatever its rate (MI355X_MICROARCH.md, "one wave alone: 4"), so
+# 1,024 SIMDs x 64 lanes / 4 cycles x 2.4 GHz = 39.3 T lane-ops/s; the dependent-chain
+# microbenchmark at one wave per SIMD measured 27-30 T (profiles/r01_ubench_valu_1wps.txt:
+# alignbit 29.9, bitop3 28.9, lshl_add_u64 27.2 - the SHA-512 kernel's three main ops).
+PEAK_TOPS_ONE_WAVE = 256 * 4 * 64 / 4 * 2.4e9 / 1e12
+UBENCH_TOPS_ONE_WAVE = (29.85 + 28.94 + 27.17) / 3
+
+
+def pmc_sha_valu(units: int):
+    """VALU lane-ops of one config-3 k_sha512_digest32 launch from the committed PMC pass
+    (SQ_INSTS_VALU x 64, profiles/<tag>/pmc.json via profiles/traffic.json), scaled to
+    `units` messages. None when absent."""
+    try:
+        src = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))[
+            "k_sha512_digest32"]["source"]
+        d = json.load(open(os.path.join(ROOT, src)))
+        e = next(v for k, v in d.items() if k.startswith("k_sha512_digest32@grid65536"))
+        return e["SQ_INSTS_VALU"] * 64 * units / 65536, src
+    except (OSError, KeyError, ValueError, StopIteration):
+        return None, None
+
+
 def enc_y(y: int, sign: int) -> bytes:
     b = bytearray(y.to_bytes(32, "little"))
     b[31] |= sign << 7
@@ -774,10 +797,21 @@ def main():
                                 "GB_per_s": gbs, "kernel_GB_per_s": kgbs,
                                 "hbm_frac": kgbs / PEAK_HBM_GBS,
                                 "valu_Tops": tops, "valu_frac": tops / PEAK_TOPS_FULL,
+                                "valu_note": "valu_* use SURVEY's 4,800 ops/block against the "
+                                             "full-rate peak; issue_* use the kernel's PMC "
+                                             "VALU count against one wave per SIMD's rate",
                                 "kernel_ms": s["kernel_ms"],
                                 "traffic": straffic, "traffic_source": ssrc,
                                 "algorithmic_bytes": s["bytes"] + 32 * s["n"],
                                 "parity": "ok" if s["parity"] else "FAIL"}
+            lops, lsrc = pmc_sha_valu(s["n"])
+            if lops:
+                iss = lops / (s["kernel_ms"] * 1e-3) / 1e12
+                result["sha512"].update({"issue_Tops": iss, "issue_peak_Tops": PEAK_TOPS_ONE_WAVE,
+                                         "issue_frac": iss / PEAK_TOPS_ONE_WAVE,
+                                         "issue_ubench_one_wave_Tops": UBENCH_TOPS_ONE_WAVE,
+                                         "issue_source": f"{lsrc} (SQ_INSTS_VALU) / "
+                                                         "profiles/r01_ubench_valu_1wps.txt"})
             if rank == 0 and world == 1 and not args.no_cpu_baseline:
                 result["sha512"]["cpu_baseline"] = cpu_baseline_sha(s["sample"],
                                                                     min(3.0, args.cpu_seconds))
