@@ -4,8 +4,10 @@
 //                         (worker/src/processor.rs:38, primary/src/messages.rs:70-84 ...).
 //   k_verify_strict       crypto::Signature::verify (crypto/src/lib.rs:200-204), one lane per
 //                         signature: decompress A and R, small-order tests, k = H(R||A||M)
-//                         mod l, [s]B + [k](-A) by a joint signed-window ladder (A table in
-//                         per-lane scratch, 8-bit B table in LDS), projective compare with R.
+//                         mod l, half-size scalars, [v]R + [u]A + [w]B == 0 by one joint
+//                         signed-window ladder (A and R tables in per-lane scratch, w in
+//                         24-bit windows over device-built global tables), identity test.
+//   k_btab_build          the strict kernel's B tables, once per device.
 //   (crypto::Signature::verify_batch lives in nw_batch.hip.)
 //
 // Everything here is integer VALU work; no MFMA (modular arithmetic is not a contraction).
@@ -19,7 +21,6 @@
 #include <algorithm>
 #include <atomic>
 #include <mutex>
-#include <vector>
 
 namespace nw {
 
@@ -250,7 +251,7 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
   const btab_pair bt{s_btab, s_b128};
   (void)btw;
 #else
-  const btab_wide bt{btw, (1u << (NW_BWIN - 1)) + 1};
+  const btab_wide bt{btw, bdigits<NW_BWIN>::ENTRIES};
 #endif
   ge_cached* tabA = tabs + 16 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
   ge_cached* tabR = tabA + 8;
@@ -388,53 +389,84 @@ __global__ __launch_bounds__(256) void k_sign(const uint32_t* __restrict__ sks,
 
 }  // namespace nw
 
+namespace nw {
+// The strict kernel's wide B tables, built on the device once per process and device:
+// out[h * n + j] = j * 2^(128 h) * B (h = 0, 1; j = 0..n-1) in padded affine niels form, one
+// lane per entry: fixed-base product over the 8-bit LDS table, then one inversion.
+__global__ __launch_bounds__(256) void k_btab_build(ge_niels_pad* __restrict__ out, uint32_t n) {
+  __shared__ ge_niels s_btab[129];
+  load_btab(s_btab);
+  __syncthreads();
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= 2ull * n) return;
+  const uint32_t h = g >= n ? 1u : 0u, j = (uint32_t)(g - (uint64_t)h * n);
+  sc s;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s.w[i] = 0;
+  s.w[h ? 4 : 0] = j;
+  ge P;
+  fixed_base_mul(P, s, s_btab);
+  ge_niels nb;
+  ge_to_niels(nb, P, g_consts.k.d2);
+  out[g].n = nb;
+  out[g].pad[0] = out[g].pad[1] = 0;
+}
+}  // namespace nw
+
 // ---------------------------------------------------------------------------------------
 // Host side: constants and launchers
 // ---------------------------------------------------------------------------------------
 namespace nw {
 
-// The strict kernel's wide B tables (nw_consts.hpp compute_wide_btab), one copy per device,
-// indexed by HIP device id; built on the host once per process, uploaded by upload_consts.
+// The strict kernel's wide B tables (k_btab_build), one copy per device, indexed by HIP
+// device id, built on the device the first time a strict launch needs them there (24-bit
+// windows: 2 x 8,388,609 entries = 2.15 GB and ~0.2 s per device; lazily, so a process
+// that initialises every device but verifies on one builds one table).
 static constexpr int kMaxDevIds = 64;
-static ge_niels_pad* g_btw[kMaxDevIds];
-static constexpr size_t kBtwEntries = 2 * ((size_t(1) << (NW_BWIN - 1)) + 1);
+static std::atomic<ge_niels_pad*> g_btw[kMaxDevIds];
+static std::mutex g_btw_mu;
+static constexpr uint32_t kBtwPerHalf = bdigits<NW_BWIN>::ENTRIES;
 
-static const ge_niels_pad* btw_for_current_device() {
+static hipError_t btw_for_current_device(const ge_niels_pad** out) {
+  *out = nullptr;
+  if (NW_BWIN == 8) return hipSuccess;
   int dev = 0;
-  (void)hipGetDevice(&dev);
-  return dev >= 0 && dev < kMaxDevIds ? g_btw[dev] : nullptr;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= kMaxDevIds) return hipErrorInvalidDevice;
+  if ((*out = g_btw[dev].load(std::memory_order_acquire))) return hipSuccess;
+  std::lock_guard<std::mutex> lock(g_btw_mu);
+  if ((*out = g_btw[dev].load(std::memory_order_relaxed))) return hipSuccess;
+  void* p = nullptr;
+  const uint64_t entries = 2ull * kBtwPerHalf;
+  e = hipMalloc(&p, entries * sizeof(ge_niels_pad));
+  if (e != hipSuccess) return e;
+  hipStream_t s = nullptr;
+  e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_btab_build, dim3((unsigned)((entries + 255) / 256)), dim3(256), 0, s,
+                       static_cast<ge_niels_pad*>(p), kBtwPerHalf);
+    e = hipGetLastError();
+    const hipError_t e2 = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = e2;
+    (void)hipStreamDestroy(s);
+  }
+  if (e != hipSuccess) { (void)hipFree(p); return e; }
+  g_btw[dev].store(static_cast<ge_niels_pad*>(p), std::memory_order_release);
+  *out = static_cast<ge_niels_pad*>(p);
+  return hipSuccess;
 }
 
 hipError_t upload_consts() {
   static dev_consts host;
-  static std::vector<ge_niels_pad> btw;
   static std::once_flag once;
   std::call_once(once, [] {
     compute_consts(host.k, host.btab);
     compute_strict_consts(host.sk, host.b128);
-#if NW_BWIN != 8
-    btw.resize(kBtwEntries);
-    compute_wide_btab(btw.data(), NW_BWIN);
-#endif
   });
   hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_consts), &host, sizeof(host), 0,
                                    hipMemcpyHostToDevice);
-  if (e != hipSuccess) return e;
-#if NW_BWIN != 8
-  int dev = 0;
-  e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  if (dev < 0 || dev >= kMaxDevIds) return hipErrorInvalidDevice;
-  if (!g_btw[dev]) {
-    void* p = nullptr;
-    e = hipMalloc(&p, kBtwEntries * sizeof(ge_niels_pad));
-    if (e != hipSuccess) return e;
-    e = hipMemcpy(p, btw.data(), kBtwEntries * sizeof(ge_niels_pad), hipMemcpyHostToDevice);
-    if (e != hipSuccess) { (void)hipFree(p); return e; }
-    g_btw[dev] = static_cast<ge_niels_pad*>(p);
-  }
-#endif
-  return upload_batch_consts();
+  return e != hipSuccess ? e : upload_batch_consts();
 }
 
 static inline unsigned grid_for(uint64_t n, unsigned block) {
@@ -481,8 +513,9 @@ hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
   if (n == 0) return hipSuccess;
   const unsigned grid = std::min<uint64_t>(strict_grid(), grid_for(n, 256));
   const key_tables_t kt = keys ? *keys : key_tables_t{nullptr, nullptr, nullptr};
-  const ge_niels_pad* btw = btw_for_current_device();
-  if (NW_BWIN != 8 && !btw) return hipErrorNotInitialized;
+  const ge_niels_pad* btw = nullptr;
+  const hipError_t eb = btw_for_current_device(&btw);
+  if (eb != hipSuccess) return eb;
   hipLaunchKernelGGL(k_verify_strict, dim3(grid), dim3(256), 0, stream, msgs, msg_stride_words,
                      pks, sigs, n, status, bitmap, static_cast<ge_cached*>(workspace), kt, btw);
   return hipGetLastError();

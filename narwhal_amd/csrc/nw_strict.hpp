@@ -11,15 +11,15 @@
 //      w = -v s mod l; then  R + [k]A - [s]B == 0  <=>  [v]R + [u]A + [w]B == 0.
 //   4. One ladder of ~128 doublings: signed 4-bit windows over u (table j*A) and |v|
 //      (table j*R, digits negated when v < 0), per-lane tables in private memory;
-//      w = w0 + 2^128 w1 by signed NW_BWIN-bit windows over two affine tables (j*B and
-//      j*2^128 B): 16-bit windows over 2 x 32,769 entries in global memory (8.4 MB, L2 /
-//      MALL resident; 16 B additions per verify), or 8-bit windows over 2 x 129 entries
-//      in LDS (32 B additions; NW_BWIN=8).
+//      w by signed NW_BWIN-bit windows over two affine tables (j*B and j*2^128 B, bdigits
+//      below): 16-bit windows over 2 x 32,769 entries in global memory (8.4 MB; 16 B
+//      additions per verify), 20-bit (2 x 524,289, 134 MB; 13 additions), 24-bit
+//      (2 x 8,388,609, 2.1 GB; 11 additions), or 8-bit over 2 x 129 entries in LDS (32).
 #pragma once
 #include "narwhal_amd.h"
 
 #ifndef NW_BWIN
-#define NW_BWIN 16
+#define NW_BWIN 24
 #endif
 
 #ifndef NW_TAB_RELOAD
@@ -150,7 +150,8 @@ struct strict_src_arrays {
 
 // The B term's tables: entry ad of j * 2^(128 h) * B (h = 0, 1) into e's YpX / YmX / T2d.
 // btab_pair: two 129-entry arrays (8-bit windows, LDS); btab_wide: one array of 2 x n
-// padded entries (16-bit windows, global memory, nw_consts.hpp compute_wide_btab).
+// padded entries (BW >= 16, global memory: k_btab_build on the device; the host self-check
+// builds the 16-bit one with nw_consts.hpp compute_wide_btab).
 struct btab_pair {
   const ge_niels* t0;
   const ge_niels* t1;
@@ -172,6 +173,65 @@ struct btab_wide {
   }
 };
 
+// Signed BW-bit digits of w (< 2^253) for the B term: NB = ceil(253 / BW) digits, digit m at
+// bit BW m. All are signed (bias 2^(BW-1)) except, when NB * BW > 256, the top one: it is
+// taken unsigned (< 2^13 + 2), so the biased sum still fits 256 bits. Digits below bit 128
+// use table 0 (j * B) at ladder window BW m / 4; the others table 1 (j * 2^128 B) at window
+// (BW m - 128) / 4 — every position is a multiple of 4 for BW in {8, 16, 20, 24}.
+template <int BW>
+struct bdigits {
+  static_assert(BW == 8 || BW == 16 || BW == 20 || BW == 24, "B windows of 8/16/20/24 bits");
+  static constexpr int NB = (253 + BW - 1) / BW;
+  static constexpr bool TOP_UNSIGNED = NB * BW > 256;
+  static constexpr int NSIGNED = TOP_UNSIGNED ? NB - 1 : NB;
+  static constexpr uint32_t ENTRIES = (1u << (BW - 1)) + 1;   // |d| <= 2^(BW-1)
+  NW_HD static constexpr uint32_t bias_word(int i) {
+    uint32_t b = 0;
+    for (int m = 0; m < NSIGNED; ++m) {
+      const int p = BW * m + BW - 1;
+      if ((p >> 5) == i) b |= 1u << (p & 31);
+    }
+    return b;
+  }
+  // out = w + sum over signed digits of 2^(BW-1) 2^(BW m)
+  NW_HD static void recode(uint32_t out[8], const sc& w) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      c += (uint64_t)w.w[i] + bias_word(i);
+      out[i] = (uint32_t)c;
+      c >>= 32;
+    }
+  }
+  // digit m (wave-uniform) of the recoded words
+  NW_HD static int digit(const uint32_t wd[8], int m) {
+    const int p = BW * m, wi = p >> 5, sh = p & 31;
+    const uint32_t lo = sel8(wd, wi), hi = wi < 7 ? sel8(wd, wi + 1) : 0u;
+    const uint32_t v = (uint32_t)(((((uint64_t)hi) << 32) | lo) >> sh) & ((1u << BW) - 1);
+    return m < NSIGNED ? (int)v - (1 << (BW - 1)) : (int)v;
+  }
+};
+
+// The B tables computed on demand (host self-check only: fixed-base product + inversion
+// per lookup), for window widths whose tables the host does not hold.
+struct btab_lazy {
+  const ge_niels* btab8;   // j * B, j = 0..128 (fixed_base_mul's table)
+  const fe* d2;
+  NW_HD void operator()(int h, int ad, ge_cached& e) const {
+    sc s;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s.w[i] = 0;
+    s.w[h ? 4 : 0] = (uint32_t)ad;
+    ge P;
+    fixed_base_mul(P, s, btab8);
+    ge_niels nb;
+    ge_to_niels(nb, P, *d2);
+    fe_copy(e.YpX, nb.ypx);
+    fe_copy(e.YmX, nb.ymx);
+    fe_copy(e.T2d, nb.xy2d);
+  }
+};
+
 // Status of one strict verification. wave_max maps this lane's ladder length (in 4-bit
 // windows) to the wave's maximum (identity on the host). tabA/tabR: 8 entries each of
 // per-lane scratch. bt: j*B and j*2^128 B, j = 0..2^(BW-1) (btab_pair / btab_wide).
@@ -183,12 +243,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
                              ge_cached* tabA, ge_cached* tabR,
                              WaveMax wave_max, const ge_cached* keytab = nullptr,
                              uint32_t keyflags = 0) {
-  static_assert(BW == 8 || BW == 16, "B windows of 8 or 16 bits");
-  constexpr int WPB = BW / 4;          // 4-bit ladder windows per B window
-  constexpr int DPW = 32 / BW;         // B digits per 32-bit word
-  constexpr uint32_t BBIAS = BW == 8 ? 0x80808080u : 0x80008000u;
-  constexpr uint32_t BMASK = (1u << BW) - 1;
-  constexpr int BHALF = 1 << (BW - 1);
+  using BD = bdigits<BW>;
   // Decompress A, then R, in one rolled loop (one copy of the sqrt_ratio_i chain in the
   // code object): P, its small-order flag and its 8-entry table j * P. Only the point is
   // live here: the scalars are computed afterwards (register pressure).
@@ -236,7 +291,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
   const uint32_t ubias = keytab ? 0x80808080u : 0x88888888u;
   sc_recode(ud, ur, ubias);
   sc_recode(vd, vr, 0x88888888u);
-  sc_recode(wd, w, BBIAS);
+  BD::recode(wd, w);
   // ladder length in 4-bit windows: up to the highest nonzero signed digit of u and |v|
   // (digit j is nonzero iff nibble j of the recoded word is not 8), at least 32 for the
   // two 128-bit halves of w
@@ -253,7 +308,8 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
 
   // One rolled doubling and one addition routine serve every term (code size: the ladder
   // body stays inside the instruction cache). Per 4-bit window j: 4 doublings, then the
-  // A digit, the R digit and, on j < 32 with j % (BW / 4) == 0, the two BW-bit B digits.
+  // A digit, the R digit and, on j < 32, the B digits at this window (bdigits: at most one
+  // per table).
   ge acc;
   ge_identity(acc);
 #pragma unroll 1
@@ -266,7 +322,10 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
 #endif
       for (int t = 0; t < 4; ++t) ge_dbl(acc, acc, t == 3);
     }
-    const int nslots = (j % WPB == 0 && j < 32) ? 4 : 2;
+    const int p0 = 4 * j, p1 = 4 * j + 128;
+    const bool has0 = j < 32 && p0 % BW == 0;
+    const bool has1 = j < 32 && p1 % BW == 0 && p1 / BW < BD::NB;
+    const int nslots = 2 + (has0 ? 1 : 0) + (has1 ? 1 : 0);
 #pragma unroll 1
     for (int slot = 0; slot < nslots; ++slot) {
       int d;
@@ -277,10 +336,9 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
         d = j < 40 ? digit4_of(vd, 5, j) : 0;
         if (h.vneg) d = -d;
       } else {
-        // BW-bit window m of w0 (word m / DPW) and of w1 (word 4 + m / DPW)
-        const int m = j / WPB;
-        d = (int)((sel8(wd, (slot == 2 ? 0 : 4) + m / DPW) >> ((m % DPW) * BW)) & BMASK) -
-            BHALF;
+        // the table-0 digit first (when present), then the table-1 digit
+        const bool t1 = slot == 3 || !has0;
+        d = BD::digit(wd, t1 ? p1 / BW : p0 / BW);
       }
       if (d != 0) {
         const int ad = d < 0 ? -d : d;
@@ -290,7 +348,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
         } else if (slot < 2) {
           e = (slot == 0 ? tabA : tabR)[ad - 1];
         } else {
-          bt(slot - 2, ad, e);
+          bt((slot == 3 || !has0) ? 1 : 0, ad, e);
         }
         ge_cached_cneg(e, d < 0);
         ge_add_any(acc, acc, e, slot >= 2, NW_LAST_T || slot != nslots - 1);

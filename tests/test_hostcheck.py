@@ -155,7 +155,7 @@ def test_half_split_lehmer_equals_one_step(hc):
         assert outs[0] == outs[1], k
 
 
-@pytest.mark.parametrize("bw", [16, 8])
+@pytest.mark.parametrize("bw", [16, 8, 20, 24])
 def test_strict_half_edge_corpus(hc, golden, bw):
     for it in golden["edge_corpus"]["items"]:
         m, pk, sig = (bytes.fromhex(it[k]) for k in ("msg", "pk", "sig"))
@@ -172,7 +172,8 @@ def _limbs_to_int(limbs):
 
 
 def test_wide_btab_entries(hc):
-    """The strict kernel's wide B tables (nw_consts.hpp compute_wide_btab, 16-bit windows):
+    """The host copy of the 16-bit wide B tables (nw_consts.hpp compute_wide_btab; the device
+    builds its own with k_btab_build, checked end to end by the GPU strict tests):
     entry j of half h is j * 2^(128 h) * B in affine niels form, against the oracle."""
     rng = np.random.Generator(np.random.PCG64(13))
     js = [0, 1, 2, 3, 127, 128, 129, 32767, 32768] + [int(x) for x in rng.integers(0, 32769, 24)]
@@ -202,5 +203,5 @@ def test_strict_half_random_and_tampered(hc):
             sig[int(rng.integers(0, 32))] ^= 1 << int(rng.integers(0, 8))
         k = O.hram(bytes(sig[:32]), pk, m)
         want = O.verify_strict(m, pk, bytes(sig))
-        for bw in (16, 8):
+        for bw in (16, 8, 20, 24):
             assert hc.hc_verify_strict_half(_b(pk), _b(bytes(sig)), _b(k), bw) == want
