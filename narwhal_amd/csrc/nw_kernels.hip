@@ -424,7 +424,7 @@ namespace nw {
 // that initialises every device but verifies on one builds one table).
 static constexpr int kMaxDevIds = 64;
 static std::atomic<ge_niels_pad*> g_btw[kMaxDevIds];
-static std::mutex g_btw_mu;
+static std::mutex g_btw_mu[kMaxDevIds];   // per device: devices build in parallel
 static constexpr uint32_t kBtwPerHalf = bdigits<NW_BWIN>::ENTRIES;
 
 static hipError_t btw_for_current_device(const ge_niels_pad** out) {
@@ -435,7 +435,7 @@ static hipError_t btw_for_current_device(const ge_niels_pad** out) {
   if (e != hipSuccess) return e;
   if (dev < 0 || dev >= kMaxDevIds) return hipErrorInvalidDevice;
   if ((*out = g_btw[dev].load(std::memory_order_acquire))) return hipSuccess;
-  std::lock_guard<std::mutex> lock(g_btw_mu);
+  std::lock_guard<std::mutex> lock(g_btw_mu[dev]);
   if ((*out = g_btw[dev].load(std::memory_order_relaxed))) return hipSuccess;
   void* p = nullptr;
   const uint64_t entries = 2ull * kBtwPerHalf;
