@@ -92,15 +92,24 @@ void do_init() {
     hipDeviceProp_t p;
     if (hipGetDeviceProperties(&p, d) != hipSuccess) continue;
     if (strncmp(p.gcnArchName, "gfx950", 6) != 0) continue;
-    if (hipSetDevice(d) != hipSuccess) continue;
-    if (nw::upload_consts() != hipSuccess) {
-      g_init_status = NW_E_DEVICE;
-      return;
-    }
-    g_dev_ids[n++] = d;
+    g_dev_ids[n++] = d;   // constants are uploaded on the device's first use (activate)
   }
   g_ndev = n;
   g_init_status = n > 0 ? n : NW_E_NO_DEVICE;
+}
+
+// Per-device first use: the constant tables go to a device only when a call selects it, so a
+// process that drives one GPU (one rank per GPU) never loads the module on the others.
+std::once_flag g_dev_once[kMaxDevices];
+hipError_t g_dev_status[kMaxDevices];
+
+int activate(int dev) {
+  hipError_t e = hipSetDevice(g_dev_ids[dev]);
+  if (e != hipSuccess) return set_err(NW_E_DEVICE, "hipSetDevice", e);
+  std::call_once(g_dev_once[dev], [dev] { g_dev_status[dev] = nw::upload_consts(); });
+  if (g_dev_status[dev] != hipSuccess)
+    return set_err(NW_E_DEVICE, "device initialisation (constant upload)", g_dev_status[dev]);
+  return 0;
 }
 
 int ensure_init() {
@@ -121,11 +130,11 @@ int begin(DevCtx** out) {
     return set_err(NW_E_INVALID_ARG, "this entry point runs on one device: nw_set_device(d), "
                                      "d >= 0 (NW_ALL_DEVICES fans out host-buffer calls only)");
   if (dev < 0 || dev >= g_ndev) return set_err(NW_E_INVALID_ARG, "bad device index");
-  hipError_t e = hipSetDevice(g_dev_ids[dev]);
-  if (e != hipSuccess) return set_err(NW_E_DEVICE, "hipSetDevice", e);
+  rc = activate(dev);
+  if (rc) return rc;
   DevCtx& c = t_state.ctx[dev];
   if (!c.stream) {
-    e = hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking);
+    hipError_t e = hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking);
     if (e != hipSuccess) return set_err(NW_E_DEVICE, "hipStreamCreate", e);
   }
   *out = &c;
@@ -968,8 +977,8 @@ int select_device(int* dev_index) {
   if (rc) return rc;
   const int dev = t_state.device;
   if (dev < 0 || dev >= g_ndev) return ::set_err(NW_E_INVALID_ARG, "bad device index");
-  hipError_t e = hipSetDevice(g_dev_ids[dev]);
-  if (e != hipSuccess) return ::set_err(NW_E_DEVICE, "hipSetDevice", e);
+  rc = ::activate(dev);
+  if (rc) return rc;
   *dev_index = dev;
   return 0;
 }
@@ -978,9 +987,7 @@ int use_device(int dev_index) {
   int rc = ::ensure_init();
   if (rc) return rc;
   if (dev_index < 0 || dev_index >= g_ndev) return ::set_err(NW_E_INVALID_ARG, "bad device index");
-  hipError_t e = hipSetDevice(g_dev_ids[dev_index]);
-  if (e != hipSuccess) return ::set_err(NW_E_DEVICE, "hipSetDevice", e);
-  return 0;
+  return ::activate(dev_index);
 }
 
 int thread_device() { return t_state.device; }
