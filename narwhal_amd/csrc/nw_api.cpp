@@ -1056,7 +1056,7 @@ int Lease::key_tables(size_t nkeys, void** tabs, uint32_t** ok) {
     d.ktabs = nullptr;
     d.kok = nullptr;
     d.kcap = 0;
-    const size_t cap = nkeys < 256 ? 256 : nkeys;
+    const size_t cap = nkeys < 16 ? 16 : nkeys;   // 660 KB of comb tables per key
     hipError_t e = hipMalloc(&d.ktabs, nw::key_tables_bytes(cap));
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.kok), 4 * cap);
     if (e != hipSuccess) return ::set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (key tables)", e);

@@ -547,7 +547,7 @@ __global__ __launch_bounds__(256) void k_bv_chunks(
         if ((j & 1) == 0 && j < 32) {
           const ge_cached* kt = ktabs + kKeyTab * (uint64_t)it->key;
           add_key_entry(acc, kt, digit8(it->c, j >> 1));
-          add_key_entry(acc, kt + 129, digit8(it->c, 16 + (j >> 1)));
+          add_key_entry(acc, kt + kKeyHalf, digit8(it->c, 16 + (j >> 1)));
         }
       } else {
         add_entry(acc, tab, digit4(it->c[j >> 3], j));
@@ -1333,10 +1333,13 @@ size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems) {
 // Caller key tables (a committee's keys, decompressed once per call): per key
 // j*A and j*2^128 A for j = 0..128 in cached form (258 entries, 41 KB), used by keyed
 // chunks' 8-bit windows and short ladders.
-//   k_key_base  one lane per key: decompress (dalek semantics), 2^128 A by 128 doublings.
-//   k_key_tabs  one lane per (key, table, j): j*P by double-and-add over the 8 bits of j.
+//   k_key_base  one lane per key: decompress (dalek semantics), the comb bases 2^(8t) A
+//               (t = 0..31) by 248 doublings; base[2 key] = A, base[2 key + 1] = 2^128 A
+//               for the group path, comb[32 key + t] for k_key_tabs.
+//   k_key_tabs  one lane per (key, table t, j): j * 2^(8t) A by double-and-add over j's bits.
 __global__ __launch_bounds__(256) void k_key_base(const uint32_t* __restrict__ pks,
                                                   uint64_t nkeys, ge* __restrict__ base,
+                                                  ge* __restrict__ comb,
                                                   uint32_t* __restrict__ ok) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nkeys) return;
@@ -1348,17 +1351,23 @@ __global__ __launch_bounds__(256) void k_key_base(const uint32_t* __restrict__ p
   ok[i] = (dec ? 1u : 0u) | (dec && ge_is_small_order(P) ? 2u : 0u);   // bit 1: 8A == 0
   base[2 * i] = P;
 #pragma unroll 1
-  for (int t = 0; t < 128; ++t) ge_dbl(P, P, t == 127);
-  base[2 * i + 1] = P;
+  for (int t = 0; t < (int)kKeyCombT; ++t) {
+    if (t) {
+#pragma unroll 1
+      for (int d = 0; d < 8; ++d) ge_dbl(P, P, d == 7);
+    }
+    comb[kKeyCombT * i + t] = P;
+    if (t == 16) base[2 * i + 1] = P;
+  }
 }
 
-__global__ __launch_bounds__(256) void k_key_tabs(uint64_t nkeys, const ge* __restrict__ base,
+__global__ __launch_bounds__(256) void k_key_tabs(uint64_t nkeys, const ge* __restrict__ comb,
                                                   ge_cached* __restrict__ tabs) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= nkeys * kKeyTab) return;
-  const uint64_t pt = g / 129;           // 2 * key + table
+  const uint64_t pt = g / 129;           // kKeyCombT * key + t
   const int j = (int)(g % 129);
-  const ge P = base[pt];
+  const ge P = comb[pt];
   ge acc;
   ge_identity(acc);
 #pragma unroll 1
@@ -1377,17 +1386,18 @@ __global__ __launch_bounds__(256) void k_key_tabs(uint64_t nkeys, const ge* __re
 
 size_t key_tables_bytes(uint64_t nkeys) {
   const uint64_t n = nkeys ? nkeys : 1;
-  return sizeof(ge_cached) * kKeyTab * n + sizeof(ge) * 2 * n;
+  return sizeof(ge_cached) * kKeyTab * n + sizeof(ge) * (2 + kKeyCombT) * n;
 }
 
 hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, ge_cached* tabs, uint32_t* ok,
                              hipStream_t stream) {
   if (nkeys == 0) return hipSuccess;
   ge* base = reinterpret_cast<ge*>(tabs + kKeyTab * nkeys);
+  ge* comb = base + 2 * nkeys;
   hipLaunchKernelGGL(k_key_base, dim3((unsigned)((nkeys + 63) / 64)), dim3(64), 0, stream, pks,
-                     nkeys, base, ok);
+                     nkeys, base, comb, ok);
   hipLaunchKernelGGL(k_key_tabs, dim3((unsigned)((nkeys * kKeyTab + 255) / 256)), dim3(256), 0,
-                     stream, nkeys, base, tabs);
+                     stream, nkeys, comb, tabs);
   return hipGetLastError();
 }
 
@@ -1886,7 +1896,7 @@ __global__ __launch_bounds__(256) void k_sgrp_ladder(
         const sgrp_key& e = *reinterpret_cast<const sgrp_key*>(slots + 16 * (uint64_t)m);
         const ge_cached* kt = ktabs + kKeyTab * (uint64_t)e.key;
         add_key_entry(acc, kt, digit8(e.c, j >> 1));
-        add_key_entry(acc, kt + 129, digit8(e.c, 16 + (j >> 1)));
+        add_key_entry(acc, kt + kKeyHalf, digit8(e.c, 16 + (j >> 1)));
       }
       if (k == 0) {
         add_digit_niels(acc, s_btab, digit8(h.bb, j >> 1), true);

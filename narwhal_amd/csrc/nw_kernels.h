@@ -42,18 +42,22 @@ hipError_t launch_sign(const uint32_t* sks, uint32_t sk_stride_words, const uint
 // the workspace slices).
 hipError_t upload_batch_consts();
 
-// Pre-decompressed public keys (a committee): per key the tables j*A and j*2^128 A
-// (j = 0..128, cached form) and whether it decompressed. vote_key[i] = key index of vote i,
-// or kNoKey to decompress that vote's key in the kernel (the verdict semantics are
-// unchanged: a key's decompression is deterministic). Chunks whose votes are all keyed
-// run 8-bit A windows and a 128-doubling ladder.
+// Pre-decompressed public keys (a committee): per key the comb tables j * 2^(8t) A
+// (t = 0..31, j = 0..128, cached form; t = 0 and t = 16 are j*A and j*2^128 A) and whether
+// it decompressed. vote_key[i] = key index of vote i, or kNoKey to decompress that vote's
+// key in the kernel (the verdict semantics are unchanged: a key's decompression is
+// deterministic). Keyed strict verifications take [k]A from the 32 tables with no
+// doublings; chunks whose votes are all keyed run 8-bit A windows over tables t = 0, 16 and
+// a 128-doubling ladder.
 struct key_tables_t {
   const struct ge_cached* tabs;   // nkeys x 8
   const uint32_t* ok;             // nkeys
   const uint32_t* vote_key;       // nitems (global item index)
 };
 constexpr uint32_t kNoKey = 0xffffffffu;
-constexpr uint32_t kKeyTab = 258;   // entries per key: j*A, then j*2^128 A, j = 0..128
+constexpr uint32_t kKeyCombT = 32;                // comb tables per key (8-bit windows)
+constexpr uint32_t kKeyTab = kKeyCombT * 129;      // entries per key: j * 2^(8t) A
+constexpr uint32_t kKeyHalf = 16 * 129;            // offset of the j * 2^128 A table
 // ok[key]: bit 0 = decompressed, bit 1 = small order (8A == identity)
 size_t key_tables_bytes(uint64_t nkeys);
 // tabs: key_tables_bytes(nkeys) of device memory; ok: nkeys words.

@@ -48,15 +48,18 @@ __device__ __forceinline__ void load_table(ge_niels* dst_tab, const ge_niels* sr
 }
 __device__ __forceinline__ void load_btab(ge_niels* s_btab) { load_table(s_btab, g_consts.btab); }
 
-// Maximum of a per-lane value over the wave (wave-uniform result).
+// Maximum of a per-lane value 0 <= w < 128 over the ACTIVE lanes of the wave (wave-uniform
+// result), bit by bit with ballots, so it is exact inside divergent code too (a lane shuffle
+// would read inactive lanes' stale registers).
 struct WaveMax {
   __device__ int operator()(int w) const {
+    int r = 0;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const int x = __shfl_xor(w, o);
-      w = x > w ? x : w;
+    for (int b = 6; b >= 0; --b) {
+      const int c = r | (1 << b);
+      if (__ballot(w >= c) != 0) r = c;
     }
-    return __builtin_amdgcn_readfirstlane(w);
+    return r;
   }
 };
 
@@ -241,7 +244,8 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
                                                        uint64_t* __restrict__ bitmap,
                                                        ge_cached* __restrict__ tabs,
                                                        key_tables_t keys,
-                                                       const ge_niels_pad* __restrict__ btw) {
+                                                       const ge_niels_pad* __restrict__ btw,
+                                                       const ge_niels_pad* __restrict__ bcomb) {
 #if NW_BWIN == 8
   __shared__ ge_niels s_btab[129];
   __shared__ ge_niels s_b128[129];
@@ -264,8 +268,11 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
     const strict_src_global src{pks + 8 * i, sigs + 16 * i, msgs + (uint64_t)msg_stride_words * i};
     const uint32_t kk = keys.vote_key ? keys.vote_key[i] : kNoKey;
     const ge_cached* keytab = kk != kNoKey ? keys.tabs + kKeyTab * (uint64_t)kk : nullptr;
-    const int st = strict_verify_core<NW_BWIN>(src, g_consts.sk, bt, tabA, tabR, WaveMax{},
-                                               keytab, kk != kNoKey ? keys.ok[kk] : 0u);
+    // committee keys: [s]B - [k]A from comb tables, no ladder; others: the half-size ladder
+    const int st = keytab ? strict_keyed_comb(src, g_consts.sk, bcomb_wide{bcomb}, keytab,
+                                              keys.ok[kk])
+                          : strict_verify_core<NW_BWIN>(src, g_consts.sk, bt, tabA, tabR,
+                                                        WaveMax{});
     if (active) status[gi] = st;
     const uint64_t mask = __ballot(active && st == NW_OK);
     if ((threadIdx.x & 63) == 0 && gi < n) bitmap[gi >> 6] = mask;
@@ -390,20 +397,25 @@ __global__ __launch_bounds__(256) void k_sign(const uint32_t* __restrict__ sks,
 }  // namespace nw
 
 namespace nw {
-// The strict kernel's wide B tables, built on the device once per process and device:
-// out[h * n + j] = j * 2^(128 h) * B (h = 0, 1; j = 0..n-1) in padded affine niels form, one
-// lane per entry: fixed-base product over the 8-bit LDS table, then one inversion.
-__global__ __launch_bounds__(256) void k_btab_build(ge_niels_pad* __restrict__ out, uint32_t n) {
+// The strict kernel's wide B tables, built on the device once per process and device, in
+// padded affine niels form, one lane per entry: fixed-base product over the 8-bit LDS table,
+// then one inversion.
+// out[h * n + j] = j * 2^(shift h) * B for h < ntab (shift 128: the ladder's two tables;
+// shift 16: the keyed comb's sixteen).
+__global__ __launch_bounds__(256) void k_btab_build(ge_niels_pad* __restrict__ out, uint32_t n,
+                                                    uint32_t ntab, uint32_t shift) {
   __shared__ ge_niels s_btab[129];
   load_btab(s_btab);
   __syncthreads();
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= 2ull * n) return;
-  const uint32_t h = g >= n ? 1u : 0u, j = (uint32_t)(g - (uint64_t)h * n);
+  if (g >= (uint64_t)ntab * n) return;
+  const uint32_t h = (uint32_t)(g / n), j = (uint32_t)(g % n);
   sc s;
 #pragma unroll
   for (int i = 0; i < 8; ++i) s.w[i] = 0;
-  s.w[h ? 4 : 0] = j;
+  const uint32_t bit = shift * h, wi = bit >> 5, sh = bit & 31;   // j < 2^24, bit <= 240
+  s.w[wi] = j << sh;
+  if (sh && wi < 7) s.w[wi + 1] = j >> (32 - sh);
   ge P;
   fixed_base_mul(P, s, s_btab);
   ge_niels nb;
@@ -427,32 +439,40 @@ static std::atomic<ge_niels_pad*> g_btw[kMaxDevIds];
 static std::mutex g_btw_mu[kMaxDevIds];   // per device: devices build in parallel
 static constexpr uint32_t kBtwPerHalf = bdigits<NW_BWIN>::ENTRIES;
 
-static hipError_t btw_for_current_device(const ge_niels_pad** out) {
+static std::atomic<ge_niels_pad*> g_bcomb[kMaxDevIds];
+static_assert(kStrictKeyTables == (int)kKeyCombT, "keyed comb table count");
+
+// Table set `which` of the current device (0: the ladder's 2 x kBtwPerHalf; 1: the keyed
+// comb's 16 x 32,769), built on first use.
+static hipError_t btab_for_current_device(int which, const ge_niels_pad** out) {
   *out = nullptr;
-  if (NW_BWIN == 8) return hipSuccess;
+  if (which == 0 && NW_BWIN == 8) return hipSuccess;
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
   if (dev < 0 || dev >= kMaxDevIds) return hipErrorInvalidDevice;
-  if ((*out = g_btw[dev].load(std::memory_order_acquire))) return hipSuccess;
+  std::atomic<ge_niels_pad*>& slot = which ? g_bcomb[dev] : g_btw[dev];
+  if ((*out = slot.load(std::memory_order_acquire))) return hipSuccess;
   std::lock_guard<std::mutex> lock(g_btw_mu[dev]);
-  if ((*out = g_btw[dev].load(std::memory_order_relaxed))) return hipSuccess;
+  if ((*out = slot.load(std::memory_order_relaxed))) return hipSuccess;
+  const uint32_t n = which ? kBCombN : kBtwPerHalf, ntab = which ? kBCombT : 2;
+  const uint32_t shift = which ? 16 : 128;
   void* p = nullptr;
-  const uint64_t entries = 2ull * kBtwPerHalf;
+  const uint64_t entries = (uint64_t)ntab * n;
   e = hipMalloc(&p, entries * sizeof(ge_niels_pad));
   if (e != hipSuccess) return e;
   hipStream_t s = nullptr;
   e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(k_btab_build, dim3((unsigned)((entries + 255) / 256)), dim3(256), 0, s,
-                       static_cast<ge_niels_pad*>(p), kBtwPerHalf);
+                       static_cast<ge_niels_pad*>(p), n, ntab, shift);
     e = hipGetLastError();
     const hipError_t e2 = hipStreamSynchronize(s);
     if (e == hipSuccess) e = e2;
     (void)hipStreamDestroy(s);
   }
   if (e != hipSuccess) { (void)hipFree(p); return e; }
-  g_btw[dev].store(static_cast<ge_niels_pad*>(p), std::memory_order_release);
+  slot.store(static_cast<ge_niels_pad*>(p), std::memory_order_release);
   *out = static_cast<ge_niels_pad*>(p);
   return hipSuccess;
 }
@@ -514,10 +534,13 @@ hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
   const unsigned grid = std::min<uint64_t>(strict_grid(), grid_for(n, 256));
   const key_tables_t kt = keys ? *keys : key_tables_t{nullptr, nullptr, nullptr};
   const ge_niels_pad* btw = nullptr;
-  const hipError_t eb = btw_for_current_device(&btw);
+  const ge_niels_pad* bcomb = nullptr;
+  hipError_t eb = btab_for_current_device(0, &btw);
+  if (eb == hipSuccess && kt.vote_key) eb = btab_for_current_device(1, &bcomb);
   if (eb != hipSuccess) return eb;
   hipLaunchKernelGGL(k_verify_strict, dim3(grid), dim3(256), 0, stream, msgs, msg_stride_words,
-                     pks, sigs, n, status, bitmap, static_cast<ge_cached*>(workspace), kt, btw);
+                     pks, sigs, n, status, bitmap, static_cast<ge_cached*>(workspace), kt, btw,
+                     bcomb);
   return hipGetLastError();
 }
 

@@ -232,6 +232,107 @@ struct btab_lazy {
   }
 };
 
+// The B comb for keyed verifications: 16 tables j * 2^(16 m) * B (m = 0..15, j = 0..32,768),
+// so [s]B = sum_m T_m[d_m] over s's signed 16-bit digits with no doublings. bcomb_wide: the
+// device copy (global memory, padded entries); bcomb_lazy: entries computed per lookup
+// (host self-check).
+constexpr int kBCombT = 16;
+constexpr int kStrictKeyTables = 32;   // = nw_kernels.h kKeyCombT
+constexpr uint32_t kBCombN = (1u << 15) + 1;
+struct bcomb_wide {
+  const ge_niels_pad* t;
+  NW_HD void operator()(int m, int ad, ge_cached& e) const {
+    const ge_niels& nb = t[(uint32_t)m * kBCombN + (uint32_t)ad].n;
+    fe_copy(e.YpX, nb.ypx);
+    fe_copy(e.YmX, nb.ymx);
+    fe_copy(e.T2d, nb.xy2d);
+  }
+};
+struct bcomb_lazy {
+  const ge_niels* btab8;
+  const fe* d2;
+  NW_HD void operator()(int m, int ad, ge_cached& e) const {
+    sc s;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s.w[i] = 0;
+    s.w[m >> 1] = (uint32_t)ad << (16 * (m & 1));
+    ge P;
+    fixed_base_mul(P, s, btab8);
+    ge_niels nb;
+    ge_to_niels(nb, P, *d2);
+    fe_copy(e.YpX, nb.ypx);
+    fe_copy(e.YmX, nb.ymx);
+    fe_copy(e.T2d, nb.xy2d);
+  }
+};
+
+// Keyed strict verification: A is a committee key with comb tables keytab[129 t + j] =
+// j * 2^(8t) A (t = 0..31, nw_kernels.h kKeyTab), keyflags bit 0 = decoded, bit 1 = small
+// order. Then R' = [s]B - [k]A is 16 + 32 table additions with no doublings and no scalar
+// split, and the equation is dalek's own projective comparison R == R' (R decompressed,
+// Z = 1). Same checks and order as strict_verify_core; A is neither decompressed nor
+// tabulated per signature.
+template <class BComb, class Src>
+NW_HD int strict_keyed_comb(const Src& src, const strict_consts& K, const BComb& bc,
+                            const ge_cached* keytab, uint32_t keyflags) {
+  const bool okA = (keyflags & 1) != 0, smallA = (keyflags & 2) != 0;
+  ge R;
+  bool okR, smallR;
+  {
+    uint32_t x[8];
+    src.R(x);
+    okR = ge_frombytes(R, x, K.k);
+    smallR = small_order_by_y(R.Y, K.small_y);
+  }
+  uint32_t Sw[8];
+  src.S(Sw);
+  sc s;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s.w[j] = Sw[j];
+  const bool s_high = (Sw[7] >> 29) != 0;
+  const bool s_canon = sc_is_canonical(s);
+  // Reference order: crypto/src/lib.rs:201 (s high bits), 202 (decompress A), then dalek
+  // verify_strict: check_scalar, decompress R, small order (R || A), equation.
+  if (s_high) return NW_ERR_S_HIGH_BITS;
+  if (!okA) return NW_ERR_A_DECODE;
+  if (!s_canon) return NW_ERR_S_NONCANONICAL;
+  if (!okR) return NW_ERR_R_DECODE;
+  if (smallR) return NW_ERR_R_SMALL_ORDER;
+  if (smallA) return NW_ERR_A_SMALL_ORDER;
+  uint32_t kw[8];
+  src.K(kw);
+  sc k;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) k.w[j] = kw[j];
+  uint32_t kd[8], sd[8];
+  sc_recode(kd, k, 0x80808080u);   // k < l: 32 signed 8-bit digits
+  sc_recode(sd, s, 0x80008000u);   // s < l: 16 signed 16-bit digits
+  ge acc;
+  ge_identity(acc);
+  // -[k]A: digit t of k against table t, negated
+#pragma unroll 1
+  for (int t = 0; t < kStrictKeyTables; ++t) {
+    const int d = (int)((sel8(kd, t >> 2) >> ((t & 3) * 8)) & 255u) - 128;
+    if (d != 0) {
+      ge_cached e = keytab[129 * t + (d < 0 ? -d : d)];
+      ge_cached_cneg(e, d > 0);
+      ge_add_any(acc, acc, e, false, true);
+    }
+  }
+  // +[s]B
+#pragma unroll 1
+  for (int m = 0; m < kBCombT; ++m) {
+    const int d = (int)((sel8(sd, m >> 1) >> ((m & 1) * 16)) & 0xffffu) - 32768;
+    if (d != 0) {
+      ge_cached e;
+      bc(m, d < 0 ? -d : d, e);
+      ge_cached_cneg(e, d < 0);
+      ge_add_any(acc, acc, e, true, true);
+    }
+  }
+  return ge_eq_affine(acc, R) ? NW_OK : NW_ERR_EQUATION;
+}
+
 // Status of one strict verification. wave_max maps this lane's ladder length (in 4-bit
 // windows) to the wave's maximum (identity on the host). tabA/tabR: 8 entries each of
 // per-lane scratch. bt: j*B and j*2^128 B, j = 0..2^(BW-1) (btab_pair / btab_wide).

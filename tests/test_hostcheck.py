@@ -190,6 +190,27 @@ def test_wide_btab_entries(hc):
             assert enc == O.scalarmult_base(s.to_bytes(32, "little")), (h, j)
 
 
+def test_strict_keyed_comb(hc, golden):
+    """Committee-key strict path (no ladder: [s]B - [k]A from comb tables) against the
+    oracle on the edge corpus and on random honest / tampered signatures."""
+    for it in golden["edge_corpus"]["items"]:
+        m, pk, sig = (bytes.fromhex(it[k]) for k in ("msg", "pk", "sig"))
+        k = O.hram(sig[:32], pk, m)
+        assert hc.hc_verify_strict_keyed(_b(pk), _b(sig), _b(k)) == it["status"], it["class"]
+    rng = np.random.Generator(np.random.PCG64(15))
+    for i in range(24):
+        pk, sk = O.keypair_from_seed(rng.bytes(32))
+        m = rng.bytes(32)
+        sig = bytearray(O.sign(sk, m))
+        if i % 3 == 1:
+            sig[32 + int(rng.integers(0, 31))] ^= 1 << int(rng.integers(0, 8))
+        elif i % 3 == 2:
+            sig[int(rng.integers(0, 32))] ^= 1 << int(rng.integers(0, 8))
+        k = O.hram(bytes(sig[:32]), pk, m)
+        assert hc.hc_verify_strict_keyed(_b(pk), _b(bytes(sig)), _b(k)) == \
+            O.verify_strict(m, pk, bytes(sig))
+
+
 def test_strict_half_random_and_tampered(hc):
     rng = np.random.Generator(np.random.PCG64(12))
     for i in range(120):

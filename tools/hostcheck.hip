@@ -145,6 +145,36 @@ int hc_verify_strict_half(const uint8_t pk[32], const uint8_t sig[64], const uin
   return strict_verify_core<16>(src, SK, btab_wide{BTW, BTW_N}, ta, tr, id);
 }
 
+// The keyed strict path (nw_strict.hpp strict_keyed_comb): the key's 32 comb tables
+// j * 2^(8t) A built here as the device's k_key_base / k_key_tabs define them, the B comb
+// computed per lookup. Returns the status; -1 when A does not decode is reported through the
+// key flags exactly as the device does (status 3).
+int hc_verify_strict_keyed(const uint8_t pk[32], const uint8_t sig[64], const uint8_t k32[32]) {
+  init();
+  uint32_t Aw[8], Rw[8], Sw[8], kw[8];
+  load8(Aw, pk); load8(Rw, sig); load8(Sw, sig + 32); load8(kw, k32);
+  ge A;
+  const bool dec = ge_frombytes(A, Aw, K);
+  const uint32_t flags = (dec ? 1u : 0u) | (dec && ge_is_small_order(A) ? 2u : 0u);
+  static ge_cached tab[32 * 129];
+  ge base = A;
+  for (int t = 0; t < 32; ++t) {
+    if (t) for (int d = 0; d < 8; ++d) { ge x; ge_dbl(x, base, d == 7); base = x; }
+    ge_cached cb;
+    ge_to_cached(cb, base, K.d2);
+    ge acc;
+    ge_identity(acc);
+    for (int j = 0; j <= 128; ++j) {
+      ge_to_cached(tab[129 * t + j], acc, K.d2);
+      ge nx;
+      ge_add_cached(nx, acc, cb, true);
+      acc = nx;
+    }
+  }
+  const strict_src_arrays src{Aw, Rw, Sw, kw};
+  return strict_keyed_comb(src, SK, bcomb_lazy{BT, &SK.k.d2}, tab, flags);
+}
+
 // Entry j of the wide B table half h (ypx || ymx || xy2d as 30 limbs), for the table test.
 void hc_wide_btab_entry(int h, uint32_t j, uint32_t out[30]) {
   init();
