@@ -536,7 +536,7 @@ int cert_pipeline(const nw_committee& com, const nw_certificates& cs,
   if (!rc) rc = lease.key_tables(com.nauth, &ktabs_v, &kok);
   if (!rc) rc = lease.strict_ws(&sws);
   if (rc) return rc;
-  nw::ge_cached* ktabs = static_cast<nw::ge_cached*>(ktabs_v);
+  nw::ge_niels_pad* ktabs = static_cast<nw::ge_niels_pad*>(ktabs_v);
   NW_HIP(nw::launch_key_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth, ktabs, kok,
                                s),
          "k_key_tables");

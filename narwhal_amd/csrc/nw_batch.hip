@@ -456,12 +456,13 @@ __device__ __forceinline__ int digit8(const uint32_t* w, int m) {
   return (int)((sel8(w, m >> 2) >> ((m & 3) * 8)) & 255u) - 128;
 }
 
-// Keyed vote: A's digit from its key table (129 entries j*A or j*2^128 A, cached form).
-__device__ __forceinline__ void add_key_entry(ge& acc, const ge_cached* tab129, int d) {
+// Keyed vote: A's digit from its key table (129 entries j*A or j*2^128 A, affine niels:
+// a mixed addition).
+__device__ __forceinline__ void add_key_entry(ge& acc, const ge_niels_pad* tab129, int d) {
   if (d != 0) {
-    ge_cached e = tab129[d < 0 ? -d : d];
-    ge_cached_cneg(e, d < 0);
-    ge_add_cached(acc, acc, e, true);
+    ge_niels nb = tab129[d < 0 ? -d : d].n;
+    ge_niels_cneg(nb, d < 0);
+    ge_add_niels(acc, acc, nb, true);
   }
 }
 
@@ -476,7 +477,7 @@ __device__ __forceinline__ void add_key_entry(ge& acc, const ge_cached* tab129, 
 __global__ __launch_bounds__(256) void k_bv_chunks(
     const bv_chunk* __restrict__ chunks, uint32_t nchunks, const uint64_t* __restrict__ offsets,
     uint64_t b0, uint64_t i0, const bv_item* __restrict__ items,
-    const ge_cached* __restrict__ tabs, const ge_cached* __restrict__ ktabs,
+    const ge_cached* __restrict__ tabs, const ge_niels_pad* __restrict__ ktabs,
     bv_chunk_out* __restrict__ out, int32_t* __restrict__ status,
     uint64_t* __restrict__ fail_index, const uint32_t* __restrict__ ctotal) {
   __shared__ ge_niels s_btab[129];
@@ -545,7 +546,7 @@ __global__ __launch_bounds__(256) void k_bv_chunks(
       const ge_cached* tab = tabs + 16 * (l0 + t);
       if (keyed) {
         if ((j & 1) == 0 && j < 32) {
-          const ge_cached* kt = ktabs + kKeyTab * (uint64_t)it->key;
+          const ge_niels_pad* kt = ktabs + kKeyTab * (uint64_t)it->key;
           add_key_entry(acc, kt, digit8(it->c, j >> 1));
           add_key_entry(acc, kt + kKeyHalf, digit8(it->c, 16 + (j >> 1)));
         }
@@ -1362,7 +1363,7 @@ __global__ __launch_bounds__(256) void k_key_base(const uint32_t* __restrict__ p
 }
 
 __global__ __launch_bounds__(256) void k_key_tabs(uint64_t nkeys, const ge* __restrict__ comb,
-                                                  ge_cached* __restrict__ tabs) {
+                                                  ge_niels_pad* __restrict__ tabs) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= nkeys * kKeyTab) return;
   const uint64_t pt = g / 129;           // kKeyCombT * key + t
@@ -1379,17 +1380,18 @@ __global__ __launch_bounds__(256) void k_key_tabs(uint64_t nkeys, const ge* __re
       ge_add_cached(acc, acc, c, true);
     }
   }
-  ge_cached out;
-  ge_to_cached(out, acc, g_bc.k.d2);
-  tabs[g] = out;
+  ge_niels out;
+  ge_to_niels(out, acc, g_bc.k.d2);   // one inversion per entry: affine, mixed additions
+  tabs[g].n = out;
+  tabs[g].pad[0] = tabs[g].pad[1] = 0;
 }
 
 size_t key_tables_bytes(uint64_t nkeys) {
   const uint64_t n = nkeys ? nkeys : 1;
-  return sizeof(ge_cached) * kKeyTab * n + sizeof(ge) * (2 + kKeyCombT) * n;
+  return sizeof(ge_niels_pad) * kKeyTab * n + sizeof(ge) * (2 + kKeyCombT) * n;
 }
 
-hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, ge_cached* tabs, uint32_t* ok,
+hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, ge_niels_pad* tabs, uint32_t* ok,
                              hipStream_t stream) {
   if (nkeys == 0) return hipSuccess;
   ge* base = reinterpret_cast<ge*>(tabs + kKeyTab * nkeys);
@@ -1552,7 +1554,7 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
   return hipSuccess;
 }
 
-const ge* key_tables_base(const ge_cached* tabs, uint64_t nkeys) {
+const ge* key_tables_base(const ge_niels_pad* tabs, uint64_t nkeys) {
   return reinterpret_cast<const ge*>(tabs + kKeyTab * nkeys);
 }
 
@@ -1845,7 +1847,7 @@ __global__ __launch_bounds__(64) void k_sgrp_keys(
 __global__ __launch_bounds__(256) void k_sgrp_ladder(
     const uint64_t* __restrict__ cvo, uint64_t g0, uint64_t g1, uint64_t ncert, uint64_t K,
     uint32_t nch, uint64_t i0, const bv_item* __restrict__ items,
-    const ge_cached* __restrict__ tabs, const ge_cached* __restrict__ ktabs,
+    const ge_cached* __restrict__ tabs, const ge_niels_pad* __restrict__ ktabs,
     bv_chunk_out* __restrict__ out) {
   __shared__ ge_niels s_btab[129];
   __shared__ ge_niels s_b128[129];
@@ -1894,7 +1896,7 @@ __global__ __launch_bounds__(256) void k_sgrp_ladder(
 #pragma unroll 1
       for (uint32_t m = k; m < h.nkeys; m += nch) {
         const sgrp_key& e = *reinterpret_cast<const sgrp_key*>(slots + 16 * (uint64_t)m);
-        const ge_cached* kt = ktabs + kKeyTab * (uint64_t)e.key;
+        const ge_niels_pad* kt = ktabs + kKeyTab * (uint64_t)e.key;
         add_key_entry(acc, kt, digit8(e.c, j >> 1));
         add_key_entry(acc, kt + kKeyHalf, digit8(e.c, 16 + (j >> 1)));
       }

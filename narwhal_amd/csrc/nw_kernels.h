@@ -50,7 +50,7 @@ hipError_t upload_batch_consts();
 // doublings; chunks whose votes are all keyed run 8-bit A windows over tables t = 0, 16 and
 // a 128-doubling ladder.
 struct key_tables_t {
-  const struct ge_cached* tabs;   // nkeys x 8
+  const struct ge_niels_pad* tabs;   // nkeys x kKeyTab, affine niels (mixed additions)
   const uint32_t* ok;             // nkeys
   const uint32_t* vote_key;       // nitems (global item index)
 };
@@ -61,7 +61,7 @@ constexpr uint32_t kKeyHalf = 16 * 129;            // offset of the j * 2^128 A 
 // ok[key]: bit 0 = decompressed, bit 1 = small order (8A == identity)
 size_t key_tables_bytes(uint64_t nkeys);
 // tabs: key_tables_bytes(nkeys) of device memory; ok: nkeys words.
-hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, struct ge_cached* tabs,
+hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, struct ge_niels_pad* tabs,
                              uint32_t* ok, hipStream_t stream);
 size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems);
 // skip_group_ok (optional, device): batch b is settled (status Ok) when
@@ -94,7 +94,7 @@ hipError_t launch_group_feedback(const uint32_t* group_ok, uint64_t ncert, uint6
                                  const int32_t* pre2, const int32_t* hdr_st, uint32_t* cnt,
                                  uint32_t* fb, hipStream_t stream);
 size_t cert_groups_bytes(uint64_t ncert);
-const ge* key_tables_base(const ge_cached* tabs, uint64_t nkeys);
+const ge* key_tables_base(const ge_niels_pad* tabs, uint64_t nkeys);
 hipError_t launch_cert_groups(const uint32_t* cert_digest, const uint64_t* cvo,
                               const uint64_t* host_cvo, uint64_t ncert, const uint32_t* pks,
                               const uint32_t* sigs, uint64_t nvotes, const z_key_t& zkey,

@@ -267,7 +267,7 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
     const uint64_t i = active ? gi : n - 1;
     const strict_src_global src{pks + 8 * i, sigs + 16 * i, msgs + (uint64_t)msg_stride_words * i};
     const uint32_t kk = keys.vote_key ? keys.vote_key[i] : kNoKey;
-    const ge_cached* keytab = kk != kNoKey ? keys.tabs + kKeyTab * (uint64_t)kk : nullptr;
+    const ge_niels_pad* keytab = kk != kNoKey ? keys.tabs + kKeyTab * (uint64_t)kk : nullptr;
     // committee keys: [s]B - [k]A from comb tables, no ladder; others: the half-size ladder
     const int st = keytab ? strict_keyed_comb(src, g_consts.sk, bcomb_wide{bcomb}, keytab,
                                               keys.ok[kk])

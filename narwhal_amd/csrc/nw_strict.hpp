@@ -267,14 +267,14 @@ struct bcomb_lazy {
 };
 
 // Keyed strict verification: A is a committee key with comb tables keytab[129 t + j] =
-// j * 2^(8t) A (t = 0..31, nw_kernels.h kKeyTab), keyflags bit 0 = decoded, bit 1 = small
-// order. Then R' = [s]B - [k]A is 16 + 32 table additions with no doublings and no scalar
+// j * 2^(8t) A (t = 0..31, nw_kernels.h kKeyTab; affine niels), keyflags bit 0 = decoded,
+// bit 1 = small order. Then R' = [s]B - [k]A is 16 + 32 table additions with no doublings and no scalar
 // split, and the equation is dalek's own projective comparison R == R' (R decompressed,
 // Z = 1). Same checks and order as strict_verify_core; A is neither decompressed nor
 // tabulated per signature.
 template <class BComb, class Src>
 NW_HD int strict_keyed_comb(const Src& src, const strict_consts& K, const BComb& bc,
-                            const ge_cached* keytab, uint32_t keyflags) {
+                            const ge_niels_pad* keytab, uint32_t keyflags) {
   const bool okA = (keyflags & 1) != 0, smallA = (keyflags & 2) != 0;
   ge R;
   bool okR, smallR;
@@ -314,9 +314,9 @@ NW_HD int strict_keyed_comb(const Src& src, const strict_consts& K, const BComb&
   for (int t = 0; t < kStrictKeyTables; ++t) {
     const int d = (int)((sel8(kd, t >> 2) >> ((t & 3) * 8)) & 255u) - 128;
     if (d != 0) {
-      ge_cached e = keytab[129 * t + (d < 0 ? -d : d)];
-      ge_cached_cneg(e, d > 0);
-      ge_add_any(acc, acc, e, false, true);
+      ge_niels nb = keytab[129 * t + (d < 0 ? -d : d)].n;
+      ge_niels_cneg(nb, d > 0);
+      ge_add_niels(acc, acc, nb, true);
     }
   }
   // +[s]B
@@ -336,21 +336,17 @@ NW_HD int strict_keyed_comb(const Src& src, const strict_consts& K, const BComb&
 // Status of one strict verification. wave_max maps this lane's ladder length (in 4-bit
 // windows) to the wave's maximum (identity on the host). tabA/tabR: 8 entries each of
 // per-lane scratch. bt: j*B and j*2^128 B, j = 0..2^(BW-1) (btab_pair / btab_wide).
-// keytab (optional): A's pre-decompressed key table j*A, j = 0..128 (cached form) with
-// keyflags bit 0 = decoded, bit 1 = small order; then A is neither decompressed nor
-// tabulated here and u is taken in signed 8-bit windows over that table.
 template <int BW, class BTab, class Src, class WaveMax>
 NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab& bt,
                              ge_cached* tabA, ge_cached* tabR,
-                             WaveMax wave_max, const ge_cached* keytab = nullptr,
-                             uint32_t keyflags = 0) {
+                             WaveMax wave_max) {
   using BD = bdigits<BW>;
   // Decompress A, then R, in one rolled loop (one copy of the sqrt_ratio_i chain in the
   // code object): P, its small-order flag and its 8-entry table j * P. Only the point is
   // live here: the scalars are computed afterwards (register pressure).
-  bool okA = (keyflags & 1) != 0, smallA = (keyflags & 2) != 0, okR = false, smallR = false;
+  bool okA = false, smallA = false, okR = false, smallR = false;
 #pragma unroll 1
-  for (int pt = keytab ? 1 : 0; pt < 2; ++pt) {
+  for (int pt = 0; pt < 2; ++pt) {
     uint32_t x[8];
     if (pt) src.R(x); else src.A(x);
     ge P;
@@ -389,7 +385,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
 #pragma unroll
   for (int j = 0; j < 8; ++j) { ur.w[j] = h.u[j]; vr.w[j] = vm.w[j]; }
   uint32_t ud[8], vd[8], wd[8];
-  const uint32_t ubias = keytab ? 0x80808080u : 0x88888888u;
+  const uint32_t ubias = 0x88888888u;
   sc_recode(ud, ur, ubias);
   sc_recode(vd, vr, 0x88888888u);
   BD::recode(wd, w);
@@ -431,8 +427,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
     for (int slot = 0; slot < nslots; ++slot) {
       int d;
       if (slot == 0) {
-        d = !keytab ? digit4_of(ud, 8, j)
-                    : (j & 1) ? 0 : (int)((sel8(ud, j >> 3) >> (((j >> 1) & 3) * 8)) & 255u) - 128;
+        d = digit4_of(ud, 8, j);
       } else if (slot == 1) {
         d = j < 40 ? digit4_of(vd, 5, j) : 0;
         if (h.vneg) d = -d;
@@ -444,9 +439,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
       if (d != 0) {
         const int ad = d < 0 ? -d : d;
         ge_cached e;
-        if (slot == 0 && keytab) {
-          e = keytab[ad];
-        } else if (slot < 2) {
+        if (slot < 2) {
           e = (slot == 0 ? tabA : tabR)[ad - 1];
         } else {
           bt((slot == 3 || !has0) ? 1 : 0, ad, e);

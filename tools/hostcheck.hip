@@ -156,7 +156,7 @@ int hc_verify_strict_keyed(const uint8_t pk[32], const uint8_t sig[64], const ui
   ge A;
   const bool dec = ge_frombytes(A, Aw, K);
   const uint32_t flags = (dec ? 1u : 0u) | (dec && ge_is_small_order(A) ? 2u : 0u);
-  static ge_cached tab[32 * 129];
+  static ge_niels_pad tab[32 * 129];
   ge base = A;
   for (int t = 0; t < 32; ++t) {
     if (t) for (int d = 0; d < 8; ++d) { ge x; ge_dbl(x, base, d == 7); base = x; }
@@ -165,7 +165,7 @@ int hc_verify_strict_keyed(const uint8_t pk[32], const uint8_t sig[64], const ui
     ge acc;
     ge_identity(acc);
     for (int j = 0; j <= 128; ++j) {
-      ge_to_cached(tab[129 * t + j], acc, K.d2);
+      ge_to_niels(tab[129 * t + j].n, acc, K.d2);
       ge nx;
       ge_add_cached(nx, acc, cb, true);
       acc = nx;
