@@ -189,14 +189,14 @@ def mutated_stream(N: int = 4, copies: int = 1, seed: int = 5):
     return com, pack(recs), np.array(exp_st, np.int32), np.array(exp_ix, np.uint64), cls_of
 
 
-def votes_case(N: int = 4, seed: int = 3):
+def votes_case(N: int = 4, seed: int = 3, count: int = 24):
     """Vote stream (Vote::verify): honest votes plus tampered / unknown-author ones.
     Returns (committee, packed votes, n, expected status)."""
     keys = O.keys(N)
     outsider = O.keypair_from_seed(bytes([0xA5]) * 32)
     rng = np.random.Generator(np.random.PCG64(seed))
     ids, rounds, origins, authors, sigs, exp = [], [], [], [], [], []
-    for i in range(24):
+    for i in range(count):
         hid = rng.bytes(32)
         rnd = int(rng.integers(0, 2**63))
         origin = keys[i % N][0]

@@ -82,6 +82,14 @@ def test_votes_vs_oracle():
     assert st.tolist() == exp.tolist() == O.votes_verify_many(com, p, n).tolist()
 
 
+def test_votes_keyed_comb_many_vs_oracle():
+    """Many votes of a 16-key committee through the keyed strict path (comb tables for the
+    keys and for B, no ladder): every status equals the oracle's Vote::verify."""
+    com, p, n, exp = votes_case(N=16, seed=21, count=3000)
+    st = M.verify_votes_many(_Com(com), p)
+    assert st.tolist() == exp.tolist() == O.votes_verify_many(com, p, n).tolist()
+
+
 def test_certificate_stream_large_committee_payload():
     keys = O.keys(50)
     s = W.certificate_stream(40, keys, oracle_sign_many, oracle_digest_many, payload=3, seed=9)
