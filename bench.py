@@ -54,6 +54,10 @@ MAC_PER_BATCH_ITEM_SMALL = 2000 * 64       # batch item, small n (certificate vo
 # mults) + <= 17 bucket additions (7 mults each) + its share of the key sums ~ 400 F_p mults;
 # the SURVEY small-n constant above describes per-certificate Straus, not this algorithm.
 MAC_PER_GROUP_VOTE = 400 * 64              # 25,600 MACs
+# Keyed strict verification (Header::verify by a committee key): R's
+# decompression (~265 F_p mults) + 48 comb-table additions (~7.5 each) ~ 650 F_p mults;
+# SURVEY's 204,800 describes an unkeyed ladder verification.
+MAC_PER_KEYED_STRICT = 650 * 64            # 41,600 MACs
 SHA_OPS_PER_BLOCK = 4800                   # int32 ops per 128-B block
 # Peaks (DESIGN.md "Measurement"): v_mad_u64_u32 issues at half rate on gfx950, so the spec
 # MAC peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz; the measured one is the microbenchmark's
@@ -464,15 +468,16 @@ def run_cert(args, dev, stream, rank, world, N: int, invalid: float = 0.0, strea
     ok = bool(torch.equal(st, exp_st) and torch.equal(ix, exp_ix))
     sec = elapsed / args.cert_steps
     mac_survey = MAC_PER_STRICT_VERIFY + q * MAC_PER_BATCH_ITEM_SMALL
-    mac_group = MAC_PER_STRICT_VERIFY + q * MAC_PER_GROUP_VOTE
+    mac_group = MAC_PER_KEYED_STRICT + q * MAC_PER_GROUP_VOTE
     ach = n * mac_group / (kernel_ms * 1e-3) / 1e12
     res = {"committee": N, "quorum": q, "certs_per_gpu": n, "unique_certs": uniq,
            "invalid_fraction": float((exp_st_u != 0).mean()),
            "certs_per_s": n * world / sec, "sig_checks_per_s": n * (q + 1) * world / sec,
            "ms_per_step": sec * 1e3,
            "achieved_TMAC_s": ach, "frac": ach / PEAK_TMAC, "frac_measured": ach / PEAK_TMAC_MEASURED,
-           "work_per_cert": f"{mac_group} MAC (strict header 204,800 + q x {MAC_PER_GROUP_VOTE} "
-                            f"per grouped vote: 1 R decompression + <= 17 bucket additions)",
+           "work_per_cert": f"{mac_group} MAC (keyed strict header {MAC_PER_KEYED_STRICT} + q x "
+                            f"{MAC_PER_GROUP_VOTE} per grouped vote: 1 R decompression + <= 17 "
+                            f"bucket additions)",
            "survey_TMAC_s": n * mac_survey / (kernel_ms * 1e-3) / 1e12,
            "survey_work_note": "SURVEY 8(d) small-n constant (per-certificate Straus, 128,000 "
                                "MAC/vote) overstates the grouped algorithm's work; not a roofline",
