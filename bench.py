@@ -92,15 +92,15 @@ def pmc_traffic(kernel: str, units: int):
 
 def pmc_issue_peak():
     """Issue-bound peak of k_verify_strict (verifies/s) from its committed PMC instruction mix
-    (profiles/r02c/pmc_mix.json, tools/pmc_mix.sh): per-verify 64-bit / 32-bit integer and
+    (profiles/r02d/pmc_mix.json, tools/pmc_mix.sh): per-verify 64-bit / 32-bit integer and
     other VALU lane-ops, each priced at its microbenchmarked issue rate
     (profiles/r01_ubench_valu_4wps.txt; 32-bit integer ops at the half rate, an upper bound
     on their cost). None when the profile is absent."""
     try:
-        m = json.load(open(os.path.join(ROOT, "profiles", "r02c", "pmc_mix.json")))
+        m = json.load(open(os.path.join(ROOT, "profiles", "r02d", "pmc_mix.json")))
     except (OSError, ValueError):
         return None, None
-    return m["issue_peak_verifies_per_s"], "profiles/r02c/pmc_mix.json"
+    return m["issue_peak_verifies_per_s"], "profiles/r02d/pmc_mix.json"
 
 
 # One wave per SIMD (config 3: 65,536 messages = 1,024 waves): a lone wave issues one VALU
