@@ -84,6 +84,12 @@ const char* nw_last_error(void);
 const char* nw_version(void);
 /* Wait for all work this thread queued on its device stream. */
 int nw_synchronize(void);
+/* Build, now, the per-device tables the engine otherwise builds on first use (the strict
+ * kernel's B tables, 2.15 GB, ~0.2 s; the keyed comb's B tables, 67 MB) on the calling
+ * thread's device, or on every device under NW_ALL_DEVICES. Optional: call it before
+ * capturing nw_dev_* calls into a hipGraph (a first use allocates) or to keep the first
+ * verification's latency low. */
+int nw_prepare(void);
 
 /* ---- host-buffer (blocking) entry points: the drop-in ------------------------------ */
 

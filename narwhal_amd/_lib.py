@@ -54,7 +54,7 @@ def lib() -> ctypes.CDLL:
     sig = {
         "nw_init": ([], I), "nw_device_count": ([], I), "nw_set_device": ([I], I),
         "nw_get_device": ([], I), "nw_last_error": ([], ctypes.c_char_p),
-        "nw_version": ([], ctypes.c_char_p), "nw_synchronize": ([], I),
+        "nw_version": ([], ctypes.c_char_p), "nw_synchronize": ([], I), "nw_prepare": ([], I),
         "nw_sha512_digest32_many": ([P, P, P, S, P], I),
         "nw_signature_verify": ([P, P, P], I),
         "nw_verify_strict_many": ([P, S, P, P, S, P, P], I),

@@ -207,6 +207,21 @@ const char* nw_last_error(void) { return t_state.err.c_str(); }
 
 const char* nw_version(void) { return "narwhal_amd 0.1.0 gfx950"; }
 
+int nw_prepare(void) {
+  int rc = ensure_init();
+  if (rc) return rc;
+  const int dev = t_state.device;
+  if (dev != NW_ALL_DEVICES && (dev < 0 || dev >= g_ndev))
+    return set_err(NW_E_INVALID_ARG, "bad device index");
+  for (int d = dev == NW_ALL_DEVICES ? 0 : dev; d < (dev == NW_ALL_DEVICES ? g_ndev : dev + 1);
+       ++d) {
+    rc = activate(d);
+    if (rc) return rc;
+    NW_HIP(nw::prepare_strict_tables(), "strict table build");
+  }
+  return 0;
+}
+
 int nw_synchronize(void) {
   DevCtx* c;
   int rc = begin(&c);

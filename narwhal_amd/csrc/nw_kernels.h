@@ -26,6 +26,8 @@ hipError_t launch_sha512_digest32(const uint8_t* data, const uint64_t* offsets,
 // tables; reusable across launches on one stream).
 size_t strict_workspace_bytes();
 // keys (optional): pre-decompressed key tables with vote_key = per-item key index.
+// Builds the current device's lazily built strict tables (nw_prepare).
+hipError_t prepare_strict_tables();
 hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
                                 const uint32_t* pks, const uint32_t* sigs, uint64_t n,
                                 int32_t* status, uint64_t* bitmap, void* workspace,

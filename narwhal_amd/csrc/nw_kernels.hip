@@ -477,6 +477,12 @@ static hipError_t btab_for_current_device(int which, const ge_niels_pad** out) {
   return hipSuccess;
 }
 
+hipError_t prepare_strict_tables() {
+  const ge_niels_pad* p = nullptr;
+  hipError_t e = btab_for_current_device(0, &p);
+  return e != hipSuccess ? e : btab_for_current_device(1, &p);
+}
+
 hipError_t upload_consts() {
   static dev_consts host;
   static std::once_flag once;

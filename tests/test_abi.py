@@ -28,6 +28,7 @@ def test_no_device_fails_loudly():
     L = _lib.lib()
     assert L.nw_init() == -2            # NW_E_NO_DEVICE
     assert L.nw_device_count() == 0
+    assert L.nw_prepare() == -2
     with pytest.raises(_lib.EngineError):
         C.Signature(bytes(32), bytes(32)).verify(C.Digest(bytes(32)), C.PublicKey(bytes(32)))
     with pytest.raises(_lib.EngineError):

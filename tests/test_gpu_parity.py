@@ -6,6 +6,7 @@ import hashlib
 import numpy as np
 import pytest
 
+from narwhal_amd import _lib
 from narwhal_amd import crypto as C
 from narwhal_amd import workloads as W
 from oracle import oracle as O
@@ -232,3 +233,24 @@ def test_keygen_and_sign_vs_oracle(golden):
     sig = C.Signature.new(d, sk)
     assert sig.flatten().hex() == golden["keys"]["hello_sig_key3"]
     sig.verify(d, pk)
+
+
+@pytest.mark.gpu
+def test_prepare_then_strict():
+    """nw_prepare builds the lazily built strict tables now (also under NW_ALL_DEVICES);
+    verification afterwards is unchanged."""
+    L = _lib.lib()
+    assert L.nw_prepare() == 0, L.nw_last_error()
+    assert L.nw_set_device(-1) == 0
+    try:
+        assert L.nw_prepare() == 0, L.nw_last_error()
+    finally:
+        assert L.nw_set_device(0) == 0
+    ks = O.keys(2)
+    d = O.digest32(b"prepare")
+    pks = np.array([np.frombuffer(ks[i % 2][0], np.uint8) for i in range(4)])
+    sigs = np.array([np.frombuffer(O.sign(ks[i % 2][1], d), np.uint8) for i in range(4)])
+    sigs[1, 40] ^= 4
+    st, _ = C.verify_strict_many(np.frombuffer(d, np.uint8), pks, sigs, shared_digest=True)
+    ref = O.verify_strict_many(np.frombuffer(d, np.uint8), pks, sigs, shared_msg=True)
+    assert np.array_equal(st, ref)
