@@ -49,6 +49,9 @@ struct SharedDev {
   void* ktabs = nullptr;       // committee key tables (grow-only)
   uint32_t* kok = nullptr;
   size_t kcap = 0;             // keys
+  uint32_t* ksaved = nullptr;  // the keys the tables were last built from (device)
+  uint32_t* kflag = nullptr;   // rebuild flag (device, written by k_key_cmp)
+  size_t ksaved_n = 0;         // their count; 0 = none
   hipEvent_t last = nullptr;   // completion of the last leased launch sequence
   bool last_valid = false;
 };
@@ -548,13 +551,17 @@ int cert_pipeline(const nw_committee& com, const nw_certificates& cs,
   uint32_t* kok = nullptr;
   void* sws = nullptr;
   int rc = lease.acquire(t_state.device, s);
-  if (!rc) rc = lease.key_tables(com.nauth, &ktabs_v, &kok);
+  uint32_t* ksaved = nullptr;
+  uint32_t* kflag = nullptr;
+  bool kforce = true;
+  if (!rc) rc = lease.key_tables(com.nauth, &ktabs_v, &kok, &ksaved, &kflag, &kforce);
   if (!rc) rc = lease.strict_ws(&sws);
   if (rc) return rc;
   nw::ge_niels_pad* ktabs = static_cast<nw::ge_niels_pad*>(ktabs_v);
   NW_HIP(nw::launch_key_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth, ktabs, kok,
-                               s),
+                               s, ksaved, kflag, kforce),
          "k_key_tables");
+  lease.keys_built(com.nauth);
   NW_HIP(nw::launch_cert_prepare(dc, ds, headers_only, w.hdr_digest, w.authors, w.cert_digest,
                                  w.pre1, w.pre2, w.idx1, w.idx2,
                                  headers_only ? nullptr : w.vote_key, w.author_key, s),
@@ -1061,26 +1068,37 @@ int Lease::strict_ws(void** out) {
   return 0;
 }
 
-int Lease::key_tables(size_t nkeys, void** tabs, uint32_t** ok) {
+int Lease::key_tables(size_t nkeys, void** tabs, uint32_t** ok, uint32_t** saved,
+                      uint32_t** flag, bool* force) {
   SharedDev& d = g_shared[dev_];
   if (nkeys > d.kcap || !d.ktabs) {
     // every earlier user of the old tables is ordered before d.last
     if (d.last_valid) (void)hipEventSynchronize(d.last);
     if (d.ktabs) (void)hipFree(d.ktabs);
     if (d.kok) (void)hipFree(d.kok);
+    if (d.ksaved) (void)hipFree(d.ksaved);
+    if (d.kflag) (void)hipFree(d.kflag);
     d.ktabs = nullptr;
-    d.kok = nullptr;
-    d.kcap = 0;
-    const size_t cap = nkeys < 16 ? 16 : nkeys;   // 660 KB of comb tables per key
+    d.kok = d.ksaved = d.kflag = nullptr;
+    d.kcap = d.ksaved_n = 0;
+    const size_t cap = nkeys < 16 ? 16 : nkeys;   // 528 KB of comb tables per key
     hipError_t e = hipMalloc(&d.ktabs, nw::key_tables_bytes(cap));
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.kok), 4 * cap);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.ksaved), 32 * cap);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.kflag), 4);
     if (e != hipSuccess) return ::set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (key tables)", e);
     d.kcap = cap;
   }
   *tabs = d.ktabs;
   *ok = d.kok;
+  if (saved) *saved = d.ksaved;
+  if (flag) *flag = d.kflag;
+  if (force) *force = d.ksaved_n != nkeys;
+  d.ksaved_n = 0;   // until keys_built: a failed launch leaves no tables to keep
   return 0;
 }
+
+void Lease::keys_built(size_t nkeys) { g_shared[dev_].ksaved_n = nkeys; }
 
 int Lease::release() {
   if (!held_) return 0;

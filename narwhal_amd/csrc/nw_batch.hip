@@ -1338,12 +1338,26 @@ size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems) {
 //               (t = 0..31) by 248 doublings; base[2 key] = A, base[2 key + 1] = 2^128 A
 //               for the group path, comb[32 key + t] for k_key_tabs.
 //   k_key_tabs  one lane per (key, table t, j): j * 2^(8t) A by double-and-add over j's bits.
+// One block: flag = force or (pks != saved); then saved = pks when they differ.
+__global__ __launch_bounds__(256) void k_key_cmp(const uint32_t* __restrict__ pks,
+                                                 uint32_t* __restrict__ saved, uint64_t nkeys,
+                                                 uint32_t force, uint32_t* __restrict__ flag) {
+  int diff = force ? 1 : 0;
+  for (uint64_t i = threadIdx.x; i < 8 * nkeys && !diff; i += blockDim.x)
+    diff = pks[i] != saved[i];
+  diff = __syncthreads_or(diff);
+  if (diff)
+    for (uint64_t i = threadIdx.x; i < 8 * nkeys; i += blockDim.x) saved[i] = pks[i];
+  if (threadIdx.x == 0) *flag = diff ? 1u : 0u;
+}
+
 __global__ __launch_bounds__(256) void k_key_base(const uint32_t* __restrict__ pks,
                                                   uint64_t nkeys, ge* __restrict__ base,
                                                   ge* __restrict__ comb,
-                                                  uint32_t* __restrict__ ok) {
+                                                  uint32_t* __restrict__ ok,
+                                                  const uint32_t* __restrict__ flag) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nkeys) return;
+  if (i >= nkeys || (flag && *flag == 0)) return;   // same committee: tables kept
   uint32_t Aw[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) Aw[j] = pks[8 * i + j];
@@ -1363,9 +1377,10 @@ __global__ __launch_bounds__(256) void k_key_base(const uint32_t* __restrict__ p
 }
 
 __global__ __launch_bounds__(256) void k_key_tabs(uint64_t nkeys, const ge* __restrict__ comb,
-                                                  ge_niels_pad* __restrict__ tabs) {
+                                                  ge_niels_pad* __restrict__ tabs,
+                                                  const uint32_t* __restrict__ flag) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= nkeys * kKeyTab) return;
+  if (g >= nkeys * kKeyTab || (flag && *flag == 0)) return;
   const uint64_t pt = g / 129;           // kKeyCombT * key + t
   const int j = (int)(g % 129);
   const ge P = comb[pt];
@@ -1392,14 +1407,18 @@ size_t key_tables_bytes(uint64_t nkeys) {
 }
 
 hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, ge_niels_pad* tabs, uint32_t* ok,
-                             hipStream_t stream) {
+                             hipStream_t stream, uint32_t* saved, uint32_t* flag, bool force) {
   if (nkeys == 0) return hipSuccess;
   ge* base = reinterpret_cast<ge*>(tabs + kKeyTab * nkeys);
   ge* comb = base + 2 * nkeys;
+  const uint32_t* fl = saved && flag ? flag : nullptr;
+  if (fl)
+    hipLaunchKernelGGL(k_key_cmp, dim3(1), dim3(256), 0, stream, pks, saved, nkeys,
+                       force ? 1u : 0u, flag);
   hipLaunchKernelGGL(k_key_base, dim3((unsigned)((nkeys + 63) / 64)), dim3(64), 0, stream, pks,
-                     nkeys, base, comb, ok);
+                     nkeys, base, comb, ok, fl);
   hipLaunchKernelGGL(k_key_tabs, dim3((unsigned)((nkeys * kKeyTab + 255) / 256)), dim3(256), 0,
-                     stream, nkeys, comb, tabs);
+                     stream, nkeys, comb, tabs, fl);
   return hipGetLastError();
 }
 

@@ -62,9 +62,13 @@ constexpr uint32_t kKeyTab = kKeyCombT * 129;      // entries per key: j * 2^(8t
 constexpr uint32_t kKeyHalf = 16 * 129;            // offset of the j * 2^128 A table
 // ok[key]: bit 0 = decompressed, bit 1 = small order (8A == identity)
 size_t key_tables_bytes(uint64_t nkeys);
-// tabs: key_tables_bytes(nkeys) of device memory; ok: nkeys words.
+// tabs: key_tables_bytes(nkeys) of device memory; ok: nkeys words. saved (nkeys x 8 words)
+// and flag (1 word), optional: the keys the tables were last built from; the tables are
+// rebuilt only when force or the keys differ (a device-side compare, so the call stays
+// asynchronous), and saved is updated — the committee of an epoch is tabulated once.
 hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, struct ge_niels_pad* tabs,
-                             uint32_t* ok, hipStream_t stream);
+                             uint32_t* ok, hipStream_t stream, uint32_t* saved = nullptr,
+                             uint32_t* flag = nullptr, bool force = true);
 size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems);
 // skip_group_ok (optional, device): batch b is settled (status Ok) when
 // skip_group_ok[b / skip_per_group] != 0 (launch_cert_groups).

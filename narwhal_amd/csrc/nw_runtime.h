@@ -45,8 +45,13 @@ class Lease {
   int acquire(int dev_index, hipStream_t stream);
   // The device's strict workspace (nw::strict_workspace_bytes(), allocated once).
   int strict_ws(void** out);
-  // Key tables for nkeys keys (grow-only): tabs (nw::key_tables_bytes) and ok words.
-  int key_tables(size_t nkeys, void** tabs, uint32_t** ok);
+  // Key tables for nkeys keys (grow-only): tabs (nw::key_tables_bytes) and ok words, plus
+  // the reuse state of nw::launch_key_tables: the device copy of the keys they were last
+  // built from, the rebuild flag word, and whether a rebuild is forced (new size/buffers).
+  int key_tables(size_t nkeys, void** tabs, uint32_t** ok, uint32_t** saved = nullptr,
+                 uint32_t** flag = nullptr, bool* force = nullptr);
+  // After a successful launch_key_tables: the saved keys now describe the tables.
+  void keys_built(size_t nkeys);
   // Record the chain event on the stream and unlock (idempotent). 0 or NW_E_DEVICE.
   int release();
 

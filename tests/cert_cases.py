@@ -189,10 +189,11 @@ def mutated_stream(N: int = 4, copies: int = 1, seed: int = 5):
     return com, pack(recs), np.array(exp_st, np.int32), np.array(exp_ix, np.uint64), cls_of
 
 
-def votes_case(N: int = 4, seed: int = 3, count: int = 24):
+def votes_case(N: int = 4, seed: int = 3, count: int = 24, keys=None):
     """Vote stream (Vote::verify): honest votes plus tampered / unknown-author ones.
-    Returns (committee, packed votes, n, expected status)."""
-    keys = O.keys(N)
+    Returns (committee, packed votes, n, expected status). keys: the committee's
+    (pk, sk) pairs (default: the first N fixture keys)."""
+    keys = O.keys(N) if keys is None else keys
     outsider = O.keypair_from_seed(bytes([0xA5]) * 32)
     rng = np.random.Generator(np.random.PCG64(seed))
     ids, rounds, origins, authors, sigs, exp = [], [], [], [], [], []

@@ -90,6 +90,18 @@ def test_votes_keyed_comb_many_vs_oracle():
     assert st.tolist() == exp.tolist() == O.votes_verify_many(com, p, n).tolist()
 
 
+def test_committee_tables_reused_and_rebuilt():
+    """Committee key tables are kept across calls with the same committee and rebuilt when
+    it changes (device-side compare): committees A, B (same size, other keys), A again,
+    each against the oracle."""
+    ka = [O.keypair_from_seed(bytes([i + 1]) * 32) for i in range(6)]
+    kb = [O.keypair_from_seed(bytes([i + 101]) * 32) for i in range(6)]
+    for keys, seed in ((ka, 31), (kb, 32), (ka, 33), (ka, 34)):
+        com, p, n, exp = votes_case(N=6, seed=seed, count=40, keys=keys)
+        st = M.verify_votes_many(_Com(com), p)
+        assert st.tolist() == exp.tolist() == O.votes_verify_many(com, p, n).tolist()
+
+
 def test_certificate_stream_large_committee_payload():
     keys = O.keys(50)
     s = W.certificate_stream(40, keys, oracle_sign_many, oracle_digest_many, payload=3, seed=9)
