@@ -2017,7 +2017,8 @@ hipError_t launch_cert_sgroups(const uint32_t* cert_digest, const uint64_t* cvo,
   // the 132 doublings are shared by as many votes as possible (balanced split per group);
   // fallback chunks as in launch_verify_batch
   const uint64_t target_lanes = 256ull * 4 * 2 * 64;
-  const uint64_t Cg = std::min<uint64_t>(32, std::max<uint64_t>(4, nvotes / target_lanes));
+  const uint64_t Cg = env_u64("NW_SGRP_CHUNK",
+                              std::min<uint64_t>(32, std::max<uint64_t>(4, nvotes / target_lanes)));
   const uint64_t kq = std::min(K, ncert) * qmax;
   const uint32_t nch = (uint32_t)std::min<uint64_t>(cap, std::max<uint64_t>(1, (kq + Cg - 1) / Cg));
   // Fallback chunks: only the failed groups' certificates run (about a fraction
