@@ -126,7 +126,8 @@ NW_HD void build_table8(ge_cached tab[8], const ge& P, const fe& d2) {
     ge_cached c = *t0;
     ge_add_cached(acc, acc, c, true);
 #else
-    ge_add_cached(acc, acc, c1, true);
+    // P is affine (Z = 1): 2 Z1 Z2 = 2 Z1, one multiplication fewer than a cached addition
+    ge_add_any(acc, acc, c1, true, true);
 #endif
     ge_to_cached(cj, acc, d2);
     tab[j - 1] = cj;
