@@ -466,15 +466,19 @@ size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
 // the same committee size then picks:
 //   big    Pippenger groups of ~32k votes (launch_cert_groups) while at most a quarter of
 //          them would fail at that p, 1 - (1 - p)^K <= 1/4;
-//   small  K-certificate keyed Straus groups with the fallback ladders run from the same
-//          per-vote items (launch_cert_sgroups), K cost-optimal at that p
-//          (cert_sgroup_size), when they beat every certificate's own ladder;
-//   per-certificate otherwise.
+//   keyed  otherwise: every vote through the keyed comb on its own (launch_votes_keyed, 48
+//          table additions, no doublings, nothing shared that a bad vote can spoil), then
+//          verify_batch for the certificates with a failing vote only;
+//   small  (NW_CERT_KEYED=0 instead of keyed, or when merging does not apply) K-certificate
+//          keyed Straus groups with the fallback ladders run from the same per-vote items
+//          (launch_cert_sgroups), K cost-optimal at that p (cert_sgroup_size), when they
+//          beat every certificate's own ladder; per-certificate otherwise.
 // Mid-size Pippenger groups do not help: a group's Pippenger tail (4,160 buckets, 33 window
 // sums, the Horner) is paid per group (at 1,024 votes per group N = 100 ran 3.2 M certs/s
 // all-valid against 5.7 M with 32k-vote groups). Verdicts do not depend on the choice
 // (DESIGN.md 2); NW_CERT_GROUP_VOTES fixes big groups of that size, NW_CERT_SMALL_K small
-// groups of K certificates, NW_CERT_MERGE=0 turns merging off.
+// groups of K certificates, NW_CERT_KEYED=1 the keyed checks, NW_CERT_MERGE=0 turns merging
+// off.
 constexpr uint32_t kGroupDefault = 32768;
 
 struct GroupPolicy {
@@ -580,9 +584,19 @@ int cert_pipeline(const nw_committee& com, const nw_certificates& cs,
     double p_cert = 0.0;
     uint64_t K = nw::cert_group_size(host_vote_offsets, n, com.nauth, z16 != nullptr, kGroupDefault);
     bool small = getenv("NW_CERT_SMALL_K") != nullptr;
-    if (!z16 && !small && !nw::cert_group_env_fixed()) {
+    const char* ke = getenv("NW_CERT_KEYED");
+    bool keyed = ke && atoi(ke) != 0;
+    if (!z16 && !small && !keyed && !nw::cert_group_env_fixed()) {
       p_cert = group_failure_rate(t_state.device, com.nauth, s, &fb_dev, &fb_cnt);
-      if (!K || 1.0 - std::pow(1.0 - p_cert, (double)K) > 0.25) small = true;
+      if (!K) small = true;   // merging does not apply; cert_sgroup_size decides
+      else if (1.0 - std::pow(1.0 - p_cert, (double)K) > 0.25) {
+        if (ke) small = true;   // NW_CERT_KEYED=0: the small-group policy instead
+        else keyed = true;
+      }
+    }
+    if (keyed) {
+      small = false;
+      K = 1;
     }
     if (small) {
       bool wins = false;
@@ -591,9 +605,17 @@ int cert_pipeline(const nw_committee& com, const nw_certificates& cs,
     }
     if (getenv("NW_DEBUG_GROUPS"))
       fprintf(stderr, "[narwhal_amd] certificates: n=%zu keys=%zu %s K=%llu p=%.4g\n", (size_t)n,
-              (size_t)com.nauth, small ? "small" : "big", (unsigned long long)K, p_cert);
+              (size_t)com.nauth, keyed ? "keyed" : small ? "small" : "big",
+              (unsigned long long)K, p_cert);
     uint32_t* group_ok = nullptr;
-    if (K && !small)
+    if (keyed) {
+      group_ok = static_cast<uint32_t*>(w.group_ws);
+      NW_HIP(nw::launch_votes_keyed(w.cert_digest, cs.vote_offsets, n,
+                                    reinterpret_cast<const uint32_t*>(cs.vote_pks),
+                                    reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
+                                    w.pre1, w.pre2, w.hdr_st, kt, group_ok, s),
+             "keyed vote checks");
+    } else if (K && !small)
       NW_HIP(nw::launch_cert_groups(w.cert_digest, cs.vote_offsets, host_vote_offsets, n,
                                     reinterpret_cast<const uint32_t*>(cs.vote_pks),
                                     reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
@@ -614,10 +636,12 @@ int cert_pipeline(const nw_committee& com, const nw_certificates& cs,
                                      reinterpret_cast<const uint32_t*>(cs.vote_pks),
                                      reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
                                      static_cast<const uint32_t*>(z16), key, w.batch_ws,
-                                     w.batch_st, w.batch_idx, s, &kt, group_ok, K),
+                                     w.batch_st, w.batch_idx, s, &kt, group_ok, K,
+                                     keyed ? std::max(p_cert, 1e-3) : 1.0),
              "verify_batch (votes)");
     if (fb_dev)
-      NW_HIP(nw::launch_group_feedback(group_ok, n, K, ((small ? 1u : 0u) << 24) | (uint32_t)K,
+      NW_HIP(nw::launch_group_feedback(group_ok, n, K,
+                                       ((keyed ? 2u : small ? 1u : 0u) << 24) | (uint32_t)K,
                                        w.batch_st, w.pre1, w.pre2, w.hdr_st, fb_cnt, fb_dev,
                                        s),
              "group feedback");

@@ -313,24 +313,13 @@ __global__ __launch_bounds__(256) void k_bv_expand(const uint64_t* __restrict__ 
 }
 
 // ------------------------------------------------------------------------------ items
-__global__ __launch_bounds__(256) void k_bv_items(
-    const uint32_t* __restrict__ digests, const uint64_t* __restrict__ offsets, uint64_t b0,
-    uint64_t b1, uint64_t i0, uint64_t i1, uint32_t pmin, const uint32_t* __restrict__ pks,
-    const uint32_t* __restrict__ sigs, const uint32_t* __restrict__ z16, z_key_t zkey,
-    bv_item* __restrict__ items, ge_cached* __restrict__ tabs, key_tables_t keys,
-    batch_skip_t sk) {
-  const uint64_t gi = i0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gi >= i1) return;
-  const uint64_t li = gi - i0;
+// Item gi (slot li = gi - i0) of batch lo: flags, scalars and the R (and A) tables.
+__device__ __forceinline__ void bv_item_build(
+    uint64_t gi, uint64_t li, uint64_t lo, const uint32_t* __restrict__ digests,
+    const uint32_t* __restrict__ pks, const uint32_t* __restrict__ sigs,
+    const uint32_t* __restrict__ z16, const z_key_t& zkey, bv_item* __restrict__ items,
+    ge_cached* __restrict__ tabs, const key_tables_t& keys) {
   const curve_consts& K = g_bc.k;
-  // batch of this item: largest b in [b0, b1) with offsets[b] <= gi
-  uint64_t lo = b0, hi = b1;
-  while (hi - lo > 1) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (offsets[mid] <= gi) lo = mid; else hi = mid;
-  }
-  if (offsets[lo + 1] - offsets[lo] >= pmin) return;   // k_pip_points
-  if (skipped(sk, lo)) return;
   uint32_t Aw[8], Rw[8], Sw[8], Mw[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -412,6 +401,44 @@ __global__ __launch_bounds__(256) void k_bv_items(
   }
   it.flags = flags;
   items[li] = it;
+}
+
+__global__ __launch_bounds__(256) void k_bv_items(
+    const uint32_t* __restrict__ digests, const uint64_t* __restrict__ offsets, uint64_t b0,
+    uint64_t b1, uint64_t i0, uint64_t i1, uint32_t pmin, const uint32_t* __restrict__ pks,
+    const uint32_t* __restrict__ sigs, const uint32_t* __restrict__ z16, z_key_t zkey,
+    bv_item* __restrict__ items, ge_cached* __restrict__ tabs, key_tables_t keys,
+    batch_skip_t sk) {
+  const uint64_t gi = i0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi >= i1) return;
+  // batch of this item: largest b in [b0, b1) with offsets[b] <= gi
+  uint64_t lo = b0, hi = b1;
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (offsets[mid] <= gi) lo = mid; else hi = mid;
+  }
+  if (offsets[lo + 1] - offsets[lo] >= pmin) return;   // k_pip_points
+  if (skipped(sk, lo)) return;
+  bv_item_build(gi, gi - i0, lo, digests, pks, sigs, z16, zkey, items, tabs, keys);
+}
+
+// The same items driven by the chunk list (k_bv_expand): lane = chunk * C + j. When a skip
+// list leaves only a few scattered batches to run (launch_votes_keyed's failed
+// certificates), a lane per vote would leave most waves with one or two live lanes each
+// paying a whole decompression and table build; here the live items are dense.
+__global__ __launch_bounds__(256) void k_bv_items_chunked(
+    const bv_chunk* __restrict__ chunks, uint32_t nchunks, const uint32_t* __restrict__ ctotal,
+    uint32_t C, const uint32_t* __restrict__ digests, uint64_t b0, uint64_t i0,
+    const uint32_t* __restrict__ pks, const uint32_t* __restrict__ sigs,
+    const uint32_t* __restrict__ z16, z_key_t zkey, bv_item* __restrict__ items,
+    ge_cached* __restrict__ tabs, key_tables_t keys) {
+  const uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t ci = l / C, j = l % C;
+  if (ci >= nchunks || ci >= *ctotal) return;   // host bound, device total
+  const bv_chunk ch = chunks[ci];
+  if (j >= ch.count) return;
+  const uint64_t gi = ch.start + j;
+  bv_item_build(gi, gi - i0, b0 + ch.batch, digests, pks, sigs, z16, zkey, items, tabs, keys);
 }
 
 // ------------------------------------------------------------------------------ chunks
@@ -1496,7 +1523,7 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                const uint32_t* z16, const z_key_t& zkey, void* workspace,
                                int32_t* status, uint64_t* fail_index, hipStream_t stream,
                                const key_tables_t* keys, const uint32_t* skip_group_ok,
-                               uint64_t skip_per_group) {
+                               uint64_t skip_per_group, double active_frac) {
   const key_tables_t kt = keys ? *keys : key_tables_t{nullptr, nullptr, nullptr};
   const batch_skip_t sk{skip_group_ok, skip_per_group ? skip_per_group : 1};
   if (nbatches == 0) return hipSuccess;
@@ -1505,9 +1532,16 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
   bv_layout(cap, static_cast<char*>(workspace), &w);
   // Chunk size: fill the chip (~2 waves per SIMD of chunk lanes) but share the 252
   // doublings over as many votes as possible.
+  // With a skip list only a fraction active_frac of the votes runs (the caller's estimate):
+  // chunks are then cut small enough (>= 4 votes) that those votes alone fill the chip — a
+  // 67-vote certificate in one chunk is one lane's 2,300 serial additions.
   const uint64_t target_lanes = 256ull * 4 * 2 * 64;
-  uint32_t C = (uint32_t)std::min<uint64_t>(kMaxChunk, std::max<uint64_t>(1, nitems / target_lanes));
+  const double frac = skip_group_ok ? std::min(1.0, std::max(1e-6, active_frac)) : 1.0;
+  const uint64_t run_votes = (uint64_t)(frac * (double)std::min(nitems, cap));
+  uint32_t C = (uint32_t)std::min<uint64_t>(
+      kMaxChunk, std::max<uint64_t>(skip_group_ok && frac < 1.0 ? 4 : 1, run_votes / target_lanes));
   C = (uint32_t)std::min<uint64_t>(kMaxChunk, env_u64("NW_BATCH_CHUNK", C));
+  const bool compact = skip_group_ok && frac < 1.0;   // items from the chunk list
   // Batches of at least pmin votes take the Pippenger path (NW_BATCH_PIPPENGER_MIN test
   // hook; never below kPipFloor, whose item slots are the smallest that hold the region).
   // With a skip list no batch may (launch_cert_groups only skips below pmin).
@@ -1551,7 +1585,12 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
     if (chunks)
       hipLaunchKernelGGL(k_bv_expand, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
                          stream, offsets, b, e - b, (uint32_t)chunks, w.chunk_start, w.chunks);
-    if (i1 > i0 && npip != e - b)
+    if (compact && chunks)
+      hipLaunchKernelGGL(k_bv_items_chunked, dim3((unsigned)((chunks * C + 255) / 256)),
+                         dim3(256), 0, stream, w.chunks, (uint32_t)chunks,
+                         w.chunk_start + (e - b), C, digests, b, i0, pks, sigs, z16, zkey,
+                         w.items, w.tabs, kt);
+    else if (i1 > i0 && npip != e - b && !compact)
       hipLaunchKernelGGL(k_bv_items, dim3((unsigned)((i1 - i0 + 255) / 256)), dim3(256), 0,
                          stream, digests, offsets, b, e, i0, i1, pmin, pks, sigs, z16, zkey,
                          w.items, w.tabs, kt, sk);

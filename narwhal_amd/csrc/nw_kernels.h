@@ -71,7 +71,8 @@ hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, struct ge_niel
                              uint32_t* flag = nullptr, bool force = true);
 size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems);
 // skip_group_ok (optional, device): batch b is settled (status Ok) when
-// skip_group_ok[b / skip_per_group] != 0 (launch_cert_groups).
+// skip_group_ok[b / skip_per_group] != 0 (launch_cert_groups, launch_votes_keyed);
+// active_frac: the caller's estimate of the fraction of votes not skipped (chunk sizing).
 hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                const uint64_t* host_offsets, uint64_t nbatches,
                                const uint32_t* pks, const uint32_t* sigs, uint64_t nitems,
@@ -79,7 +80,7 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                int32_t* status, uint64_t* fail_index, hipStream_t stream,
                                const key_tables_t* keys = nullptr,
                                const uint32_t* skip_group_ok = nullptr,
-                               uint64_t skip_per_group = 0);
+                               uint64_t skip_per_group = 0, double active_frac = 1.0);
 
 // Certificate::verify vote batches merged over groups of certificates (nw_batch.hip):
 // cert_group_size() = certificates per group, 0 when the merge does not apply;
@@ -124,6 +125,15 @@ hipError_t launch_cert_sgroups(const uint32_t* cert_digest, const uint64_t* cvo,
                                const key_tables_t& keys, uint32_t nkeys, uint64_t K,
                                double p_cert, int32_t* status, uint64_t* fail_index,
                                uint32_t** group_ok_out, hipStream_t stream);
+// Keyed vote checks (nw_kernels.hip): every undecided certificate's votes
+// through the keyed comb one by one; cert_ok[c] = 1 when all of them pass (then verify_batch
+// is Ok too), 0 otherwise. Follow with launch_verify_batch(skip_group_ok = cert_ok,
+// skip_per_group = 1). cert_ok: ncert words (the start of the group scratch). keys.vote_key
+// required.
+hipError_t launch_votes_keyed(const uint32_t* cert_digest, const uint64_t* cvo, uint64_t ncert,
+                              const uint32_t* pks, const uint32_t* sigs, uint64_t nvotes,
+                              const int32_t* pre1, const int32_t* pre2, const int32_t* hdr_st,
+                              const key_tables_t& keys, uint32_t* cert_ok, hipStream_t stream);
 
 // ---- primary messages (nw_cert.hip) ----------------------------------------------------
 struct cert_committee_t {

@@ -289,6 +289,48 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
   }
 }
 
+// Certificate votes checked one by one with the keyed comb (Certificate::verify's
+// Signature::verify_batch, messages.rs:212, for streams where merged groups keep failing).
+// A vote whose strict check passes satisfies R == [s]B - [k]A exactly, so its term of any
+// random linear combination vanishes: a certificate all of whose votes pass is Ok under
+// verify_batch too. Every other certificate keeps cert_ok = 0 and gets its own verify_batch
+// (launch_verify_batch with skip_group_ok = cert_ok, one certificate per group), so
+// statuses and fail indices are the per-certificate path's. Certificates already decided
+// by an earlier check are left alone (their batch status is never read).
+__global__ __launch_bounds__(256) void k_votes_keyed_init(const uint64_t* __restrict__ cvo,
+                                                          uint64_t ncert,
+                                                          uint32_t* __restrict__ cert_ok) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < ncert) cert_ok[c] = cvo[c + 1] > cvo[c] ? 1u : 0u;   // no votes: its own batch
+}
+
+__global__ __launch_bounds__(256) void k_votes_keyed(
+    const uint32_t* __restrict__ cert_digest, const uint64_t* __restrict__ cvo, uint64_t ncert,
+    const uint32_t* __restrict__ pks, const uint32_t* __restrict__ sigs, uint64_t nvotes,
+    const int32_t* __restrict__ pre1, const int32_t* __restrict__ pre2,
+    const int32_t* __restrict__ hdr_st, key_tables_t keys,
+    const ge_niels_pad* __restrict__ bcomb, uint32_t* __restrict__ cert_ok) {
+  const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= nvotes) return;
+  uint64_t lo = 0, hi = ncert;   // the certificate c with cvo[c] <= v < cvo[c + 1]
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) / 2;
+    if (cvo[mid] <= v) lo = mid;
+    else hi = mid;
+  }
+  const uint64_t c = lo;
+  if (pre1[c] != 0 || hdr_st[c] != 0 || pre2[c] != 0) return;
+  const uint32_t kk = keys.vote_key[v];
+  if (kk == kNoKey) {   // not a committee key (cannot happen for an undecided certificate)
+    cert_ok[c] = 0;
+    return;
+  }
+  const strict_src_global src{pks + 8 * v, sigs + 16 * v, cert_digest + 8 * c};
+  const int st = strict_keyed_comb(src, g_consts.sk, bcomb_wide{bcomb},
+                                   keys.tabs + kKeyTab * (uint64_t)kk, keys.ok[kk]);
+  if (st != NW_OK) cert_ok[c] = 0;   // same value from every failing lane
+}
+
 // ---------------------------------------------------------------------------------------
 // Key generation and signing (crypto::generate_keypair / Signature::new, lib.rs:167-191;
 // dalek Keypair::generate + ExpandedSecretKey::sign = RFC 8032)
@@ -557,6 +599,24 @@ hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
   hipLaunchKernelGGL(k_verify_strict, dim3(grid), dim3(256), 0, stream, msgs, msg_stride_words,
                      pks, sigs, n, status, bitmap, static_cast<ge_cached*>(workspace), kt, btw,
                      bcomb);
+  return hipGetLastError();
+}
+
+hipError_t launch_votes_keyed(const uint32_t* cert_digest, const uint64_t* cvo, uint64_t ncert,
+                              const uint32_t* pks, const uint32_t* sigs, uint64_t nvotes,
+                              const int32_t* pre1, const int32_t* pre2, const int32_t* hdr_st,
+                              const key_tables_t& keys, uint32_t* cert_ok, hipStream_t stream) {
+  if (ncert == 0) return hipSuccess;
+  if (!keys.vote_key || !keys.tabs || !keys.ok) return hipErrorInvalidValue;
+  const ge_niels_pad* bcomb = nullptr;
+  hipError_t eb = btab_for_current_device(1, &bcomb);
+  if (eb != hipSuccess) return eb;
+  hipLaunchKernelGGL(k_votes_keyed_init, dim3(grid_for(ncert, 256)), dim3(256), 0, stream, cvo,
+                     ncert, cert_ok);
+  if (nvotes)
+    hipLaunchKernelGGL(k_votes_keyed, dim3(grid_for(nvotes, 256)), dim3(256), 0, stream,
+                       cert_digest, cvo, ncert, pks, sigs, nvotes, pre1, pre2, hdr_st, keys, bcomb,
+                       cert_ok);
   return hipGetLastError();
 }
 

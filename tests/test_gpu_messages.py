@@ -301,9 +301,51 @@ def test_certificate_small_groups_early_failures(monkeypatch):
         assert st.tolist() == exp and ix.tolist() == expi, K
 
 
+@pytest.mark.parametrize("N,n", [(4, 6000), (10, 3000), (50, 800), (100, 600)])
+def test_certificate_keyed_votes_mixed_validity(monkeypatch, N, n):
+    """Keyed vote checks (launch_votes_keyed, NW_CERT_KEYED=1: every vote through the keyed
+    comb, then verify_batch only for certificates with a failing vote): about 1% of the
+    certificates carry one invalid vote of every class (workloads.mutate_votes); statuses
+    and indices equal the construction and the unmerged path; an honest stream is all Ok."""
+    from narwhal_amd import crypto as C
+    keys = O.keys(N)
+    s = W.certificate_stream(n, keys, lambda sk, m: C.sign_many(sk, m), oracle_digest_many,
+                             seed=300 + N)
+    bad = np.arange(5 % n, n, 89)
+    m, exp_st, exp_ix = W.mutate_votes(s, bad, seed=N + 3)
+    com = _Com(s["committee"])
+    monkeypatch.setenv("NW_CERT_KEYED", "1")
+    st, ix = M.verify_certificates_many(com, m, None)
+    assert st.tolist() == exp_st.tolist() and ix.tolist() == exp_ix.tolist()
+    st, _ = M.verify_certificates_many(com, s, None)
+    assert (st == 0).all()
+    monkeypatch.delenv("NW_CERT_KEYED")
+    monkeypatch.setenv("NW_CERT_MERGE", "0")
+    st0, ix0 = M.verify_certificates_many(com, m, None)
+    assert st0.tolist() == exp_st.tolist() and ix0.tolist() == exp_ix.tolist()
+
+
+def test_certificate_keyed_votes_early_failures(monkeypatch):
+    """Keyed vote checks over honest certificates mixed with every header-level, pre-check
+    and vote-level failure class (mutated_stream): statuses and indices equal the expected
+    per-certificate ones."""
+    from cert_cases import pack, unpack
+    from narwhal_amd import crypto as C
+    com, ms, exp_st, exp_ix, cls = mutated_stream(N=4, copies=12, seed=19)
+    honest = W.certificate_stream(600, O.keys(4), lambda sk, m: C.sign_many(sk, m),
+                                  oracle_digest_many, seed=23, n_votes=4)
+    hrec, mrec = unpack(honest), unpack(ms)
+    p = pack(hrec[:300] + mrec + hrec[300:])
+    exp = [0] * 300 + [int(x) for x in exp_st] + [0] * 300
+    expi = [0] * 300 + [int(x) for x in exp_ix] + [0] * 300
+    monkeypatch.setenv("NW_CERT_KEYED", "1")
+    st, ix = M.verify_certificates_many(_Com(com), p, None)
+    assert st.tolist() == exp and ix.tolist() == expi
+
+
 def test_certificate_groups_adaptive_repeated_calls():
     """Adaptive merging (nw_api.cpp group_failure_rate): a stream with ~1% failing
-    certificates moves from the big merged groups to small groups from the next call on (the
+    certificates moves from the big merged groups to keyed vote checks from the next call on (the
     measured rate makes most big groups fail), and back once an honest stream reports no
     failures; every call's statuses and indices equal the construction, whichever path ran."""
     from narwhal_amd import crypto as C
