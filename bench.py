@@ -643,6 +643,105 @@ def run_wire(args, dev, stream, rank, world, N: int = 4):
             "parity_check": "status and index of every frame's certificate == construction"}
 
 
+def run_service_latency(args, rank, world, N: int, cache=None):
+    """SURVEY 8(f) rank 1: the primary's Core::sanitize_certificate calls
+    Certificate::verify one certificate at a time (primary/src/core.rs:338-346). Here single
+    certificates arrive at a fixed offered rate (1k / 10k / 100k per second) and go through
+    the aggregating VerificationService (narwhal_amd/service.py: coalesced per max_delay
+    into nw_submit_certificates_verify_many jobs, completion by nw_job_notify); latency =
+    verdict time - scheduled arrival time, per certificate. 1 % of the certificates carry
+    one invalid vote; every (status, index) is checked against the construction. Beside it:
+    the CPU oracle's single-certificate Certificate::verify latency and rate on 1 thread
+    (the reference verifies inline on the single Core task)."""
+    import asyncio
+    from narwhal_amd import service as SV
+    uniq = args.service_unique
+    keys = [(bytes(pk), bytes(sd) + bytes(pk)) for sd, pk in
+            zip(W.fixture_seeds(N), C.keypair_from_seed_many(W.fixture_seeds(N)))]
+    s = W.certificate_stream(uniq, keys, lambda sk, m: C.sign_many(sk, m),
+                             lambda d, o: C.sha512_digest32_many(d, o[:-1], np.diff(o)),
+                             seed=300 + rank)
+    s, exp_st, exp_ix = W.mutate_votes(s, np.arange(50, uniq, 100), seed=N + 11)
+    hb, ho, vo = s["header_bytes"].tobytes(), s["header_offsets"], s["vote_offsets"]
+    rows = [SV.CertRow(hb[int(ho[i]):int(ho[i + 1])], int(s["payload_counts"][i]),
+                       s["ids"][i].tobytes(), s["header_sigs"][i].tobytes(),
+                       s["vote_pks"][int(vo[i]):int(vo[i + 1])].tobytes(),
+                       s["vote_sigs"][int(vo[i]):int(vo[i + 1])].tobytes(),
+                       int(vo[i + 1] - vo[i])) for i in range(uniq)]
+    expect = [(int(a), int(b)) for a, b in zip(exp_st, exp_ix)]
+
+    class _Com:
+        def packed(self):
+            return s["committee"]
+    com = _Com()
+
+    async def one_load(rate: float, seconds: float):
+        svc = SV.VerificationService(max_delay=args.service_delay)
+        loop = asyncio.get_running_loop()
+        total = max(1, int(rate * seconds))
+        lat = np.zeros(total)
+        ok = [True]
+        tasks = []
+
+        async def one(i, t_arr):
+            r = await svc.certificate_status(com, rows[i % uniq])
+            lat[i] = loop.time() - t_arr
+            if r != expect[i % uniq]:
+                ok[0] = False
+        # warm the committee's tables and the job pool (not timed)
+        await asyncio.gather(*[svc.certificate_status(com, rows[i]) for i in range(64)])
+        t0 = loop.time()
+        i = 0
+        while i < total:
+            now = loop.time()
+            while i < total and t0 + i / rate <= now:
+                tasks.append(loop.create_task(one(i, t0 + i / rate)))
+                i += 1
+            await asyncio.sleep(min(0.0002, max(0.0, t0 + i / rate - loop.time())))
+        await asyncio.gather(*tasks)
+        el = loop.time() - t0
+        await svc.drain()
+        return {"offered_certs_per_s": rate, "certs": total, "achieved_certs_per_s": total / el,
+                "p50_ms": float(np.percentile(lat, 50) * 1e3),
+                "p99_ms": float(np.percentile(lat, 99) * 1e3),
+                "max_ms": float(lat.max() * 1e3), "jobs": svc.jobs_submitted,
+                "certs_per_job": total / max(1, svc.jobs_submitted - 1),
+                "parity": "ok" if ok[0] else "FAIL"}
+
+    loads = [asyncio.run(one_load(r, min(args.service_seconds, 200_000 / r)))
+             for r in (1_000, 10_000, 100_000)]
+    res = {"committee": N, "quorum": int(W.quorum(N)), "max_delay_ms": args.service_delay * 1e3,
+           "invalid_fraction": float((exp_st != 0).mean()), "loads": loads,
+           "path": "asyncio VerificationService.certificate_status -> "
+                   "nw_submit_certificates_verify_many + nw_job_notify",
+           "parity": "ok" if all(x["parity"] == "ok" for x in loads) else "FAIL"}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        O = oracle_module()
+
+        def prefix(a, m):
+            return {"header_bytes": s["header_bytes"][int(ho[a]):int(ho[m])],
+                    "header_offsets": ho[a:m + 1] - ho[a], "payload_counts": s["payload_counts"][a:m],
+                    "ids": s["ids"][a:m], "header_sigs": s["header_sigs"][a:m],
+                    "vote_offsets": vo[a:m + 1] - vo[a],
+                    "vote_pks": s["vote_pks"][int(vo[a]):int(vo[m])],
+                    "vote_sigs": s["vote_sigs"][int(vo[a]):int(vo[m])]}
+        singles = [prefix(i, i + 1) for i in range(200)]
+        for p1 in singles[:5]:
+            O.certificates_verify_many(s["committee"], p1, nthreads=1)
+        secs = []
+        for p1 in singles:
+            t = time.perf_counter()
+            O.certificates_verify_many(s["committee"], p1, nthreads=1)
+            secs.append(time.perf_counter() - t)
+        res["cpu_oracle_one_thread"] = {
+            "p50_ms": float(np.percentile(secs, 50) * 1e3),
+            "p99_ms": float(np.percentile(secs, 99) * 1e3),
+            "certs_per_s": 1.0 / float(np.mean(secs)), "cores": 1, "kind": "port",
+            "sample": "200 single Certificate::verify calls (oracle certificates_verify_many, "
+                      "1 thread, per-certificate verify_batch as the reference)"}
+    return res
+
+
 def cpu_baseline_batch(sample, seconds: float):
     """Config 1 on the host: the oracle's verify_batch (the
     dalek-equivalent restatement, crypto/src/lib.rs:206-219) on the same 10k batch --
@@ -695,12 +794,61 @@ def cpu_baseline_strict(sample, seconds: float):
                        f"corpus, oracle verify_strict_many, {T} threads", run_s=secs), agree
 
 
+def summary(r: dict) -> dict:
+    """Compact digest of every leg, printed LAST in the JSON line (the driver keeps the
+    line's tail): headline, SHA-512, config 2 per committee (all-valid and 1 % invalid),
+    config 1, wire ingest and the certificate service's latency."""
+    def g(d, *ks):
+        for k in ks:
+            if not isinstance(d, dict) or k not in d:
+                return None
+            d = d[k]
+        return d
+
+    def rnd(x, n=3):
+        return None if x is None else round(float(x), n)
+    out = {"value": rnd(r.get("value"), 0), "unit": r.get("unit"), "parity": r.get("parity"),
+           "roofline_frac": rnd(g(r, "roofline", "frac")),
+           "issue_frac": rnd(g(r, "roofline", "issue_frac")),
+           "cpu_baseline": rnd(g(r, "cpu_baseline", "value"), 0)}
+    if "sha512" in r:
+        out["sha512"] = {"GB_s": rnd(g(r, "sha512", "GB_per_s"), 1),
+                         "hbm_frac": rnd(g(r, "sha512", "hbm_frac")),
+                         "issue_frac": rnd(g(r, "sha512", "issue_frac")),
+                         "cpu_GB_s": rnd(g(r, "sha512", "cpu_baseline", "value"), 2)}
+    for leg in ("cert_stream", "cert_stream_invalid", "cert_stream_alternating"):
+        if r.get(leg):
+            out[leg + "_Mcerts_s"] = {k: rnd(v.get("certs_per_s", 0) / 1e6, 2)
+                                      for k, v in r[leg].items()}
+    if r.get("cert_stream_invalid"):
+        out["cert_invalid_vs_all_valid"] = {k: rnd(v.get("vs_all_valid"))
+                                            for k, v in r["cert_stream_invalid"].items()}
+    if r.get("cert_stream"):
+        out["cert_cpu_certs_s"] = {k: rnd(g(v, "cpu_baseline", "value"), 0)
+                                   for k, v in r["cert_stream"].items()}
+    if "verify_batch_10k" in r:
+        b = r["verify_batch_10k"]
+        out["batch10k"] = {"latency_ms": rnd(b.get("latency_ms")),
+                           "resident_M_s": rnd(b.get("verifies_per_s_resident", 0) / 1e6, 1),
+                           "cpu_1thread_k_s": rnd(g(b, "cpu_baseline", "one_thread", "value")
+                                                  and g(b, "cpu_baseline", "one_thread", "value") / 1e3, 1)}
+    if "wire_ingest" in r:
+        out["wire_Mcerts_s"] = rnd(r["wire_ingest"].get("certs_per_s", 0) / 1e6, 2)
+    if r.get("service_latency"):
+        out["service"] = {k: {"p50_p99_ms": [[int(x["offered_certs_per_s"]), rnd(x["p50_ms"], 2),
+                                               rnd(x["p99_ms"], 2)] for x in v["loads"]],
+                              "cpu_1cert_ms": rnd(g(v, "cpu_oracle_one_thread", "p50_ms"), 2)}
+                          for k, v in r["service_latency"].items()}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["strict", "sha", "cert", "batch"], default="strict")
+    ap.add_argument("--workload", choices=["strict", "sha", "cert", "batch", "service"],
+                    default="strict")
     ap.add_argument("--items-per-gpu", type=int, default=12_500_000)
     ap.add_argument("--unique", type=int, default=1 << 18)
     ap.add_argument("--sha-batches", type=int, default=65536)
@@ -720,6 +868,13 @@ def main():
     ap.add_argument("--no-wire", action="store_true", help="skip the wire-ingest leg")
     ap.add_argument("--wire-frames", type=int, default=65536)
     ap.add_argument("--wire-steps", type=int, default=3)
+    ap.add_argument("--no-service", action="store_true",
+                    help="skip the certificate service latency leg")
+    ap.add_argument("--service-committees", default="4,50")
+    ap.add_argument("--service-unique", type=int, default=8192)
+    ap.add_argument("--service-seconds", type=float, default=1.0)
+    ap.add_argument("--service-delay", type=float, default=0.0005,
+                    help="VerificationService max_delay (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -855,6 +1010,13 @@ def main():
             result["wire_ingest"] = rw
             if rw["parity"] != "ok":
                 result["parity"] = "FAIL"
+        if not args.no_service:
+            result["service_latency"] = {}
+            for N in [int(x) for x in args.service_committees.split(",") if x]:
+                rs = run_service_latency(args, rank, world, N)
+                result["service_latency"][f"N{N}"] = rs
+                if rs["parity"] != "ok":
+                    result["parity"] = "FAIL"
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             cb, agree = cpu_baseline_strict(sample, args.cpu_seconds)
             result["cpu_baseline"] = cb
@@ -881,6 +1043,18 @@ def main():
                   "cert_stream": res, "cert_stream_invalid": res_bad,
                   "parity": "ok" if all(r["parity"] == "ok" for r in
                                         list(res.values()) + list(res_bad.values())) else "FAIL"}
+    elif args.workload == "service":
+        res = {f"N{N}": run_service_latency(args, rank, world, N)
+               for N in [int(x) for x in args.service_committees.split(",") if x]}
+        last = list(res.values())[-1]["loads"][-1]
+        result = {"metric": METRIC, "value": last["achieved_certs_per_s"], "unit": "certs/s",
+                  "n_gpus": world, "steps": 1, "warmup": 1, "ms_per_step": None,
+                  "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                  "dtype": "u32", "data": "synthetic",
+                  "config": {"workload": "certificate_service_latency",
+                             "parallelism": f"shard{world}"},
+                  "service_latency": res,
+                  "parity": "ok" if all(r["parity"] == "ok" for r in res.values()) else "FAIL"}
     elif args.workload == "batch":
         r1, bsample = run_batch10k(args, dev, stream, rank, world)
         result = {"metric": METRIC, "value": r1["verifies_per_s_resident"], "unit": "verifies/s",
@@ -911,6 +1085,7 @@ def main():
         }
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline_sha(s["sample"], min(3.0, args.cpu_seconds))
+    result["summary"] = summary(result)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

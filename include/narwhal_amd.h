@@ -86,9 +86,12 @@ const char* nw_version(void);
 int nw_synchronize(void);
 /* Build, now, the per-device tables the engine otherwise builds on first use (the strict
  * kernel's B tables, 2.15 GB, ~0.2 s; the keyed comb's B tables, 67 MB) on the calling
- * thread's device, or on every device under NW_ALL_DEVICES. Optional: call it before
- * capturing nw_dev_* calls into a hipGraph (a first use allocates) or to keep the first
- * verification's latency low. */
+ * thread's device, or on every device under NW_ALL_DEVICES. Optional: keeps the first
+ * verification's latency low. hipGraph capture: nw_dev_sha512_digest32_many,
+ * nw_dev_keypair_from_seed_many and nw_dev_sign_many may be captured (after one
+ * uncaptured call on the device); strict / Header / Vote / Certificate launches share
+ * per-device tables under an event chain that a graph replay would bypass, so they return
+ * NW_E_INVALID_ARG on a capturing stream. */
 int nw_prepare(void);
 
 /* ---- host-buffer (blocking) entry points: the drop-in ------------------------------ */
@@ -145,6 +148,8 @@ int nw_sign_many(const uint8_t* sks, size_t sk_stride, const uint8_t* digests,
  * the library writes them. A job is used by one thread at a time; jobs are independent.
  * The blocking calls above are exactly submit + wait + release. */
 typedef struct nw_job nw_job;
+struct nw_committee;
+struct nw_certificates;
 
 /* Signature::verify over n items (as nw_verify_strict_many). */
 int nw_submit_verify_strict(const uint8_t* digests, size_t digest_stride, const uint8_t* pks,
@@ -158,12 +163,32 @@ int nw_submit_verify_batch_many(const uint8_t* digests, const uint8_t* pks, cons
 int nw_submit_sha512_digest32_many(const uint8_t* data, const uint64_t* offsets,
                                    const uint64_t* lengths, size_t n, uint8_t* out32,
                                    nw_job** job);
+/* Header::verify / Vote::verify / Certificate::verify (as nw_headers_verify_many /
+ * nw_votes_verify_many / nw_certificates_verify_many below; the committee and every array
+ * are copied at submit). The non-blocking form of the primary's sanitize_header /
+ * sanitize_vote / sanitize_certificate (primary/src/core.rs:306-346), with the same device
+ * pipeline as the blocking and device entry points: the per-device committee key tables
+ * (kept across jobs while the committee is unchanged), certificate grouping and the shared
+ * strict workspace, all ordered by the device's lease. status_out is required. */
+int nw_submit_certificates_verify_many(const struct nw_committee* committee,
+                                       const struct nw_certificates* certs, const uint8_t* z16,
+                                       int32_t* status_out, uint64_t* index_out, nw_job** job);
+int nw_submit_headers_verify_many(const struct nw_committee* committee,
+                                  const struct nw_certificates* headers, int32_t* status_out,
+                                  uint64_t* index_out, nw_job** job);
+int nw_submit_votes_verify_many(const struct nw_committee* committee, const uint8_t* ids,
+                                const uint64_t* rounds, const uint8_t* origins,
+                                const uint8_t* authors, const uint8_t* sigs, size_t n,
+                                int32_t* status_out, nw_job** job);
 /* 1 = done (outputs written), 0 = still running, < 0 = runtime error. Never blocks. */
 int nw_job_poll(nw_job* job);
 /* Block until done (outputs written): 0 or a runtime error. */
 int nw_job_wait(nw_job* job);
 /* Call fn(arg) from a HIP runtime thread once the job's device work has finished (e.g. to
- * wake an async task, which then calls nw_job_poll). fn must not call into this library. */
+ * wake an async task, which then calls nw_job_poll). fn must not call into this library.
+ * fn runs exactly once whenever this returns 0, and never when it returns an error (on a
+ * fanned-out job: one part could not be armed; the parts already armed are disarmed), so
+ * the caller may free arg and fall back to nw_job_wait. */
 int nw_job_notify(nw_job* job, void (*fn)(void*), void* arg);
 /* Return the job's buffers to the pool (waits first if it is still running). */
 void nw_job_release(nw_job* job);

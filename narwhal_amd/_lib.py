@@ -76,6 +76,9 @@ def lib() -> ctypes.CDLL:
         "nw_submit_verify_strict": ([P, S, P, P, S, P, P, ctypes.POINTER(P)], I),
         "nw_submit_verify_batch_many": ([P, P, P, P, S, P, P, P, ctypes.POINTER(P)], I),
         "nw_submit_sha512_digest32_many": ([P, P, P, S, P, ctypes.POINTER(P)], I),
+        "nw_submit_certificates_verify_many": ([P, P, P, P, P, ctypes.POINTER(P)], I),
+        "nw_submit_headers_verify_many": ([P, P, P, P, ctypes.POINTER(P)], I),
+        "nw_submit_votes_verify_many": ([P, P, P, P, P, P, S, P, ctypes.POINTER(P)], I),
         "nw_job_poll": ([P], I), "nw_job_wait": ([P], I),
         "nw_job_notify": ([P, NOTIFY_FN, P], I), "nw_job_release": ([P], None),
         "nw_primary_messages_verify_wire": ([P, P, P, S, P, P, P], I),

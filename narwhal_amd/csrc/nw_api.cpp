@@ -13,12 +13,8 @@
 
 #include <atomic>
 #include <cmath>
-#include <condition_variable>
-#include <deque>
-#include <functional>
 #include <mutex>
 #include <string>
-#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -413,7 +409,9 @@ int nw_dev_verify_batch_many(const void* digests, const void* pks, const void* s
 
 // ------------------------------------------------------------------------------------
 // Primary messages: Header::verify / Vote::verify / Certificate::verify
-// (primary/src/messages.rs:48-67, 131-142, 189-215)
+// (primary/src/messages.rs:48-67, 131-142, 189-215). The device pipelines below serve the
+// device-pointer entry point here and the job entry points (nw_submit_certificates_* /
+// nw_submit_headers_* / nw_submit_votes_*, nw_jobs.cpp), which the blocking calls wrap.
 // ------------------------------------------------------------------------------------
 namespace {
 
@@ -529,13 +527,25 @@ double group_failure_rate(int dev, uint64_t nkeys, hipStream_t s, uint32_t** fb_
   return p.p;
 }
 
+}  // namespace
+
+namespace nw {
+namespace rt {
+
+size_t cert_workspace_bytes(size_t n, size_t nvotes) {
+  return cert_ws_layout(n, nvotes, nullptr, nullptr);
+}
+
 // The whole device pipeline; every pointer is a device pointer.
-int cert_pipeline(const nw_committee& com, const nw_certificates& cs,
+int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
                   const uint64_t* host_vote_offsets, int headers_only, const void* z16,
-                  const nw::z_key_t& key, void* workspace, int32_t* status, uint64_t* index,
+                  const uint8_t zkey32[32], void* workspace, int32_t* status, uint64_t* index,
                   hipStream_t s) {
   const uint64_t n = cs.n;
   if (n == 0) return 0;
+  nw::z_key_t key;
+  int rc = fill_key(key, zkey32);
+  if (rc) return rc;
   CertWs w;
   cert_ws_layout(n, headers_only ? 0 : cs.nvotes, static_cast<char*>(workspace), &w);
   nw::cert_committee_t dc{com.nauth, reinterpret_cast<const uint32_t*>(com.pks), com.stakes,
@@ -554,7 +564,7 @@ int cert_pipeline(const nw_committee& com, const nw_certificates& cs,
   void* ktabs_v = nullptr;
   uint32_t* kok = nullptr;
   void* sws = nullptr;
-  int rc = lease.acquire(t_state.device, s);
+  rc = lease.acquire(dev, s);
   uint32_t* ksaved = nullptr;
   uint32_t* kflag = nullptr;
   bool kforce = true;
@@ -587,7 +597,7 @@ int cert_pipeline(const nw_committee& com, const nw_certificates& cs,
     const char* ke = getenv("NW_CERT_KEYED");
     bool keyed = ke && atoi(ke) != 0;
     if (!z16 && !small && !keyed && !nw::cert_group_env_fixed()) {
-      p_cert = group_failure_rate(t_state.device, com.nauth, s, &fb_dev, &fb_cnt);
+      p_cert = group_failure_rate(dev, com.nauth, s, &fb_dev, &fb_cnt);
       if (!K) small = true;   // merging does not apply; cert_sgroup_size decides
       else if (1.0 - std::pow(1.0 - p_cert, (double)K) > 0.25) {
         if (ke) small = true;   // NW_CERT_KEYED=0: the small-group policy instead
@@ -651,7 +661,60 @@ int cert_pipeline(const nw_committee& com, const nw_certificates& cs,
   return lease.release();
 }
 
-int check_committee_host(const nw_committee* com) {
+// Vote::verify: k_vote_prepare (stake, Vote::digest, the author's committee index), then the
+// strict check with the committee's key tables — an author that is a committee member (the
+// only kind whose signature can decide a verdict) takes the ladder-free keyed comb.
+size_t votes_workspace_bytes(size_t n) {
+  const size_t m = n ? n : 1;
+  return a256(32 * m) + 4 * a256(4 * m) + a256(8 * ((m + 63) / 64));
+}
+
+int votes_pipeline(int dev, const nw_committee& com, size_t n, const uint8_t* ids,
+                   const uint64_t* rounds, const uint8_t* origins, const uint8_t* authors,
+                   const uint8_t* sigs, void* workspace, int32_t* status, hipStream_t s) {
+  if (n == 0) return 0;
+  char* p = static_cast<char*>(workspace);
+  uint32_t* d_dig = reinterpret_cast<uint32_t*>(p); p += a256(32 * n);
+  int32_t* d_pre = reinterpret_cast<int32_t*>(p); p += a256(4 * n);
+  int32_t* d_sst = reinterpret_cast<int32_t*>(p); p += a256(4 * n);
+  uint32_t* d_key = reinterpret_cast<uint32_t*>(p); p += a256(4 * n);
+  p += a256(4 * n);
+  uint64_t* d_bm = reinterpret_cast<uint64_t*>(p);
+  nw::cert_committee_t dc{com.nauth, reinterpret_cast<const uint32_t*>(com.pks), com.stakes,
+                          com.worker_offsets, com.worker_ids};
+  NW_HIP(nw::launch_vote_prepare(dc, n, reinterpret_cast<const uint32_t*>(ids), rounds,
+                                 reinterpret_cast<const uint32_t*>(origins),
+                                 reinterpret_cast<const uint32_t*>(authors), d_dig, d_pre, d_key,
+                                 s),
+         "k_vote_prepare");
+  nw::rt::Lease lease;
+  void* ktabs = nullptr;
+  uint32_t* kok = nullptr;
+  uint32_t* ksaved = nullptr;
+  uint32_t* kflag = nullptr;
+  bool kforce = true;
+  void* sws = nullptr;
+  int rc = lease.acquire(dev, s);
+  if (!rc) rc = lease.key_tables(com.nauth, &ktabs, &kok, &ksaved, &kflag, &kforce);
+  if (!rc) rc = lease.strict_ws(&sws);
+  if (rc) return rc;
+  NW_HIP(nw::launch_key_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth,
+                               static_cast<nw::ge_niels_pad*>(ktabs), kok, s, ksaved, kflag,
+                               kforce),
+         "k_key_tables");
+  lease.keys_built(com.nauth);
+  const nw::key_tables_t kt{static_cast<nw::ge_niels_pad*>(ktabs), kok, d_key};
+  NW_HIP(nw::launch_verify_strict(d_dig, 8, reinterpret_cast<const uint32_t*>(authors),
+                                  reinterpret_cast<const uint32_t*>(sigs), n, d_sst, d_bm, sws, s,
+                                  &kt),
+         "k_verify_strict (votes)");
+  rc = lease.release();
+  if (rc) return rc;
+  NW_HIP(nw::launch_vote_finalize(n, d_pre, d_sst, status, s), "k_vote_finalize");
+  return 0;
+}
+
+int check_committee(const nw_committee* com) {
   if (!com || (com->nauth && (!com->pks || !com->stakes || !com->worker_offsets)))
     return set_err(NW_E_INVALID_ARG, "committee: null pointer");
   for (size_t a = 1; a < com->nauth; ++a)
@@ -665,48 +728,9 @@ int check_committee_host(const nw_committee* com) {
   return 0;
 }
 
-// Copies a host-memory committee into `p` (device), returns the device view.
-struct Stage {
-  char* p;
-  hipStream_t s;
-  int err = 0;
-  template <class T>
-  T* put(const T* src, size_t count) {
-    char* dst = p;
-    const size_t bytes = sizeof(T) * count;
-    if (bytes && !err) {
-      hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
-      if (e != hipSuccess) err = set_err(NW_E_DEVICE, "H2D staging", e);
-    }
-    p += a256(bytes ? bytes : 1);
-    return reinterpret_cast<T*>(dst);
-  }
-};
-
-size_t committee_bytes(const nw_committee* com) {
-  const size_t na = com->nauth, nw_ = com->nauth ? com->worker_offsets[com->nauth] : 0;
-  return a256(32 * na + 1) + a256(4 * na + 1) + a256(8 * (na + 1)) + a256(4 * nw_ + 1);
-}
-
-nw_committee stage_committee(Stage& st, const nw_committee* com) {
-  nw_committee d;
-  d.nauth = com->nauth;
-  const size_t nwk = com->nauth ? com->worker_offsets[com->nauth] : 0;
-  d.pks = st.put(com->pks, 32 * com->nauth);
-  d.stakes = st.put(com->stakes, com->nauth);
-  d.worker_offsets = st.put(com->worker_offsets, com->nauth + 1);
-  d.worker_ids = st.put(com->worker_ids, nwk);
-  return d;
-}
-
-int certs_host(const nw_committee* com, const nw_certificates* cs, int headers_only,
-               const uint8_t* z16, int32_t* status_out, uint64_t* index_out) {
-  DevCtx* c;
-  int rc = begin(&c);
-  if (rc) return rc;
-  if (!cs || !status_out) return set_err(NW_E_INVALID_ARG, "null pointer");
-  rc = check_committee_host(com);
-  if (rc) return rc;
+int check_certificates(const nw_certificates* cs, int headers_only, size_t* nvotes) {
+  *nvotes = 0;
+  if (!cs) return set_err(NW_E_INVALID_ARG, "null pointer");
   const size_t n = cs->n;
   if (n == 0) return 0;
   if (!cs->header_bytes || !cs->header_offsets || !cs->payload_counts || !cs->ids ||
@@ -720,196 +744,22 @@ int certs_host(const nw_committee* com, const nw_certificates* cs, int headers_o
     if (len < fixed || (len - fixed) % 32 != 0)
       return set_err(NW_E_INVALID_ARG, "header bytes do not match payload_counts");
   }
-  size_t nvotes = 0;
-  if (!headers_only) {
-    if (!cs->vote_offsets) return set_err(NW_E_INVALID_ARG, "vote_offsets is NULL");
-    if (cs->vote_offsets[0] != 0) return set_err(NW_E_INVALID_ARG, "vote_offsets[0] must be 0");
-    for (size_t i = 0; i < n; ++i)
-      if (cs->vote_offsets[i + 1] < cs->vote_offsets[i])
-        return set_err(NW_E_INVALID_ARG, "vote_offsets not monotone");
-    nvotes = cs->vote_offsets[n];
-    if (nvotes && (!cs->vote_pks || !cs->vote_sigs))
-      return set_err(NW_E_INVALID_ARG, "votes: null pointer");
-  }
-  const uint64_t hb0 = cs->header_offsets[0], hlen = cs->header_offsets[n] - hb0;
-  std::vector<uint64_t> ho(n + 1);
-  for (size_t i = 0; i <= n; ++i) ho[i] = cs->header_offsets[i] - hb0;
-  const size_t ws = cert_ws_layout(n, nvotes, nullptr, nullptr);
-  const size_t need = committee_bytes(com) + a256(hlen + 1) + a256(8 * (n + 1)) + a256(4 * n) +
-                      a256(32 * n) + a256(64 * n) + a256(8 * (n + 1)) + a256(32 * nvotes + 1) +
-                      a256(64 * nvotes + 1) + a256(16 * nvotes + 1) + a256(4 * n) +
-                      a256(8 * n) + a256(ws);
-  rc = reserve(*c, need);
-  if (rc) return rc;
-  hipStream_t s = c->stream;
-  Stage st{static_cast<char*>(c->dbuf), s};
-  nw_committee dcom = stage_committee(st, com);
-  nw_certificates d{};
-  d.n = n;
-  d.header_bytes = st.put(cs->header_bytes + hb0, hlen);
-  d.header_offsets = st.put(ho.data(), n + 1);
-  d.payload_counts = st.put(cs->payload_counts, n);
-  d.ids = st.put(cs->ids, 32 * n);
-  d.header_sigs = st.put(cs->header_sigs, 64 * n);
-  d.header_bytes_len = hlen;
-  const uint8_t* dz = nullptr;
-  if (!headers_only) {
-    d.vote_offsets = st.put(cs->vote_offsets, n + 1);
-    d.vote_pks = st.put(cs->vote_pks, 32 * nvotes);
-    d.vote_sigs = st.put(cs->vote_sigs, 64 * nvotes);
-    d.nvotes = nvotes;
-    if (z16) dz = st.put(z16, 16 * nvotes);
-  }
-  int32_t* dst = reinterpret_cast<int32_t*>(st.p); st.p += a256(4 * n);
-  uint64_t* dix = reinterpret_cast<uint64_t*>(st.p); st.p += a256(8 * n);
-  void* dws = st.p;
-  if (st.err) return st.err;
-  nw::z_key_t key;
-  rc = fill_key(key, nullptr);
-  if (rc) return rc;
-  rc = cert_pipeline(dcom, d, cs->vote_offsets, headers_only, dz, key, dws, dst, dix, s);
-  if (rc) return rc;
-  NW_HIP(hipMemcpyAsync(status_out, dst, 4 * n, hipMemcpyDeviceToHost, s), "D2H status");
-  if (index_out) NW_HIP(hipMemcpyAsync(index_out, dix, 8 * n, hipMemcpyDeviceToHost, s), "D2H index");
-  NW_HIP(hipStreamSynchronize(s), "sync");
-  return 0;
-}
-
-// ---- fan-out of the blocking message calls (nw_set_device(NW_ALL_DEVICES)) ----------
-// One persistent host worker thread per part (its thread-local stream and staging buffers
-// persist across calls); a call splits its messages into contiguous parts, runs part p on
-// worker p with device devs[p], waits for all and returns the first failure.
-class PartWorker {
- public:
-  PartWorker() : th_([this] { loop(); }) { th_.detach(); }
-  void post(std::function<void()> f) {
-    {
-      std::lock_guard<std::mutex> g(m_);
-      q_.push_back(std::move(f));
-    }
-    cv_.notify_one();
-  }
-
- private:
-  void loop() {
-    for (;;) {
-      std::function<void()> f;
-      {
-        std::unique_lock<std::mutex> g(m_);
-        cv_.wait(g, [this] { return !q_.empty(); });
-        f = std::move(q_.front());
-        q_.pop_front();
-      }
-      f();
-    }
-  }
-  std::mutex m_;
-  std::condition_variable cv_;
-  std::deque<std::function<void()>> q_;
-  std::thread th_;
-};
-
-PartWorker* part_worker(size_t p) {
-  static std::mutex m;
-  static PartWorker* w[kMaxDevices] = {};   // never destroyed (detached threads)
-  std::lock_guard<std::mutex> g(m);
-  if (!w[p]) w[p] = new PartWorker;
-  return w[p];
-}
-
-// fn(begin, end) for every non-empty part [b[p], b[p+1]) on its worker, the worker's
-// nw_set_device set to devs[p]; blocks until all parts are done.
-template <class Fn>
-int fan_out_blocking(const std::vector<int>& devs, const std::vector<size_t>& b, Fn fn) {
-  const size_t P = devs.size();
-  std::vector<int> rc(P, 0);
-  std::vector<std::string> err(P);
-  std::mutex m;
-  std::condition_variable cv;
-  size_t left = 0;
-  for (size_t p = 0; p < P; ++p) left += b[p + 1] > b[p];
-  for (size_t p = 0; p < P; ++p) {
-    if (b[p + 1] == b[p]) continue;
-    part_worker(p)->post([&, p] {
-      t_state.device = devs[p];
-      const int r = fn(b[p], b[p + 1]);
-      std::lock_guard<std::mutex> g(m);
-      rc[p] = r;
-      if (r < 0) err[p] = t_state.err;
-      if (--left == 0) cv.notify_all();
-    });
-  }
-  {
-    std::unique_lock<std::mutex> g(m);
-    cv.wait(g, [&] { return left == 0; });
-  }
-  for (size_t p = 0; p < P; ++p)
-    if (rc[p] < 0) return set_err(rc[p], err[p].c_str());
-  return 0;
-}
-
-// Contiguous parts of n messages with about equal weight (prefix sums w[0..n]).
-std::vector<size_t> parts_by_weight(size_t n, size_t P, const std::vector<uint64_t>& w) {
-  std::vector<size_t> b(P + 1, 0);
-  size_t i = 0;
-  for (size_t p = 1; p < P; ++p) {
-    const uint64_t target = w[n] * p / P;
-    while (i < n && w[i] < target) ++i;
-    b[p] = i;
-  }
-  b[P] = n;
-  return b;
-}
-
-int certs_fanout(const std::vector<int>& devs, const nw_committee* com, const nw_certificates* cs,
-                 int headers_only, const uint8_t* z16, int32_t* status_out, uint64_t* index_out) {
-  if (!cs || !status_out) return set_err(NW_E_INVALID_ARG, "null pointer");
-  const size_t n = cs->n;
-  if (!headers_only && n && !cs->vote_offsets)
-    return set_err(NW_E_INVALID_ARG, "vote_offsets is NULL");
-  std::vector<uint64_t> w(n + 1, 0);
+  if (headers_only) return 0;
+  if (!cs->vote_offsets) return set_err(NW_E_INVALID_ARG, "vote_offsets is NULL");
+  if (cs->vote_offsets[0] != 0) return set_err(NW_E_INVALID_ARG, "vote_offsets[0] must be 0");
   for (size_t i = 0; i < n; ++i)
-    w[i + 1] = w[i] + 1 + (headers_only ? 0 : cs->vote_offsets[i + 1] - cs->vote_offsets[i]);
-  return fan_out_blocking(devs, parts_by_weight(n, devs.size(), w), [&](size_t a, size_t e) {
-    nw_certificates part = *cs;
-    part.n = e - a;
-    part.header_offsets = cs->header_offsets + a;   // absolute: certs_host rebases
-    part.payload_counts = cs->payload_counts + a;
-    part.ids = cs->ids + 32 * a;
-    part.header_sigs = cs->header_sigs + 64 * a;
-    std::vector<uint64_t> vo;
-    const uint8_t* pz = z16;
-    if (!headers_only) {
-      const uint64_t v0 = cs->vote_offsets[a];
-      vo.resize(e - a + 1);
-      for (size_t i = a; i <= e; ++i) vo[i - a] = cs->vote_offsets[i] - v0;
-      part.vote_offsets = vo.data();
-      part.vote_pks = cs->vote_pks ? cs->vote_pks + 32 * v0 : nullptr;
-      part.vote_sigs = cs->vote_sigs ? cs->vote_sigs + 64 * v0 : nullptr;
-      if (z16) pz = z16 + 16 * v0;
-    }
-    return certs_host(com, &part, headers_only, pz, status_out + a,
-                      index_out ? index_out + a : nullptr);
-  });
+    if (cs->vote_offsets[i + 1] < cs->vote_offsets[i])
+      return set_err(NW_E_INVALID_ARG, "vote_offsets not monotone");
+  *nvotes = cs->vote_offsets[n];
+  if (*nvotes && (!cs->vote_pks || !cs->vote_sigs))
+    return set_err(NW_E_INVALID_ARG, "votes: null pointer");
+  return 0;
 }
 
-}  // namespace
+}  // namespace rt
+}  // namespace nw
 
 extern "C" {
-
-int nw_certificates_verify_many(const nw_committee* committee, const nw_certificates* certs,
-                                const uint8_t* z16, int32_t* status_out, uint64_t* index_out) {
-  const std::vector<int> devs = nw::rt::fanout_devices();
-  if (!devs.empty()) return certs_fanout(devs, committee, certs, 0, z16, status_out, index_out);
-  return certs_host(committee, certs, 0, z16, status_out, index_out);
-}
-
-int nw_headers_verify_many(const nw_committee* committee, const nw_certificates* headers,
-                           int32_t* status_out, uint64_t* index_out) {
-  const std::vector<int> devs = nw::rt::fanout_devices();
-  if (!devs.empty()) return certs_fanout(devs, committee, headers, 1, nullptr, status_out, index_out);
-  return certs_host(committee, headers, 1, nullptr, status_out, index_out);
-}
 
 size_t nw_dev_certificates_workspace(size_t n, size_t nvotes) {
   return cert_ws_layout(n, nvotes, nullptr, nullptr);
@@ -925,9 +775,6 @@ int nw_dev_certificates_verify_many(const nw_committee* committee, const nw_cert
   if (!committee || !certs || !workspace || !status_out)
     return set_err(NW_E_INVALID_ARG, "null pointer");
   if (certs->n == 0) return 0;
-  nw::z_key_t key;
-  rc = fill_key(key, zkey32);
-  if (rc) return rc;
   hipStream_t s = pick_stream(stream, c);
   std::vector<uint64_t> tmp;
   const uint64_t* hvo = nullptr;
@@ -937,75 +784,8 @@ int nw_dev_certificates_verify_many(const nw_committee* committee, const nw_cert
     if (hvo[0] != 0 || hvo[certs->n] != certs->nvotes)
       return set_err(NW_E_INVALID_ARG, "vote_offsets must run from 0 to nvotes");
   }
-  return cert_pipeline(*committee, *certs, hvo, headers_only, z16, key, workspace,
-                       status_out, index_out, s);
-}
-
-int nw_votes_verify_many(const nw_committee* committee, const uint8_t* ids,
-                         const uint64_t* rounds, const uint8_t* origins,
-                         const uint8_t* authors, const uint8_t* sigs, size_t n,
-                         int32_t* status_out) {
-  const std::vector<int> devs = nw::rt::fanout_devices();
-  if (!devs.empty()) {
-    if (n && (!ids || !rounds || !origins || !authors || !sigs || !status_out))
-      return set_err(NW_E_INVALID_ARG, "null pointer");
-    std::vector<uint64_t> w(n + 1);
-    for (size_t i = 0; i <= n; ++i) w[i] = i;
-    return fan_out_blocking(devs, parts_by_weight(n, devs.size(), w), [&](size_t a, size_t e) {
-      return nw_votes_verify_many(committee, ids + 32 * a, rounds + a, origins + 32 * a,
-                                  authors + 32 * a, sigs + 64 * a, e - a, status_out + a);
-    });
-  }
-  DevCtx* c;
-  int rc = begin(&c);
-  if (rc) return rc;
-  rc = check_committee_host(committee);
-  if (rc) return rc;
-  if (n == 0) return 0;
-  if (!ids || !rounds || !origins || !authors || !sigs || !status_out)
-    return set_err(NW_E_INVALID_ARG, "null pointer");
-  const size_t need = committee_bytes(committee) + a256(32 * n) + a256(8 * n) + a256(32 * n) +
-                      a256(32 * n) + a256(64 * n) + a256(32 * n) + 3 * a256(4 * n) +
-                      a256(8 * ((n + 63) / 64));
-  rc = reserve(*c, need);
-  if (rc) return rc;
-  hipStream_t s = c->stream;
-  Stage st{static_cast<char*>(c->dbuf), s};
-  nw_committee dcom = stage_committee(st, committee);
-  const uint8_t* d_id = st.put(ids, 32 * n);
-  const uint64_t* d_round = st.put(rounds, n);
-  const uint8_t* d_org = st.put(origins, 32 * n);
-  const uint8_t* d_au = st.put(authors, 32 * n);
-  const uint8_t* d_sig = st.put(sigs, 64 * n);
-  if (st.err) return st.err;
-  uint32_t* d_dig = reinterpret_cast<uint32_t*>(st.p); st.p += a256(32 * n);
-  int32_t* d_pre = reinterpret_cast<int32_t*>(st.p); st.p += a256(4 * n);
-  int32_t* d_sst = reinterpret_cast<int32_t*>(st.p); st.p += a256(4 * n);
-  int32_t* d_st = reinterpret_cast<int32_t*>(st.p); st.p += a256(4 * n);
-  uint64_t* d_bm = reinterpret_cast<uint64_t*>(st.p);
-  nw::cert_committee_t dc{dcom.nauth, reinterpret_cast<const uint32_t*>(dcom.pks), dcom.stakes,
-                          dcom.worker_offsets, dcom.worker_ids};
-  NW_HIP(nw::launch_vote_prepare(dc, n, reinterpret_cast<const uint32_t*>(d_id), d_round,
-                                 reinterpret_cast<const uint32_t*>(d_org),
-                                 reinterpret_cast<const uint32_t*>(d_au), d_dig, d_pre, s),
-         "k_vote_prepare");
-  {
-    nw::rt::Lease lease;
-    void* sws;
-    rc = lease.acquire(t_state.device, s);
-    if (!rc) rc = lease.strict_ws(&sws);
-    if (rc) return rc;
-    NW_HIP(nw::launch_verify_strict(d_dig, 8, reinterpret_cast<const uint32_t*>(d_au),
-                                    reinterpret_cast<const uint32_t*>(d_sig), n, d_sst, d_bm, sws,
-                                    s),
-           "k_verify_strict (votes)");
-    rc = lease.release();
-    if (rc) return rc;
-  }
-  NW_HIP(nw::launch_vote_finalize(n, d_pre, d_sst, d_st, s), "k_vote_finalize");
-  NW_HIP(hipMemcpyAsync(status_out, d_st, 4 * n, hipMemcpyDeviceToHost, s), "D2H status");
-  NW_HIP(hipStreamSynchronize(s), "sync");
-  return 0;
+  return nw::rt::cert_pipeline(t_state.device, *committee, *certs, hvo, headers_only, z16, zkey32,
+                               workspace, status_out, index_out, s);
 }
 
 }  // extern "C"
@@ -1063,6 +843,12 @@ int os_random(void* buf, size_t n) { return ::os_random(buf, n); }
 int Lease::acquire(int dev_index, hipStream_t stream) {
   if (held_) return ::set_err(NW_E_INVALID_ARG, "lease already held");
   if (dev_index < 0 || dev_index >= kMaxDevices) return ::set_err(NW_E_INVALID_ARG, "bad device");
+  // The event chain cannot be captured into a hipGraph (a replay would skip the lease and
+  // race other callers on the shared buffers): refuse, before taking the lock.
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone)
+    return ::set_err(NW_E_INVALID_ARG, "strict / Header / Vote / Certificate launches use the "
+                                       "device's shared tables and cannot be graph-captured");
   SharedDev& d = g_shared[dev_index];
   d.m.lock();
   dev_ = dev_index;

@@ -8,7 +8,8 @@
 //   k_cert_finalize   first failure in the reference's order, combining those checks with
 //                     the header's strict verdict (k_verify_strict) and the votes' batch
 //                     verdict (k_batch_*).
-//   k_vote_prepare    Vote::verify (131-153): stake(author) > 0 and Vote::digest.
+//   k_vote_prepare    Vote::verify (131-153): stake(author) > 0, Vote::digest and the
+//                     author's committee index (for the keyed comb).
 //   k_vote_finalize
 //
 // These are byte/integer bookkeeping kernels (a few hundred bytes per item); the
@@ -226,7 +227,8 @@ __global__ __launch_bounds__(256) void k_vote_prepare(cert_committee_t com, uint
                                                       const uint32_t* __restrict__ origins,
                                                       const uint32_t* __restrict__ authors,
                                                       uint32_t* __restrict__ digests,
-                                                      int32_t* __restrict__ pre) {
+                                                      int32_t* __restrict__ pre,
+                                                      uint32_t* __restrict__ author_key) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t id[8], org[8], au[8], d[8];
@@ -239,7 +241,10 @@ __global__ __launch_bounds__(256) void k_vote_prepare(cert_committee_t com, uint
   digest_72(d, id, rounds[i], org);
 #pragma unroll
   for (int j = 0; j < 8; ++j) digests[8 * i + j] = d[j];
-  pre[i] = committee_stake(com, committee_find(com, au)) == 0 ? NW_DAG_UNKNOWN_AUTHORITY : 0;
+  const int a = committee_find(com, au);
+  pre[i] = committee_stake(com, a) == 0 ? NW_DAG_UNKNOWN_AUTHORITY : 0;
+  // a member's signature is checked against its pre-decompressed key tables (keyed comb)
+  if (author_key) author_key[i] = a >= 0 ? (uint32_t)a : kNoKey;
 }
 
 __global__ __launch_bounds__(256) void k_vote_finalize(uint64_t n, const int32_t* __restrict__ pre,
@@ -279,10 +284,10 @@ hipError_t launch_cert_finalize(uint64_t n, int headers_only, const int32_t* pre
 hipError_t launch_vote_prepare(const cert_committee_t& com, uint64_t n, const uint32_t* ids,
                                const uint64_t* rounds, const uint32_t* origins,
                                const uint32_t* authors, uint32_t* digests, int32_t* pre,
-                               hipStream_t stream) {
+                               uint32_t* author_key, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_vote_prepare, dim3(blocks_for(n)), dim3(256), 0, stream, com, n, ids,
-                     rounds, origins, authors, digests, pre);
+                     rounds, origins, authors, digests, pre, author_key);
   return hipGetLastError();
 }
 

@@ -320,6 +320,167 @@ int submit_sha(int dev, const uint8_t* data, const uint64_t* offsets, const uint
   return 0;
 }
 
+// ---- primary messages ------------------------------------------------------------------
+// 256-byte aligned sections of a job's staging buffers (pinned and device share one layout).
+struct Packer {
+  size_t off = 0;
+  size_t add(size_t bytes) {
+    const size_t o = off;
+    off += a256(bytes ? bytes : 1);
+    return o;
+  }
+};
+
+void put(nw_job* j, size_t off, const void* src, size_t bytes) {
+  if (bytes) memcpy(j->hbuf + off, src, bytes);
+}
+
+// The committee's arrays in the staging buffer; returns its device view.
+struct CommitteeOffs {
+  size_t pks, stakes, wo, wi;
+};
+CommitteeOffs plan_committee(Packer& P, const nw_committee* com) {
+  const size_t na = com->nauth, nwk = na ? com->worker_offsets[na] : 0;
+  CommitteeOffs o;
+  o.pks = P.add(32 * na);
+  o.stakes = P.add(4 * na);
+  o.wo = P.add(8 * (na + 1));
+  o.wi = P.add(4 * nwk);
+  return o;
+}
+nw_committee stage_committee(nw_job* j, const CommitteeOffs& o, const nw_committee* com) {
+  const size_t na = com->nauth, nwk = na ? com->worker_offsets[na] : 0;
+  put(j, o.pks, com->pks, 32 * na);
+  put(j, o.stakes, com->stakes, 4 * na);
+  put(j, o.wo, com->worker_offsets, 8 * (na + 1));
+  put(j, o.wi, com->worker_ids, 4 * nwk);
+  nw_committee d;
+  d.nauth = na;
+  d.pks = reinterpret_cast<const uint8_t*>(j->dbuf + o.pks);
+  d.stakes = reinterpret_cast<const uint32_t*>(j->dbuf + o.stakes);
+  d.worker_offsets = reinterpret_cast<const uint64_t*>(j->dbuf + o.wo);
+  d.worker_ids = reinterpret_cast<const uint32_t*>(j->dbuf + o.wi);
+  return d;
+}
+
+// Header::verify / Certificate::verify over one device: the committee and the stream are
+// packed into the job's pinned buffer (one H2D copy), then the device pipeline
+// (nw::rt::cert_pipeline: shared lease, committee key tables kept across calls, adaptive
+// grouping) and one D2H copy of the statuses and indices.
+int submit_certs(int dev, const nw_committee* com, const nw_certificates* cs, int headers_only,
+                 const uint8_t* z16, int32_t* status_out, uint64_t* index_out, nw_job** job) {
+  size_t nv = 0;
+  int rc = nw::rt::check_committee(com);
+  if (!rc) rc = nw::rt::check_certificates(cs, headers_only, &nv);
+  if (rc) return rc;
+  if (cs->n && !status_out) return set_err(NW_E_INVALID_ARG, "null status_out");
+  nw_job* j;
+  rc = job_acquire(dev, &j);
+  if (rc) return rc;
+  const size_t n = cs->n;
+  if (n == 0) {
+    *job = j;
+    return 0;
+  }
+  const uint64_t hb0 = cs->header_offsets[0], hlen = cs->header_offsets[n] - hb0;
+  Packer P;
+  const CommitteeOffs oc = plan_committee(P, com);
+  const size_t o_hb = P.add(hlen), o_ho = P.add(8 * (n + 1)), o_pc = P.add(4 * n),
+               o_id = P.add(32 * n), o_hs = P.add(64 * n);
+  size_t o_vo = 0, o_vp = 0, o_vs = 0, o_z = 0;
+  if (!headers_only) {
+    o_vo = P.add(8 * (n + 1));
+    o_vp = P.add(32 * nv);
+    o_vs = P.add(64 * nv);
+    if (z16) o_z = P.add(16 * nv);
+  }
+  const size_t o_st = P.add(4 * n), o_ix = P.add(8 * n), out_end = P.off;
+  const size_t o_ws = P.add(nw::rt::cert_workspace_bytes(n, nv));
+  rc = job_reserve(j, out_end, P.off);
+  if (rc) return job_abort(j, rc);
+  const nw_committee dcom = stage_committee(j, oc, com);
+  put(j, o_hb, cs->header_bytes + hb0, hlen);
+  uint64_t* ho = reinterpret_cast<uint64_t*>(j->hbuf + o_ho);
+  for (size_t i = 0; i <= n; ++i) ho[i] = cs->header_offsets[i] - hb0;
+  put(j, o_pc, cs->payload_counts, 4 * n);
+  put(j, o_id, cs->ids, 32 * n);
+  put(j, o_hs, cs->header_sigs, 64 * n);
+  nw_certificates d{};
+  d.n = n;
+  d.header_bytes = reinterpret_cast<const uint8_t*>(j->dbuf + o_hb);
+  d.header_offsets = reinterpret_cast<const uint64_t*>(j->dbuf + o_ho);
+  d.payload_counts = reinterpret_cast<const uint32_t*>(j->dbuf + o_pc);
+  d.ids = reinterpret_cast<const uint8_t*>(j->dbuf + o_id);
+  d.header_sigs = reinterpret_cast<const uint8_t*>(j->dbuf + o_hs);
+  d.header_bytes_len = hlen;
+  const uint64_t* hvo = nullptr;
+  if (!headers_only) {
+    put(j, o_vo, cs->vote_offsets, 8 * (n + 1));
+    put(j, o_vp, cs->vote_pks, 32 * nv);
+    put(j, o_vs, cs->vote_sigs, 64 * nv);
+    if (z16) put(j, o_z, z16, 16 * nv);
+    d.vote_offsets = reinterpret_cast<const uint64_t*>(j->dbuf + o_vo);
+    d.vote_pks = reinterpret_cast<const uint8_t*>(j->dbuf + o_vp);
+    d.vote_sigs = reinterpret_cast<const uint8_t*>(j->dbuf + o_vs);
+    d.nvotes = nv;
+    hvo = reinterpret_cast<const uint64_t*>(j->hbuf + o_vo);   // read while planning only
+  }
+  rc = job_run(j, o_st, o_st, out_end - o_st, [&]() -> int {
+    return nw::rt::cert_pipeline(dev, dcom, d, hvo, headers_only, z16 ? j->dbuf + o_z : nullptr,
+                                 nullptr, j->dbuf + o_ws,
+                                 reinterpret_cast<int32_t*>(j->dbuf + o_st),
+                                 reinterpret_cast<uint64_t*>(j->dbuf + o_ix), j->stream);
+  });
+  if (rc) return job_abort(j, rc);
+  job_out(j, status_out, o_st, 4 * n);
+  job_out(j, index_out, o_ix, 8 * n);
+  *job = j;
+  return 0;
+}
+
+// Vote::verify over one device (nw::rt::votes_pipeline: committee members' signatures take
+// the keyed comb over the shared key tables).
+int submit_votes(int dev, const nw_committee* com, const uint8_t* ids, const uint64_t* rounds,
+                 const uint8_t* origins, const uint8_t* authors, const uint8_t* sigs, size_t n,
+                 int32_t* status_out, nw_job** job) {
+  int rc = nw::rt::check_committee(com);
+  if (rc) return rc;
+  if (n && (!ids || !rounds || !origins || !authors || !sigs || !status_out))
+    return set_err(NW_E_INVALID_ARG, "null pointer");
+  nw_job* j;
+  rc = job_acquire(dev, &j);
+  if (rc) return rc;
+  if (n == 0) {
+    *job = j;
+    return 0;
+  }
+  Packer P;
+  const CommitteeOffs oc = plan_committee(P, com);
+  const size_t o_id = P.add(32 * n), o_rd = P.add(8 * n), o_or = P.add(32 * n),
+               o_au = P.add(32 * n), o_sg = P.add(64 * n);
+  const size_t o_st = P.add(4 * n), out_end = P.off;
+  const size_t o_ws = P.add(nw::rt::votes_workspace_bytes(n));
+  rc = job_reserve(j, out_end, P.off);
+  if (rc) return job_abort(j, rc);
+  const nw_committee dcom = stage_committee(j, oc, com);
+  put(j, o_id, ids, 32 * n);
+  put(j, o_rd, rounds, 8 * n);
+  put(j, o_or, origins, 32 * n);
+  put(j, o_au, authors, 32 * n);
+  put(j, o_sg, sigs, 64 * n);
+  rc = job_run(j, o_st, o_st, out_end - o_st, [&]() -> int {
+    const auto* b = reinterpret_cast<const uint8_t*>(j->dbuf);
+    return nw::rt::votes_pipeline(dev, dcom, n, b + o_id,
+                                  reinterpret_cast<const uint64_t*>(b + o_rd), b + o_or,
+                                  b + o_au, b + o_sg, j->dbuf + o_ws,
+                                  reinterpret_cast<int32_t*>(j->dbuf + o_st), j->stream);
+  });
+  if (rc) return job_abort(j, rc);
+  job_out(j, status_out, o_st, 4 * n);
+  *job = j;
+  return 0;
+}
+
 // ---- fan-out --------------------------------------------------------------------------
 // Runs submit(device, begin, end, &job) for each non-empty part [b[p], b[p+1]) and returns a
 // parent over the parts (or, for a single device without NW_ALL_DEVICES, the job itself).
@@ -361,6 +522,51 @@ std::vector<size_t> weighted_bounds(size_t n, size_t P, const std::vector<uint64
   }
   b[P] = n;
   return b;
+}
+
+// Header / Certificate submits: one device, or whole messages per device with about equal
+// work (1 per header + 1 per vote).
+int submit_messages(const nw_committee* com, const nw_certificates* cs, int headers_only,
+                    const uint8_t* z16, int32_t* status_out, uint64_t* index_out,
+                    nw_job** job) {
+  const std::vector<int> devs = nw::rt::fanout_devices();
+  if (devs.empty()) {
+    int dev = 0;
+    int rc = nw::rt::select_device(&dev);
+    return rc ? rc : submit_certs(dev, com, cs, headers_only, z16, status_out, index_out, job);
+  }
+  size_t nv = 0;
+  int rc = nw::rt::check_committee(com);
+  if (!rc) rc = nw::rt::check_certificates(cs, headers_only, &nv);
+  if (rc) return rc;
+  const size_t n = cs->n;
+  std::vector<uint64_t> w(n + 1, 0);
+  for (size_t i = 0; i < n; ++i)
+    w[i + 1] = w[i] + 1 + (headers_only ? 0 : cs->vote_offsets[i + 1] - cs->vote_offsets[i]);
+  return fan_out(devs, weighted_bounds(n, devs.size(), w),
+                 [&](int dev, size_t a, size_t e, nw_job** sub) {
+                   nw_certificates part = *cs;
+                   part.n = e - a;
+                   part.header_offsets = cs->header_offsets + a;   // absolute: rebased
+                   part.payload_counts = cs->payload_counts + a;
+                   part.ids = cs->ids + 32 * a;
+                   part.header_sigs = cs->header_sigs + 64 * a;
+                   std::vector<uint64_t> vo;
+                   const uint8_t* pz = z16;
+                   if (!headers_only) {
+                     const uint64_t v0 = cs->vote_offsets[a];
+                     vo.resize(e - a + 1);
+                     for (size_t i = a; i <= e; ++i) vo[i - a] = cs->vote_offsets[i] - v0;
+                     part.vote_offsets = vo.data();   // copied into the part's staging
+                     part.vote_pks = cs->vote_pks ? cs->vote_pks + 32 * v0 : nullptr;
+                     part.vote_sigs = cs->vote_sigs ? cs->vote_sigs + 64 * v0 : nullptr;
+                     if (z16) pz = z16 + 16 * v0;
+                   }
+                   return submit_certs(dev, com, &part, headers_only, pz,
+                                       status_out ? status_out + a : nullptr,
+                                       index_out ? index_out + a : nullptr, sub);
+                 },
+                 job);
 }
 
 }  // namespace
@@ -453,6 +659,47 @@ int nw_submit_sha512_digest32_many(const uint8_t* data, const uint64_t* offsets,
                  job);
 }
 
+int nw_submit_certificates_verify_many(const nw_committee* committee,
+                                       const nw_certificates* certs, const uint8_t* z16,
+                                       int32_t* status_out, uint64_t* index_out, nw_job** job) {
+  if (!job) return set_err(NW_E_INVALID_ARG, "null job pointer");
+  *job = nullptr;
+  return submit_messages(committee, certs, 0, z16, status_out, index_out, job);
+}
+
+int nw_submit_headers_verify_many(const nw_committee* committee, const nw_certificates* headers,
+                                  int32_t* status_out, uint64_t* index_out, nw_job** job) {
+  if (!job) return set_err(NW_E_INVALID_ARG, "null job pointer");
+  *job = nullptr;
+  return submit_messages(committee, headers, 1, nullptr, status_out, index_out, job);
+}
+
+int nw_submit_votes_verify_many(const nw_committee* committee, const uint8_t* ids,
+                                const uint64_t* rounds, const uint8_t* origins,
+                                const uint8_t* authors, const uint8_t* sigs, size_t n,
+                                int32_t* status_out, nw_job** job) {
+  if (!job) return set_err(NW_E_INVALID_ARG, "null job pointer");
+  *job = nullptr;
+  if (n && (!ids || !rounds || !origins || !authors || !sigs || !status_out))
+    return set_err(NW_E_INVALID_ARG, "null pointer");
+  const std::vector<int> devs = nw::rt::fanout_devices();
+  if (devs.empty()) {
+    int dev = 0;
+    int rc = nw::rt::select_device(&dev);
+    return rc ? rc : submit_votes(dev, committee, ids, rounds, origins, authors, sigs, n,
+                                  status_out, job);
+  }
+  int rc = nw::rt::check_committee(committee);
+  if (rc) return rc;
+  return fan_out(devs, even_bounds(n, devs.size(), 1),
+                 [&](int dev, size_t a, size_t e, nw_job** sub) {
+                   return submit_votes(dev, committee, ids + 32 * a, rounds + a, origins + 32 * a,
+                                       authors + 32 * a, sigs + 64 * a, e - a, status_out + a,
+                                       sub);
+                 },
+                 job);
+}
+
 int nw_job_poll(nw_job* job) {
   if (!job) return set_err(NW_E_INVALID_ARG, "null job");
   if (!job->parts.empty()) {
@@ -489,16 +736,18 @@ int nw_job_wait(nw_job* job) {
 }
 
 namespace {
-// fn(arg) once every part of a fan-out job has finished (from the last part's callback)
+// fn(arg) once every part of a fan-out job has finished (from the last part's callback),
+// unless arming failed (cancelled: the last tick only frees the countdown).
 struct Countdown {
   std::atomic<int> left;
+  std::atomic<bool> cancelled{false};
   void (*fn)(void*);
   void* arg;
 };
 void countdown_tick(void* p) {
   Countdown* c = static_cast<Countdown*>(p);
   if (c->left.fetch_sub(1) == 1) {
-    c->fn(c->arg);
+    if (!c->cancelled.load()) c->fn(c->arg);
     delete c;
   }
 }
@@ -515,11 +764,14 @@ int nw_job_notify(nw_job* job, void (*fn)(void*), void* arg) {
     int first = 0;
     for (nw_job* x : job->parts) {
       const int rc = nw_job_notify(x, countdown_tick, c);
-      if (rc && !first) {
-        first = rc;
+      if (rc) {
+        if (!first) first = rc;
         countdown_tick(c);   // this part will never tick: count it now
       }
     }
+    // our hold (+1) keeps the count above zero until here, so no part's tick can have
+    // called fn yet: after an error, cancel before releasing it
+    if (first) c->cancelled.store(true);
     countdown_tick(c);
     return first;
   }
@@ -590,6 +842,30 @@ int nw_verify_batch_many(const uint8_t* digests, const uint8_t* pks, const uint8
   nw_job* j = nullptr;
   return run_blocking(nw_submit_verify_batch_many(digests, pks, sigs, offsets, nbatches, z16,
                                                   status_out, nullptr, &j),
+                      j);
+}
+
+int nw_certificates_verify_many(const nw_committee* committee, const nw_certificates* certs,
+                                const uint8_t* z16, int32_t* status_out, uint64_t* index_out) {
+  nw_job* j = nullptr;
+  return run_blocking(
+      nw_submit_certificates_verify_many(committee, certs, z16, status_out, index_out, &j), j);
+}
+
+int nw_headers_verify_many(const nw_committee* committee, const nw_certificates* headers,
+                           int32_t* status_out, uint64_t* index_out) {
+  nw_job* j = nullptr;
+  return run_blocking(nw_submit_headers_verify_many(committee, headers, status_out, index_out, &j),
+                      j);
+}
+
+int nw_votes_verify_many(const nw_committee* committee, const uint8_t* ids,
+                         const uint64_t* rounds, const uint8_t* origins,
+                         const uint8_t* authors, const uint8_t* sigs, size_t n,
+                         int32_t* status_out) {
+  nw_job* j = nullptr;
+  return run_blocking(nw_submit_votes_verify_many(committee, ids, rounds, origins, authors, sigs,
+                                                  n, status_out, &j),
                       j);
 }
 

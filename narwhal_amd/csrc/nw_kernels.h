@@ -167,7 +167,7 @@ hipError_t launch_cert_finalize(uint64_t n, int headers_only, const int32_t* pre
 hipError_t launch_vote_prepare(const cert_committee_t& com, uint64_t n, const uint32_t* ids,
                                const uint64_t* rounds, const uint32_t* origins,
                                const uint32_t* authors, uint32_t* digests, int32_t* pre,
-                               hipStream_t stream);
+                               uint32_t* author_key, hipStream_t stream);
 hipError_t launch_vote_finalize(uint64_t n, const int32_t* pre, const int32_t* sig_status,
                                 int32_t* status, hipStream_t stream);
 

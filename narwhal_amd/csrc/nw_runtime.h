@@ -3,8 +3,11 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
+#include <stdint.h>
 
 #include <vector>
+
+#include "narwhal_amd.h"
 
 namespace nw {
 namespace rt {
@@ -27,6 +30,26 @@ std::vector<int> fanout_devices();
 int set_err(int code, const char* what, hipError_t e = hipSuccess);
 // Fill buf from the OS CSPRNG (getrandom).
 int os_random(void* buf, size_t n);
+
+// ---- primary messages (nw_api.cpp), shared by the blocking, job and device entry points ----
+// Host-side argument checks of a host-memory committee / certificate stream (0 or
+// NW_E_INVALID_ARG with the error text set); *nvotes = vote_offsets[n] (0 for headers).
+int check_committee(const nw_committee* com);
+int check_certificates(const nw_certificates* cs, int headers_only, size_t* nvotes);
+// Device bytes of the Header / Certificate pipeline's scratch, and the pipeline itself on
+// library device dev (current for HIP): every pointer inside dcom / dcs and the buffers are
+// device pointers, host_vote_offsets the vote offsets in host memory (read during the call
+// only). Queues the whole check on `s` and returns without waiting.
+size_t cert_workspace_bytes(size_t n, size_t nvotes);
+int cert_pipeline(int dev, const nw_committee& dcom, const nw_certificates& dcs,
+                  const uint64_t* host_vote_offsets, int headers_only, const void* z16,
+                  const uint8_t zkey32[32], void* workspace, int32_t* status, uint64_t* index,
+                  hipStream_t s);
+// Vote::verify for n votes (device pointers), scratch = votes_workspace_bytes(n).
+size_t votes_workspace_bytes(size_t n);
+int votes_pipeline(int dev, const nw_committee& dcom, size_t n, const uint8_t* ids,
+                   const uint64_t* rounds, const uint8_t* origins, const uint8_t* authors,
+                   const uint8_t* sigs, void* workspace, int32_t* status, hipStream_t s);
 
 // Per-device buffers shared by every caller of the library (host-buffer jobs, blocking
 // calls and nw_dev_* calls on caller streams): the strict kernel's per-lane table workspace

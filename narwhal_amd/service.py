@@ -37,7 +37,7 @@ import numpy as np
 from . import _lib
 from ._lib import EngineError, check
 
-__all__ = ["Job", "GpuBackend", "VerificationService"]
+__all__ = ["Job", "GpuBackend", "VerificationService", "CertRow", "cert_row", "vote_row"]
 
 _P = ctypes.c_void_p
 
@@ -170,6 +170,92 @@ class GpuBackend:
         return Job(h, {"digests": out})
 
 
+    @staticmethod
+    def submit_certificates(committee: dict, certs: dict, z16: np.ndarray | None = None,
+                            headers_only: bool = False) -> Job:
+        """committee: messages.pack_committee arrays; certs: messages.pack_certificates
+        arrays -> outputs 'status' (NW_DAG_*), 'index'. Everything is copied at submit."""
+        from .messages import certificates_struct, committee_struct
+        n = len(certs["header_offsets"]) - 1
+        cc, cs = committee_struct(committee), certificates_struct(certs, n)
+        st = np.zeros(max(n, 1), np.int32)
+        ix = np.zeros(max(n, 1), np.uint64)
+        h = _P()
+        if headers_only:
+            check(_lib.lib().nw_submit_headers_verify_many(ctypes.byref(cc), ctypes.byref(cs),
+                                                           _ptr(st), _ptr(ix), ctypes.byref(h)),
+                  "nw_submit_headers_verify_many")
+        else:
+            z = None if z16 is None else np.ascontiguousarray(z16, np.uint8)
+            check(_lib.lib().nw_submit_certificates_verify_many(
+                ctypes.byref(cc), ctypes.byref(cs), _ptr(z), _ptr(st), _ptr(ix),
+                ctypes.byref(h)), "nw_submit_certificates_verify_many")
+        return Job(h, {"status": st[:n], "index": ix[:n]})
+
+    @staticmethod
+    def submit_votes(committee: dict, votes: dict, n: int) -> Job:
+        """votes: messages.pack_votes arrays (n votes) -> outputs 'status' (NW_DAG_*)."""
+        from .messages import committee_struct
+        cc = committee_struct(committee)
+        st = np.zeros(max(n, 1), np.int32)
+        h = _P()
+        check(_lib.lib().nw_submit_votes_verify_many(
+            ctypes.byref(cc), _ptr(votes["ids"]), _ptr(votes["rounds"]), _ptr(votes["origins"]),
+            _ptr(votes["authors"]), _ptr(votes["sigs"]), n, _ptr(st), ctypes.byref(h)),
+            "nw_submit_votes_verify_many")
+        return Job(h, {"status": st[:n]})
+
+
+# ---- one message, packed (the rows a flush concatenates) ------------------------------
+@dataclass
+class CertRow:
+    """One Header / Certificate in nw_certificates row form: the bytes `Hash for Header`
+    hashes (primary/src/messages.rs:70-84), its payload count, id, signature and votes."""
+    header_bytes: bytes
+    payload_count: int
+    id: bytes
+    signature: bytes
+    vote_pks: bytes = b""
+    vote_sigs: bytes = b""
+    nvotes: int = 0
+
+
+def cert_row(msg) -> CertRow:
+    """A messages.Certificate (or Header) as a CertRow."""
+    from .messages import Certificate
+    h = msg.header if isinstance(msg, Certificate) else msg
+    votes = msg.votes if isinstance(msg, Certificate) else []
+    return CertRow(h.digest_bytes(), len(h.payload), h.id.value, h.signature.flatten(),
+                   b"".join(pk.value for pk, _ in votes),
+                   b"".join(sg.flatten() for _, sg in votes), len(votes))
+
+
+def vote_row(v) -> tuple:
+    """A messages.Vote as (id, round, origin, author, signature) bytes/ints."""
+    return (v.id.value, int(v.round), v.origin.value, v.author.value, v.signature.flatten())
+
+
+def _pack_rows(rows: list[CertRow]) -> dict[str, np.ndarray]:
+    n = len(rows)
+    ho = np.zeros(n + 1, np.uint64)
+    ho[1:] = np.cumsum([len(r.header_bytes) for r in rows])
+    vo = np.zeros(n + 1, np.uint64)
+    vo[1:] = np.cumsum([r.nvotes for r in rows])
+
+    def cat(parts, w):
+        b = b"".join(parts)
+        return np.frombuffer(b or bytes(w), np.uint8).reshape(-1, w)
+    return {"header_bytes": np.frombuffer(b"".join(r.header_bytes for r in rows) or b"\0",
+                                          np.uint8),
+            "header_offsets": ho,
+            "payload_counts": np.array([r.payload_count for r in rows], np.uint32),
+            "ids": cat([r.id for r in rows], 32),
+            "header_sigs": cat([r.signature for r in rows], 64),
+            "vote_offsets": vo,
+            "vote_pks": cat([r.vote_pks for r in rows], 32),
+            "vote_sigs": cat([r.vote_sigs for r in rows], 64)}
+
+
 @dataclass
 class _Pending:
     payload: tuple
@@ -237,22 +323,80 @@ class VerificationService:
     verify(digest, pk, sig)          -> status of crypto::Signature::verify
     verify_batch(digest, votes)      -> status of crypto::Signature::verify_batch
     digest(message)                  -> 32-byte Digest(Sha512(message)[..32])
+    verify_certificate(committee, c) -> Certificate::verify (raises DagError)
+    verify_header(committee, h)      -> Header::verify (raises DagError)
+    verify_vote(committee, v)        -> Vote::verify (raises DagError)
+    certificate_status / header_status / vote_status -> the (NW_DAG_* status, index) pairs
 
     Requests issued concurrently (e.g. by many Core/Processor tasks) are coalesced: one
     device job per ``max_items`` items or per ``max_delay`` seconds, whichever comes first.
+    The message checks run the engine's committee-aware pipeline (primary/src/core.rs:306-346
+    sanitize_header / sanitize_vote / sanitize_certificate call these one message at a time
+    on the single Core task): requests for the same committee share one job, so the
+    committee's key tables, built once on the device, serve every message of it.
     ``backend`` is the device backend (GpuBackend by default).
     """
 
     def __init__(self, backend=None, max_items: int = 1 << 16, max_delay: float = 0.0005):
         self.backend = backend if backend is not None else GpuBackend()
+        self.max_items = max_items
+        self.max_delay = max_delay
         self._strict = _Aggregator(self._flush_strict, max_items, max_delay, lambda p: 1)
         self._batch = _Aggregator(self._flush_batch, max_items, max_delay,
                                   lambda p: max(1, len(p[1])))
         self._sha = _Aggregator(self._flush_sha, max_items, max_delay, lambda p: 1)
+        self._msg: dict[tuple, _Aggregator] = {}   # (kind, committee) -> aggregator
 
     @property
     def jobs_submitted(self) -> int:
-        return self._strict.jobs + self._batch.jobs + self._sha.jobs
+        return (self._strict.jobs + self._batch.jobs + self._sha.jobs
+                + sum(a.jobs for a in self._msg.values()))
+
+    def _msg_aggregator(self, kind: str, committee) -> _Aggregator:
+        key = (kind, id(committee))
+        a = self._msg.get(key)
+        if a is None:
+            packed = committee.packed()
+            if kind == "vote":
+                fn = lambda payloads: self._flush_votes(packed, payloads)   # noqa: E731
+                size = lambda p: 1                                        # noqa: E731
+            else:
+                fn = lambda payloads, h=(kind == "header"): self._flush_certs(  # noqa: E731
+                    packed, payloads, h)
+                size = lambda p: 1 + p[0].nvotes                          # noqa: E731
+            a = _Aggregator(fn, self.max_items, self.max_delay, size)
+            a.committee = committee            # keeps id(committee) from being reused
+            self._msg[key] = a
+        return a
+
+    # ---- primary messages ------------------------------------------------------------
+    async def certificate_status(self, committee, cert) -> tuple[int, int]:
+        """(status, index) of Certificate::verify; cert: messages.Certificate or CertRow."""
+        row = cert if isinstance(cert, CertRow) else cert_row(cert)
+        return await self._msg_aggregator("cert", committee).add((row,))
+
+    async def header_status(self, committee, header) -> tuple[int, int]:
+        row = header if isinstance(header, CertRow) else cert_row(header)
+        return await self._msg_aggregator("header", committee).add((row,))
+
+    async def vote_status(self, committee, vote) -> int:
+        row = vote if isinstance(vote, tuple) else vote_row(vote)
+        return await self._msg_aggregator("vote", committee).add((row,))
+
+    async def verify_certificate(self, committee, cert) -> None:
+        """Core::sanitize_certificate's check (messages.rs:189-215): None or DagError."""
+        from .messages import raise_for_status
+        st, ix = await self.certificate_status(committee, cert)
+        raise_for_status(st, ix, cert.header, None, cert.votes)
+
+    async def verify_header(self, committee, header) -> None:
+        from .messages import raise_for_status
+        st, ix = await self.header_status(committee, header)
+        raise_for_status(st, ix, header, None)
+
+    async def verify_vote(self, committee, vote) -> None:
+        from .messages import raise_for_status
+        raise_for_status(await self.vote_status(committee, vote), 0, None, vote)
 
     # ---- requests --------------------------------------------------------------------
     async def verify(self, digest: bytes, pk: bytes, sig: bytes) -> int:
@@ -267,7 +411,7 @@ class VerificationService:
         return await self._sha.add((bytes(message),))
 
     async def drain(self):
-        for a in (self._strict, self._batch, self._sha):
+        for a in (self._strict, self._batch, self._sha, *self._msg.values()):
             await a.drain()
 
     # ---- flushes: one device job per aggregated group --------------------------------
@@ -305,3 +449,23 @@ class VerificationService:
         out = await job.done()
         job.release()
         return [bytes(r) for r in out["digests"]]
+
+    async def _flush_certs(self, committee: dict, payloads: list[tuple], headers_only: bool):
+        job = self.backend.submit_certificates(committee, _pack_rows([p[0] for p in payloads]),
+                                               headers_only=headers_only)
+        out = await job.done()
+        job.release()
+        return [(int(s), int(i)) for s, i in zip(out["status"], out["index"])]
+
+    async def _flush_votes(self, committee: dict, payloads: list[tuple]):
+        rows = [p[0] for p in payloads]
+        n = len(rows)
+        v = {"ids": np.frombuffer(b"".join(r[0] for r in rows), np.uint8).reshape(n, 32),
+             "rounds": np.array([r[1] for r in rows], np.uint64),
+             "origins": np.frombuffer(b"".join(r[2] for r in rows), np.uint8).reshape(n, 32),
+             "authors": np.frombuffer(b"".join(r[3] for r in rows), np.uint8).reshape(n, 32),
+             "sigs": np.frombuffer(b"".join(r[4] for r in rows), np.uint8).reshape(n, 64)}
+        job = self.backend.submit_votes(committee, v, n)
+        out = await job.done()
+        job.release()
+        return [int(s) for s in out["status"]]

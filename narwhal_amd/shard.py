@@ -24,16 +24,20 @@ def shard_range(n: int, rank: int, world: int, align: int = 64) -> tuple[int, in
 
 def gather_bitmaps(local_words: torch.Tensor, n_total: int, world: int,
                    group=None) -> torch.Tensor | None:
-    """all_gather the u64 bitmap words of every rank's shard (int64 tensor, same device as
-    the process group's backend expects). Returns the concatenated bitmap as uint8
-    (ceil(n_total/8) bytes) on every rank."""
+    """all_gather the u64 bitmap words of every rank's shard (int64 tensor; on the device
+    for RCCL, which gathers device memory over xGMI directly; staged through host memory
+    for gloo). Returns the concatenated bitmap as uint8 (ceil(n_total/8) bytes) on every
+    rank, on local_words' device."""
     if world <= 1:
         return local_words.view(torch.uint8)[: (n_total + 7) // 8]
     sizes = [shard_range(n_total, r, world) for r in range(world)]
     max_words = max((e - s + 63) // 64 for s, e in sizes)
-    buf = torch.zeros(max_words, dtype=torch.int64, device=local_words.device)
+    comm_dev = local_words.device
+    if dist.get_backend(group) == "gloo" and comm_dev.type != "cpu":
+        comm_dev = torch.device("cpu")
+    buf = torch.zeros(max_words, dtype=torch.int64, device=comm_dev)
     buf[: local_words.numel()] = local_words
     out = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(out, buf, group=group)
     parts = [o[: (e - s + 63) // 64] for o, (s, e) in zip(out, sizes)]
-    return torch.cat(parts).view(torch.uint8)[: (n_total + 7) // 8]
+    return torch.cat(parts).to(local_words.device).view(torch.uint8)[: (n_total + 7) // 8]

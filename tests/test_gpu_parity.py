@@ -84,10 +84,24 @@ def test_strict_edge_corpus(golden):
 
 
 def test_strict_rfc8032_and_reference_keys(golden):
-    for v in golden["keys"]["rfc8032"]:
-        m = bytes.fromhex(v["msg"])
-        if len(m) != 32:
-            continue   # the engine signs/verifies 32-byte digests (crypto/src/lib.rs:200)
+    """RFC 8032 section 7.1 keys (libsodium-pinned in tests/test_oracle.py): the GPU derives
+    each RFC public key from its seed, and since Narwhal only ever signs 32-byte digests
+    (crypto/src/lib.rs:185-204), each RFC message goes in as Digest(Sha512(msg)[..32]): the
+    GPU signature over it equals the oracle's (RFC 8032 signing, pinned by libsodium),
+    verifies, and fails for the neighbouring key."""
+    vec = golden["keys"]["rfc8032"]
+    seeds = np.array([np.frombuffer(bytes.fromhex(v["seed"]), np.uint8) for v in vec])
+    pks = C.keypair_from_seed_many(seeds)
+    assert [p.tobytes().hex() for p in pks] == [v["pk"] for v in vec]
+    digs = np.array([np.frombuffer(O.digest32(bytes.fromhex(v["msg"])), np.uint8) for v in vec])
+    sigs = C.sign_many(np.concatenate([seeds, pks], axis=1), digs)
+    for v, d, sg in zip(vec, digs, sigs):
+        sk = bytes.fromhex(v["seed"]) + bytes.fromhex(v["pk"])
+        assert sg.tobytes() == O.sign(sk, d.tobytes())
+    st, _ = C.verify_strict_many(digs, pks, sigs)
+    assert st.tolist() == [0] * len(vec)
+    st, _ = C.verify_strict_many(digs, np.roll(pks, 1, axis=0), sigs)
+    assert all(x != 0 for x in st.tolist())
     ks = O.keys(4)
     d = C.Digest(O.digest32(b"Hello, world!"))
     sig = C.Signature.from_bytes(bytes.fromhex(golden["keys"]["hello_sig_key3"]))

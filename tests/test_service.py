@@ -66,6 +66,16 @@ class _OracleBackend:
         self.submits.append(("sha", len(lens)))
         return _OracleJob({"digests": O.sha512_digest32_many(data, offs, lens)})
 
+    def submit_certificates(self, com, certs, z16=None, headers_only=False):
+        n = len(certs["header_offsets"]) - 1
+        self.submits.append(("headers" if headers_only else "certs", n))
+        st, ix = O.certificates_verify_many(com, certs, z16, headers_only=headers_only)
+        return _OracleJob({"status": st, "index": ix})
+
+    def submit_votes(self, com, votes, n):
+        self.submits.append(("votes", n))
+        return _OracleJob({"status": O.votes_verify_many(com, votes, n)})
+
 
 # ------------------------------------------------------------------ CPU: aggregation
 def test_service_coalesces_concurrent_requests():
@@ -133,6 +143,91 @@ def test_service_device_failure_reaches_every_waiter():
 
     res = asyncio.run(main())
     assert all(isinstance(e, _lib.EngineError) for e in res)
+
+
+def _rows(s):
+    """A packed certificate stream as one CertRow per certificate."""
+    from cert_cases import unpack
+    return [S.CertRow(r["hb"], r["np"], r["id"], r["sig"], b"".join(pk for pk, _ in r["votes"]),
+                      b"".join(sg for _, sg in r["votes"]), len(r["votes"])) for r in unpack(s)]
+
+
+class _Committee:
+    def __init__(self, packed):
+        self._p = packed
+
+    def packed(self):
+        return self._p
+
+
+def test_service_coalesces_certificates_per_committee():
+    """Core::sanitize_certificate-style requests (one certificate each, many concurrent) are
+    coalesced into one job per committee; (status, index) per certificate == the oracle's
+    per-certificate Certificate::verify; votes and headers likewise."""
+    from cert_cases import mutated_stream, votes_case
+    com4, s4, st4, ix4, _ = mutated_stream(N=4, copies=2, seed=41)
+    com10, s10, st10, ix10, _ = mutated_stream(N=10, copies=1, seed=42)
+    vcom, vp, vn, vexp = votes_case(N=4, seed=43, count=12)
+    c4, c10, cv = _Committee(com4), _Committee(com10), _Committee(vcom)
+    r4, r10 = _rows(s4), _rows(s10)
+    votes = [(vp["ids"][i].tobytes(), int(vp["rounds"][i]), vp["origins"][i].tobytes(),
+              vp["authors"][i].tobytes(), vp["sigs"][i].tobytes()) for i in range(vn)]
+
+    async def main():
+        b = _OracleBackend()
+        svc = S.VerificationService(backend=b, max_delay=0.01)
+        got = await asyncio.gather(*[svc.certificate_status(c4, r) for r in r4],
+                                   *[svc.certificate_status(c10, r) for r in r10],
+                                   *[svc.header_status(c4, r) for r in r4],
+                                   *[svc.vote_status(cv, v) for v in votes])
+        return got, b.submits
+
+    got, submits = asyncio.run(main())
+    n4, n10 = len(r4), len(r10)
+    assert got[:n4] == [(int(a), int(b)) for a, b in zip(st4, ix4)]
+    assert got[n4:n4 + n10] == [(int(a), int(b)) for a, b in zip(st10, ix10)]
+    hst, hix = O.certificates_verify_many(com4, s4, headers_only=True)
+    assert got[n4 + n10:2 * n4 + n10] == [(int(a), int(b)) for a, b in zip(hst, hix)]
+    assert got[2 * n4 + n10:] == [int(x) for x in vexp]
+    assert sorted(submits) == sorted([("certs", n4), ("certs", n10), ("headers", n4),
+                                      ("votes", vn)])
+
+
+def test_service_verify_certificate_raises_dag_errors():
+    """verify_certificate / verify_header / verify_vote raise the reference's DagError
+    variants (primary/src/error.rs:26-59) exactly as Certificate/Header/Vote.verify do."""
+    from narwhal_amd import messages as M
+    from narwhal_amd.crypto import PublicKey, Signature
+    ks = O.keys(4)
+    com = M.Committee({PublicKey(pk): M.Authority(1) for pk, _ in ks})
+    h = M.Header(author=PublicKey(ks[0][0]), round=2)
+    h.id = M.Digest(O.digest32(h.digest_bytes()))
+    h.signature = Signature.from_bytes(O.sign(ks[0][1], h.id.value))
+    cert = M.Certificate(h)
+    cd = O.digest_72(h.id.value, h.round, h.author.value)        # Certificate::digest
+    cert.votes = [(PublicKey(pk), Signature.from_bytes(O.sign(sk, cd))) for pk, sk in ks[:3]]
+    reuse = M.Certificate(h, cert.votes[:2] + [cert.votes[0]])
+    short = M.Certificate(h, cert.votes[:2])
+    badsig = M.Certificate(h, cert.votes[:2] + [(cert.votes[2][0], Signature())])
+    vote = M.Vote(h.id, h.round, h.author, PublicKey(ks[1][0]),
+                  Signature.from_bytes(O.sign(ks[1][1], cd)))
+
+    async def main():
+        svc = S.VerificationService(backend=_OracleBackend(), max_delay=0.001)
+        await svc.verify_certificate(com, cert)
+        await svc.verify_header(com, h)
+        await svc.verify_vote(com, vote)
+        out = []
+        for c in (reuse, short, badsig):
+            try:
+                await svc.verify_certificate(com, c)
+                out.append(None)
+            except M.DagError as e:
+                out.append(type(e))
+        return out
+
+    assert asyncio.run(main()) == [M.AuthorityReuse, M.CertificateRequiresQuorum,
+                                   M.InvalidSignature]
 
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="CPU-only behaviour")
@@ -205,3 +300,107 @@ def test_blocking_calls_are_submit_plus_wait():
     assert np.array_equal(job.wait()["status"], st)
     job.release()
     assert np.array_equal(np.unpackbits(bm, bitorder="little")[:130].astype(bool), st == 0)
+
+
+# ------------------------------------------------------------------ GPU: message jobs
+def _zeroed(d):
+    for a in d.values():
+        a[...] = 0
+
+
+@pytest.mark.gpu
+def test_message_jobs_in_flight_vs_oracle():
+    """Certificate, Header and Vote jobs (nw_submit_certificates_verify_many /
+    nw_submit_headers_verify_many / nw_submit_votes_verify_many) in flight together, on two
+    committees, every input array overwritten right after its submit (copy-on-submit):
+    statuses and indices equal the oracle's, whichever grouping each job ran."""
+    from cert_cases import mutated_stream, oracle_digest_many, votes_case
+    from narwhal_amd import workloads as W
+    B = S.GpuBackend()
+    com4, s4, st4, ix4, _ = mutated_stream(N=4, copies=3, seed=51)
+    com10, s10, st10, ix10, _ = mutated_stream(N=10, copies=2, seed=52)
+    hst, hix = O.certificates_verify_many(com4, s4, headers_only=True)
+    vcom, vp, vn, vexp = votes_case(N=4, seed=53, count=64)
+    hon = W.certificate_stream(3000, O.keys(4), lambda sk, m: C.sign_many(sk, m),
+                               oracle_digest_many, seed=54)
+    m, mst, mix = W.mutate_votes(hon, np.arange(17, 3000, 100), seed=3)
+    expect = [(st4, ix4), (st10, ix10), (hst, hix), (vexp, None), (mst, mix)]
+    jobs = []
+    for com, s, kind in ((com4, s4, "c"), (com10, s10, "c"), (com4, s4, "h"), (vcom, vp, "v"),
+                         (m["committee"], m, "c")):
+        com = {k: np.array(v) for k, v in com.items()}
+        s = {k: np.array(v) for k, v in s.items() if k != "committee"}
+        if kind == "v":
+            jobs.append(B.submit_votes(com, s, vn))
+        else:
+            jobs.append(B.submit_certificates(com, s, headers_only=kind == "h"))
+        _zeroed(com)
+        _zeroed(s)                                   # caller reuses its buffers
+    assert all(j.poll() in (True, False) for j in jobs)
+    for j, (est, eix) in zip(jobs, expect):
+        out = j.wait()
+        assert out["status"].tolist() == [int(x) for x in est]
+        if eix is not None:
+            assert out["index"].tolist() == [int(x) for x in eix]
+        j.release()
+
+
+@pytest.mark.gpu
+def test_same_size_committees_switch_key_tables():
+    """Committees A, B (same size, other keys), A, A: the per-device key tables are reused
+    while the committee is unchanged and rebuilt when a same-size committee differs (the
+    device-side compare, k_key_cmp). Certificates, headers and votes of each against the
+    oracle with injected coefficients, plus the CSPRNG path against the same statuses."""
+    from cert_cases import oracle_digest_many, votes_case
+    from narwhal_amd import messages as M
+    from narwhal_amd import workloads as W
+    ka = [O.keypair_from_seed(bytes([i + 1]) * 32) for i in range(6)]
+    kb = [O.keypair_from_seed(bytes([i + 101]) * 32) for i in range(6)]
+    other = {id(ka): kb, id(kb): ka}
+    for keys, seed in ((ka, 61), (kb, 62), (ka, 63), (ka, 64)):
+        s = W.certificate_stream(40, keys, lambda sk, m: C.sign_many(sk, m), oracle_digest_many,
+                                 seed=seed)
+        # a quarter of the certificates carry one invalid vote; the honest ones pass only
+        # if this committee's tables (not the previous same-size committee's) are used
+        s2, _, _ = W.mutate_votes(s, np.arange(0, 40, 4), seed=seed)
+        com = _Committee(s["committee"])
+        z16 = np.random.Generator(np.random.PCG64(seed)).integers(
+            0, 256, size=(len(s2["vote_pks"]), 16), dtype=np.uint8)
+        st, ix = M.verify_certificates_many(com, s2, z16)
+        ost, oix = O.certificates_verify_many(s["committee"], s2, z16)
+        assert st.tolist() == ost.tolist() and ix.tolist() == oix.tolist()
+        st, ix = M.verify_certificates_many(com, s2, None)
+        assert st.tolist() == ost.tolist() and ix.tolist() == oix.tolist()
+        hs, hi = M.verify_headers_many(com, s2)
+        ohs, ohi = O.certificates_verify_many(s["committee"], s2, headers_only=True)
+        assert hs.tolist() == ohs.tolist() and hi.tolist() == ohi.tolist()
+        vcom, vp, vn, vexp = votes_case(N=6, seed=seed, count=40, keys=keys)
+        assert M.verify_votes_many(_Committee(vcom), vp).tolist() == vexp.tolist()
+        # votes by the OTHER committee's keys: unknown authorities here
+        ocom, op, on, _ = votes_case(N=6, seed=seed, count=12, keys=other[id(keys)])
+        assert (M.verify_votes_many(_Committee(vcom), op) == 17).all()
+
+
+@pytest.mark.gpu
+def test_service_messages_on_gpu_vs_oracle():
+    """The aggregating service's certificate / header / vote paths on the device: many
+    concurrent single-message requests become a few jobs; every (status, index) equals the
+    oracle's."""
+    from cert_cases import mutated_stream, votes_case
+    com4, s4, st4, ix4, _ = mutated_stream(N=4, copies=4, seed=71)
+    vcom, vp, vn, vexp = votes_case(N=4, seed=72, count=40)
+    c4, cv = _Committee(com4), _Committee(vcom)
+    rows = _rows(s4)
+    votes = [(vp["ids"][i].tobytes(), int(vp["rounds"][i]), vp["origins"][i].tobytes(),
+              vp["authors"][i].tobytes(), vp["sigs"][i].tobytes()) for i in range(vn)]
+
+    async def main():
+        svc = S.VerificationService(max_delay=0.002)
+        got = await asyncio.gather(*[svc.certificate_status(c4, r) for r in rows],
+                                   *[svc.vote_status(cv, v) for v in votes])
+        return got, svc.jobs_submitted
+
+    got, jobs = asyncio.run(main())
+    assert got[:len(rows)] == [(int(a), int(b)) for a, b in zip(st4, ix4)]
+    assert got[len(rows):] == [int(x) for x in vexp]
+    assert jobs <= 4

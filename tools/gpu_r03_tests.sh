@@ -1,0 +1,14 @@
+#!/bin/bash
+# GPU-box helper: the -m gpu suite, then the certificate-service latency leg.
+#   bash tools/gpu_r03_tests.sh OUTDIR [pytest -k expr]
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+OUT=${1:-gpurun_out/r03}; mkdir -p "$OUT"
+K=${2:-}
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread \
+  ${K:+-k "$K"} > "$OUT/pytest_gpu.log" 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 "$OUT/pytest_gpu.log"
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u bench.py --workload service > "$OUT/bench_service.json" 2> "$OUT/bench_service.log"
+rc=$?; echo "service bench rc=$rc"; exit $rc
