@@ -11,6 +11,7 @@
 #include <string.h>
 #include <sys/random.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <mutex>
@@ -423,18 +424,24 @@ struct CertWs {
   uint32_t* vote_key;
   uint32_t* author_key;
   void* group_ws;
+  uint32_t* vote_cert;
+  size_t batch_ws_bytes;
 };
 
 size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
   const size_t m = n ? n : 1;
-  const size_t sizes[15] = {a256(32 * m), a256(32 * m), a256(32 * m), a256(4 * m), a256(4 * m),
+  // the verify_batch workspace doubles as the keyed vote checks' scratch (they run first)
+  const size_t bws = nvotes ? a256(std::max(nw::batch_workspace_bytes(n, nvotes),
+                                            64 * nw::votes_keyed_bytes_per_vote()))
+                            : 256;
+  const size_t sizes[16] = {a256(32 * m), a256(32 * m), a256(32 * m), a256(4 * m), a256(4 * m),
                             a256(4 * m),  a256(4 * m),  a256(8 * m),  a256(8 * m), a256(8 * m),
-                            a256(8 * ((m + 63) / 64)),
-                            nvotes ? a256(nw::batch_workspace_bytes(n, nvotes)) : 256,
+                            a256(8 * ((m + 63) / 64)), bws,
                             a256(4 * (nvotes ? nvotes : 1)), a256(4 * m),
-                            nvotes ? a256(nw::cert_groups_bytes(n)) : 256};
-  size_t off[15], tot = 0;
-  for (int k = 0; k < 15; ++k) { off[k] = tot; tot += sizes[k]; }
+                            nvotes ? a256(nw::cert_groups_bytes(n)) : 256,
+                            a256(4 * (nvotes ? nvotes : 1))};
+  size_t off[16], tot = 0;
+  for (int k = 0; k < 16; ++k) { off[k] = tot; tot += sizes[k]; }
   if (w) {
     w->hdr_digest = reinterpret_cast<uint32_t*>(base + off[0]);
     w->authors = reinterpret_cast<uint32_t*>(base + off[1]);
@@ -451,6 +458,8 @@ size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
     w->vote_key = reinterpret_cast<uint32_t*>(base + off[12]);
     w->author_key = reinterpret_cast<uint32_t*>(base + off[13]);
     w->group_ws = base + off[14];
+    w->vote_cert = reinterpret_cast<uint32_t*>(base + off[15]);
+    w->batch_ws_bytes = bws;
   }
   return tot;
 }
@@ -578,7 +587,8 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
   lease.keys_built(com.nauth);
   NW_HIP(nw::launch_cert_prepare(dc, ds, headers_only, w.hdr_digest, w.authors, w.cert_digest,
                                  w.pre1, w.pre2, w.idx1, w.idx2,
-                                 headers_only ? nullptr : w.vote_key, w.author_key, s),
+                                 headers_only ? nullptr : w.vote_key, w.author_key,
+                                 headers_only ? nullptr : w.vote_cert, s),
          "k_cert_prepare");
   const nw::key_tables_t hk{ktabs, kok, w.author_key};
   NW_HIP(nw::launch_verify_strict(reinterpret_cast<const uint32_t*>(cs.ids), 8, w.authors,
@@ -620,10 +630,11 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
     uint32_t* group_ok = nullptr;
     if (keyed) {
       group_ok = static_cast<uint32_t*>(w.group_ws);
-      NW_HIP(nw::launch_votes_keyed(w.cert_digest, cs.vote_offsets, n,
+      NW_HIP(nw::launch_votes_keyed(w.cert_digest, cs.vote_offsets, n, w.vote_cert,
                                     reinterpret_cast<const uint32_t*>(cs.vote_pks),
                                     reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
-                                    w.pre1, w.pre2, w.hdr_st, kt, group_ok, s),
+                                    w.pre1, w.pre2, w.hdr_st, kt, group_ok, w.batch_ws,
+                                    w.batch_ws_bytes, s),
              "keyed vote checks");
     } else if (K && !small)
       NW_HIP(nw::launch_cert_groups(w.cert_digest, cs.vote_offsets, host_vote_offsets, n,

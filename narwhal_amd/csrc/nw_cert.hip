@@ -86,7 +86,8 @@ __global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com, cert
                                                       uint64_t* __restrict__ idx1,
                                                       uint64_t* __restrict__ idx2,
                                                       uint32_t* __restrict__ vote_key,
-                                                      uint32_t* __restrict__ author_key) {
+                                                      uint32_t* __restrict__ author_key,
+                                                      uint32_t* __restrict__ vote_cert) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cs.n) return;
   const uint8_t* h = cs.header_bytes + cs.header_offsets[i];
@@ -141,6 +142,8 @@ __global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com, cert
     // votes the loop below does not reach keep kNoKey (decompressed in the batch kernel)
     if (vote_key)
       for (uint64_t v = vb; v < ve; ++v) vote_key[v] = kNoKey;
+    if (vote_cert)   // each vote's certificate (the keyed vote checks run one lane per vote)
+      for (uint64_t v = vb; v < ve; ++v) vote_cert[v] = (uint32_t)i;
     uint32_t weight = 0;
     // `used` only ever holds names that passed the stake check, i.e. committee members, so
     // AuthorityReuse is "this committee index was seen before" (a bitmap for committees of
@@ -261,11 +264,11 @@ hipError_t launch_cert_prepare(const cert_committee_t& com, const cert_stream_t&
                                int headers_only, const uint32_t* hdr_digest, uint32_t* authors,
                                uint32_t* cert_digest, int32_t* pre1, int32_t* pre2,
                                uint64_t* idx1, uint64_t* idx2, uint32_t* vote_key,
-                               uint32_t* author_key, hipStream_t stream) {
+                               uint32_t* author_key, uint32_t* vote_cert, hipStream_t stream) {
   if (cs.n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_cert_prepare, dim3(blocks_for(cs.n)), dim3(256), 0, stream, com, cs,
                      headers_only, hdr_digest, authors, cert_digest, pre1, pre2, idx1, idx2,
-                     vote_key, author_key);
+                     vote_key, author_key, vote_cert);
   return hipGetLastError();
 }
 

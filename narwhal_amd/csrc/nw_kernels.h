@@ -126,14 +126,19 @@ hipError_t launch_cert_sgroups(const uint32_t* cert_digest, const uint64_t* cvo,
                                double p_cert, int32_t* status, uint64_t* fail_index,
                                uint32_t** group_ok_out, hipStream_t stream);
 // Keyed vote checks (nw_kernels.hip): every undecided certificate's votes
-// through the keyed comb one by one; cert_ok[c] = 1 when all of them pass (then verify_batch
-// is Ok too), 0 otherwise. Follow with launch_verify_batch(skip_group_ok = cert_ok,
-// skip_per_group = 1). cert_ok: ncert words (the start of the group scratch). keys.vote_key
-// required.
+// through the keyed comb one by one, R compared in compressed form (no decompression; the
+// x parities in batched inversions); cert_ok[c] = 1 when all of them pass (then
+// verify_batch is Ok too), 0 otherwise. Follow with launch_verify_batch(skip_group_ok =
+// cert_ok, skip_per_group = 1). vote_cert: certificate of each vote (k_cert_prepare);
+// cert_ok: ncert words; scratch: >= 64 x votes_keyed_bytes_per_vote() bytes (slices of the
+// votes go through it). keys.vote_key required.
+size_t votes_keyed_bytes_per_vote();
 hipError_t launch_votes_keyed(const uint32_t* cert_digest, const uint64_t* cvo, uint64_t ncert,
-                              const uint32_t* pks, const uint32_t* sigs, uint64_t nvotes,
-                              const int32_t* pre1, const int32_t* pre2, const int32_t* hdr_st,
-                              const key_tables_t& keys, uint32_t* cert_ok, hipStream_t stream);
+                              const uint32_t* vote_cert, const uint32_t* pks,
+                              const uint32_t* sigs, uint64_t nvotes, const int32_t* pre1,
+                              const int32_t* pre2, const int32_t* hdr_st,
+                              const key_tables_t& keys, uint32_t* cert_ok, void* scratch,
+                              size_t scratch_bytes, hipStream_t stream);
 
 // ---- primary messages (nw_cert.hip) ----------------------------------------------------
 struct cert_committee_t {
@@ -158,7 +163,7 @@ hipError_t launch_cert_prepare(const cert_committee_t& com, const cert_stream_t&
                                int headers_only, const uint32_t* hdr_digest, uint32_t* authors,
                                uint32_t* cert_digest, int32_t* pre1, int32_t* pre2,
                                uint64_t* idx1, uint64_t* idx2, uint32_t* vote_key,
-                               uint32_t* author_key, hipStream_t stream);
+                               uint32_t* author_key, uint32_t* vote_cert, hipStream_t stream);
 hipError_t launch_cert_finalize(uint64_t n, int headers_only, const int32_t* pre1,
                                 const int32_t* pre2, const uint64_t* idx1, const uint64_t* idx2,
                                 const int32_t* hdr_status, const int32_t* batch_status,

@@ -290,13 +290,20 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
 }
 
 // Certificate votes checked one by one with the keyed comb (Certificate::verify's
-// Signature::verify_batch, messages.rs:212, for streams where merged groups keep failing).
-// A vote whose strict check passes satisfies R == [s]B - [k]A exactly, so its term of any
-// random linear combination vanishes: a certificate all of whose votes pass is Ok under
-// verify_batch too. Every other certificate keeps cert_ok = 0 and gets its own verify_batch
-// (launch_verify_batch with skip_group_ok = cert_ok, one certificate per group), so
-// statuses and fail indices are the per-certificate path's. Certificates already decided
-// by an earlier check are left alone (their batch status is never read).
+// Signature::verify_batch, messages.rs:212, without merging). A vote whose strict check
+// passes satisfies R == [s]B - [k]A exactly, so its term of any random linear combination
+// vanishes: a certificate all of whose votes pass is Ok under verify_batch too. Every other
+// certificate keeps cert_ok = 0 and gets its own verify_batch (launch_verify_batch with
+// skip_group_ok = cert_ok, one certificate per group), so statuses and fail indices are the
+// per-certificate path's. Certificates already decided by an earlier check are left alone
+// (their batch status is never read).
+//
+// R is never decompressed (nw_strict.hpp keyed_vote_check): R' = [s]B - [k]A is compared
+// with R's encoding through Y' == y_R Z' and the parity of X'/Z'. The parity needs 1/Z':
+// k_votes_keyed writes X', Z' of the votes that got that far into limb planes, and
+// k_votes_keyed_inv inverts them in batches (Montgomery's trick, one lane per strided chunk
+// of votes: 4 multiplications per vote and one inversion per chunk instead of the ~265
+// squarings of a decompression per vote).
 __global__ __launch_bounds__(256) void k_votes_keyed_init(const uint64_t* __restrict__ cvo,
                                                           uint64_t ncert,
                                                           uint32_t* __restrict__ cert_ok) {
@@ -304,36 +311,96 @@ __global__ __launch_bounds__(256) void k_votes_keyed_init(const uint64_t* __rest
   if (c < ncert) cert_ok[c] = cvo[c + 1] > cvo[c] ? 1u : 0u;   // no votes: its own batch
 }
 
-// 141 VGPRs = 3 waves per SIMD; forcing 4 (128 VGPRs, 56 B of spills) measured the same
-// (N = 4: 81.8 vs 81.3, N = 100: 5.20 vs 5.23 M certs/s at 1 % invalid).
+// Limb planes of the pending votes of a slice: X' limb k at planes[k S + i], Z' limb k at
+// planes[(10 + k) S + i] (coalesced in both kernels); state[i] = kVote* of vote v0 + i.
+struct vote_planes_t {
+  uint32_t* planes;
+  uint32_t* state;
+  uint64_t S;
+};
+
 #ifndef NW_KEYED_WAVES
 #define NW_KEYED_WAVES 1
 #endif
 __global__ __launch_bounds__(256, NW_KEYED_WAVES) void k_votes_keyed(
-    const uint32_t* __restrict__ cert_digest, const uint64_t* __restrict__ cvo, uint64_t ncert,
-    const uint32_t* __restrict__ pks, const uint32_t* __restrict__ sigs, uint64_t nvotes,
-    const int32_t* __restrict__ pre1, const int32_t* __restrict__ pre2,
-    const int32_t* __restrict__ hdr_st, key_tables_t keys,
-    const ge_niels_pad* __restrict__ bcomb, uint32_t* __restrict__ cert_ok) {
-  const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= nvotes) return;
-  uint64_t lo = 0, hi = ncert;   // the certificate c with cvo[c] <= v < cvo[c + 1]
-  while (hi - lo > 1) {
-    const uint64_t mid = (lo + hi) / 2;
-    if (cvo[mid] <= v) lo = mid;
-    else hi = mid;
+    const uint32_t* __restrict__ cert_digest, const uint32_t* __restrict__ vote_cert,
+    uint64_t v0, uint64_t nv, const uint32_t* __restrict__ pks,
+    const uint32_t* __restrict__ sigs, const int32_t* __restrict__ pre1,
+    const int32_t* __restrict__ pre2, const int32_t* __restrict__ hdr_st, key_tables_t keys,
+    const ge_niels_pad* __restrict__ bcomb, uint32_t* __restrict__ cert_ok, vote_planes_t vp) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nv) return;
+  const uint64_t v = v0 + i;
+  const uint32_t c = vote_cert[v];
+  uint32_t st = kVotePass;
+  if (pre1[c] == 0 && hdr_st[c] == 0 && pre2[c] == 0) {
+    const uint32_t kk = keys.vote_key[v];
+    if (kk == kNoKey) {   // not a committee key (cannot happen for an undecided certificate)
+      st = kVoteFail;
+    } else {
+      const strict_src_global src{pks + 8 * v, sigs + 16 * v, cert_digest + 8 * (uint64_t)c};
+      fe X, Z;
+      st = keyed_vote_check(src, g_consts.sk, bcomb_wide{bcomb},
+                            keys.tabs + kKeyTab * (uint64_t)kk, keys.ok[kk], X, Z);
+      if (st >= kVotePending) {
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+          vp.planes[(uint64_t)k * vp.S + i] = X.v[k];
+          vp.planes[(uint64_t)(10 + k) * vp.S + i] = Z.v[k];
+        }
+      }
+    }
+    if (st == kVoteFail) cert_ok[c] = 0;   // same value from every failing lane
   }
-  const uint64_t c = lo;
-  if (pre1[c] != 0 || hdr_st[c] != 0 || pre2[c] != 0) return;
-  const uint32_t kk = keys.vote_key[v];
-  if (kk == kNoKey) {   // not a committee key (cannot happen for an undecided certificate)
-    cert_ok[c] = 0;
-    return;
+  vp.state[i] = st;
+}
+
+// One lane per chunk {i = j * nchunks + lane}: Montgomery's trick over the chunk's pending
+// votes. Forward: W_i = X'_i * (product of the earlier Z'), acc *= Z'_i (W_i over X'_i);
+// one inversion of the product; backward: x_i = W_i * inv, inv *= Z'_i. A vote whose x
+// parity differs from its sign bit fails its certificate.
+__global__ __launch_bounds__(256) void k_votes_keyed_inv(const uint32_t* __restrict__ vote_cert,
+                                                         uint64_t v0, uint64_t nv,
+                                                         uint64_t nchunks,
+                                                         uint32_t* __restrict__ cert_ok,
+                                                         vote_planes_t vp) {
+  const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= nchunks) return;
+  auto load = [&](fe& f, int base, uint64_t i) {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) f.v[k] = vp.planes[(uint64_t)(base + k) * vp.S + i];
+  };
+  fe acc;
+  fe_1(acc);
+  uint64_t last = ~0ull;
+#pragma unroll 1
+  for (uint64_t i = lane; i < nv; i += nchunks) {
+    if (vp.state[i] < kVotePending) continue;
+    fe X, Z, W;
+    load(X, 0, i);
+    load(Z, 10, i);
+    fe_mul(W, X, acc);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) vp.planes[(uint64_t)k * vp.S + i] = W.v[k];
+    fe_mul(acc, acc, Z);
+    last = i;
   }
-  const strict_src_global src{pks + 8 * v, sigs + 16 * v, cert_digest + 8 * c};
-  const int st = strict_keyed_comb(src, g_consts.sk, bcomb_wide{bcomb},
-                                   keys.tabs + kKeyTab * (uint64_t)kk, keys.ok[kk]);
-  if (st != NW_OK) cert_ok[c] = 0;   // same value from every failing lane
+  if (last == ~0ull) return;
+  fe inv;
+  fe_invert(inv, acc);
+#pragma unroll 1
+  for (uint64_t i = last;; i -= nchunks) {
+    const uint32_t st = vp.state[i];
+    if (st >= kVotePending) {
+      fe W, Z, x;
+      load(W, 0, i);
+      load(Z, 10, i);
+      fe_mul(x, W, inv);
+      if (fe_isnegative(x) != (st & 1)) cert_ok[vote_cert[v0 + i]] = 0;
+      fe_mul(inv, inv, Z);
+    }
+    if (i < nchunks) break;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -607,21 +674,37 @@ hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
   return hipGetLastError();
 }
 
+size_t votes_keyed_bytes_per_vote() { return 4 * 21; }   // 20 limb planes + state
+
 hipError_t launch_votes_keyed(const uint32_t* cert_digest, const uint64_t* cvo, uint64_t ncert,
-                              const uint32_t* pks, const uint32_t* sigs, uint64_t nvotes,
-                              const int32_t* pre1, const int32_t* pre2, const int32_t* hdr_st,
-                              const key_tables_t& keys, uint32_t* cert_ok, hipStream_t stream) {
+                              const uint32_t* vote_cert, const uint32_t* pks,
+                              const uint32_t* sigs, uint64_t nvotes, const int32_t* pre1,
+                              const int32_t* pre2, const int32_t* hdr_st,
+                              const key_tables_t& keys, uint32_t* cert_ok, void* scratch,
+                              size_t scratch_bytes, hipStream_t stream) {
   if (ncert == 0) return hipSuccess;
-  if (!keys.vote_key || !keys.tabs || !keys.ok) return hipErrorInvalidValue;
+  if (!keys.vote_key || !keys.tabs || !keys.ok || !vote_cert) return hipErrorInvalidValue;
   const ge_niels_pad* bcomb = nullptr;
   hipError_t eb = btab_for_current_device(1, &bcomb);
   if (eb != hipSuccess) return eb;
   hipLaunchKernelGGL(k_votes_keyed_init, dim3(grid_for(ncert, 256)), dim3(256), 0, stream, cvo,
                      ncert, cert_ok);
-  if (nvotes)
-    hipLaunchKernelGGL(k_votes_keyed, dim3(grid_for(nvotes, 256)), dim3(256), 0, stream,
-                       cert_digest, cvo, ncert, pks, sigs, nvotes, pre1, pre2, hdr_st, keys, bcomb,
-                       cert_ok);
+  // slices of S votes through the scratch (the caller's verify_batch workspace, free until
+  // the failed certificates' batches run)
+  const uint64_t S = std::min<uint64_t>(nvotes, scratch_bytes / votes_keyed_bytes_per_vote()) & ~63ull;
+  if (nvotes && S == 0) return hipErrorInvalidValue;
+  uint32_t* base = static_cast<uint32_t*>(scratch);
+  const vote_planes_t vp{base, base + 20 * S, S};
+  for (uint64_t v0 = 0; v0 < nvotes; v0 += S) {
+    const uint64_t nv = std::min(S, nvotes - v0);
+    hipLaunchKernelGGL(k_votes_keyed, dim3(grid_for(nv, 256)), dim3(256), 0, stream,
+                       cert_digest, vote_cert, v0, nv, pks, sigs, pre1, pre2, hdr_st, keys, bcomb,
+                       cert_ok, vp);
+    // chunks: ~2 waves per SIMD of lanes, each over nv / nchunks votes (>= 1)
+    const uint64_t nchunks = std::min<uint64_t>(nv, 256ull * 4 * 2 * 64);
+    hipLaunchKernelGGL(k_votes_keyed_inv, dim3(grid_for(nchunks, 256)), dim3(256), 0, stream,
+                       vote_cert, v0, nv, nchunks, cert_ok, vp);
+  }
   return hipGetLastError();
 }
 

@@ -267,6 +267,81 @@ struct bcomb_lazy {
   }
 };
 
+// acc = [s]B - [k]A for k, s < l: -[k]A as k's 32 signed 8-bit digits against the key's comb
+// tables (keytab[129 t + j] = j * 2^(8t) A, affine niels), [s]B as s's 16 signed 16-bit
+// digits against the B comb (bc). No doublings.
+template <class BComb>
+NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
+                          const ge_niels_pad* keytab) {
+  uint32_t kd[8], sd[8];
+  sc_recode(kd, k, 0x80808080u);   // k < l: 32 signed 8-bit digits
+  sc_recode(sd, s, 0x80008000u);   // s < l: 16 signed 16-bit digits
+  ge_identity(acc);
+  // -[k]A: digit t of k against table t, negated
+#pragma unroll 1
+  for (int t = 0; t < kStrictKeyTables; ++t) {
+    const int d = (int)((sel8(kd, t >> 2) >> ((t & 3) * 8)) & 255u) - 128;
+    if (d != 0) {
+      ge_niels nb = keytab[129 * t + (d < 0 ? -d : d)].n;
+      ge_niels_cneg(nb, d > 0);
+      ge_add_niels(acc, acc, nb, true);
+    }
+  }
+  // +[s]B
+#pragma unroll 1
+  for (int m = 0; m < kBCombT; ++m) {
+    const int d = (int)((sel8(sd, m >> 1) >> ((m & 1) * 16)) & 0xffffu) - 32768;
+    if (d != 0) {
+      ge_cached e;
+      bc(m, d < 0 ? -d : d, e);
+      ge_cached_cneg(e, d < 0);
+      ge_add_any(acc, acc, e, true, true);
+    }
+  }
+}
+
+// Keyed check of a certificate vote WITHOUT decompressing R (pass / fail only: a failing
+// vote sends its certificate to its own verify_batch, which names the failure). With
+// R' = [s]B - [k]A and y_R, sign = R's encoding (y taken unreduced as dalek does, so y >= p
+// means y - p), dalek's verify_strict passes iff s has no high bits, A decodes, s < l, R
+// decodes, neither R nor A is small and R' == decode(R). Since R' is a curve point,
+// Y' == y_R Z' means R' = (+-x0, y_R) for the root x0 >= 0 of y_R (so R decodes, to
+// (sign ? -x0 : x0, y_R)); R' == decode(R) then iff x0 == 0 (X' == 0) or the parity of
+// X'/Z' equals the sign bit. Returns kVotePass / kVoteFail, or kVotePending (| sign) when
+// only that parity is left: the caller batches the inversions of Z' (k_votes_keyed_inv).
+constexpr uint32_t kVotePass = 0, kVoteFail = 1, kVotePending = 2;
+template <class BComb, class Src>
+NW_HD uint32_t keyed_vote_check(const Src& src, const strict_consts& K, const BComb& bc,
+                                const ge_niels_pad* keytab, uint32_t keyflags, fe& X, fe& Z) {
+  const bool okA = (keyflags & 1) != 0, smallA = (keyflags & 2) != 0;
+  uint32_t Sw[8];
+  src.S(Sw);
+  sc s;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s.w[j] = Sw[j];
+  if ((Sw[7] >> 29) != 0 || !okA || smallA || !sc_is_canonical(s)) return kVoteFail;
+  uint32_t Rw[8];
+  src.R(Rw);
+  const uint32_t sign = Rw[7] >> 31;
+  fe yR;
+  fe_frombytes(yR, Rw);
+  if (small_order_by_y(yR, K.small_y)) return kVoteFail;   // R small (if it decodes at all)
+  uint32_t kw[8];
+  src.K(kw);
+  sc k;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) k.w[j] = kw[j];
+  ge acc;
+  keyed_comb_sum(acc, k, s, bc, keytab);
+  fe t;
+  fe_mul(t, yR, acc.Z);
+  if (!fe_eq(t, acc.Y)) return kVoteFail;
+  if (fe_iszero(acc.X)) return kVotePass;
+  fe_copy(X, acc.X);
+  fe_copy(Z, acc.Z);
+  return kVotePending | sign;
+}
+
 // Keyed strict verification: A is a committee key with comb tables keytab[129 t + j] =
 // j * 2^(8t) A (t = 0..31, nw_kernels.h kKeyTab; affine niels), keyflags bit 0 = decoded,
 // bit 1 = small order. Then R' = [s]B - [k]A is 16 + 32 table additions with no doublings and no scalar
@@ -305,32 +380,8 @@ NW_HD int strict_keyed_comb(const Src& src, const strict_consts& K, const BComb&
   sc k;
 #pragma unroll
   for (int j = 0; j < 8; ++j) k.w[j] = kw[j];
-  uint32_t kd[8], sd[8];
-  sc_recode(kd, k, 0x80808080u);   // k < l: 32 signed 8-bit digits
-  sc_recode(sd, s, 0x80008000u);   // s < l: 16 signed 16-bit digits
   ge acc;
-  ge_identity(acc);
-  // -[k]A: digit t of k against table t, negated
-#pragma unroll 1
-  for (int t = 0; t < kStrictKeyTables; ++t) {
-    const int d = (int)((sel8(kd, t >> 2) >> ((t & 3) * 8)) & 255u) - 128;
-    if (d != 0) {
-      ge_niels nb = keytab[129 * t + (d < 0 ? -d : d)].n;
-      ge_niels_cneg(nb, d > 0);
-      ge_add_niels(acc, acc, nb, true);
-    }
-  }
-  // +[s]B
-#pragma unroll 1
-  for (int m = 0; m < kBCombT; ++m) {
-    const int d = (int)((sel8(sd, m >> 1) >> ((m & 1) * 16)) & 0xffffu) - 32768;
-    if (d != 0) {
-      ge_cached e;
-      bc(m, d < 0 ? -d : d, e);
-      ge_cached_cneg(e, d < 0);
-      ge_add_any(acc, acc, e, true, true);
-    }
-  }
+  keyed_comb_sum(acc, k, s, bc, keytab);
   return ge_eq_affine(acc, R) ? NW_OK : NW_ERR_EQUATION;
 }
 

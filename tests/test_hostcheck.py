@@ -211,6 +211,57 @@ def test_strict_keyed_comb(hc, golden):
             O.verify_strict(m, pk, bytes(sig))
 
 
+def _scalar_a(seed: bytes) -> int:
+    import hashlib
+    h = bytearray(hashlib.sha512(seed).digest()[:32])
+    h[0] &= 248
+    h[31] = (h[31] & 127) | 64
+    return int.from_bytes(h, "little")
+
+
+def test_keyed_vote_check_compressed_r(hc, golden):
+    """Certificate votes' keyed check with R compared in compressed form (Y' == y_R Z' and
+    the parity of X'/Z', no decompression of R): pass iff the oracle's strict verify is Ok,
+    on the edge corpus (every Appendix A class), random honest / tampered signatures, and
+    signatures by the key's owner with [s]B - [k]A == -R (same y, other x sign: dalek
+    rejects them, so must the parity check)."""
+    hc.hc_keyed_vote_check.restype = ctypes.c_int
+    for it in golden["edge_corpus"]["items"]:
+        m, pk, sig = (bytes.fromhex(it[k]) for k in ("msg", "pk", "sig"))
+        k = O.hram(sig[:32], pk, m)
+        assert hc.hc_keyed_vote_check(_b(pk), _b(sig), _b(k)) == int(it["status"] != 0), \
+            it["class"]
+    rng = np.random.Generator(np.random.PCG64(16))
+    for i in range(36):
+        seed = rng.bytes(32)
+        pk, sk = O.keypair_from_seed(seed)
+        m = rng.bytes(32)
+        sig = bytearray(O.sign(sk, m))
+        if i % 3 == 1:
+            sig[32 + int(rng.integers(0, 31))] ^= 1 << int(rng.integers(0, 8))
+        elif i % 3 == 2:
+            sig[int(rng.integers(0, 32))] ^= 1 << int(rng.integers(0, 8))
+        k = O.hram(bytes(sig[:32]), pk, m)
+        want = int(O.verify_strict(m, pk, bytes(sig)) != 0)
+        assert hc.hc_keyed_vote_check(_b(pk), _b(bytes(sig)), _b(k)) == want
+    for i in range(12):                        # R' = -R: y matches, x sign does not
+        seed = rng.bytes(32)
+        pk, sk = O.keypair_from_seed(seed)
+        a = _scalar_a(seed) % L_ORDER
+        m = rng.bytes(32)
+        r = int.from_bytes(rng.bytes(32), "little") % L_ORDER
+        R = O.scalarmult_base(r.to_bytes(32, "little"))
+        kk = int.from_bytes(O.hram(R, pk, m), "little")
+        s = (kk * a - r) % L_ORDER
+        sig = R + s.to_bytes(32, "little")
+        assert O.verify_strict(m, pk, sig) != 0
+        assert hc.hc_keyed_vote_check(_b(pk), _b(sig), _b(O.hram(R, pk, m))) == 1
+        s_ok = (r + kk * a) % L_ORDER               # the honest s for the same R: passes
+        sig = R + s_ok.to_bytes(32, "little")
+        assert O.verify_strict(m, pk, sig) == 0
+        assert hc.hc_keyed_vote_check(_b(pk), _b(sig), _b(O.hram(R, pk, m))) == 0
+
+
 def test_strict_half_random_and_tampered(hc):
     rng = np.random.Generator(np.random.PCG64(12))
     for i in range(120):

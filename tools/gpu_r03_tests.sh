@@ -1,5 +1,6 @@
 #!/bin/bash
-# GPU-box helper: the -m gpu suite, then the certificate-service latency leg.
+# GPU-box helper: the -m gpu suite, the certificate-service latency leg, and config 2 with
+# the default grouping policy and with the keyed vote checks forced (NW_CERT_KEYED=1).
 #   bash tools/gpu_r03_tests.sh OUTDIR [pytest -k expr]
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -11,4 +12,8 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout
 rc=$?; echo "pytest rc=$rc"; tail -3 "$OUT/pytest_gpu.log"
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py --workload service > "$OUT/bench_service.json" 2> "$OUT/bench_service.log"
-rc=$?; echo "service bench rc=$rc"; exit $rc
+rc=$?; echo "service bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u bench.py --workload cert --no-cpu-baseline > "$OUT/bench_cert.json" 2> "$OUT/bench_cert.log"
+rc=$?; echo "cert bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
+NW_CERT_KEYED=1 timeout -k 10 300 python -u bench.py --workload cert --no-cpu-baseline > "$OUT/bench_cert_keyed.json" 2> "$OUT/bench_cert_keyed.log"
+rc=$?; echo "keyed cert bench rc=$rc"; exit $rc

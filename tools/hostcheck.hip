@@ -149,14 +149,10 @@ int hc_verify_strict_half(const uint8_t pk[32], const uint8_t sig[64], const uin
 // j * 2^(8t) A built here as the device's k_key_base / k_key_tabs define them, the B comb
 // computed per lookup. Returns the status; -1 when A does not decode is reported through the
 // key flags exactly as the device does (status 3).
-int hc_verify_strict_keyed(const uint8_t pk[32], const uint8_t sig[64], const uint8_t k32[32]) {
-  init();
-  uint32_t Aw[8], Rw[8], Sw[8], kw[8];
-  load8(Aw, pk); load8(Rw, sig); load8(Sw, sig + 32); load8(kw, k32);
+static uint32_t keyed_tables(ge_niels_pad* tab, const uint32_t Aw[8]) {
   ge A;
   const bool dec = ge_frombytes(A, Aw, K);
   const uint32_t flags = (dec ? 1u : 0u) | (dec && ge_is_small_order(A) ? 2u : 0u);
-  static ge_niels_pad tab[32 * 129];
   ge base = A;
   for (int t = 0; t < 32; ++t) {
     if (t) for (int d = 0; d < 8; ++d) { ge x; ge_dbl(x, base, d == 7); base = x; }
@@ -171,8 +167,36 @@ int hc_verify_strict_keyed(const uint8_t pk[32], const uint8_t sig[64], const ui
       acc = nx;
     }
   }
+  return flags;
+}
+
+int hc_verify_strict_keyed(const uint8_t pk[32], const uint8_t sig[64], const uint8_t k32[32]) {
+  init();
+  uint32_t Aw[8], Rw[8], Sw[8], kw[8];
+  load8(Aw, pk); load8(Rw, sig); load8(Sw, sig + 32); load8(kw, k32);
+  static ge_niels_pad tab[32 * 129];
+  const uint32_t flags = keyed_tables(tab, Aw);
   const strict_src_arrays src{Aw, Rw, Sw, kw};
   return strict_keyed_comb(src, SK, bcomb_lazy{BT, &SK.k.d2}, tab, flags);
+}
+
+// The certificate-vote keyed check without R decompression (nw_strict.hpp
+// keyed_vote_check) followed by what k_votes_keyed_inv does for a pending vote (here one
+// inversion per vote): 0 = the vote passes, 1 = it fails.
+int hc_keyed_vote_check(const uint8_t pk[32], const uint8_t sig[64], const uint8_t k32[32]) {
+  init();
+  uint32_t Aw[8], Rw[8], Sw[8], kw[8];
+  load8(Aw, pk); load8(Rw, sig); load8(Sw, sig + 32); load8(kw, k32);
+  static ge_niels_pad tab[32 * 129];
+  const uint32_t flags = keyed_tables(tab, Aw);
+  const strict_src_arrays src{Aw, Rw, Sw, kw};
+  fe X, Z;
+  const uint32_t st = keyed_vote_check(src, SK, bcomb_lazy{BT, &SK.k.d2}, tab, flags, X, Z);
+  if (st < kVotePending) return (int)st;
+  fe zi, x;
+  fe_invert(zi, Z);
+  fe_mul(x, X, zi);
+  return fe_isnegative(x) == (st & 1) ? 0 : 1;
 }
 
 // Entry j of the wide B table half h (ypx || ymx || xy2d as 30 limbs), for the table test.
