@@ -464,28 +464,24 @@ size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
   return tot;
 }
 
-// Adaptive certificate grouping. A merged group whose random linear
-// combination fails sends every certificate of the group through its own verify_batch, so
-// when invalid certificates are spread through the stream (say 1%: every 32k-vote group
-// holds some) big groups cost the merged check AND the per-certificate path. Every call
-// reports the fraction p of its counted certificates whose vote batch failed (k_grp_count /
-// k_grp_publish, into host-mapped memory after the per-certificate pass); a later call with
-// the same committee size then picks:
+// Certificate vote policy. The default is the keyed vote checks (every vote
+// of an undecided certificate through its committee key's comb tables, R compared in
+// compressed form; verify_batch only for certificates with a failing vote): faster than
+// merged groups at every committee size (config 2 all-valid, N = 4 / 10 / 50 / 100: 113.6 /
+// 60.8 / 15.1 / 7.84 vs 95.2 / 48.9 / 11.6 / 6.08 M certs/s with big groups,
+// gpurun_out/r03a) and with nothing shared that a bad vote can spoil. With NW_CERT_KEYED=0
+// the merged-group policy runs instead, adaptive on the fraction p of counted certificates
+// whose vote batch failed in earlier calls (k_grp_count / k_grp_publish, host-mapped):
 //   big    Pippenger groups of ~32k votes (launch_cert_groups) while at most a quarter of
 //          them would fail at that p, 1 - (1 - p)^K <= 1/4;
-//   keyed  otherwise: every vote through the keyed comb on its own (launch_votes_keyed, 48
-//          table additions, no doublings, nothing shared that a bad vote can spoil), then
-//          verify_batch for the certificates with a failing vote only;
-//   small  (NW_CERT_KEYED=0 instead of keyed, or when merging does not apply) K-certificate
-//          keyed Straus groups with the fallback ladders run from the same per-vote items
-//          (launch_cert_sgroups), K cost-optimal at that p (cert_sgroup_size), when they
-//          beat every certificate's own ladder; per-certificate otherwise.
-// Mid-size Pippenger groups do not help: a group's Pippenger tail (4,160 buckets, 33 window
-// sums, the Horner) is paid per group (at 1,024 votes per group N = 100 ran 3.2 M certs/s
-// all-valid against 5.7 M with 32k-vote groups). Verdicts do not depend on the choice
-// (DESIGN.md 2); NW_CERT_GROUP_VOTES fixes big groups of that size, NW_CERT_SMALL_K small
-// groups of K certificates, NW_CERT_KEYED=1 the keyed checks, NW_CERT_MERGE=0 turns merging
-// off.
+//   small  otherwise (or when merging does not apply) K-certificate keyed Straus groups with
+//          the fallback ladders run from the same per-vote items (launch_cert_sgroups), K
+//          cost-optimal at that p (cert_sgroup_size), when they beat every certificate's own
+//          ladder; per-certificate otherwise.
+// In keyed mode the reported p only sizes the fallback batches' chunks. Verdicts never
+// depend on the choice; NW_CERT_GROUP_VOTES fixes big groups of that size,
+// NW_CERT_SMALL_K small groups of K certificates, NW_CERT_MERGE=0 turns merging (and the
+// keyed checks) off: every certificate's own verify_batch.
 constexpr uint32_t kGroupDefault = 32768;
 
 struct GroupPolicy {
@@ -596,32 +592,41 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
                                   w.bitmap, sws, s, &hk), "k_verify_strict (headers)");
   if (!headers_only) {
     const nw::key_tables_t kt{ktabs, kok, w.vote_key};
-    // With random coefficients the votes of many certificates are checked as one random
-    // linear combination per group (launch_cert_groups); only the certificates of groups
-    // that fail it go through their own verify_batch below.
+    // Default: the keyed vote checks (launch_votes_keyed): every vote of an undecided
+    // certificate through its committee key's comb tables, R compared in compressed form,
+    // then verify_batch only for the certificates with a failing vote. A vote that passes
+    // its strict check has a zero term in ANY random linear combination, so a certificate
+    // whose votes all pass is Ok under verify_batch for every z (random or injected); every
+    // other certificate gets its own verify_batch with the call's z. Nothing is shared that
+    // one bad vote can spoil, so invalid certificates cost only their own batches.
+    // NW_CERT_KEYED=0 selects the merged-group policy instead (big Pippenger groups / small
+    // keyed Straus groups, adaptive on the failure rate the previous calls reported),
+    // NW_CERT_MERGE=0 every certificate's own verify_batch.
+    const char* ke = getenv("NW_CERT_KEYED");
+    const char* me = getenv("NW_CERT_MERGE");
+    const bool keyed = com.nauth > 0 && !(ke && atoi(ke) == 0) && !(me && me[0] == '0') &&
+                       !getenv("NW_CERT_SMALL_K") && !nw::cert_group_env_fixed();
     uint32_t* fb_dev = nullptr;
     uint32_t* fb_cnt = nullptr;
     double p_cert = 0.0;
-    uint64_t K = nw::cert_group_size(host_vote_offsets, n, com.nauth, z16 != nullptr, kGroupDefault);
-    bool small = getenv("NW_CERT_SMALL_K") != nullptr;
-    const char* ke = getenv("NW_CERT_KEYED");
-    bool keyed = ke && atoi(ke) != 0;
-    if (!z16 && !small && !keyed && !nw::cert_group_env_fixed()) {
-      p_cert = group_failure_rate(dev, com.nauth, s, &fb_dev, &fb_cnt);
-      if (!K) small = true;   // merging does not apply; cert_sgroup_size decides
-      else if (1.0 - std::pow(1.0 - p_cert, (double)K) > 0.25) {
-        if (ke) small = true;   // NW_CERT_KEYED=0: the small-group policy instead
-        else keyed = true;
-      }
-    }
+    uint64_t K = 1;
+    bool small = false;
     if (keyed) {
-      small = false;
-      K = 1;
-    }
-    if (small) {
-      bool wins = false;
-      K = nw::cert_sgroup_size(host_vote_offsets, n, com.nauth, z16 != nullptr, p_cert, &wins);
-      if (!wins) K = 0;
+      // the reported failure rate only sizes the fallback batches' chunks
+      p_cert = group_failure_rate(dev, com.nauth, s, &fb_dev, &fb_cnt);
+    } else {
+      K = nw::cert_group_size(host_vote_offsets, n, com.nauth, z16 != nullptr, kGroupDefault);
+      small = getenv("NW_CERT_SMALL_K") != nullptr;
+      if (!z16 && !small && !nw::cert_group_env_fixed()) {
+        p_cert = group_failure_rate(dev, com.nauth, s, &fb_dev, &fb_cnt);
+        // merging does not apply, or most big groups would fail at the measured rate
+        if (!K || 1.0 - std::pow(1.0 - p_cert, (double)K) > 0.25) small = true;
+      }
+      if (small) {
+        bool wins = false;
+        K = nw::cert_sgroup_size(host_vote_offsets, n, com.nauth, z16 != nullptr, p_cert, &wins);
+        if (!wins) K = 0;
+      }
     }
     if (getenv("NW_DEBUG_GROUPS"))
       fprintf(stderr, "[narwhal_amd] certificates: n=%zu keys=%zu %s K=%llu p=%.4g\n", (size_t)n,

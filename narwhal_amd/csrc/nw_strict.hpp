@@ -270,13 +270,46 @@ struct bcomb_lazy {
 // acc = [s]B - [k]A for k, s < l: -[k]A as k's 32 signed 8-bit digits against the key's comb
 // tables (keytab[129 t + j] = j * 2^(8t) A, affine niels), [s]B as s's 16 signed 16-bit
 // digits against the B comb (bc). No doublings.
+#ifndef NW_KEYED_SPLIT
+#define NW_KEYED_SPLIT 0   // 1: the A and B terms in two interleaved accumulators (ILP)
+#endif
 template <class BComb>
 NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
-                          const ge_niels_pad* keytab) {
+                          const ge_niels_pad* keytab, const fe& d2) {
   uint32_t kd[8], sd[8];
   sc_recode(kd, k, 0x80808080u);   // k < l: 32 signed 8-bit digits
   sc_recode(sd, s, 0x80008000u);   // s < l: 16 signed 16-bit digits
   ge_identity(acc);
+#if NW_KEYED_SPLIT
+  // two independent chains, one step of each per iteration: -[k]A in acc, [s]B in accB,
+  // joined by one cached addition (T3 not needed by the callers' comparisons)
+  ge accB;
+  ge_identity(accB);
+#pragma unroll 1
+  for (int t = 0; t < kStrictKeyTables; ++t) {
+    const int d = (int)((sel8(kd, t >> 2) >> ((t & 3) * 8)) & 255u) - 128;
+    if (d != 0) {
+      ge_niels nb = keytab[129 * t + (d < 0 ? -d : d)].n;
+      ge_niels_cneg(nb, d > 0);
+      ge_add_niels(acc, acc, nb, true);
+    }
+    if (t < kBCombT) {
+      const int e = (int)((sel8(sd, t >> 1) >> ((t & 1) * 16)) & 0xffffu) - 32768;
+      if (e != 0) {
+        ge_cached c;
+        bc(t, e < 0 ? -e : e, c);
+        ge_cached_cneg(c, e < 0);
+        ge_add_any(accB, accB, c, true, true);
+      }
+    }
+  }
+  ge_cached cb;
+  ge_to_cached(cb, accB, d2);
+  ge_add_cached(acc, acc, cb, false);
+  return;
+#else
+  (void)d2;
+#endif
   // -[k]A: digit t of k against table t, negated
 #pragma unroll 1
   for (int t = 0; t < kStrictKeyTables; ++t) {
@@ -332,7 +365,7 @@ NW_HD uint32_t keyed_vote_check(const Src& src, const strict_consts& K, const BC
 #pragma unroll
   for (int j = 0; j < 8; ++j) k.w[j] = kw[j];
   ge acc;
-  keyed_comb_sum(acc, k, s, bc, keytab);
+  keyed_comb_sum(acc, k, s, bc, keytab, K.k.d2);
   fe t;
   fe_mul(t, yR, acc.Z);
   if (!fe_eq(t, acc.Y)) return kVoteFail;
@@ -381,7 +414,7 @@ NW_HD int strict_keyed_comb(const Src& src, const strict_consts& K, const BComb&
 #pragma unroll
   for (int j = 0; j < 8; ++j) k.w[j] = kw[j];
   ge acc;
-  keyed_comb_sum(acc, k, s, bc, keytab);
+  keyed_comb_sum(acc, k, s, bc, keytab, K.k.d2);
   return ge_eq_affine(acc, R) ? NW_OK : NW_ERR_EQUATION;
 }
 

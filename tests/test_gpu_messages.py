@@ -211,9 +211,11 @@ def test_certificate_groups_vs_per_certificate(monkeypatch):
 
 @pytest.mark.parametrize("N", [4, 10, 50, 100])
 def test_certificate_groups_honest_and_one_bad(monkeypatch, N):
-    """Default group size over an honest stream (every group passes the merged check), then
-    one bad vote signature: only that certificate fails (its group falls back)."""
+    """Merged groups (NW_CERT_KEYED=0) of the default size over an honest stream (every
+    group passes the merged check), then one bad vote signature: only that certificate
+    fails (its group falls back); the default keyed checks and the unmerged path agree."""
     from narwhal_amd import crypto as C
+    monkeypatch.setenv("NW_CERT_KEYED", "0")
     keys = O.keys(N)
     n = max(2000, 70000 // (2 * N // 3 + 1))
     s = W.certificate_stream(n, keys, lambda sk, m: C.sign_many(sk, m), oracle_digest_many,
@@ -226,6 +228,9 @@ def test_certificate_groups_honest_and_one_bad(monkeypatch, N):
     s["vote_sigs"][v, 7] ^= 0x40
     st, ix = M.verify_certificates_many(com, s, None)
     assert st[bad] != 0 and (np.delete(st, bad) == 0).all()
+    monkeypatch.delenv("NW_CERT_KEYED")
+    stk, ixk = M.verify_certificates_many(com, s, None)
+    assert stk.tolist() == st.tolist() and ixk[bad] == ix[bad]
     monkeypatch.setenv("NW_CERT_MERGE", "0")
     st0, ix0 = M.verify_certificates_many(com, s, None)
     assert st0.tolist() == st.tolist() and ix0[bad] == ix[bad]
@@ -343,12 +348,14 @@ def test_certificate_keyed_votes_early_failures(monkeypatch):
     assert st.tolist() == exp and ix.tolist() == expi
 
 
-def test_certificate_groups_adaptive_repeated_calls():
-    """Adaptive merging (nw_api.cpp group_failure_rate): a stream with ~1% failing
-    certificates moves from the big merged groups to keyed vote checks from the next call on (the
-    measured rate makes most big groups fail), and back once an honest stream reports no
-    failures; every call's statuses and indices equal the construction, whichever path ran."""
+def test_certificate_groups_adaptive_repeated_calls(monkeypatch):
+    """The merged-group policy (NW_CERT_KEYED=0; nw_api.cpp group_failure_rate): a stream
+    with ~1% failing certificates moves from the big merged groups to small groups from the
+    next call on (the measured rate makes most big groups fail), and back once an honest
+    stream reports no failures; every call's statuses and indices equal the construction,
+    whichever path ran. Then the same calls with the default keyed checks."""
     from narwhal_amd import crypto as C
+    monkeypatch.setenv("NW_CERT_KEYED", "0")
     N, n = 10, 5200
     s = W.certificate_stream(n, O.keys(N), lambda sk, m: C.sign_many(sk, m), oracle_digest_many,
                              seed=77)
@@ -359,4 +366,10 @@ def test_certificate_groups_adaptive_repeated_calls():
         assert st.tolist() == exp_st.tolist() and ix.tolist() == exp_ix.tolist()
     for _ in range(3):
         st, ix = M.verify_certificates_many(com, s, None)     # honest again
+        assert (st == 0).all()
+    monkeypatch.delenv("NW_CERT_KEYED")
+    for _ in range(3):
+        st, ix = M.verify_certificates_many(com, m, None)
+        assert st.tolist() == exp_st.tolist() and ix.tolist() == exp_ix.tolist()
+        st, ix = M.verify_certificates_many(com, s, None)
         assert (st == 0).all()

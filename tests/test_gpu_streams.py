@@ -148,3 +148,45 @@ def test_two_threads_host_calls_different_committees():
     for t in th:
         t.join()
     assert not errors, errors
+
+
+def test_graph_capture_sha512_replays_and_strict_refuses():
+    """hipGraph capture (include/narwhal_amd.h, nw_prepare): nw_dev_sha512_digest32_many
+    captured into a torch CUDA graph replays correctly on new inputs written into the same
+    buffers; a strict launch (shared tables under the device lease) refuses to be captured
+    with NW_E_INVALID_ARG instead of recording an event chain a replay would bypass."""
+    import hashlib
+    L = _lib.lib()
+    dev = torch.device("cuda", 0)
+    n, ln = 64, 300
+    rng = np.random.Generator(np.random.PCG64(5))
+    data = torch.from_numpy(rng.integers(0, 256, size=n * ln, dtype=np.uint8)).to(dev)
+    offs = torch.arange(n, dtype=torch.int64, device=dev) * ln
+    lens = torch.full((n,), ln, dtype=torch.int64, device=dev)
+    out = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    s = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(s):          # one uncaptured call first (module load, constants)
+        assert L.nw_dev_sha512_digest32_many(P(data), P(offs), P(lens), n, P(out),
+                                             ctypes.c_void_p(s.cuda_stream)) == 0
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        cs = torch.cuda.current_stream()
+        assert L.nw_dev_sha512_digest32_many(P(data), P(offs), P(lens), n, P(out),
+                                             ctypes.c_void_p(cs.cuda_stream)) == 0
+        m = torch.zeros((4, 32), dtype=torch.uint8, device=dev)
+        st = torch.zeros(4, dtype=torch.int32, device=dev)
+        bm = torch.zeros(8, dtype=torch.uint8, device=dev)
+        rc = L.nw_dev_verify_strict_many(P(m), 32, P(m), P(torch.zeros((4, 64), dtype=torch.uint8,
+                                                                         device=dev)),
+                                         4, P(st), P(bm), ctypes.c_void_p(cs.cuda_stream))
+        assert rc == -1                 # NW_E_INVALID_ARG
+    for rep in range(3):
+        host = rng.integers(0, 256, size=n * ln, dtype=np.uint8)
+        data.copy_(torch.from_numpy(host))
+        g.replay()
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        for i in range(n):
+            assert got[i].tobytes() == hashlib.sha512(host[i * ln:(i + 1) * ln].tobytes()).digest()[:32]

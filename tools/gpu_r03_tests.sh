@@ -16,4 +16,9 @@ rc=$?; echo "service bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py --workload cert --no-cpu-baseline > "$OUT/bench_cert.json" 2> "$OUT/bench_cert.log"
 rc=$?; echo "cert bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
 NW_CERT_KEYED=1 timeout -k 10 300 python -u bench.py --workload cert --no-cpu-baseline > "$OUT/bench_cert_keyed.json" 2> "$OUT/bench_cert_keyed.log"
-rc=$?; echo "keyed cert bench rc=$rc"; exit $rc
+rc=$?; echo "keyed cert bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
+for V in $VARIANTS; do
+  NW_LIB=exp/$V/libnarwhal_amd.so NW_CERT_KEYED=1 timeout -k 10 300 python -u bench.py --workload cert \
+    --no-cpu-baseline > "$OUT/bench_cert_keyed_$V.json" 2> "$OUT/bench_cert_keyed_$V.log"
+  rc=$?; echo "keyed cert bench $V rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
