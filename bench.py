@@ -50,10 +50,11 @@ P_FIELD = 2**255 - 19
 MAC_PER_STRICT_VERIFY = 3200 * 64          # 204,800 32x32->64 MACs
 MAC_PER_BATCH_ITEM_LARGE = 1000 * 64       # batch item, n >= 10k (64,000 MACs)
 MAC_PER_BATCH_ITEM_SMALL = 2000 * 64       # batch item, small n (certificate votes)
-# Certificate groups: a counted vote costs one R decompression (~265 F_p
-# mults) + <= 17 bucket additions (7 mults each) + its share of the key sums ~ 400 F_p mults;
-# the SURVEY small-n constant above describes per-certificate Straus, not this algorithm.
-MAC_PER_GROUP_VOTE = 400 * 64              # 25,600 MACs
+# Keyed vote check: 48 comb-table additions (~7.5 F_p mults each) + one
+# product for the y comparison + a share of the batched inversion ~ 370 F_p mults, no R
+# decompression; the SURVEY small-n constant above describes per-certificate Straus, not
+# this algorithm.
+MAC_PER_KEYED_VOTE = 370 * 64              # 23,680 MACs
 # Keyed strict verification (Header::verify by a committee key): R's
 # decompression (~265 F_p mults) + 48 comb-table additions (~7.5 each) ~ 650 F_p mults;
 # SURVEY's 204,800 describes an unkeyed ladder verification.
@@ -403,6 +404,73 @@ def cpu_baseline_sha(sample, seconds: float):
                 parity="ok" if ok else "FAIL")
 
 
+def cert_stream_for(args, rank, N: int, stream_cache=None):
+    """65,536 unique honest certificates for committee N (signed on the GPU), cached."""
+    uniq = min(args.cert_unique, args.certs)
+    if stream_cache is not None and N in stream_cache:
+        return stream_cache[N]
+    keys = [(bytes(pk), bytes(sd) + bytes(pk)) for sd, pk in
+            zip(W.fixture_seeds(N), C.keypair_from_seed_many(W.fixture_seeds(N)))]
+    log(f"cert stream N={N}: building {uniq} unique certificates, tiled to {args.certs}")
+    s = W.certificate_stream(uniq, keys, lambda sk, m: C.sign_many(sk, m),
+                             lambda d, o: C.sha512_digest32_many(d, o[:-1], np.diff(o)),
+                             seed=rank)
+    if stream_cache is not None:
+        stream_cache[N] = s
+    return s
+
+
+class ResidentCerts:
+    """A certificate stream tiled to `n` certificates in HBM with the nw_certificates /
+    nw_committee views and the device workspace of nw_dev_certificates_verify_many, plus
+    the expected status / index of every certificate (the construction)."""
+
+    def __init__(self, L, dev, s, exp_st_u, exp_ix_u, n, ws=None):
+        uniq = len(s["header_offsets"]) - 1
+        q = s["q"]
+        Lh = int(s["header_offsets"][1])
+        reps = (n + uniq - 1) // uniq
+
+        def dev_tile(a, rows):
+            t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+            return t.repeat((reps,) + (1,) * (t.dim() - 1))[:rows].contiguous()
+        self.T = {"header_bytes": dev_tile(s["header_bytes"].reshape(uniq, Lh), n).view(-1),
+                  "ids": dev_tile(s["ids"], n), "header_sigs": dev_tile(s["header_sigs"], n),
+                  "vote_pks": dev_tile(s["vote_pks"].reshape(uniq, q * 32), n).view(-1, 32),
+                  "vote_sigs": dev_tile(s["vote_sigs"].reshape(uniq, q * 64), n).view(-1, 64),
+                  "payload_counts": torch.zeros(n, dtype=torch.int32, device=dev),
+                  "header_offsets": torch.arange(n + 1, dtype=torch.int64, device=dev) * Lh,
+                  "vote_offsets": torch.arange(n + 1, dtype=torch.int64, device=dev) * q}
+        self.Cm = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+                   for k, v in s["committee"].items()}
+        nv = n * q
+        self.host_vo = np.arange(n + 1, dtype=np.uint64) * q
+        self.ws = ws if ws is not None else torch.empty(L.nw_dev_certificates_workspace(n, nv),
+                                                        dtype=torch.uint8, device=dev)
+        self.st = torch.empty(n, dtype=torch.int32, device=dev)
+        self.ix = torch.empty(n, dtype=torch.int64, device=dev)
+        P = lambda t: t.data_ptr()
+        self.cc = M._CCommittee(len(s["committee"]["stakes"]), P(self.Cm["pks"]),
+                                P(self.Cm["stakes"]), P(self.Cm["worker_offsets"]),
+                                P(self.Cm["worker_ids"]))
+        self.cs = M._CCertificates(n, P(self.T["header_bytes"]), P(self.T["header_offsets"]),
+                                   P(self.T["payload_counts"]), P(self.T["ids"]),
+                                   P(self.T["header_sigs"]), P(self.T["vote_offsets"]),
+                                   P(self.T["vote_pks"]), P(self.T["vote_sigs"]), Lh * n, nv,
+                                   self.host_vo.ctypes.data)
+        self.exp_st = torch.from_numpy(exp_st_u).to(dev).repeat(reps)[:n]
+        self.exp_ix = torch.from_numpy(exp_ix_u.astype(np.int64)).to(dev).repeat(reps)[:n]
+        self.L, self.n, self.q = L, n, q
+
+    def launch(self, stream):
+        check(self.L.nw_dev_certificates_verify_many(ctypes.byref(self.cc), ctypes.byref(self.cs),
+                                                     0, None, None, ptr(self.ws), ptr(self.st),
+                                                     ptr(self.ix), stream), "certificates")
+
+    def parity(self) -> bool:
+        return bool(torch.equal(self.st, self.exp_st) and torch.equal(self.ix, self.exp_ix))
+
+
 def run_cert(args, dev, stream, rank, world, N: int, invalid: float = 0.0, stream_cache=None):
     """Config 2: Certificate::verify stream, committee N, q = 2N/3 + 1 votes per cert.
     65,536 unique certificates (signed on the GPU), tiled to --certs; no dedup/caching.
@@ -411,81 +479,81 @@ def run_cert(args, dev, stream, rank, world, N: int, invalid: float = 0.0, strea
     bits, R not on the curve); statuses AND indices are checked against the construction
     for every certificate of the tiled stream."""
     L = _lib.lib()
-    uniq = min(args.cert_unique, args.certs)
-    if stream_cache is not None and N in stream_cache:
-        s = stream_cache[N]
-    else:
-        keys = [(bytes(pk), bytes(sd) + bytes(pk)) for sd, pk in
-                zip(W.fixture_seeds(N), C.keypair_from_seed_many(W.fixture_seeds(N)))]
-        log(f"cert stream N={N}: building {uniq} unique certificates, tiled to {args.certs}")
-        s = W.certificate_stream(uniq, keys, lambda sk, m: C.sign_many(sk, m),
-                                 lambda d, o: C.sha512_digest32_many(d, o[:-1], np.diff(o)),
-                                 seed=rank)
-        if stream_cache is not None:
-            stream_cache[N] = s
+    s = cert_stream_for(args, rank, N, stream_cache)
+    uniq = len(s["header_offsets"]) - 1
     exp_st_u = np.zeros(uniq, np.int32)
     exp_ix_u = np.zeros(uniq, np.uint64)
     if invalid > 0:
         step = max(1, int(round(1 / invalid)))
         s, exp_st_u, exp_ix_u = W.mutate_votes(s, np.arange(step // 2, uniq, step), seed=N)
     q, n = s["q"], args.certs
-    Lh = int(s["header_offsets"][1])
-    reps = (n + uniq - 1) // uniq
-
-    def dev_tile(a, rows):
-        t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-        return t.repeat((reps,) + (1,) * (t.dim() - 1))[:rows].contiguous()
-
-    T = {"header_bytes": dev_tile(s["header_bytes"].reshape(uniq, Lh), n).view(-1),
-         "ids": dev_tile(s["ids"], n), "header_sigs": dev_tile(s["header_sigs"], n),
-         "vote_pks": dev_tile(s["vote_pks"].reshape(uniq, q * 32), n).view(-1, 32),
-         "vote_sigs": dev_tile(s["vote_sigs"].reshape(uniq, q * 64), n).view(-1, 64),
-         "payload_counts": torch.zeros(n, dtype=torch.int32, device=dev),
-         "header_offsets": torch.arange(n + 1, dtype=torch.int64, device=dev) * Lh,
-         "vote_offsets": torch.arange(n + 1, dtype=torch.int64, device=dev) * q}
-    Cm = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in s["committee"].items()}
-    nv = n * q
-    host_vo = (np.arange(n + 1, dtype=np.uint64) * q)
-    ws = torch.empty(L.nw_dev_certificates_workspace(n, nv), dtype=torch.uint8, device=dev)
-    st = torch.empty(n, dtype=torch.int32, device=dev)
-    ix = torch.empty(n, dtype=torch.int64, device=dev)
-    P = lambda t: t.data_ptr()
-    cc = M._CCommittee(N, P(Cm["pks"]), P(Cm["stakes"]), P(Cm["worker_offsets"]),
-                       P(Cm["worker_ids"]))
-    cs = M._CCertificates(n, P(T["header_bytes"]), P(T["header_offsets"]),
-                          P(T["payload_counts"]), P(T["ids"]), P(T["header_sigs"]),
-                          P(T["vote_offsets"]), P(T["vote_pks"]), P(T["vote_sigs"]), Lh * n, nv,
-                          host_vo.ctypes.data)
+    rc = ResidentCerts(L, dev, s, exp_st_u, exp_ix_u, n)
     torch.cuda.synchronize()
-
-    def launch():
-        check(L.nw_dev_certificates_verify_many(ctypes.byref(cc), ctypes.byref(cs), 0, None, None,
-                                                ptr(ws), ptr(st), ptr(ix), stream), "certificates")
-
-    elapsed, kernel_ms = timed_steps(launch, args.cert_steps, 1, world)
-    exp_st = torch.from_numpy(exp_st_u).to(dev).repeat(reps)[:n]
-    exp_ix = torch.from_numpy(exp_ix_u.astype(np.int64)).to(dev).repeat(reps)[:n]
-    ok = bool(torch.equal(st, exp_st) and torch.equal(ix, exp_ix))
+    elapsed, kernel_ms = timed_steps(lambda: rc.launch(stream), args.cert_steps, 1, world)
+    ok = rc.parity()
     sec = elapsed / args.cert_steps
     mac_survey = MAC_PER_STRICT_VERIFY + q * MAC_PER_BATCH_ITEM_SMALL
-    mac_group = MAC_PER_KEYED_STRICT + q * MAC_PER_GROUP_VOTE
-    ach = n * mac_group / (kernel_ms * 1e-3) / 1e12
+    mac_keyed = MAC_PER_KEYED_STRICT + q * MAC_PER_KEYED_VOTE
+    ach = n * mac_keyed / (kernel_ms * 1e-3) / 1e12
     res = {"committee": N, "quorum": q, "certs_per_gpu": n, "unique_certs": uniq,
            "invalid_fraction": float((exp_st_u != 0).mean()),
            "certs_per_s": n * world / sec, "sig_checks_per_s": n * (q + 1) * world / sec,
            "ms_per_step": sec * 1e3,
            "achieved_TMAC_s": ach, "frac": ach / PEAK_TMAC, "frac_measured": ach / PEAK_TMAC_MEASURED,
-           "work_per_cert": f"{mac_group} MAC (keyed strict header {MAC_PER_KEYED_STRICT} + q x "
-                            f"{MAC_PER_GROUP_VOTE} per grouped vote: 1 R decompression + <= 17 "
-                            f"bucket additions)",
+           "work_per_cert": f"{mac_keyed} MAC (keyed strict header {MAC_PER_KEYED_STRICT} + q x "
+                            f"{MAC_PER_KEYED_VOTE} per keyed vote check: 48 comb additions, no "
+                            f"R decompression)",
            "survey_TMAC_s": n * mac_survey / (kernel_ms * 1e-3) / 1e12,
            "survey_work_note": "SURVEY 8(d) small-n constant (per-certificate Straus, 128,000 "
-                               "MAC/vote) overstates the grouped algorithm's work; not a roofline",
+                               "MAC/vote) overstates the keyed algorithm's work; not a roofline",
            "parity": "ok" if ok else "FAIL",
            "parity_check": "status and index of every certificate == construction"}
-    del T, ws, st, ix
+    del rc
     torch.cuda.empty_cache()
     return res, (s, exp_st_u, exp_ix_u)
+
+
+def run_cert_alternating(args, dev, stream, rank, world, N: int, invalid: float,
+                         stream_cache=None):
+    """Arrival pattern that alternates honest and invalid calls: the
+    all-valid stream and the same stream with `invalid` of its certificates carrying one bad
+    vote, both resident, called H, I, H, I, ... on one stream; per-call kernel time by
+    events; reported as the worst per-call rate relative to the mean all-valid call. Every
+    call's statuses and indices are checked."""
+    L = _lib.lib()
+    s = cert_stream_for(args, rank, N, stream_cache)
+    uniq = len(s["header_offsets"]) - 1
+    step = max(1, int(round(1 / invalid)))
+    sb, bst, bix = W.mutate_votes(s, np.arange(step // 2, uniq, step), seed=N)
+    n = args.certs
+    good = ResidentCerts(L, dev, s, np.zeros(uniq, np.int32), np.zeros(uniq, np.uint64), n)
+    bad = ResidentCerts(L, dev, sb, bst, bix, n, ws=good.ws)
+    torch.cuda.synchronize()
+    good.launch(stream)
+    bad.launch(stream)
+    torch.cuda.synchronize()
+    ms = {"good": [], "bad": []}
+    ok = True
+    for k in range(2 * max(2, args.cert_steps)):
+        which = good if k % 2 == 0 else bad
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        which.launch(stream)
+        e1.record()
+        torch.cuda.synchronize()
+        ms["good" if which is good else "bad"].append(e0.elapsed_time(e1))
+        ok &= which.parity()
+    mean_good = float(np.mean(ms["good"]))
+    res = {"committee": N, "pattern": "honest, invalid, honest, invalid, ...",
+           "invalid_fraction": float((bst != 0).mean()), "honest_call_ms": ms["good"],
+           "invalid_call_ms": ms["bad"],
+           "worst_call_vs_all_valid": mean_good / max(ms["good"] + ms["bad"]),
+           "certs_per_s": 2 * n * world / ((sum(ms["good"]) + sum(ms["bad"])) * 1e-3 /
+                                           len(ms["good"])),
+           "parity": "ok" if ok else "FAIL"}
+    del good, bad
+    torch.cuda.empty_cache()
+    return res
 
 
 def cpu_baseline_cert(sample, N: int, seconds: float):
@@ -816,13 +884,16 @@ def summary(r: dict) -> dict:
                          "hbm_frac": rnd(g(r, "sha512", "hbm_frac")),
                          "issue_frac": rnd(g(r, "sha512", "issue_frac")),
                          "cpu_GB_s": rnd(g(r, "sha512", "cpu_baseline", "value"), 2)}
-    for leg in ("cert_stream", "cert_stream_invalid", "cert_stream_alternating"):
+    for leg in ("cert_stream", "cert_stream_invalid"):
         if r.get(leg):
             out[leg + "_Mcerts_s"] = {k: rnd(v.get("certs_per_s", 0) / 1e6, 2)
                                       for k, v in r[leg].items()}
     if r.get("cert_stream_invalid"):
         out["cert_invalid_vs_all_valid"] = {k: rnd(v.get("vs_all_valid"))
                                             for k, v in r["cert_stream_invalid"].items()}
+    if r.get("cert_stream_alternating"):
+        out["cert_alternating_worst_vs_all_valid"] = {
+            k: rnd(v.get("worst_call_vs_all_valid")) for k, v in r["cert_stream_alternating"].items()}
     if r.get("cert_stream"):
         out["cert_cpu_certs_s"] = {k: rnd(g(v, "cpu_baseline", "value"), 0)
                                    for k, v in r["cert_stream"].items()}
@@ -997,6 +1068,11 @@ def main():
                     result["cert_stream_invalid"][f"N{N}"] = r3
                     if r3["parity"] != "ok":
                         result["parity"] = "FAIL"
+                    r4 = run_cert_alternating(args, dev, stream, rank, world, N,
+                                              args.cert_invalid, stream_cache=cache)
+                    result.setdefault("cert_stream_alternating", {})[f"N{N}"] = r4
+                    if r4["parity"] != "ok":
+                        result["parity"] = "FAIL"
                 cache.pop(N, None)
         if not args.no_batch:
             r1, bsample = run_batch10k(args, dev, stream, rank, world)
@@ -1024,7 +1100,7 @@ def main():
                 result["parity"] = "FAIL"
                 log("oracle disagrees with GPU statuses on the cpu_baseline sample")
     elif args.workload == "cert":
-        res, res_bad, cache = {}, {}, {}
+        res, res_bad, res_alt, cache = {}, {}, {}, {}
         for N in [int(x) for x in args.committees.split(",") if x]:
             res[f"N{N}"] = run_cert(args, dev, stream, rank, world, N, stream_cache=cache)[0]
             if args.cert_invalid > 0:
@@ -1032,6 +1108,8 @@ def main():
                               stream_cache=cache)[0]
                 r3["vs_all_valid"] = r3["certs_per_s"] / res[f"N{N}"]["certs_per_s"]
                 res_bad[f"N{N}"] = r3
+                res_alt[f"N{N}"] = run_cert_alternating(args, dev, stream, rank, world, N,
+                                                        args.cert_invalid, stream_cache=cache)
             cache.pop(N, None)
         last = list(res.values())[-1]
         result = {"metric": METRIC, "value": last["sig_checks_per_s"], "unit": "verifies/s",
@@ -1041,8 +1119,10 @@ def main():
                   "config": {"workload": "config2_certificate_stream",
                              "certs_per_gpu": args.certs, "parallelism": f"shard{world}"},
                   "cert_stream": res, "cert_stream_invalid": res_bad,
+                  "cert_stream_alternating": res_alt,
                   "parity": "ok" if all(r["parity"] == "ok" for r in
-                                        list(res.values()) + list(res_bad.values())) else "FAIL"}
+                                        list(res.values()) + list(res_bad.values()) +
+                                        list(res_alt.values())) else "FAIL"}
     elif args.workload == "service":
         res = {f"N{N}": run_service_latency(args, rank, world, N)
                for N in [int(x) for x in args.service_committees.split(",") if x]}

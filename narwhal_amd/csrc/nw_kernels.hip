@@ -691,7 +691,8 @@ hipError_t launch_votes_keyed(const uint32_t* cert_digest, const uint64_t* cvo, 
                      ncert, cert_ok);
   // slices of S votes through the scratch (the caller's verify_batch workspace, free until
   // the failed certificates' batches run)
-  const uint64_t S = std::min<uint64_t>(nvotes, scratch_bytes / votes_keyed_bytes_per_vote()) & ~63ull;
+  const uint64_t cap = scratch_bytes / votes_keyed_bytes_per_vote();
+  const uint64_t S = nvotes <= cap ? nvotes : cap & ~63ull;
   if (nvotes && S == 0) return hipErrorInvalidValue;
   uint32_t* base = static_cast<uint32_t*>(scratch);
   const vote_planes_t vp{base, base + 20 * S, S};

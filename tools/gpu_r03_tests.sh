@@ -1,6 +1,7 @@
 #!/bin/bash
 # GPU-box helper: the -m gpu suite, the certificate-service latency leg, and config 2 with
-# the default grouping policy and with the keyed vote checks forced (NW_CERT_KEYED=1).
+# the default policy (keyed vote checks; MERGED=1: also the merged-group policy) and with
+# variant builds (VARIANTS="name ..." = exp/<name>/libnarwhal_amd.so).
 #   bash tools/gpu_r03_tests.sh OUTDIR [pytest -k expr]
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -15,10 +16,10 @@ timeout -k 10 300 python -u bench.py --workload service > "$OUT/bench_service.js
 rc=$?; echo "service bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py --workload cert --no-cpu-baseline > "$OUT/bench_cert.json" 2> "$OUT/bench_cert.log"
 rc=$?; echo "cert bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
-NW_CERT_KEYED=1 timeout -k 10 300 python -u bench.py --workload cert --no-cpu-baseline > "$OUT/bench_cert_keyed.json" 2> "$OUT/bench_cert_keyed.log"
-rc=$?; echo "keyed cert bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
+[ -n "$MERGED" ] && { NW_CERT_KEYED=0 timeout -k 10 300 python -u bench.py --workload cert --no-cpu-baseline > "$OUT/bench_cert_merged.json" 2> "$OUT/bench_cert_merged.log"
+rc=$?; echo "merged-groups cert bench rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
 for V in $VARIANTS; do
-  NW_LIB=exp/$V/libnarwhal_amd.so NW_CERT_KEYED=1 timeout -k 10 300 python -u bench.py --workload cert \
+  NW_LIB=exp/$V/libnarwhal_amd.so timeout -k 10 300 python -u bench.py --workload cert \
     --no-cpu-baseline > "$OUT/bench_cert_keyed_$V.json" 2> "$OUT/bench_cert_keyed_$V.log"
   rc=$?; echo "keyed cert bench $V rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
