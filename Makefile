@@ -8,7 +8,7 @@ HDRS := $(wildcard $(CSRC)/*.hpp) $(CSRC)/nw_kernels.h $(CSRC)/nw_runtime.h incl
 LIB := narwhal_amd/libnarwhal_amd.so
 BUILD := build
 
-all: $(LIB) oracle hostcheck
+all: $(LIB) oracle hostcheck loadgen
 
 $(BUILD)/nw_kernels.o: $(CSRC)/nw_kernels.hip $(HDRS)
 	@mkdir -p $(BUILD)
@@ -30,11 +30,15 @@ $(BUILD)/nw_wire.o: $(CSRC)/nw_wire.cpp $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
+$(BUILD)/nw_service.o: $(CSRC)/nw_service.cpp $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
 $(BUILD)/nw_api.o: $(CSRC)/nw_api.cpp $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-$(LIB): $(BUILD)/nw_kernels.o $(BUILD)/nw_batch.o $(BUILD)/nw_cert.o $(BUILD)/nw_api.o $(BUILD)/nw_jobs.o $(BUILD)/nw_wire.o
+$(LIB): $(BUILD)/nw_kernels.o $(BUILD)/nw_batch.o $(BUILD)/nw_cert.o $(BUILD)/nw_api.o $(BUILD)/nw_jobs.o $(BUILD)/nw_wire.o $(BUILD)/nw_service.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 oracle:
@@ -44,12 +48,16 @@ hostcheck: tools/libnw_hostcheck.so
 tools/libnw_hostcheck.so: tools/hostcheck.hip $(HDRS)
 	$(HIPCC) --cuda-host-only -O2 -std=c++17 -fPIC -shared -Iinclude $< -o $@
 
+loadgen: tools/libnw_loadgen.so
+tools/libnw_loadgen.so: tools/nw_loadgen.cpp include/narwhal_amd.h $(LIB)
+	g++ -O2 -std=c++17 -fPIC -shared -Iinclude $< -o $@ -Lnarwhal_amd -lnarwhal_amd -Wl,-rpath,'$$ORIGIN/../narwhal_amd' -pthread
+
 ubench: tools/ubench_valu
 tools/ubench_valu: tools/ubench_valu.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 $< -o $@
 
 clean:
-	rm -rf $(BUILD) $(LIB) tools/libnw_hostcheck.so
+	rm -rf $(BUILD) $(LIB) tools/libnw_hostcheck.so tools/libnw_loadgen.so
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle hostcheck ubench clean
+.PHONY: all oracle hostcheck loadgen ubench clean

@@ -190,6 +190,10 @@ def ptr(t: torch.Tensor) -> ctypes.c_void_p:
     return ctypes.c_void_p(t.data_ptr())
 
 
+def ptr_np(a: np.ndarray) -> ctypes.c_void_p:
+    return ctypes.c_void_p(a.ctypes.data)
+
+
 def check(rc: int, what: str) -> None:
     if rc != 0:
         raise RuntimeError(f"{what}: rc={rc} {_lib.lib().nw_last_error().decode()}")
@@ -711,18 +715,34 @@ def run_wire(args, dev, stream, rank, world, N: int = 4):
             "parity_check": "status and index of every frame's certificate == construction"}
 
 
+def loadgen_lib():
+    """tools/libnw_loadgen.so (bench tooling over the public C ABI, tools/nw_loadgen.cpp)."""
+    path = os.path.join(ROOT, "tools", "libnw_loadgen.so")
+    L = ctypes.CDLL(path)
+    P = ctypes.c_void_p
+    L.nw_loadgen_certificates.argtypes = [P, P, P, P, ctypes.c_double, ctypes.c_uint64,
+                                          ctypes.c_size_t, ctypes.c_uint32, ctypes.c_size_t,
+                                          ctypes.c_uint32, P, P]
+    L.nw_loadgen_certificates.restype = ctypes.c_int
+    return L
+
+
 def run_service_latency(args, rank, world, N: int, cache=None):
     """SURVEY 8(f) rank 1: the primary's Core::sanitize_certificate calls
-    Certificate::verify one certificate at a time (primary/src/core.rs:338-346). Here single
-    certificates arrive at a fixed offered rate (1k / 10k / 100k per second) and go through
-    the aggregating VerificationService (narwhal_amd/service.py: coalesced per max_delay
-    into nw_submit_certificates_verify_many jobs, completion by nw_job_notify); latency =
-    verdict time - scheduled arrival time, per certificate. 1 % of the certificates carry
-    one invalid vote; every (status, index) is checked against the construction. Beside it:
-    the CPU oracle's single-certificate Certificate::verify latency and rate on 1 thread
-    (the reference verifies inline on the single Core task)."""
+    Certificate::verify one certificate at a time (primary/src/core.rs:338-346). Single
+    certificates arrive at a fixed offered rate (1k .. 1M per second, open loop) and go
+    through the library's native aggregation service (nw_service_certificate: coalesced per
+    max_delay / max_items into nw_submit_certificates_verify_many jobs, verdicts by
+    callback), driven by tools/nw_loadgen.cpp from `producers` threads, as a Rust crate's
+    tokio tasks would call it; latency = verdict time - scheduled arrival time, per
+    certificate. Beside it, the asyncio front end (narwhal_amd/service.py NativeService) at
+    the rates Python itself can issue. 1 % of the certificates carry one invalid vote; every
+    (status, index) is checked against the construction. CPU reference point: the oracle's
+    single-certificate Certificate::verify latency and rate on 1 thread (the reference
+    verifies inline on the single Core task)."""
     import asyncio
     from narwhal_amd import service as SV
+    from narwhal_amd.messages import certificates_struct, committee_struct
     uniq = args.service_unique
     keys = [(bytes(pk), bytes(sd) + bytes(pk)) for sd, pk in
             zip(W.fixture_seeds(N), C.keypair_from_seed_many(W.fixture_seeds(N)))]
@@ -730,7 +750,32 @@ def run_service_latency(args, rank, world, N: int, cache=None):
                              lambda d, o: C.sha512_digest32_many(d, o[:-1], np.diff(o)),
                              seed=300 + rank)
     s, exp_st, exp_ix = W.mutate_votes(s, np.arange(50, uniq, 100), seed=N + 11)
+    exp_st = np.ascontiguousarray(exp_st, np.int32)
+    exp_ix = np.ascontiguousarray(exp_ix, np.uint64)
     hb, ho, vo = s["header_bytes"].tobytes(), s["header_offsets"], s["vote_offsets"]
+    LG = loadgen_lib()
+    cc, cs = committee_struct(s["committee"]), certificates_struct(s, uniq)
+    delay_us = int(args.service_delay * 1e6)
+
+    def native_load(rate: float, seconds: float):
+        total = max(1, int(rate * seconds))
+        lat = np.zeros(total)
+        out3 = np.zeros(3)
+        rc = LG.nw_loadgen_certificates(ctypes.byref(cc), ctypes.byref(cs), ptr_np(exp_st),
+                                        ptr_np(exp_ix), rate, total, args.service_max_items,
+                                        delay_us, args.service_inflight, args.service_producers,
+                                        ptr_np(lat), ptr_np(out3))
+        check(rc, "nw_loadgen_certificates")
+        el, jobs, bad = float(out3[0]), int(out3[1]), int(out3[2])
+        return {"offered_certs_per_s": rate, "certs": total,
+                "achieved_certs_per_s": total / el if el > 0 else None,
+                "p50_ms": float(np.percentile(lat, 50) * 1e3),
+                "p90_ms": float(np.percentile(lat, 90) * 1e3),
+                "p99_ms": float(np.percentile(lat, 99) * 1e3),
+                "max_ms": float(lat.max() * 1e3), "jobs": jobs,
+                "certs_per_job": total / max(1, jobs),
+                "parity": "ok" if bad == 0 else f"FAIL ({bad} verdicts differ)"}
+
     rows = [SV.CertRow(hb[int(ho[i]):int(ho[i + 1])], int(s["payload_counts"][i]),
                        s["ids"][i].tobytes(), s["header_sigs"][i].tobytes(),
                        s["vote_pks"][int(vo[i]):int(vo[i + 1])].tobytes(),
@@ -738,51 +783,62 @@ def run_service_latency(args, rank, world, N: int, cache=None):
                        int(vo[i + 1] - vo[i])) for i in range(uniq)]
     expect = [(int(a), int(b)) for a, b in zip(exp_st, exp_ix)]
 
-    class _Com:
-        def packed(self):
-            return s["committee"]
-    com = _Com()
-
-    async def one_load(rate: float, seconds: float):
-        svc = SV.VerificationService(max_delay=args.service_delay)
+    async def asyncio_load(rate: float, seconds: float):
+        svc = SV.NativeService(s["committee"], max_items=args.service_max_items,
+                               max_delay=args.service_delay, max_inflight=args.service_inflight)
         loop = asyncio.get_running_loop()
         total = max(1, int(rate * seconds))
         lat = np.zeros(total)
-        ok = [True]
-        tasks = []
+        bad = [0]
+        done = loop.create_future()
+        left = [total]
 
-        async def one(i, t_arr):
-            r = await svc.certificate_status(com, rows[i % uniq])
-            lat[i] = loop.time() - t_arr
-            if r != expect[i % uniq]:
-                ok[0] = False
-        # warm the committee's tables and the job pool (not timed)
-        await asyncio.gather(*[svc.certificate_status(com, rows[i]) for i in range(64)])
+        def make_cb(i, t_arr):
+            def cb(f):
+                lat[i] = loop.time() - t_arr
+                if f.result() != expect[i % uniq]:
+                    bad[0] += 1
+                left[0] -= 1
+                if left[0] == 0:
+                    done.set_result(None)
+            return cb
+        await asyncio.gather(*[svc.certificate_status(rows[i]) for i in range(64)])   # warm
+        jobs0 = svc.stats()[1]
         t0 = loop.time()
         i = 0
         while i < total:
             now = loop.time()
             while i < total and t0 + i / rate <= now:
-                tasks.append(loop.create_task(one(i, t0 + i / rate)))
+                (lp, fut), f = svc._future()
+                svc.submit_certificate(rows[i % uniq], (lp, fut))
+                f.add_done_callback(make_cb(i, t0 + i / rate))
                 i += 1
             await asyncio.sleep(min(0.0002, max(0.0, t0 + i / rate - loop.time())))
-        await asyncio.gather(*tasks)
+        await done
         el = loop.time() - t0
-        await svc.drain()
+        jobs = svc.stats()[1] - jobs0
+        svc.close()
         return {"offered_certs_per_s": rate, "certs": total, "achieved_certs_per_s": total / el,
                 "p50_ms": float(np.percentile(lat, 50) * 1e3),
                 "p99_ms": float(np.percentile(lat, 99) * 1e3),
-                "max_ms": float(lat.max() * 1e3), "jobs": svc.jobs_submitted,
-                "certs_per_job": total / max(1, svc.jobs_submitted - 1),
-                "parity": "ok" if ok[0] else "FAIL"}
+                "max_ms": float(lat.max() * 1e3), "jobs": jobs,
+                "certs_per_job": total / max(1, jobs),
+                "parity": "ok" if bad[0] == 0 else "FAIL"}
 
-    loads = [asyncio.run(one_load(r, min(args.service_seconds, 200_000 / r)))
-             for r in (1_000, 10_000, 100_000)]
+    rates = [float(x) for x in args.service_rates.split(",") if x]
+    loads = [native_load(r, min(args.service_seconds, args.service_max_certs / r)) for r in rates]
+    py_loads = [asyncio.run(asyncio_load(r, min(args.service_seconds, 20_000 / r)))
+                for r in (1_000.0, 10_000.0)]
     res = {"committee": N, "quorum": int(W.quorum(N)), "max_delay_ms": args.service_delay * 1e3,
+           "max_items": args.service_max_items, "max_inflight": args.service_inflight,
+           "producers": args.service_producers,
            "invalid_fraction": float((exp_st != 0).mean()), "loads": loads,
-           "path": "asyncio VerificationService.certificate_status -> "
-                   "nw_submit_certificates_verify_many + nw_job_notify",
-           "parity": "ok" if all(x["parity"] == "ok" for x in loads) else "FAIL"}
+           "path": "nw_service_certificate (native aggregation, tools/nw_loadgen.cpp producers) "
+                   "-> nw_submit_certificates_verify_many jobs -> verdict callbacks",
+           "python_asyncio": {"path": "asyncio NativeService.submit_certificate -> "
+                                      "nw_service_certificate, futures resolved by callback",
+                              "loads": py_loads},
+           "parity": "ok" if all(x["parity"] == "ok" for x in loads + py_loads) else "FAIL"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         O = oracle_module()
 
@@ -906,8 +962,10 @@ def summary(r: dict) -> dict:
     if "wire_ingest" in r:
         out["wire_Mcerts_s"] = rnd(r["wire_ingest"].get("certs_per_s", 0) / 1e6, 2)
     if r.get("service_latency"):
-        out["service"] = {k: {"p50_p99_ms": [[int(x["offered_certs_per_s"]), rnd(x["p50_ms"], 2),
-                                               rnd(x["p99_ms"], 2)] for x in v["loads"]],
+        out["service"] = {k: {"offered_achieved_p50ms_p99ms": [
+                                  [int(x["offered_certs_per_s"]),
+                                   int(x["achieved_certs_per_s"] or 0), rnd(x["p50_ms"], 2),
+                                   rnd(x["p99_ms"], 2)] for x in v["loads"]],
                               "cpu_1cert_ms": rnd(g(v, "cpu_oracle_one_thread", "p50_ms"), 2)}
                           for k, v in r["service_latency"].items()}
     return out
@@ -944,6 +1002,13 @@ def main():
     ap.add_argument("--service-committees", default="4,50")
     ap.add_argument("--service-unique", type=int, default=8192)
     ap.add_argument("--service-seconds", type=float, default=1.0)
+    ap.add_argument("--service-rates", default="1000,10000,100000,1000000")
+    ap.add_argument("--service-max-certs", type=float, default=400_000,
+                    help="certificates per offered-load run at most (runs shorter than "
+                         "--service-seconds at high rates)")
+    ap.add_argument("--service-max-items", type=int, default=1 << 16)
+    ap.add_argument("--service-inflight", type=int, default=4)
+    ap.add_argument("--service-producers", type=int, default=2)
     ap.add_argument("--service-delay", type=float, default=0.0005,
                     help="VerificationService max_delay (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -193,6 +193,56 @@ int nw_job_notify(nw_job* job, void (*fn)(void*), void* arg);
 /* Return the job's buffers to the pool (waits first if it is still running). */
 void nw_job_release(nw_job* job);
 
+/* ---- aggregation service: one request per message, coalesced into device jobs ------- */
+/* The front end a crypto-gpu crate puts behind the primary's per-message checks: Core
+ * verifies one Header / Vote / Certificate at a time (primary/src/core.rs:306-346,
+ * sanitize_header / sanitize_vote / sanitize_certificate), and a certificate carries only
+ * 3..67 signatures, so single calls are coalesced, the same request/reply shape as
+ * crypto::SignatureService (crypto/src/lib.rs:222-250). Each request is copied at submit
+ * into the open batch of its kind; a service thread submits a batch as ONE job (the
+ * nw_submit_* calls above, so the committee's key tables stay on the device across jobs)
+ * once it holds max_items units (certificate = 1 + votes, batch = its votes, else 1) or
+ * max_delay_us after its first request; at most max_inflight jobs are queued at once (the
+ * next batch keeps filling meanwhile). A second service thread waits for the jobs in
+ * order and calls fn(arg, status, index) once per accepted request: status / index as the
+ * corresponding bulk call returns them (NW_DAG_* for messages, NW_ERR_* for verify /
+ * verify_batch, index = the batch's fail index), or a negative NW_E_* if the job failed.
+ * fn runs on that thread; it may submit new requests but must not call nw_service_drain or
+ * nw_service_destroy. Submits are thread-safe and never wait for the device. The service
+ * runs on the creating thread's nw_set_device() choice (NW_ALL_DEVICES: jobs fan out).
+ * committee may be NULL for a service that only takes nw_service_verify / _verify_batch. */
+typedef struct nw_service nw_service;
+typedef void (*nw_verdict_fn)(void* arg, int32_t status, uint64_t index);
+int nw_service_create(const struct nw_committee* committee, size_t max_items,
+                      uint32_t max_delay_us, size_t max_inflight, nw_service** out);
+/* Certificate::verify (primary/src/messages.rs:189-215): header fields as nw_certificates
+ * row i (header_bytes = the bytes `Hash for Header` hashes), votes nvotes x (32 + 64). */
+int nw_service_certificate(nw_service* s, const uint8_t* header_bytes, size_t header_len,
+                           uint32_t payload_count, const uint8_t* id, const uint8_t* header_sig,
+                           const uint8_t* vote_pks, const uint8_t* vote_sigs, size_t nvotes,
+                           nw_verdict_fn fn, void* arg);
+/* Header::verify (primary/src/messages.rs:48-67). */
+int nw_service_header(nw_service* s, const uint8_t* header_bytes, size_t header_len,
+                      uint32_t payload_count, const uint8_t* id, const uint8_t* sig,
+                      nw_verdict_fn fn, void* arg);
+/* Vote::verify (primary/src/messages.rs:131-142). */
+int nw_service_vote(nw_service* s, const uint8_t* id, uint64_t round, const uint8_t* origin,
+                    const uint8_t* author, const uint8_t* sig, nw_verdict_fn fn, void* arg);
+/* crypto::Signature::verify (crypto/src/lib.rs:200-204) of one 32-byte digest. */
+int nw_service_verify(nw_service* s, const uint8_t* digest, const uint8_t* pk,
+                      const uint8_t* sig, nw_verdict_fn fn, void* arg);
+/* crypto::Signature::verify_batch (crypto/src/lib.rs:206-219) over n (pk, sig) pairs. */
+int nw_service_verify_batch(nw_service* s, const uint8_t* digest, const uint8_t* pks,
+                            const uint8_t* sigs, size_t n, nw_verdict_fn fn, void* arg);
+/* Submit every queued request now (does not wait). */
+int nw_service_flush(nw_service* s);
+/* Flush and wait until the callback of every request accepted before the call returned. */
+int nw_service_drain(nw_service* s);
+/* Requests accepted and jobs submitted so far (either pointer may be NULL). */
+int nw_service_stats(nw_service* s, uint64_t* requests, uint64_t* jobs);
+/* Drain, stop the service threads and free the service. */
+void nw_service_destroy(nw_service* s);
+
 /* ---- primary messages: Header / Vote / Certificate verification -------------------- */
 /* config::Committee (config/src/lib.rs:139-173): authorities sorted by public-key bytes
  * (BTreeMap order), their stake (config::Stake = u32) and worker ids (WorkerId = u32). */

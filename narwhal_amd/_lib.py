@@ -29,6 +29,8 @@ _lib = None
 
 # void (*fn)(void*) for nw_job_notify
 NOTIFY_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+# void (*fn)(void* arg, int32_t status, uint64_t index) for the nw_service_* requests
+VERDICT_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64)
 
 
 class EngineError(RuntimeError):
@@ -83,6 +85,14 @@ def lib() -> ctypes.CDLL:
         "nw_job_notify": ([P, NOTIFY_FN, P], I), "nw_job_release": ([P], None),
         "nw_primary_messages_verify_wire": ([P, P, P, S, P, P, P], I),
         "nw_primary_messages_scan": ([P, P, S, P, P], I),
+        "nw_service_create": ([P, S, ctypes.c_uint32, S, ctypes.POINTER(P)], I),
+        "nw_service_certificate": ([P, P, S, ctypes.c_uint32, P, P, P, P, S, VERDICT_FN, P], I),
+        "nw_service_header": ([P, P, S, ctypes.c_uint32, P, P, VERDICT_FN, P], I),
+        "nw_service_vote": ([P, P, ctypes.c_uint64, P, P, P, VERDICT_FN, P], I),
+        "nw_service_verify": ([P, P, P, P, VERDICT_FN, P], I),
+        "nw_service_verify_batch": ([P, P, P, P, S, VERDICT_FN, P], I),
+        "nw_service_flush": ([P], I), "nw_service_drain": ([P], I),
+        "nw_service_stats": ([P, P, P], I), "nw_service_destroy": ([P], None),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -1,0 +1,465 @@
+// nw_service.cpp — native aggregation service (nw_service_*): single Header / Vote /
+// Certificate / Signature::verify / Signature::verify_batch requests coalesced into device
+// jobs.
+//
+// Why: Narwhal's primary verifies one message at a time on its single Core task
+// (primary/src/core.rs:306-346: sanitize_header / sanitize_vote / sanitize_certificate call
+// Header/Vote/Certificate::verify inline), and a certificate carries only 3..67 signatures,
+// far too little work for a GPU launch. crypto::SignatureService (crypto/src/lib.rs:222-250)
+// is the reference's own shape for this: requests over a channel, replies over oneshot
+// channels. A Rust crypto-gpu crate binds these entry points and completes a oneshot
+// channel from the verdict callback, so its tokio tasks never block.
+//
+// Structure: one service per committee. A request is copied into the open batch of its
+// kind under the service mutex (a few hundred bytes, no allocation in the steady state:
+// batches are recycled). A flusher thread submits a batch as ONE device job
+// (nw_submit_*: the committee-aware pipeline with its key tables kept on the device) when it
+// holds max_items units or max_delay has passed since its first request; a completer thread
+// waits for the jobs in submission order and calls every request's verdict callback. At most
+// max_inflight jobs are queued on the device at once (backpressure on the flusher; requests
+// keep accumulating into the next, larger batch meanwhile, which is what keeps the device
+// efficient under load).
+#include <string.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "narwhal_amd.h"
+#include "nw_runtime.h"
+
+namespace {
+
+using nw::rt::set_err;
+using Clock = std::chrono::steady_clock;
+
+enum Kind { K_CERT = 0, K_HEADER, K_VOTE, K_STRICT, K_BATCH, K_COUNT };
+
+struct Req {
+  nw_verdict_fn fn;
+  void* arg;
+};
+
+template <class T>
+void append(std::vector<T>& v, const void* src, size_t count) {
+  const size_t o = v.size();
+  v.resize(o + count);
+  if (count) memcpy(v.data() + o, src, count * sizeof(T));
+}
+
+// One kind's requests in the SoA form of its nw_submit_* entry point.
+struct Batch {
+  Kind kind;
+  size_t units = 0;
+  Clock::time_point first;
+  std::vector<Req> reqs;
+  // Header / Certificate (nw_certificates)
+  std::vector<uint8_t> header_bytes;
+  std::vector<uint64_t> header_offsets{0};
+  std::vector<uint32_t> payload_counts;
+  std::vector<uint8_t> ids, header_sigs;
+  std::vector<uint64_t> vote_offsets{0};
+  std::vector<uint8_t> vote_pks, vote_sigs;
+  // Vote (nw_submit_votes_verify_many): ids and signatures reuse ids / header_sigs
+  std::vector<uint64_t> rounds;
+  std::vector<uint8_t> origins, authors;
+  // Signature::verify / verify_batch: digests (n x 32), keys, signatures, batch offsets
+  std::vector<uint8_t> digests, pks, sigs;
+  std::vector<uint64_t> batch_offsets{0};
+  // outputs and the job
+  std::vector<int32_t> status;
+  std::vector<uint64_t> index;
+  nw_job* job = nullptr;
+  int rc = 0;
+
+  explicit Batch(Kind k) : kind(k) {}
+  void clear() {
+    units = 0;
+    reqs.clear();
+    header_bytes.clear();
+    header_offsets.assign(1, 0);
+    payload_counts.clear();
+    ids.clear();
+    header_sigs.clear();
+    vote_offsets.assign(1, 0);
+    vote_pks.clear();
+    vote_sigs.clear();
+    rounds.clear();
+    origins.clear();
+    authors.clear();
+    digests.clear();
+    pks.clear();
+    sigs.clear();
+    batch_offsets.assign(1, 0);
+    job = nullptr;
+    rc = 0;
+  }
+};
+
+uint8_t g_dummy[64];
+template <class T>
+const T* nz(const std::vector<T>& v) {
+  return v.empty() ? reinterpret_cast<const T*>(g_dummy) : v.data();
+}
+
+}  // namespace
+
+struct nw_service {
+  int device = 0;   // the creating thread's nw_set_device value (NW_ALL_DEVICES = fan out)
+  bool has_committee = false;
+  std::vector<uint8_t> com_pks;
+  std::vector<uint32_t> com_stakes;
+  std::vector<uint64_t> com_wo;
+  std::vector<uint32_t> com_wi;
+  nw_committee com{};
+  size_t max_items = 1 << 16;
+  Clock::duration delay{};
+  size_t max_inflight = 4;
+
+  std::mutex m;
+  std::condition_variable cv_flush;     // flusher: new request / flush / stop
+  std::condition_variable cv_inflight;  // completer: a job was submitted
+  std::condition_variable cv_space;     // flusher: in-flight count dropped
+  std::condition_variable cv_idle;      // drain: requests completed
+  std::unique_ptr<Batch> open[K_COUNT];
+  std::vector<std::unique_ptr<Batch>> spare[K_COUNT];
+  std::deque<std::unique_ptr<Batch>> inflight;
+  bool force = false, stop = false, flusher_done = false;
+  uint64_t accepted = 0, completed = 0, jobs = 0;
+  std::thread flusher, completer;
+
+  // Adds one request to its kind's open batch (fill copies the inputs); 0 or NW_E_*.
+  template <class Fill>
+  int add(Kind k, size_t units, nw_verdict_fn fn, void* arg, Fill fill) {
+    if (!fn) return set_err(NW_E_INVALID_ARG, "null verdict callback");
+    std::lock_guard<std::mutex> g(m);
+    if (stop) return set_err(NW_E_INVALID_ARG, "service is shutting down");
+    Batch& b = *open[k];
+    const bool first_req = b.reqs.empty();
+    if (first_req) b.first = Clock::now();
+    fill(b);
+    b.reqs.push_back({fn, arg});
+    const size_t before = b.units;
+    b.units += units;
+    ++accepted;
+    // wake the flusher to arm its timer (first request) or because the batch just filled
+    if (first_req || (before < max_items && b.units >= max_items)) cv_flush.notify_one();
+    return 0;
+  }
+
+  std::unique_ptr<Batch> take_spare(Kind k) {
+    if (!spare[k].empty()) {
+      std::unique_ptr<Batch> b = std::move(spare[k].back());
+      spare[k].pop_back();
+      return b;
+    }
+    return std::unique_ptr<Batch>(new (std::nothrow) Batch(k));
+  }
+
+  // Flusher thread: one device job per batch.
+  int submit(Batch& b) {
+    const size_t n = b.reqs.size();
+    b.status.assign(n, 0);
+    b.index.assign(n, 0);
+    switch (b.kind) {
+      case K_CERT:
+      case K_HEADER: {
+        nw_certificates c{};
+        c.n = n;
+        c.header_bytes = nz(b.header_bytes);
+        c.header_offsets = b.header_offsets.data();
+        c.payload_counts = b.payload_counts.data();
+        c.ids = b.ids.data();
+        c.header_sigs = b.header_sigs.data();
+        if (b.kind == K_CERT) {
+          c.vote_offsets = b.vote_offsets.data();
+          c.vote_pks = nz(b.vote_pks);
+          c.vote_sigs = nz(b.vote_sigs);
+          return nw_submit_certificates_verify_many(&com, &c, nullptr, b.status.data(),
+                                                    b.index.data(), &b.job);
+        }
+        return nw_submit_headers_verify_many(&com, &c, b.status.data(), b.index.data(), &b.job);
+      }
+      case K_VOTE:
+        return nw_submit_votes_verify_many(&com, b.ids.data(), b.rounds.data(), b.origins.data(),
+                                           b.authors.data(), b.header_sigs.data(), n,
+                                           b.status.data(), &b.job);
+      case K_STRICT:
+        return nw_submit_verify_strict(b.digests.data(), 32, b.pks.data(), b.sigs.data(), n,
+                                       b.status.data(), nullptr, &b.job);
+      case K_BATCH:
+        return nw_submit_verify_batch_many(b.digests.data(), nz(b.pks), nz(b.sigs),
+                                           b.batch_offsets.data(), n, nullptr, b.status.data(),
+                                           b.index.data(), &b.job);
+      default:
+        return set_err(NW_E_INVALID_ARG, "bad request kind");
+    }
+  }
+
+  void flusher_main() {
+    nw_set_device(device);
+    std::unique_lock<std::mutex> lk(m);
+    for (;;) {
+      const Clock::time_point now = Clock::now();
+      Clock::time_point wake = Clock::time_point::max();
+      int pick = -1;
+      for (int k = 0; k < K_COUNT; ++k) {
+        const Batch& b = *open[k];
+        if (b.reqs.empty()) continue;
+        if (stop || force || b.units >= max_items || now >= b.first + delay) {
+          pick = k;
+          break;
+        }
+        if (b.first + delay < wake) wake = b.first + delay;
+      }
+      if (pick < 0) {
+        force = false;
+        if (stop) break;
+        if (wake == Clock::time_point::max())
+          cv_flush.wait(lk);
+        else
+          cv_flush.wait_until(lk, wake);
+        continue;
+      }
+      // backpressure: at most max_inflight jobs queued; the open batch keeps growing
+      if (inflight.size() >= max_inflight) {
+        cv_space.wait(lk);
+        continue;
+      }
+      std::unique_ptr<Batch> fresh = take_spare(static_cast<Kind>(pick));
+      if (!fresh) {   // out of memory: submit nothing new until something completes
+        cv_space.wait_for(lk, std::chrono::milliseconds(1));
+        continue;
+      }
+      std::unique_ptr<Batch> b = std::move(open[pick]);
+      open[pick] = std::move(fresh);
+      lk.unlock();
+      b->rc = submit(*b);
+      lk.lock();
+      ++jobs;
+      inflight.push_back(std::move(b));
+      cv_inflight.notify_one();
+    }
+    flusher_done = true;
+    cv_inflight.notify_all();
+  }
+
+  void completer_main() {
+    nw_set_device(device);
+    std::unique_lock<std::mutex> lk(m);
+    for (;;) {
+      cv_inflight.wait(lk, [&] { return !inflight.empty() || flusher_done; });
+      if (inflight.empty()) break;
+      std::unique_ptr<Batch> b = std::move(inflight.front());
+      inflight.pop_front();
+      cv_space.notify_one();
+      lk.unlock();
+      int rc = b->rc;
+      if (b->job) {
+        if (!rc) rc = nw_job_wait(b->job);
+        nw_job_release(b->job);
+        b->job = nullptr;
+      }
+      const size_t n = b->reqs.size();
+      for (size_t i = 0; i < n; ++i)
+        b->reqs[i].fn(b->reqs[i].arg, rc ? rc : b->status[i], rc ? 0 : b->index[i]);
+      lk.lock();
+      completed += n;
+      b->clear();
+      spare[b->kind].push_back(std::move(b));
+      cv_idle.notify_all();
+    }
+  }
+};
+
+extern "C" {
+
+int nw_service_create(const nw_committee* committee, size_t max_items, uint32_t max_delay_us,
+                      size_t max_inflight, nw_service** out) {
+  if (!out) return set_err(NW_E_INVALID_ARG, "null service pointer");
+  *out = nullptr;
+  int rc = nw::rt::ensure_init();
+  if (rc) return rc;
+  if (committee) {
+    rc = nw::rt::check_committee(committee);
+    if (rc) return rc;
+  }
+  nw_service* s = new (std::nothrow) nw_service;
+  if (!s) return set_err(NW_E_OUT_OF_MEMORY, "service allocation");
+  s->device = nw_get_device();
+  s->max_items = max_items ? max_items : 1;
+  s->delay = std::chrono::duration_cast<Clock::duration>(std::chrono::microseconds(max_delay_us));
+  s->max_inflight = max_inflight ? max_inflight : 1;
+  if (committee) {
+    const size_t na = committee->nauth, nwk = na ? committee->worker_offsets[na] : 0;
+    s->has_committee = true;
+    append(s->com_pks, committee->pks, 32 * na);
+    append(s->com_stakes, committee->stakes, na);
+    if (na) append(s->com_wo, committee->worker_offsets, na + 1);
+    else s->com_wo.assign(1, 0);
+    append(s->com_wi, committee->worker_ids, nwk);
+    s->com.nauth = na;
+    s->com.pks = nz(s->com_pks);
+    s->com.stakes = nz(s->com_stakes);
+    s->com.worker_offsets = s->com_wo.data();
+    s->com.worker_ids = nz(s->com_wi);
+  }
+  for (int k = 0; k < K_COUNT; ++k) {
+    s->open[k].reset(new (std::nothrow) Batch(static_cast<Kind>(k)));
+    if (!s->open[k]) {
+      delete s;
+      return set_err(NW_E_OUT_OF_MEMORY, "service allocation");
+    }
+  }
+  try {
+    s->flusher = std::thread([s] { s->flusher_main(); });
+    s->completer = std::thread([s] { s->completer_main(); });
+  } catch (...) {
+    {
+      std::lock_guard<std::mutex> g(s->m);
+      s->stop = true;
+    }
+    s->cv_flush.notify_all();
+    if (s->flusher.joinable()) s->flusher.join();
+    if (s->completer.joinable()) s->completer.join();
+    delete s;
+    return set_err(NW_E_OUT_OF_MEMORY, "service threads");
+  }
+  *out = s;
+  return 0;
+}
+
+static int need_committee(nw_service* s) {
+  if (!s) return set_err(NW_E_INVALID_ARG, "null service");
+  if (!s->has_committee) return set_err(NW_E_INVALID_ARG, "service has no committee");
+  return 0;
+}
+
+static int check_header(const uint8_t* header_bytes, size_t header_len, uint32_t payload_count,
+                        const uint8_t* id, const uint8_t* sig) {
+  if (!header_bytes || !id || !sig) return set_err(NW_E_INVALID_ARG, "null pointer");
+  const uint64_t fixed = 40 + 36 * (uint64_t)payload_count;
+  if (header_len < fixed || (header_len - fixed) % 32 != 0)
+    return set_err(NW_E_INVALID_ARG, "header bytes do not match payload_count");
+  return 0;
+}
+
+int nw_service_certificate(nw_service* s, const uint8_t* header_bytes, size_t header_len,
+                           uint32_t payload_count, const uint8_t* id, const uint8_t* header_sig,
+                           const uint8_t* vote_pks, const uint8_t* vote_sigs, size_t nvotes,
+                           nw_verdict_fn fn, void* arg) {
+  int rc = need_committee(s);
+  if (!rc) rc = check_header(header_bytes, header_len, payload_count, id, header_sig);
+  if (rc) return rc;
+  if (nvotes && (!vote_pks || !vote_sigs)) return set_err(NW_E_INVALID_ARG, "null votes");
+  return s->add(K_CERT, 1 + nvotes, fn, arg, [&](Batch& b) {
+    append(b.header_bytes, header_bytes, header_len);
+    b.header_offsets.push_back(b.header_bytes.size());
+    b.payload_counts.push_back(payload_count);
+    append(b.ids, id, 32);
+    append(b.header_sigs, header_sig, 64);
+    append(b.vote_pks, vote_pks, 32 * nvotes);
+    append(b.vote_sigs, vote_sigs, 64 * nvotes);
+    b.vote_offsets.push_back(b.vote_offsets.back() + nvotes);
+  });
+}
+
+int nw_service_header(nw_service* s, const uint8_t* header_bytes, size_t header_len,
+                      uint32_t payload_count, const uint8_t* id, const uint8_t* sig,
+                      nw_verdict_fn fn, void* arg) {
+  int rc = need_committee(s);
+  if (!rc) rc = check_header(header_bytes, header_len, payload_count, id, sig);
+  if (rc) return rc;
+  return s->add(K_HEADER, 1, fn, arg, [&](Batch& b) {
+    append(b.header_bytes, header_bytes, header_len);
+    b.header_offsets.push_back(b.header_bytes.size());
+    b.payload_counts.push_back(payload_count);
+    append(b.ids, id, 32);
+    append(b.header_sigs, sig, 64);
+  });
+}
+
+int nw_service_vote(nw_service* s, const uint8_t* id, uint64_t round, const uint8_t* origin,
+                    const uint8_t* author, const uint8_t* sig, nw_verdict_fn fn, void* arg) {
+  int rc = need_committee(s);
+  if (rc) return rc;
+  if (!id || !origin || !author || !sig) return set_err(NW_E_INVALID_ARG, "null pointer");
+  return s->add(K_VOTE, 1, fn, arg, [&](Batch& b) {
+    append(b.ids, id, 32);
+    b.rounds.push_back(round);
+    append(b.origins, origin, 32);
+    append(b.authors, author, 32);
+    append(b.header_sigs, sig, 64);
+  });
+}
+
+int nw_service_verify(nw_service* s, const uint8_t* digest, const uint8_t* pk,
+                      const uint8_t* sig, nw_verdict_fn fn, void* arg) {
+  if (!s) return set_err(NW_E_INVALID_ARG, "null service");
+  if (!digest || !pk || !sig) return set_err(NW_E_INVALID_ARG, "null pointer");
+  return s->add(K_STRICT, 1, fn, arg, [&](Batch& b) {
+    append(b.digests, digest, 32);
+    append(b.pks, pk, 32);
+    append(b.sigs, sig, 64);
+  });
+}
+
+int nw_service_verify_batch(nw_service* s, const uint8_t* digest, const uint8_t* pks,
+                            const uint8_t* sigs, size_t n, nw_verdict_fn fn, void* arg) {
+  if (!s) return set_err(NW_E_INVALID_ARG, "null service");
+  if (!digest || (n && (!pks || !sigs))) return set_err(NW_E_INVALID_ARG, "null pointer");
+  return s->add(K_BATCH, n ? n : 1, fn, arg, [&](Batch& b) {
+    append(b.digests, digest, 32);
+    append(b.pks, pks, 32 * n);
+    append(b.sigs, sigs, 64 * n);
+    b.batch_offsets.push_back(b.batch_offsets.back() + n);
+  });
+}
+
+int nw_service_flush(nw_service* s) {
+  if (!s) return set_err(NW_E_INVALID_ARG, "null service");
+  {
+    std::lock_guard<std::mutex> g(s->m);
+    s->force = true;
+  }
+  s->cv_flush.notify_one();
+  return 0;
+}
+
+int nw_service_drain(nw_service* s) {
+  if (!s) return set_err(NW_E_INVALID_ARG, "null service");
+  std::unique_lock<std::mutex> lk(s->m);
+  const uint64_t target = s->accepted;
+  s->force = true;
+  s->cv_flush.notify_one();
+  s->cv_idle.wait(lk, [&] { return s->completed >= target; });
+  return 0;
+}
+
+int nw_service_stats(nw_service* s, uint64_t* requests, uint64_t* jobs) {
+  if (!s) return set_err(NW_E_INVALID_ARG, "null service");
+  std::lock_guard<std::mutex> g(s->m);
+  if (requests) *requests = s->accepted;
+  if (jobs) *jobs = s->jobs;
+  return 0;
+}
+
+void nw_service_destroy(nw_service* s) {
+  if (!s) return;
+  {
+    std::lock_guard<std::mutex> g(s->m);
+    s->stop = true;
+  }
+  s->cv_flush.notify_all();
+  s->cv_space.notify_all();
+  s->flusher.join();
+  s->completer.join();
+  delete s;
+}
+
+}  // extern "C"

@@ -37,7 +37,8 @@ import numpy as np
 from . import _lib
 from ._lib import EngineError, check
 
-__all__ = ["Job", "GpuBackend", "VerificationService", "CertRow", "cert_row", "vote_row"]
+__all__ = ["Job", "GpuBackend", "VerificationService", "NativeService", "CertRow", "cert_row",
+           "vote_row"]
 
 _P = ctypes.c_void_p
 
@@ -469,3 +470,166 @@ class VerificationService:
         out = await job.done()
         job.release()
         return [int(s) for s in out["status"]]
+
+
+class NativeService:
+    """asyncio front end over the library's native aggregation service (nw_service_*,
+    include/narwhal_amd.h): the same coalescing as VerificationService, but the queueing,
+    batching and job submission run on the library's own threads, so a request costs one
+    copy under a mutex instead of Python-level bookkeeping (this is the layer a Rust
+    crypto-gpu crate binds: one request per Header / Vote / Certificate::verify from the
+    primary's Core task, primary/src/core.rs:306-346; the verdict callback completes the
+    request's future, as SignatureService's oneshot replies do, crypto/src/lib.rs:222-250).
+
+    committee: messages.Committee, a packed committee dict, or None (verify / verify_batch
+    only). Verdicts: (status, index) pairs as the bulk calls return them; a device failure
+    raises EngineError in every affected waiter."""
+
+    def __init__(self, committee=None, max_items: int = 1 << 16, max_delay: float = 0.0005,
+                 max_inflight: int = 4):
+        from .messages import committee_struct
+        L = _lib.lib()
+        n = L.nw_init()
+        if n <= 0:
+            raise EngineError(f"nw_init: {_lib.E_NAMES.get(n, n)}: "
+                              f"{L.nw_last_error().decode(errors='replace')}")
+        self._cc = None
+        if committee is not None:
+            self._packed = committee if isinstance(committee, dict) else committee.packed()
+            self._cc = committee_struct(self._packed)
+        h = _P()
+        check(L.nw_service_create(ctypes.byref(self._cc) if self._cc is not None else None,
+                                  max_items, int(max_delay * 1e6), max_inflight,
+                                  ctypes.byref(h)), "nw_service_create")
+        self._h = h
+        self._lock = threading.Lock()
+        self._pending: dict[int, tuple] = {}
+        self._ids = itertools.count(1)
+        self._cb = _lib.VERDICT_FN(self._verdict)   # one C callback for every request
+
+    # library thread: hand the verdict to the waiter's loop (or call its plain callback)
+    def _verdict(self, key, status, index):
+        with self._lock:
+            target = self._pending.pop(key)
+        if isinstance(target, tuple):
+            loop, fut = target
+            if not loop.is_closed():
+                loop.call_soon_threadsafe(_resolve, fut, int(status), int(index))
+        else:
+            target(int(status), int(index))
+
+    def _register(self, target) -> int:
+        key = next(self._ids)
+        with self._lock:
+            self._pending[key] = target
+        return key
+
+    def _submit(self, call, target) -> None:
+        key = self._register(target)
+        rc = call(key)
+        if rc != 0:
+            with self._lock:
+                self._pending.pop(key, None)
+            check(rc, "nw_service submit")
+
+    def _future(self):
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        return (loop, fut), fut
+
+    # ---- submits (target = (loop, future) or a plain callable(status, index)) ---------
+    def submit_certificate(self, cert, target) -> None:
+        r = cert if isinstance(cert, CertRow) else cert_row(cert)
+        self._submit(lambda key: _lib.lib().nw_service_certificate(
+            self._h, r.header_bytes, len(r.header_bytes), r.payload_count, r.id, r.signature,
+            r.vote_pks or None, r.vote_sigs or None, r.nvotes, self._cb, key), target)
+
+    def submit_header(self, header, target) -> None:
+        r = header if isinstance(header, CertRow) else cert_row(header)
+        self._submit(lambda key: _lib.lib().nw_service_header(
+            self._h, r.header_bytes, len(r.header_bytes), r.payload_count, r.id, r.signature,
+            self._cb, key), target)
+
+    def submit_vote(self, vote, target) -> None:
+        r = vote if isinstance(vote, tuple) else vote_row(vote)
+        self._submit(lambda key: _lib.lib().nw_service_vote(
+            self._h, r[0], r[1], r[2], r[3], r[4], self._cb, key), target)
+
+    def submit_verify(self, digest: bytes, pk: bytes, sig: bytes, target) -> None:
+        self._submit(lambda key: _lib.lib().nw_service_verify(
+            self._h, bytes(digest), bytes(pk), bytes(sig), self._cb, key), target)
+
+    def submit_verify_batch(self, digest: bytes, votes, target) -> None:
+        pks = b"".join(bytes(p) for p, _ in votes)
+        sgs = b"".join(bytes(s) for _, s in votes)
+        self._submit(lambda key: _lib.lib().nw_service_verify_batch(
+            self._h, bytes(digest), pks or None, sgs or None, len(votes), self._cb, key), target)
+
+    # ---- awaitables --------------------------------------------------------------------
+    async def certificate_status(self, cert) -> tuple[int, int]:
+        t, fut = self._future()
+        self.submit_certificate(cert, t)
+        return await fut
+
+    async def header_status(self, header) -> tuple[int, int]:
+        t, fut = self._future()
+        self.submit_header(header, t)
+        return await fut
+
+    async def vote_status(self, vote) -> int:
+        t, fut = self._future()
+        self.submit_vote(vote, t)
+        return (await fut)[0]
+
+    async def verify(self, digest: bytes, pk: bytes, sig: bytes) -> int:
+        t, fut = self._future()
+        self.submit_verify(digest, pk, sig, t)
+        return (await fut)[0]
+
+    async def verify_batch(self, digest: bytes, votes) -> int:
+        if not votes:   # crypto/src/lib.rs:206-219: no votes -> Ok
+            return 0
+        t, fut = self._future()
+        self.submit_verify_batch(digest, votes, t)
+        return (await fut)[0]
+
+    async def verify_certificate(self, cert) -> None:
+        """Core::sanitize_certificate's check (messages.rs:189-215): None or DagError."""
+        from .messages import raise_for_status
+        st, ix = await self.certificate_status(cert)
+        raise_for_status(st, ix, cert.header, None, cert.votes)
+
+    # ---- control -----------------------------------------------------------------------
+    def flush(self) -> None:
+        check(_lib.lib().nw_service_flush(self._h), "nw_service_flush")
+
+    def drain(self) -> None:
+        """Block until every accepted request's verdict has been delivered (call it from a
+        thread, or after the loop's waiters have been gathered)."""
+        check(_lib.lib().nw_service_drain(self._h), "nw_service_drain")
+
+    def stats(self) -> tuple[int, int]:
+        req, jobs = ctypes.c_uint64(), ctypes.c_uint64()
+        check(_lib.lib().nw_service_stats(self._h, ctypes.byref(req), ctypes.byref(jobs)),
+              "nw_service_stats")
+        return req.value, jobs.value
+
+    def close(self) -> None:
+        if self._h.value is not None:
+            _lib.lib().nw_service_destroy(self._h)   # drains: every callback has run
+            self._h = _P(None)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _resolve(fut: asyncio.Future, status: int, index: int) -> None:
+    if fut.done():
+        return
+    if status < 0:
+        fut.set_exception(EngineError(f"device job failed: {_lib.E_NAMES.get(status, status)}"))
+    else:
+        fut.set_result((status, index))

@@ -404,3 +404,98 @@ def test_service_messages_on_gpu_vs_oracle():
     assert got[:len(rows)] == [(int(a), int(b)) for a, b in zip(st4, ix4)]
     assert got[len(rows):] == [int(x) for x in vexp]
     assert jobs <= 4
+
+
+# ------------------------------------------------------------------ native aggregation service
+@pytest.mark.skipif(torch.cuda.is_available(), reason="CPU-only behaviour")
+def test_native_service_fails_loudly_without_device():
+    with pytest.raises(_lib.EngineError):
+        S.NativeService()
+    import ctypes
+    h = ctypes.c_void_p()
+    assert _lib.lib().nw_service_create(None, 16, 100, 2, ctypes.byref(h)) == -2
+    assert h.value is None
+
+
+@pytest.mark.gpu
+def test_native_service_certificates_from_threads_vs_oracle():
+    """nw_service_certificate from four threads at once, single certificates of two
+    committees (one service each), 1 in 100 with an invalid vote plus the early-failure
+    cases of cert_cases: every verdict callback's (status, index) equals the oracle's,
+    every request gets exactly one callback, and the requests were coalesced."""
+    import threading
+    from cert_cases import mutated_stream, oracle_digest_many
+    from narwhal_amd import workloads as W
+    com4, s4, st4, ix4, _ = mutated_stream(N=4, copies=3, seed=81)
+    hon = W.certificate_stream(2000, O.keys(10), lambda sk, m: C.sign_many(sk, m),
+                               oracle_digest_many, seed=82)
+    m, mst, mix = W.mutate_votes(hon, np.arange(7, 2000, 100), seed=5)
+    cases = [(com4, s4, st4, ix4), (m["committee"], m, mst, mix)]
+    for com, s, est, eix in cases:
+        svc = S.NativeService(com, max_items=1 << 12, max_delay=0.0005, max_inflight=3)
+        rows = _rows(s)
+        got = [None] * len(rows)
+        calls = [0] * len(rows)
+
+        def worker(t):
+            for i in range(t, len(rows), 4):
+                def cb(st, ix, i=i):
+                    got[i] = (st, ix)
+                    calls[i] += 1
+                svc.submit_certificate(rows[i], cb)
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        svc.drain()
+        req, jobs = svc.stats()
+        svc.close()
+        assert calls == [1] * len(rows)
+        assert got == [(int(a), int(b)) for a, b in zip(est, eix)]
+        assert req == len(rows) and jobs < len(rows) / 4
+
+
+@pytest.mark.gpu
+def test_native_service_all_kinds_asyncio_vs_oracle():
+    """Header, Vote, Certificate, Signature::verify and Signature::verify_batch requests
+    through the asyncio NativeService, interleaved: each kind's verdicts equal the oracle's."""
+    from cert_cases import mutated_stream, votes_case
+    com4, s4, st4, ix4, _ = mutated_stream(N=4, copies=2, seed=91)
+    hst, hix = O.certificates_verify_many(com4, s4, headers_only=True)
+    vcom, vp, vn, vexp = votes_case(N=4, seed=92, count=40, keys=None)
+    digs, pks, sigs = _strict_corpus(300, 93)
+    sexp = O.verify_strict_many(digs, pks, sigs)
+    ks = O.keys(4)
+    dig = O.digest32(b"native batch")
+    good = [(ks[i % 4][0], O.sign(ks[i % 4][1], dig)) for i in range(7)]
+    bad = list(good)
+    bad[4] = (bad[4][0], bytes(64))                 # Signature::default() in the batch
+    rows = _rows(s4)
+    votes = [(vp["ids"][i].tobytes(), int(vp["rounds"][i]), vp["origins"][i].tobytes(),
+              vp["authors"][i].tobytes(), vp["sigs"][i].tobytes()) for i in range(vn)]
+
+    async def main():
+        svc = S.NativeService(com4, max_delay=0.001)
+        vsvc = S.NativeService(vcom, max_delay=0.001)
+        got = await asyncio.gather(*[svc.certificate_status(r) for r in rows],
+                                   *[svc.header_status(r) for r in rows],
+                                   *[vsvc.vote_status(v) for v in votes],
+                                   *[svc.verify(digs[i].tobytes(), pks[i].tobytes(),
+                                                sigs[i].tobytes()) for i in range(300)],
+                                   svc.verify_batch(dig, good), svc.verify_batch(dig, bad),
+                                   svc.verify_batch(dig, []))
+        svc.close()
+        vsvc.close()
+        return got
+
+    got = asyncio.run(main())
+    n = len(rows)
+    assert got[:n] == [(int(a), int(b)) for a, b in zip(st4, ix4)]
+    assert got[n:2 * n] == [(int(a), int(b)) for a, b in zip(hst, hix)]
+    assert got[2 * n:2 * n + vn] == [int(x) for x in vexp]
+    assert got[2 * n + vn:2 * n + vn + 300] == [int(x) for x in sexp]
+    bpk = np.array([np.frombuffer(p, np.uint8) for p, _ in bad])
+    bsg = np.array([np.frombuffer(q, np.uint8) for _, q in bad])
+    assert got[-3:] == [0, int(O.verify_batch(dig, bpk, bsg)[0]), 0]
+    assert got[-2] != 0

@@ -1,0 +1,148 @@
+// nw_loadgen.cpp — open-loop load generator for the native aggregation service (bench
+// tooling; bench.py's service_latency leg loads it with ctypes). Built against the public C
+// ABI only (include/narwhal_amd.h), as a Rust crypto-gpu crate's tokio tasks would call it.
+//
+// Certificates arrive at a fixed offered rate: request i is due at t0 + i / rate and goes
+// to nw_service_certificate from one of `producers` threads (the primary's Core task is
+// one producer; several model several primaries or Core plus the synchronizer). Latency of
+// request i = verdict-callback time - scheduled arrival time, so a producer that falls
+// behind its schedule shows up as latency, not as a lower offered rate. Every verdict is
+// compared with the expected (status, index) of the corpus row it came from.
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <thread>
+#include <vector>
+
+#include "narwhal_amd.h"
+
+namespace {
+using Clock = std::chrono::steady_clock;
+
+struct Run {
+  const int32_t* exp_status;
+  const uint64_t* exp_index;
+  size_t nuniq;
+  double* lat;
+  std::atomic<uint64_t> mismatches{0};
+  std::atomic<int64_t> last_ns{0};
+  Clock::time_point t0;
+};
+
+struct Rec {
+  Run* run;
+  uint64_t i;
+  Clock::time_point due;
+};
+
+void on_verdict(void* arg, int32_t status, uint64_t index) {
+  Rec* r = static_cast<Rec*>(arg);
+  const Clock::time_point now = Clock::now();
+  Run* run = r->run;
+  run->lat[r->i] = std::chrono::duration<double>(now - r->due).count();
+  const size_t u = r->i % run->nuniq;
+  if (status != run->exp_status[u] || index != run->exp_index[u]) run->mismatches.fetch_add(1);
+  const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(now - run->t0).count();
+  int64_t prev = run->last_ns.load();
+  while (ns > prev && !run->last_ns.compare_exchange_weak(prev, ns)) {
+  }
+}
+}  // namespace
+
+extern "C" {
+
+// Returns 0 or the first negative NW_E_* from the service. lat_out: total seconds;
+// out3: elapsed seconds (t0 .. last verdict), jobs, mismatches (as doubles).
+int nw_loadgen_certificates(const nw_committee* com, const nw_certificates* corpus,
+                            const int32_t* exp_status, const uint64_t* exp_index, double rate,
+                            uint64_t total, size_t max_items, uint32_t max_delay_us,
+                            size_t max_inflight, uint32_t producers, double* lat_out,
+                            double* out3) {
+  if (!com || !corpus || !corpus->n || !exp_status || !exp_index || !lat_out || !out3 ||
+      rate <= 0 || !producers)
+    return NW_E_INVALID_ARG;
+  nw_service* s = nullptr;
+  int rc = nw_service_create(com, max_items, max_delay_us, max_inflight, &s);
+  if (rc) return rc;
+  Run run;
+  run.exp_status = exp_status;
+  run.exp_index = exp_index;
+  run.nuniq = corpus->n;
+  run.lat = lat_out;
+  std::vector<Rec> recs(total);
+  std::atomic<int> first_err{0};
+  auto submit = [&](uint64_t i) {
+    const size_t u = i % corpus->n;
+    const uint64_t h0 = corpus->header_offsets[u], h1 = corpus->header_offsets[u + 1];
+    const uint64_t v0 = corpus->vote_offsets[u], v1 = corpus->vote_offsets[u + 1];
+    const int e = nw_service_certificate(s, corpus->header_bytes + h0, h1 - h0,
+                                         corpus->payload_counts[u], corpus->ids + 32 * u,
+                                         corpus->header_sigs + 64 * u, corpus->vote_pks + 32 * v0,
+                                         corpus->vote_sigs + 64 * v0, v1 - v0, on_verdict,
+                                         &recs[i]);
+    if (e) {
+      int z = 0;
+      first_err.compare_exchange_strong(z, e);
+    }
+  };
+  // warm-up (untimed): the committee's key tables and the job pool
+  {
+    Run warm;
+    std::vector<double> wl(64);
+    warm.exp_status = exp_status;
+    warm.exp_index = exp_index;
+    warm.nuniq = corpus->n;
+    warm.lat = wl.data();
+    warm.t0 = Clock::now();
+    std::vector<Rec> wr(64);
+    for (uint64_t i = 0; i < 64 && i < total; ++i) {
+      wr[i] = {&warm, i, Clock::now()};
+      const size_t u = i % corpus->n;
+      const uint64_t h0 = corpus->header_offsets[u], h1 = corpus->header_offsets[u + 1];
+      const uint64_t v0 = corpus->vote_offsets[u], v1 = corpus->vote_offsets[u + 1];
+      rc = nw_service_certificate(s, corpus->header_bytes + h0, h1 - h0, corpus->payload_counts[u],
+                                  corpus->ids + 32 * u, corpus->header_sigs + 64 * u,
+                                  corpus->vote_pks + 32 * v0, corpus->vote_sigs + 64 * v0,
+                                  v1 - v0, on_verdict, &wr[i]);
+      if (rc) break;
+    }
+    nw_service_drain(s);
+    if (rc) {
+      nw_service_destroy(s);
+      return rc;
+    }
+  }
+  uint64_t jobs0 = 0;
+  nw_service_stats(s, nullptr, &jobs0);
+  run.t0 = Clock::now() + std::chrono::milliseconds(2);
+  const double period = 1.0 / rate;
+  for (uint64_t i = 0; i < total; ++i)
+    recs[i] = {&run, i,
+               run.t0 + std::chrono::duration_cast<Clock::duration>(
+                            std::chrono::duration<double>(period * (double)i))};
+  std::vector<std::thread> th;
+  for (uint32_t p = 0; p < producers; ++p)
+    th.emplace_back([&, p] {
+      for (uint64_t i = p; i < total; i += producers) {
+        const Clock::time_point due = recs[i].due;
+        Clock::time_point now = Clock::now();
+        if (due - now > std::chrono::microseconds(100)) std::this_thread::sleep_until(due);
+        while (Clock::now() < due) {
+        }
+        submit(i);
+      }
+    });
+  for (auto& t : th) t.join();
+  nw_service_drain(s);
+  uint64_t jobs1 = 0;
+  nw_service_stats(s, nullptr, &jobs1);
+  nw_service_destroy(s);
+  out3[0] = (double)run.last_ns.load() * 1e-9;
+  out3[1] = (double)(jobs1 - jobs0);
+  out3[2] = (double)run.mismatches.load();
+  return first_err.load();
+}
+
+}  // extern "C"

@@ -3,9 +3,9 @@
 # committee size and grouping mode, each rocprofv3 run under its own time limit, stopping at
 # the first failure (no retries).
 #   bash tools/pmc_cert.sh OUTDIR N [N ...]
-# Modes: "big" = all-valid stream with the default policy (Pippenger groups: k_grp_keys,
-# k_pip_*), "keyed" = the same stream with NW_CERT_KEYED=1 (k_votes_keyed + verify_batch of
-# failed certificates only). One bench step (plus its warmup call) at the full 1M-certificate
+# Modes (MODES="big keyed" by default): "keyed" = all-valid stream with the default policy
+# (k_votes_keyed + verify_batch of failed certificates only), "big" = the same stream with
+# NW_CERT_KEYED=0 (merged Pippenger groups: k_grp_keys, k_pip_*). One bench step (plus its warmup call) at the full 1M-certificate
 # size, so per-dispatch counters are per bench launch.
 # Summarise with: python tools/pmc_cert_summary.py OUTDIR profiles/TAG
 set -o pipefail
@@ -17,8 +17,8 @@ ARGS="--workload cert --no-sha --no-batch --no-wire --no-cpu-baseline --cert-ste
 
 run() {  # run NAME N MODE [rocprofv3 args...]
   local name=$1 n=$2 mode=$3; shift 3
-  local envk=""
-  [ "$mode" = keyed ] && envk=1
+  local envk=1
+  [ "$mode" = big ] && envk=0
   NW_CERT_KEYED=$envk timeout -s KILL 240 rocprofv3 "$@" --output-format csv \
     -d "$OUT/${mode}_n${n}_$name" -o p -- python3 bench.py $ARGS --committees "$n" \
     > "$OUT/${mode}_n${n}_$name.json" 2> "$OUT/${mode}_n${n}_$name.log"
@@ -28,7 +28,7 @@ run() {  # run NAME N MODE [rocprofv3 args...]
 }
 
 for N in "$@"; do
-  for MODE in big keyed; do
+  for MODE in ${MODES:-big keyed}; do
     run trace "$N" "$MODE" --kernel-trace --stats && \
     run fetch "$N" "$MODE" --pmc FETCH_SIZE && \
     run write "$N" "$MODE" --pmc WRITE_SIZE && \
