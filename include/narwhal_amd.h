@@ -201,8 +201,9 @@ void nw_job_release(nw_job* job);
  * crypto::SignatureService (crypto/src/lib.rs:222-250). Each request is copied at submit
  * into the open batch of its kind; a service thread submits a batch as ONE job (the
  * nw_submit_* calls above, so the committee's key tables stay on the device across jobs)
- * once it holds max_items units (certificate = 1 + votes, batch = its votes, else 1) or
- * max_delay_us after its first request; at most max_inflight jobs are queued at once (the
+ * once it holds max_items units (certificate = 1 + votes, batch = its votes, else 1),
+ * max_delay_us after its first request, or at once while no job is in flight (an idle
+ * device gains nothing from waiting); at most max_inflight jobs are queued at once (the
  * next batch keeps filling meanwhile). A second service thread waits for the jobs in
  * order and calls fn(arg, status, index) once per accepted request: status / index as the
  * corresponding bulk call returns them (NW_DAG_* for messages, NW_ERR_* for verify /

@@ -432,7 +432,8 @@ size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
   const size_t m = n ? n : 1;
   // the verify_batch workspace doubles as the keyed vote checks' scratch (they run first)
   const size_t bws = nvotes ? a256(std::max(nw::batch_workspace_bytes(n, nvotes),
-                                            64 * nw::votes_keyed_bytes_per_vote()))
+                                            nw::votes_keyed_fixed_bytes() +
+                                                64 * nw::votes_keyed_bytes_per_vote()))
                             : 256;
   const size_t sizes[16] = {a256(32 * m), a256(32 * m), a256(32 * m), a256(4 * m), a256(4 * m),
                             a256(4 * m),  a256(4 * m),  a256(8 * m),  a256(8 * m), a256(8 * m),
@@ -638,7 +639,8 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
       NW_HIP(nw::launch_votes_keyed(w.cert_digest, cs.vote_offsets, n, w.vote_cert,
                                     reinterpret_cast<const uint32_t*>(cs.vote_pks),
                                     reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
-                                    w.pre1, w.pre2, w.hdr_st, kt, group_ok, w.batch_ws,
+                                    w.pre1, w.pre2, w.hdr_st, kt, (uint32_t)com.nauth,
+                                    group_ok, w.batch_ws,
                                     w.batch_ws_bytes, s),
              "keyed vote checks");
     } else if (K && !small)

@@ -1358,14 +1358,21 @@ size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems) {
   return bv_layout(std::min<uint64_t>(nitems + nbatches, slice_units()), nullptr, nullptr);
 }
 
-// Caller key tables (a committee's keys, decompressed once per call): per key
-// j*A and j*2^128 A for j = 0..128 in cached form (258 entries, 41 KB), used by keyed
-// chunks' 8-bit windows and short ladders.
-//   k_key_base  one lane per key: decompress (dalek semantics), the comb bases 2^(8t) A
-//               (t = 0..31) by 248 doublings; base[2 key] = A, base[2 key + 1] = 2^128 A
-//               for the group path, comb[32 key + t] for k_key_tabs.
-//   k_key_tabs  one lane per (key, table t, j): j * 2^(8t) A by double-and-add over j's bits.
-// One block: flag = force or (pks != saved); then saved = pks when they differ.
+// Committee key tables (a committee's keys, tabulated once while the committee is
+// unchanged): per key the comb tables j * 2^(W t) A (W = kKeyW, t < kKeyCombT,
+// j = 0..2^(W-1), affine niels; nw_kernels.h). Keyed strict checks (headers, votes) take
+// [k]A from them with no doublings; keyed vote chunks use the j * A and j * 2^128 A tables.
+//   k_key_cmp   one block: flag = force or (pks != saved); then saved = pks when they differ.
+//   k_key_base  one lane per key: decompress (dalek semantics), the comb bases 2^(W t) A by
+//               W doublings each; base[2 key] = A, base[2 key + 1] = 2^128 A for the group
+//               path, comb[kKeyCombT key + t] for k_key_tabs.
+//   k_key_tabs  one lane per run of kKeyRun consecutive entries of one (key, t): j0 * P by
+//               double-and-add, then j * P for the run by additions of P, each point parked
+//               in its own output slot (X, Y, Z and the product of the run's earlier Z's,
+//               packed 32 bytes each), ONE inversion per run (Montgomery's trick) and a
+//               backward pass that rewrites every slot as its affine niels form: about 15
+//               multiplications per entry instead of an inversion per entry (16-bit tables:
+//               524,304 entries per key).
 __global__ __launch_bounds__(256) void k_key_cmp(const uint32_t* __restrict__ pks,
                                                  uint32_t* __restrict__ saved, uint64_t nkeys,
                                                  uint32_t force, uint32_t* __restrict__ flag) {
@@ -1396,41 +1403,85 @@ __global__ __launch_bounds__(256) void k_key_base(const uint32_t* __restrict__ p
   for (int t = 0; t < (int)kKeyCombT; ++t) {
     if (t) {
 #pragma unroll 1
-      for (int d = 0; d < 8; ++d) ge_dbl(P, P, d == 7);
+      for (int d = 0; d < (int)kKeyW; ++d) ge_dbl(P, P, d == (int)kKeyW - 1);
     }
     comb[kKeyCombT * i + t] = P;
-    if (t == 16) base[2 * i + 1] = P;
+    if (t * kKeyW == 128) base[2 * i + 1] = P;
   }
+}
+
+constexpr uint32_t kKeyRun = 64;
+constexpr uint32_t kKeyRuns = (kKeyN + kKeyRun - 1) / kKeyRun;   // runs per table
+
+NW_HD void put_fe32(uint32_t* w, const fe& f) {
+  uint32_t b[8];
+  fe_tobytes(b, f);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = b[i];
 }
 
 __global__ __launch_bounds__(256) void k_key_tabs(uint64_t nkeys, const ge* __restrict__ comb,
                                                   ge_niels_pad* __restrict__ tabs,
                                                   const uint32_t* __restrict__ flag) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= nkeys * kKeyTab || (flag && *flag == 0)) return;
-  const uint64_t pt = g / 129;           // kKeyCombT * key + t
-  const int j = (int)(g % 129);
+  if (g >= nkeys * kKeyCombT * kKeyRuns || (flag && *flag == 0)) return;
+  const uint64_t pt = g / kKeyRuns;   // kKeyCombT * key + t
+  const uint32_t j0 = (uint32_t)(g % kKeyRuns) * kKeyRun;
+  const uint32_t cnt = kKeyN - j0 < kKeyRun ? kKeyN - j0 : kKeyRun;
   const ge P = comb[pt];
+  ge_cached Pc;
+  ge_to_cached(Pc, P, g_bc.k.d2);
   ge acc;
   ge_identity(acc);
+  if (j0) {
 #pragma unroll 1
-  for (int bit = 7; bit >= 0; --bit) {
-    ge_dbl(acc, acc, true);
-    if ((j >> bit) & 1) {
-      ge_cached c;
-      ge_to_cached(c, P, g_bc.k.d2);
-      ge_add_cached(acc, acc, c, true);
+    for (int bit = 31 - __builtin_clz(j0); bit >= 0; --bit) {
+      ge_dbl(acc, acc, true);
+      if ((j0 >> bit) & 1) ge_add_cached(acc, acc, Pc, true);
     }
   }
-  ge_niels out;
-  ge_to_niels(out, acc, g_bc.k.d2);   // one inversion per entry: affine, mixed additions
-  tabs[g].n = out;
-  tabs[g].pad[0] = tabs[g].pad[1] = 0;
+  uint32_t* slot = reinterpret_cast<uint32_t*>(tabs + pt * kKeyN + j0);
+  static_assert(sizeof(ge_niels_pad) == 128, "slot = 32 words");
+  fe prefix;   // product of the Z's of the run's earlier entries
+  fe_1(prefix);
+#pragma unroll 1
+  for (uint32_t e = 0; e < cnt; ++e) {
+    uint32_t* w = slot + 32 * e;
+    put_fe32(w, acc.X);
+    put_fe32(w + 8, acc.Y);
+    put_fe32(w + 16, acc.Z);
+    put_fe32(w + 24, prefix);
+    fe_mul(prefix, prefix, acc.Z);
+    if (e + 1 < cnt) ge_add_cached(acc, acc, Pc, true);
+  }
+  fe inv;   // 1 / (Z_0 ... Z_e) while walking back
+  fe_invert(inv, prefix);
+#pragma unroll 1
+  for (int e = (int)cnt - 1; e >= 0; --e) {
+    uint32_t* w = slot + 32 * e;
+    fe X, Y, Z, pre, zi, x, y;
+    fe_frombytes(X, w);
+    fe_frombytes(Y, w + 8);
+    fe_frombytes(Z, w + 16);
+    fe_frombytes(pre, w + 24);
+    fe_mul(zi, inv, pre);   // 1 / Z_e
+    fe_mul(inv, inv, Z);
+    fe_mul(x, X, zi);
+    fe_mul(y, Y, zi);
+    ge_niels_pad out;
+    fe_add(out.n.ypx, y, x);
+    fe_carry(out.n.ypx);
+    fe_sub(out.n.ymx, y, x);
+    fe_mul(out.n.xy2d, x, y);
+    fe_mul(out.n.xy2d, out.n.xy2d, g_bc.k.d2);
+    out.pad[0] = out.pad[1] = 0;
+    tabs[pt * kKeyN + j0 + (uint32_t)e] = out;
+  }
 }
 
 size_t key_tables_bytes(uint64_t nkeys) {
   const uint64_t n = nkeys ? nkeys : 1;
-  return sizeof(ge_niels_pad) * kKeyTab * n + sizeof(ge) * (2 + kKeyCombT) * n;
+  return sizeof(ge_niels_pad) * (uint64_t)kKeyTab * n + sizeof(ge) * (2 + kKeyCombT) * n;
 }
 
 hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, ge_niels_pad* tabs, uint32_t* ok,
@@ -1444,7 +1495,8 @@ hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, ge_niels_pad* 
                        force ? 1u : 0u, flag);
   hipLaunchKernelGGL(k_key_base, dim3((unsigned)((nkeys + 63) / 64)), dim3(64), 0, stream, pks,
                      nkeys, base, comb, ok, fl);
-  hipLaunchKernelGGL(k_key_tabs, dim3((unsigned)((nkeys * kKeyTab + 255) / 256)), dim3(256), 0,
+  hipLaunchKernelGGL(k_key_tabs, dim3((unsigned)((nkeys * kKeyCombT * kKeyRuns + 255) / 256)),
+                     dim3(256), 0,
                      stream, nkeys, comb, tabs, fl);
   return hipGetLastError();
 }

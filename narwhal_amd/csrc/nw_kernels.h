@@ -44,22 +44,28 @@ hipError_t launch_sign(const uint32_t* sks, uint32_t sk_stride_words, const uint
 // the workspace slices).
 hipError_t upload_batch_consts();
 
-// Pre-decompressed public keys (a committee): per key the comb tables j * 2^(8t) A
-// (t = 0..31, j = 0..128, cached form; t = 0 and t = 16 are j*A and j*2^128 A) and whether
-// it decompressed. vote_key[i] = key index of vote i, or kNoKey to decompress that vote's
-// key in the kernel (the verdict semantics are unchanged: a key's decompression is
-// deterministic). Keyed strict verifications take [k]A from the 32 tables with no
-// doublings; chunks whose votes are all keyed run 8-bit A windows over tables t = 0, 16 and
-// a 128-doubling ladder.
+// Pre-decompressed public keys (a committee): per key the comb tables j * 2^(W t) A
+// (W = NW_KEYW = 16: t = 0..15, j = 0..32,768, 67 MB per key; W = 8: t = 0..31,
+// j = 0..128; affine niels) and whether it decompressed. vote_key[i] = key index of vote i,
+// or kNoKey to decompress that vote's key in the kernel (the verdict semantics are
+// unchanged: a key's decompression is deterministic). Keyed strict verifications take [k]A
+// from the 256 / W tables with no doublings; chunks whose votes are all keyed run 8-bit A
+// windows over the tables of j * A and j * 2^128 A (entries 0..128) and a 128-doubling
+// ladder.
 struct key_tables_t {
   const struct ge_niels_pad* tabs;   // nkeys x kKeyTab, affine niels (mixed additions)
   const uint32_t* ok;             // nkeys
   const uint32_t* vote_key;       // nitems (global item index)
 };
+#ifndef NW_KEYW
+#define NW_KEYW 16
+#endif
 constexpr uint32_t kNoKey = 0xffffffffu;
-constexpr uint32_t kKeyCombT = 32;                // comb tables per key (8-bit windows)
-constexpr uint32_t kKeyTab = kKeyCombT * 129;      // entries per key: j * 2^(8t) A
-constexpr uint32_t kKeyHalf = 16 * 129;            // offset of the j * 2^128 A table
+constexpr uint32_t kKeyW = NW_KEYW;                       // bits per comb digit of k
+constexpr uint32_t kKeyCombT = 256 / kKeyW;               // comb tables per key
+constexpr uint32_t kKeyN = (1u << (kKeyW - 1)) + 1;       // entries per table, j = 0..2^(W-1)
+constexpr uint32_t kKeyTab = kKeyCombT * kKeyN;           // entries per key
+constexpr uint32_t kKeyHalf = (128 / kKeyW) * kKeyN;      // offset of the j * 2^128 A table
 // ok[key]: bit 0 = decompressed, bit 1 = small order (8A == identity)
 size_t key_tables_bytes(uint64_t nkeys);
 // tabs: key_tables_bytes(nkeys) of device memory; ok: nkeys words. saved (nkeys x 8 words)
@@ -130,15 +136,17 @@ hipError_t launch_cert_sgroups(const uint32_t* cert_digest, const uint64_t* cvo,
 // x parities in batched inversions); cert_ok[c] = 1 when all of them pass (then
 // verify_batch is Ok too), 0 otherwise. Follow with launch_verify_batch(skip_group_ok =
 // cert_ok, skip_per_group = 1). vote_cert: certificate of each vote (k_cert_prepare);
-// cert_ok: ncert words; scratch: >= 64 x votes_keyed_bytes_per_vote() bytes (slices of the
-// votes go through it). keys.vote_key required.
+// cert_ok: ncert words; scratch: >= votes_keyed_fixed_bytes() + 64 x
+// votes_keyed_bytes_per_vote() bytes (slices of the votes go through it, each checked in
+// key-major order). keys.vote_key required; nkeys = committee size.
 size_t votes_keyed_bytes_per_vote();
+size_t votes_keyed_fixed_bytes();
 hipError_t launch_votes_keyed(const uint32_t* cert_digest, const uint64_t* cvo, uint64_t ncert,
                               const uint32_t* vote_cert, const uint32_t* pks,
                               const uint32_t* sigs, uint64_t nvotes, const int32_t* pre1,
                               const int32_t* pre2, const int32_t* hdr_st,
-                              const key_tables_t& keys, uint32_t* cert_ok, void* scratch,
-                              size_t scratch_bytes, hipStream_t stream);
+                              const key_tables_t& keys, uint32_t nkeys, uint32_t* cert_ok,
+                              void* scratch, size_t scratch_bytes, hipStream_t stream);
 
 // ---- primary messages (nw_cert.hip) ----------------------------------------------------
 struct cert_committee_t {

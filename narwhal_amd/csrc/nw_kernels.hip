@@ -18,6 +18,8 @@
 #include "nw_ladder.hpp"
 #include "nw_consts.hpp"
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <atomic>
 #include <mutex>
@@ -279,8 +281,8 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
     const uint32_t kk = keys.vote_key ? keys.vote_key[i] : kNoKey;
     const ge_niels_pad* keytab = kk != kNoKey ? keys.tabs + kKeyTab * (uint64_t)kk : nullptr;
     // committee keys: [s]B - [k]A from comb tables, no ladder; others: the half-size ladder
-    const int st = keytab ? strict_keyed_comb(src, g_consts.sk, bcomb_wide{bcomb}, keytab,
-                                              keys.ok[kk])
+    const int st = keytab ? strict_keyed_comb(src, g_consts.sk, bcomb_wide{bcomb},
+                                              keytab_wide{keytab}, keys.ok[kk])
                           : strict_verify_core<NW_BWIN>(src, g_consts.sk, bt, tabA, tabR,
                                                         WaveMax{});
     if (active) status[gi] = st;
@@ -317,7 +319,75 @@ struct vote_planes_t {
   uint32_t* planes;
   uint32_t* state;
   uint64_t S;
+  const uint32_t* perm;   // slice position -> slice vote (key-major order), or nullptr
 };
+
+// Key-major order of a slice's votes (k_vk_hist / k_vk_scan / k_vk_scatter: a counting sort
+// by committee key; the votes of already-decided certificates and non-members go to one
+// last bin whose lanes do no comb work). With 16-bit key tables (67 MB per key) a wave whose
+// lanes name ~64 different keys gathers from the whole committee's tables (6.7 GB at
+// N = 100: HBM and TLB bound); sorted, the chip works on one or two keys' tables at a time,
+// which stay in the last-level caches.
+constexpr uint32_t kVkMaxBins = 1024;
+constexpr uint32_t kVkSortMinKeys = 64;
+__device__ __forceinline__ uint32_t vk_bin(const uint32_t* __restrict__ vote_cert,
+                                           const uint32_t* __restrict__ vote_key, uint64_t v,
+                                           const int32_t* __restrict__ pre1,
+                                           const int32_t* __restrict__ pre2,
+                                           const int32_t* __restrict__ hdr_st, uint32_t nkeys) {
+  const uint32_t c = vote_cert[v];
+  if (pre1[c] != 0 || hdr_st[c] != 0 || pre2[c] != 0) return nkeys;
+  const uint32_t k = vote_key[v];
+  return k < nkeys ? k : nkeys;
+}
+__global__ __launch_bounds__(256) void k_vk_hist(const uint32_t* __restrict__ vote_cert,
+                                                 const uint32_t* __restrict__ vote_key,
+                                                 uint64_t v0, uint64_t nv,
+                                                 const int32_t* __restrict__ pre1,
+                                                 const int32_t* __restrict__ pre2,
+                                                 const int32_t* __restrict__ hdr_st,
+                                                 uint32_t nkeys, uint32_t* __restrict__ gh) {
+  __shared__ uint32_t h[kVkMaxBins];
+  for (uint32_t b = threadIdx.x; b <= nkeys; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nv) atomicAdd(&h[vk_bin(vote_cert, vote_key, v0 + i, pre1, pre2, hdr_st, nkeys)], 1u);
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b <= nkeys; b += blockDim.x)
+    if (h[b]) atomicAdd(&gh[b], h[b]);
+}
+__global__ __launch_bounds__(64) void k_vk_scan(uint32_t* __restrict__ gh, uint32_t nbins) {
+  if (threadIdx.x != 0) return;
+  uint32_t acc = 0;
+  for (uint32_t b = 0; b < nbins; ++b) {
+    const uint32_t c = gh[b];
+    gh[b] = acc;
+    acc += c;
+  }
+}
+__global__ __launch_bounds__(256) void k_vk_scatter(const uint32_t* __restrict__ vote_cert,
+                                                    const uint32_t* __restrict__ vote_key,
+                                                    uint64_t v0, uint64_t nv,
+                                                    const int32_t* __restrict__ pre1,
+                                                    const int32_t* __restrict__ pre2,
+                                                    const int32_t* __restrict__ hdr_st,
+                                                    uint32_t nkeys, uint32_t* __restrict__ cursor,
+                                                    uint32_t* __restrict__ perm) {
+  __shared__ uint32_t h[kVkMaxBins];
+  for (uint32_t b = threadIdx.x; b <= nkeys; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t b = 0, r = 0;
+  if (i < nv) {
+    b = vk_bin(vote_cert, vote_key, v0 + i, pre1, pre2, hdr_st, nkeys);
+    r = atomicAdd(&h[b], 1u);
+  }
+  __syncthreads();
+  for (uint32_t x = threadIdx.x; x <= nkeys; x += blockDim.x)
+    if (h[x]) h[x] = atomicAdd(&cursor[x], h[x]);   // this block's range in bin x
+  __syncthreads();
+  if (i < nv) perm[h[b] + r] = (uint32_t)i;
+}
 
 #ifndef NW_KEYED_WAVES
 #define NW_KEYED_WAVES 1
@@ -330,7 +400,7 @@ __global__ __launch_bounds__(256, NW_KEYED_WAVES) void k_votes_keyed(
     const ge_niels_pad* __restrict__ bcomb, uint32_t* __restrict__ cert_ok, vote_planes_t vp) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nv) return;
-  const uint64_t v = v0 + i;
+  const uint64_t v = v0 + (vp.perm ? vp.perm[i] : i);
   const uint32_t c = vote_cert[v];
   uint32_t st = kVotePass;
   if (pre1[c] == 0 && hdr_st[c] == 0 && pre2[c] == 0) {
@@ -341,7 +411,7 @@ __global__ __launch_bounds__(256, NW_KEYED_WAVES) void k_votes_keyed(
       const strict_src_global src{pks + 8 * v, sigs + 16 * v, cert_digest + 8 * (uint64_t)c};
       fe X, Z;
       st = keyed_vote_check(src, g_consts.sk, bcomb_wide{bcomb},
-                            keys.tabs + kKeyTab * (uint64_t)kk, keys.ok[kk], X, Z);
+                            keytab_wide{keys.tabs + kKeyTab * (uint64_t)kk}, keys.ok[kk], X, Z);
       if (st >= kVotePending) {
 #pragma unroll
         for (int k = 0; k < 10; ++k) {
@@ -396,7 +466,8 @@ __global__ __launch_bounds__(256) void k_votes_keyed_inv(const uint32_t* __restr
       load(W, 0, i);
       load(Z, 10, i);
       fe_mul(x, W, inv);
-      if (fe_isnegative(x) != (st & 1)) cert_ok[vote_cert[v0 + i]] = 0;
+      if (fe_isnegative(x) != (st & 1))
+        cert_ok[vote_cert[v0 + (vp.perm ? vp.perm[i] : i)]] = 0;
       fe_mul(inv, inv, Z);
     }
     if (i < nchunks) break;
@@ -564,7 +635,7 @@ static std::mutex g_btw_mu[kMaxDevIds];   // per device: devices build in parall
 static constexpr uint32_t kBtwPerHalf = bdigits<NW_BWIN>::ENTRIES;
 
 static std::atomic<ge_niels_pad*> g_bcomb[kMaxDevIds];
-static_assert(kStrictKeyTables == (int)kKeyCombT, "keyed comb table count");
+static_assert(kStrictKeyTables == (int)kKeyCombT && kStrictKeyN == kKeyN, "keyed comb tables");
 
 // Table set `which` of the current device (0: the ladder's 2 x kBtwPerHalf; 1: the keyed
 // comb's 16 x 32,769), built on first use.
@@ -674,14 +745,15 @@ hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
   return hipGetLastError();
 }
 
-size_t votes_keyed_bytes_per_vote() { return 4 * 21; }   // 20 limb planes + state
+size_t votes_keyed_bytes_per_vote() { return 4 * 22; }   // 20 limb planes, state, perm
+size_t votes_keyed_fixed_bytes() { return 4 * kVkMaxBins; }   // key histogram / cursors
 
 hipError_t launch_votes_keyed(const uint32_t* cert_digest, const uint64_t* cvo, uint64_t ncert,
                               const uint32_t* vote_cert, const uint32_t* pks,
                               const uint32_t* sigs, uint64_t nvotes, const int32_t* pre1,
                               const int32_t* pre2, const int32_t* hdr_st,
-                              const key_tables_t& keys, uint32_t* cert_ok, void* scratch,
-                              size_t scratch_bytes, hipStream_t stream) {
+                              const key_tables_t& keys, uint32_t nkeys, uint32_t* cert_ok,
+                              void* scratch, size_t scratch_bytes, hipStream_t stream) {
   if (ncert == 0) return hipSuccess;
   if (!keys.vote_key || !keys.tabs || !keys.ok || !vote_cert) return hipErrorInvalidValue;
   const ge_niels_pad* bcomb = nullptr;
@@ -691,13 +763,33 @@ hipError_t launch_votes_keyed(const uint32_t* cert_digest, const uint64_t* cvo, 
                      ncert, cert_ok);
   // slices of S votes through the scratch (the caller's verify_batch workspace, free until
   // the failed certificates' batches run)
-  const uint64_t cap = scratch_bytes / votes_keyed_bytes_per_vote();
+  if (nvotes == 0) return hipGetLastError();   // e.g. genesis certificates: no votes
+  if (scratch_bytes < votes_keyed_fixed_bytes()) return hipErrorInvalidValue;
+  const uint64_t cap = (scratch_bytes - votes_keyed_fixed_bytes()) / votes_keyed_bytes_per_vote();
   const uint64_t S = nvotes <= cap ? nvotes : cap & ~63ull;
   if (nvotes && S == 0) return hipErrorInvalidValue;
-  uint32_t* base = static_cast<uint32_t*>(scratch);
-  const vote_planes_t vp{base, base + 20 * S, S};
+  uint32_t* gh = static_cast<uint32_t*>(scratch);
+  uint32_t* base = gh + kVkMaxBins;
+  // key-major order for committees whose tables overflow the caches (>= 64 keys: 4.3 GB of
+  // 16-bit tables; config 2 N = 100: 7.58 -> 9.11 M certs/s) — below that the cert-major
+  // order's coalesced signature reads win (N = 4 / 10 / 50: 143 / 74 / 19.2 unsorted vs
+  // 137 / 72 / 17.7 sorted). NW_VOTES_KEY_MAJOR=1 / 0 forces it on / off.
+  const char* km = getenv("NW_VOTES_KEY_MAJOR");
+  const bool sort = nkeys + 1 <= kVkMaxBins &&
+                    (km ? km[0] == '1' : nkeys >= kVkSortMinKeys);
+  uint32_t* perm = base + 21 * S;
+  const vote_planes_t vp{base, base + 20 * S, S, sort ? perm : nullptr};
   for (uint64_t v0 = 0; v0 < nvotes; v0 += S) {
     const uint64_t nv = std::min(S, nvotes - v0);
+    if (sort) {
+      hipError_t e = hipMemsetAsync(gh, 0, 4 * (nkeys + 1), stream);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(k_vk_hist, dim3(grid_for(nv, 256)), dim3(256), 0, stream, vote_cert,
+                         keys.vote_key, v0, nv, pre1, pre2, hdr_st, nkeys, gh);
+      hipLaunchKernelGGL(k_vk_scan, dim3(1), dim3(64), 0, stream, gh, nkeys + 1);
+      hipLaunchKernelGGL(k_vk_scatter, dim3(grid_for(nv, 256)), dim3(256), 0, stream, vote_cert,
+                         keys.vote_key, v0, nv, pre1, pre2, hdr_st, nkeys, gh, perm);
+    }
     hipLaunchKernelGGL(k_votes_keyed, dim3(grid_for(nv, 256)), dim3(256), 0, stream,
                        cert_digest, vote_cert, v0, nv, pks, sigs, pre1, pre2, hdr_st, keys, bcomb,
                        cert_ok, vp);

@@ -14,7 +14,9 @@
 // kind under the service mutex (a few hundred bytes, no allocation in the steady state:
 // batches are recycled). A flusher thread submits a batch as ONE device job
 // (nw_submit_*: the committee-aware pipeline with its key tables kept on the device) when it
-// holds max_items units or max_delay has passed since its first request; a completer thread
+// holds max_items units, max_delay has passed since its first request, or no job is in
+// flight (an idle device gains nothing from a bigger batch, so a lone request goes at once
+// and batches grow only while the device is busy); a completer thread
 // waits for the jobs in submission order and calls every request's verdict callback. At most
 // max_inflight jobs are queued on the device at once (backpressure on the flusher; requests
 // keep accumulating into the next, larger batch meanwhile, which is what keeps the device
@@ -131,6 +133,7 @@ struct nw_service {
   std::deque<std::unique_ptr<Batch>> inflight;
   bool force = false, stop = false, flusher_done = false;
   uint64_t accepted = 0, completed = 0, jobs = 0;
+  size_t open_jobs = 0;   // submitted, callbacks not yet delivered
   std::thread flusher, completer;
 
   // Adds one request to its kind's open batch (fill copies the inputs); 0 or NW_E_*.
@@ -211,7 +214,10 @@ struct nw_service {
       for (int k = 0; k < K_COUNT; ++k) {
         const Batch& b = *open[k];
         if (b.reqs.empty()) continue;
-        if (stop || force || b.units >= max_items || now >= b.first + delay) {
+        // flush: stopping / forced, full, its delay is over, or the device is idle (no job
+        // in flight: waiting would only add latency, nothing is gained by a bigger batch)
+        if (stop || force || b.units >= max_items || now >= b.first + delay ||
+            open_jobs == 0) {
           pick = k;
           break;
         }
@@ -242,6 +248,7 @@ struct nw_service {
       b->rc = submit(*b);
       lk.lock();
       ++jobs;
+      ++open_jobs;
       inflight.push_back(std::move(b));
       cv_inflight.notify_one();
     }
@@ -270,6 +277,7 @@ struct nw_service {
         b->reqs[i].fn(b->reqs[i].arg, rc ? rc : b->status[i], rc ? 0 : b->index[i]);
       lk.lock();
       completed += n;
+      if (--open_jobs == 0) cv_flush.notify_one();   // device idle: flush what has queued
       b->clear();
       spare[b->kind].push_back(std::move(b));
       cv_idle.notify_all();

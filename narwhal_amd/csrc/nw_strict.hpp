@@ -238,8 +238,16 @@ struct btab_lazy {
 // device copy (global memory, padded entries); bcomb_lazy: entries computed per lookup
 // (host self-check).
 constexpr int kBCombT = 16;
-constexpr int kStrictKeyTables = 32;   // = nw_kernels.h kKeyCombT
 constexpr uint32_t kBCombN = (1u << 15) + 1;
+// Committee-key comb width (= nw_kernels.h kKeyW): 256 / W tables j * 2^(W t) A, j = 0..2^(W-1)
+#ifndef NW_KEYW
+#define NW_KEYW 16
+#endif
+constexpr int kStrictKeyW = NW_KEYW;
+constexpr int kStrictKeyTables = 256 / kStrictKeyW;   // = nw_kernels.h kKeyCombT
+constexpr uint32_t kStrictKeyN = (1u << (kStrictKeyW - 1)) + 1;
+constexpr uint32_t kStrictKeyMask = kStrictKeyW == 16 ? 0x80008000u : 0x80808080u;
+static_assert(kStrictKeyW == 8 || kStrictKeyW == 16, "NW_KEYW must be 8 or 16");
 struct bcomb_wide {
   const ge_niels_pad* t;
   NW_HD void operator()(int m, int ad, ge_cached& e) const {
@@ -267,18 +275,52 @@ struct bcomb_lazy {
   }
 };
 
-// acc = [s]B - [k]A for k, s < l: -[k]A as k's 32 signed 8-bit digits against the key's comb
-// tables (keytab[129 t + j] = j * 2^(8t) A, affine niels), [s]B as s's 16 signed 16-bit
-// digits against the B comb (bc). No doublings.
+// A committee key's comb tables: keytab_wide reads the device copy (keytab[kStrictKeyN t + j]
+// = j * 2^(W t) A, affine niels, built by k_key_tabs); keytab_lazy computes an entry per
+// lookup from A (host self-check: the full 16-bit tables are 67 MB per key).
+struct keytab_wide {
+  const ge_niels_pad* t;
+  NW_HD void operator()(int tab, int j, ge_niels& e) const {
+    e = t[(uint32_t)tab * kStrictKeyN + (uint32_t)j].n;
+  }
+};
+struct keytab_lazy {
+  const ge* A;
+  const fe* d2;
+  NW_HD void operator()(int tab, int j, ge_niels& e) const {
+    ge P = *A;
+    for (int d = 0; d < kStrictKeyW * tab; ++d) ge_dbl(P, P, true);
+    ge_cached c;
+    ge_to_cached(c, P, *d2);
+    ge acc;
+    ge_identity(acc);
+    for (int bit = kStrictKeyW - 1; bit >= 0; --bit) {
+      ge_dbl(acc, acc, true);
+      if ((j >> bit) & 1) ge_add_cached(acc, acc, c, true);
+    }
+    ge_to_niels(e, acc, *d2);
+  }
+};
+
+// acc = [s]B - [k]A for k, s < l: -[k]A as k's 256 / W signed W-bit digits against the
+// key's comb tables (kt), [s]B as s's 16 signed 16-bit digits against the B comb (bc). No
+// doublings.
 #ifndef NW_KEYED_SPLIT
 #define NW_KEYED_SPLIT 0   // 1: the A and B terms in two interleaved accumulators (ILP)
 #endif
-template <class BComb>
+// Signed W-bit digit t of a recoded scalar (sc_recode with kStrictKeyMask / 0x80008000).
+template <int W>
+NW_HD int comb_digit(const uint32_t rd[8], int t) {
+  constexpr int per = 32 / W;
+  constexpr uint32_t m = (W == 32) ? 0xffffffffu : ((1u << W) - 1u);
+  return (int)((sel8(rd, t / per) >> ((t % per) * W)) & m) - (1 << (W - 1));
+}
+template <class BComb, class KeyTab>
 NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
-                          const ge_niels_pad* keytab, const fe& d2) {
+                          const KeyTab& kt, const fe& d2) {
   uint32_t kd[8], sd[8];
-  sc_recode(kd, k, 0x80808080u);   // k < l: 32 signed 8-bit digits
-  sc_recode(sd, s, 0x80008000u);   // s < l: 16 signed 16-bit digits
+  sc_recode(kd, k, kStrictKeyMask);   // k < l: 256 / W signed W-bit digits
+  sc_recode(sd, s, 0x80008000u);      // s < l: 16 signed 16-bit digits
   ge_identity(acc);
 #if NW_KEYED_SPLIT
   // two independent chains, one step of each per iteration: -[k]A in acc, [s]B in accB,
@@ -286,15 +328,18 @@ NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
   ge accB;
   ge_identity(accB);
 #pragma unroll 1
-  for (int t = 0; t < kStrictKeyTables; ++t) {
-    const int d = (int)((sel8(kd, t >> 2) >> ((t & 3) * 8)) & 255u) - 128;
-    if (d != 0) {
-      ge_niels nb = keytab[129 * t + (d < 0 ? -d : d)].n;
-      ge_niels_cneg(nb, d > 0);
-      ge_add_niels(acc, acc, nb, true);
+  for (int t = 0; t < (kStrictKeyTables > kBCombT ? kStrictKeyTables : kBCombT); ++t) {
+    if (t < kStrictKeyTables) {
+      const int d = comb_digit<kStrictKeyW>(kd, t);
+      if (d != 0) {
+        ge_niels nb;
+        kt(t, d < 0 ? -d : d, nb);
+        ge_niels_cneg(nb, d > 0);
+        ge_add_niels(acc, acc, nb, true);
+      }
     }
     if (t < kBCombT) {
-      const int e = (int)((sel8(sd, t >> 1) >> ((t & 1) * 16)) & 0xffffu) - 32768;
+      const int e = comb_digit<16>(sd, t);
       if (e != 0) {
         ge_cached c;
         bc(t, e < 0 ? -e : e, c);
@@ -313,9 +358,10 @@ NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
   // -[k]A: digit t of k against table t, negated
 #pragma unroll 1
   for (int t = 0; t < kStrictKeyTables; ++t) {
-    const int d = (int)((sel8(kd, t >> 2) >> ((t & 3) * 8)) & 255u) - 128;
+    const int d = comb_digit<kStrictKeyW>(kd, t);
     if (d != 0) {
-      ge_niels nb = keytab[129 * t + (d < 0 ? -d : d)].n;
+      ge_niels nb;
+      kt(t, d < 0 ? -d : d, nb);
       ge_niels_cneg(nb, d > 0);
       ge_add_niels(acc, acc, nb, true);
     }
@@ -323,7 +369,7 @@ NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
   // +[s]B
 #pragma unroll 1
   for (int m = 0; m < kBCombT; ++m) {
-    const int d = (int)((sel8(sd, m >> 1) >> ((m & 1) * 16)) & 0xffffu) - 32768;
+    const int d = comb_digit<16>(sd, m);
     if (d != 0) {
       ge_cached e;
       bc(m, d < 0 ? -d : d, e);
@@ -343,9 +389,9 @@ NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
 // X'/Z' equals the sign bit. Returns kVotePass / kVoteFail, or kVotePending (| sign) when
 // only that parity is left: the caller batches the inversions of Z' (k_votes_keyed_inv).
 constexpr uint32_t kVotePass = 0, kVoteFail = 1, kVotePending = 2;
-template <class BComb, class Src>
+template <class BComb, class KeyTab, class Src>
 NW_HD uint32_t keyed_vote_check(const Src& src, const strict_consts& K, const BComb& bc,
-                                const ge_niels_pad* keytab, uint32_t keyflags, fe& X, fe& Z) {
+                                const KeyTab& keytab, uint32_t keyflags, fe& X, fe& Z) {
   const bool okA = (keyflags & 1) != 0, smallA = (keyflags & 2) != 0;
   uint32_t Sw[8];
   src.S(Sw);
@@ -375,15 +421,15 @@ NW_HD uint32_t keyed_vote_check(const Src& src, const strict_consts& K, const BC
   return kVotePending | sign;
 }
 
-// Keyed strict verification: A is a committee key with comb tables keytab[129 t + j] =
-// j * 2^(8t) A (t = 0..31, nw_kernels.h kKeyTab; affine niels), keyflags bit 0 = decoded,
-// bit 1 = small order. Then R' = [s]B - [k]A is 16 + 32 table additions with no doublings and no scalar
-// split, and the equation is dalek's own projective comparison R == R' (R decompressed,
+// Keyed strict verification: A is a committee key with comb tables j * 2^(W t) A
+// (keytab_wide / keytab_lazy; affine niels), keyflags bit 0 = decoded, bit 1 = small
+// order. Then R' = [s]B - [k]A is 16 + 256 / W table additions with no doublings and no
+// scalar split, and the equation is dalek's own projective comparison R == R' (R decompressed,
 // Z = 1). Same checks and order as strict_verify_core; A is neither decompressed nor
 // tabulated per signature.
-template <class BComb, class Src>
+template <class BComb, class KeyTab, class Src>
 NW_HD int strict_keyed_comb(const Src& src, const strict_consts& K, const BComb& bc,
-                            const ge_niels_pad* keytab, uint32_t keyflags) {
+                            const KeyTab& keytab, uint32_t keyflags) {
   const bool okA = (keyflags & 1) != 0, smallA = (keyflags & 2) != 0;
   ge R;
   bool okR, smallR;

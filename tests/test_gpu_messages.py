@@ -311,7 +311,8 @@ def test_certificate_keyed_votes_mixed_validity(monkeypatch, N, n):
     """Keyed vote checks (launch_votes_keyed, NW_CERT_KEYED=1: every vote through the keyed
     comb, then verify_batch only for certificates with a failing vote): about 1% of the
     certificates carry one invalid vote of every class (workloads.mutate_votes); statuses
-    and indices equal the construction and the unmerged path; an honest stream is all Ok."""
+    and indices equal the construction and the unmerged path, with the votes checked in
+    certificate order and in key-major order; an honest stream is all Ok."""
     from narwhal_amd import crypto as C
     keys = O.keys(N)
     s = W.certificate_stream(n, keys, lambda sk, m: C.sign_many(sk, m), oracle_digest_many,
@@ -320,10 +321,13 @@ def test_certificate_keyed_votes_mixed_validity(monkeypatch, N, n):
     m, exp_st, exp_ix = W.mutate_votes(s, bad, seed=N + 3)
     com = _Com(s["committee"])
     monkeypatch.setenv("NW_CERT_KEYED", "1")
-    st, ix = M.verify_certificates_many(com, m, None)
-    assert st.tolist() == exp_st.tolist() and ix.tolist() == exp_ix.tolist()
-    st, _ = M.verify_certificates_many(com, s, None)
-    assert (st == 0).all()
+    for order in ("0", "1"):   # cert-major and key-major vote order (k_vk_* counting sort)
+        monkeypatch.setenv("NW_VOTES_KEY_MAJOR", order)
+        st, ix = M.verify_certificates_many(com, m, None)
+        assert st.tolist() == exp_st.tolist() and ix.tolist() == exp_ix.tolist(), order
+        st, _ = M.verify_certificates_many(com, s, None)
+        assert (st == 0).all(), order
+    monkeypatch.delenv("NW_VOTES_KEY_MAJOR")
     monkeypatch.delenv("NW_CERT_KEYED")
     monkeypatch.setenv("NW_CERT_MERGE", "0")
     st0, ix0 = M.verify_certificates_many(com, m, None)
@@ -344,8 +348,10 @@ def test_certificate_keyed_votes_early_failures(monkeypatch):
     exp = [0] * 300 + [int(x) for x in exp_st] + [0] * 300
     expi = [0] * 300 + [int(x) for x in exp_ix] + [0] * 300
     monkeypatch.setenv("NW_CERT_KEYED", "1")
-    st, ix = M.verify_certificates_many(_Com(com), p, None)
-    assert st.tolist() == exp and ix.tolist() == expi
+    for order in ("0", "1"):   # key-major: decided certificates' votes sort into the last bin
+        monkeypatch.setenv("NW_VOTES_KEY_MAJOR", order)
+        st, ix = M.verify_certificates_many(_Com(com), p, None)
+        assert st.tolist() == exp and ix.tolist() == expi, order
 
 
 def test_certificate_groups_adaptive_repeated_calls(monkeypatch):

@@ -145,39 +145,23 @@ int hc_verify_strict_half(const uint8_t pk[32], const uint8_t sig[64], const uin
   return strict_verify_core<16>(src, SK, btab_wide{BTW, BTW_N}, ta, tr, id);
 }
 
-// The keyed strict path (nw_strict.hpp strict_keyed_comb): the key's 32 comb tables
-// j * 2^(8t) A built here as the device's k_key_base / k_key_tabs define them, the B comb
-// computed per lookup. Returns the status; -1 when A does not decode is reported through the
+// The keyed strict path (nw_strict.hpp strict_keyed_comb): the key's comb table entries
+// j * 2^(W t) A computed per lookup (keytab_lazy) by the definition the device's k_key_base /
+// k_key_tabs tabulate, the B comb likewise. Returns the status; -1 when A does not decode is reported through the
 // key flags exactly as the device does (status 3).
-static uint32_t keyed_tables(ge_niels_pad* tab, const uint32_t Aw[8]) {
-  ge A;
+static uint32_t keyed_key(ge& A, const uint32_t Aw[8]) {
   const bool dec = ge_frombytes(A, Aw, K);
-  const uint32_t flags = (dec ? 1u : 0u) | (dec && ge_is_small_order(A) ? 2u : 0u);
-  ge base = A;
-  for (int t = 0; t < 32; ++t) {
-    if (t) for (int d = 0; d < 8; ++d) { ge x; ge_dbl(x, base, d == 7); base = x; }
-    ge_cached cb;
-    ge_to_cached(cb, base, K.d2);
-    ge acc;
-    ge_identity(acc);
-    for (int j = 0; j <= 128; ++j) {
-      ge_to_niels(tab[129 * t + j].n, acc, K.d2);
-      ge nx;
-      ge_add_cached(nx, acc, cb, true);
-      acc = nx;
-    }
-  }
-  return flags;
+  return (dec ? 1u : 0u) | (dec && ge_is_small_order(A) ? 2u : 0u);
 }
 
 int hc_verify_strict_keyed(const uint8_t pk[32], const uint8_t sig[64], const uint8_t k32[32]) {
   init();
   uint32_t Aw[8], Rw[8], Sw[8], kw[8];
   load8(Aw, pk); load8(Rw, sig); load8(Sw, sig + 32); load8(kw, k32);
-  static ge_niels_pad tab[32 * 129];
-  const uint32_t flags = keyed_tables(tab, Aw);
+  ge A;
+  const uint32_t flags = keyed_key(A, Aw);
   const strict_src_arrays src{Aw, Rw, Sw, kw};
-  return strict_keyed_comb(src, SK, bcomb_lazy{BT, &SK.k.d2}, tab, flags);
+  return strict_keyed_comb(src, SK, bcomb_lazy{BT, &SK.k.d2}, keytab_lazy{&A, &SK.k.d2}, flags);
 }
 
 // The certificate-vote keyed check without R decompression (nw_strict.hpp
@@ -187,11 +171,12 @@ int hc_keyed_vote_check(const uint8_t pk[32], const uint8_t sig[64], const uint8
   init();
   uint32_t Aw[8], Rw[8], Sw[8], kw[8];
   load8(Aw, pk); load8(Rw, sig); load8(Sw, sig + 32); load8(kw, k32);
-  static ge_niels_pad tab[32 * 129];
-  const uint32_t flags = keyed_tables(tab, Aw);
+  ge A;
+  const uint32_t flags = keyed_key(A, Aw);
   const strict_src_arrays src{Aw, Rw, Sw, kw};
   fe X, Z;
-  const uint32_t st = keyed_vote_check(src, SK, bcomb_lazy{BT, &SK.k.d2}, tab, flags, X, Z);
+  const uint32_t st = keyed_vote_check(src, SK, bcomb_lazy{BT, &SK.k.d2},
+                                       keytab_lazy{&A, &SK.k.d2}, flags, X, Z);
   if (st < kVotePending) return (int)st;
   fe zi, x;
   fe_invert(zi, Z);
