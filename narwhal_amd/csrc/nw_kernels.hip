@@ -242,6 +242,54 @@ struct strict_src_global {
   }
 };
 
+// The strict ladder's LDS prefetcher (nw_strict.hpp pf_none for the contract): one
+// 160-byte slot per lane (10 chunks of 16 B, chunk k of lane l at s_pf[k][l]: the lanes of a
+// wave write and read 16 consecutive bytes each, conflict-free), 40 KB per 256-thread block,
+// 120 KB at 3 blocks per CU.
+#ifndef NW_STRICT_PF
+#define NW_STRICT_PF 1
+#endif
+#if NW_STRICT_PF && NW_BWIN != 8
+__shared__ uint4 s_pf[10][256];
+struct pf_lds {
+  static constexpr bool enabled = true;
+  uint32_t wave;   // wave index in the block (uniform)
+  __device__ void issue(const void* src, int chunks) const {
+    const uint4* g = static_cast<const uint4*>(src);
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this lane's last slot read is done
+#pragma unroll
+    for (int k = 0; k < 10; ++k)
+      if (k < chunks) __builtin_amdgcn_global_load_lds(g + k, &s_pf[k][wave * 64], 16, 0, 0);
+  }
+  __device__ void get(ge_cached& e, bool niels) const {
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the DMA into LDS has landed
+    asm volatile("" ::: "memory");
+    uint32_t* w = reinterpret_cast<uint32_t*>(&e);
+    const uint32_t l = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {   // YpX, YmX
+      const uint4 v = s_pf[k][l];
+      w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+    }
+    uint32_t t[20];
+#pragma unroll
+    for (int k = 5; k < 10; ++k) {
+      if (k < 8 || !niels) {
+        const uint4 v = s_pf[k][l];
+        t[4 * (k - 5)] = v.x; t[4 * (k - 5) + 1] = v.y; t[4 * (k - 5) + 2] = v.z;
+        t[4 * (k - 5) + 3] = v.w;
+      }
+    }
+    // cached: words 20..39 = Z2, T2d; niels: words 20..29 = xy2d (-> T2d), Z2 unused
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      e.T2d.v[i] = niels ? t[i] : t[10 + i];
+      e.Z2.v[i] = t[i];
+    }
+  }
+};
+#endif
+
 // Persistent: the grid covers the resident waves once and strides over the items, so the
 // per-lane tables j*A, j*R live in a fixed workspace (16 entries x 160 B per lane slot, lane-
 // contiguous: a lookup reads 160 consecutive bytes per lane instead of 40 scattered dwords).
@@ -283,8 +331,15 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
     // committee keys: [s]B - [k]A from comb tables, no ladder; others: the half-size ladder
     const int st = keytab ? strict_keyed_comb(src, g_consts.sk, bcomb_wide{bcomb},
                                               keytab_wide{keytab}, keys.ok[kk])
+#if NW_STRICT_PF && NW_BWIN != 8
+                          : strict_verify_core<NW_BWIN>(src, g_consts.sk, bt, tabA, tabR,
+                                                        WaveMax{},
+                                                        pf_lds{(uint32_t)__builtin_amdgcn_readfirstlane(
+                                                            threadIdx.x >> 6)});
+#else
                           : strict_verify_core<NW_BWIN>(src, g_consts.sk, bt, tabA, tabR,
                                                         WaveMax{});
+#endif
     if (active) status[gi] = st;
     const uint64_t mask = __ballot(active && st == NW_OK);
     if ((threadIdx.x & 63) == 0 && gi < n) bitmap[gi >> 6] = mask;

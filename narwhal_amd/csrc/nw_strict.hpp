@@ -166,6 +166,7 @@ struct btab_pair {
 struct btab_wide {
   const ge_niels_pad* t;
   uint32_t n;   // entries per half: 2^(bw-1) + 1
+  NW_HD const ge_niels_pad* entry(int h, int ad) const { return t + (h ? n : 0u) + (uint32_t)ad; }
   NW_HD void operator()(int h, int ad, ge_cached& e) const {
     const ge_niels& nb = t[(h ? n : 0u) + (uint32_t)ad].n;
     fe_copy(e.YpX, nb.ypx);
@@ -464,13 +465,26 @@ NW_HD int strict_keyed_comb(const Src& src, const strict_consts& K, const BComb&
   return ge_eq_affine(acc, R) ? NW_OK : NW_ERR_EQUATION;
 }
 
+// Table-entry prefetch for the strict ladder. pf_none: each addition reads its entry from
+// its table when it runs (host self-check; NW_STRICT_PF=0). The device's LDS prefetcher
+// (nw_kernels.hip pf_lds) loads the NEXT addition's entry straight into LDS
+// (global_load_lds_dwordx4, no registers) while the current addition or the window's four
+// doublings run, so the ladder's ~77 dependent table loads per verification stop stalling
+// the wave. issue(src, chunks): 16-byte chunks at src (10 = ge_cached, 8 = ge_niels_pad);
+// get(e, niels): wait for it and read it (niels: Y+x, Y-x, xy2d into YpX, YmX, T2d).
+struct pf_none {
+  static constexpr bool enabled = false;
+  NW_HD void issue(const void*, int) const {}
+  NW_HD void get(ge_cached&, bool) const {}
+};
+
 // Status of one strict verification. wave_max maps this lane's ladder length (in 4-bit
 // windows) to the wave's maximum (identity on the host). tabA/tabR: 8 entries each of
 // per-lane scratch. bt: j*B and j*2^128 B, j = 0..2^(BW-1) (btab_pair / btab_wide).
-template <int BW, class BTab, class Src, class WaveMax>
+template <int BW, class BTab, class Src, class WaveMax, class PF = pf_none>
 NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab& bt,
                              ge_cached* tabA, ge_cached* tabR,
-                             WaveMax wave_max) {
+                             WaveMax wave_max, const PF& pf = PF{}) {
   using BD = bdigits<BW>;
   // Decompress A, then R, in one rolled loop (one copy of the sqrt_ratio_i chain in the
   // code object): P, its small-order flag and its 8-entry table j * P. Only the point is
@@ -540,6 +554,67 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
   // per table).
   ge acc;
   ge_identity(acc);
+  if constexpr (PF::enabled) {
+    // The same additions in the same order as below; the entry of addition (j, slot) is
+    // requested one addition ahead (window j's first one before its doublings).
+    auto slot_src = [&](int j, int slot, int& d, bool& niels) -> const void* {
+      const int p0 = 4 * j, p1 = 4 * j + 128;
+      const bool has0 = j < 32 && p0 % BW == 0;
+      niels = slot >= 2;
+      if (slot == 0) {
+        d = digit4_of(ud, 8, j);
+      } else if (slot == 1) {
+        d = j < 40 ? digit4_of(vd, 5, j) : 0;
+        if (h.vneg) d = -d;
+      } else {
+        const bool t1 = slot == 3 || !has0;
+        d = BD::digit(wd, t1 ? p1 / BW : p0 / BW);
+        return d ? static_cast<const void*>(bt.entry(t1 ? 1 : 0, d < 0 ? -d : d)) : nullptr;
+      }
+      const int ad = d < 0 ? -d : d;
+      return d ? static_cast<const void*>((slot == 0 ? tabA : tabR) + (ad - 1)) : nullptr;
+    };
+    auto nslots_of = [&](int j) {
+      const int p0 = 4 * j, p1 = 4 * j + 128;
+      const bool has0 = j < 32 && p0 % BW == 0;
+      const bool has1 = j < 32 && p1 % BW == 0 && p1 / BW < BD::NB;
+      return 2 + (has0 ? 1 : 0) + (has1 ? 1 : 0);
+    };
+    {
+      int d0;
+      bool nl0;
+      const void* s0 = slot_src(W - 1, 0, d0, nl0);
+      if (s0) pf.issue(s0, nl0 ? 8 : 10);
+    }
+#pragma unroll 1
+    for (int j = W - 1; j >= 0; --j) {
+      if (j != W - 1) {
+#pragma unroll 1
+        for (int t = 0; t < 4; ++t) ge_dbl(acc, acc, t == 3);
+      }
+      const int nslots = nslots_of(j);
+#pragma unroll 1
+      for (int slot = 0; slot < nslots; ++slot) {
+        int d;
+        bool niels;
+        const void* cur = slot_src(j, slot, d, niels);
+        ge_cached e;
+        if (cur) pf.get(e, niels);
+        // request the next addition's entry before this one runs
+        const int j2 = slot + 1 < nslots ? j : j - 1, s2 = slot + 1 < nslots ? slot + 1 : 0;
+        if (j2 >= 0) {
+          int d2;
+          bool n2;
+          const void* nx = slot_src(j2, s2, d2, n2);
+          if (nx) pf.issue(nx, n2 ? 8 : 10);
+        }
+        if (cur) {
+          ge_cached_cneg(e, d < 0);
+          ge_add_any(acc, acc, e, niels, NW_LAST_T || slot != nslots - 1);
+        }
+      }
+    }
+  } else {
 #pragma unroll 1
   for (int j = W - 1; j >= 0; --j) {
     if (j != W - 1) {
@@ -579,6 +654,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
         ge_add_any(acc, acc, e, slot >= 2, NW_LAST_T || slot != nslots - 1);
       }
     }
+  }
   }
   const bool eq = ge_is_identity(acc);
   // Reference order: crypto/src/lib.rs:201 (s high bits), 202 (decompress A), then dalek
