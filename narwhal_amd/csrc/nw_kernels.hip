@@ -395,6 +395,10 @@ __device__ __forceinline__ uint32_t vk_bin(const uint32_t* __restrict__ vote_cer
   const uint32_t k = vote_key[v];
   return k < nkeys ? k : nkeys;
 }
+// Blocks take contiguous chunks of kVkChunk votes: one global atomic per (block, bin), not
+// per (256 votes, bin) — with ~100 bins per block the per-block form made the 26M global
+// atomics of N = 100 serialize on 100 addresses (4.9 ms per pass).
+constexpr uint32_t kVkChunk = 16384;
 __global__ __launch_bounds__(256) void k_vk_hist(const uint32_t* __restrict__ vote_cert,
                                                  const uint32_t* __restrict__ vote_key,
                                                  uint64_t v0, uint64_t nv,
@@ -405,8 +409,10 @@ __global__ __launch_bounds__(256) void k_vk_hist(const uint32_t* __restrict__ vo
   __shared__ uint32_t h[kVkMaxBins];
   for (uint32_t b = threadIdx.x; b <= nkeys; b += blockDim.x) h[b] = 0;
   __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < nv) atomicAdd(&h[vk_bin(vote_cert, vote_key, v0 + i, pre1, pre2, hdr_st, nkeys)], 1u);
+  const uint64_t c0 = (uint64_t)blockIdx.x * kVkChunk;
+  const uint64_t c1 = c0 + kVkChunk < nv ? c0 + kVkChunk : nv;
+  for (uint64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x)
+    atomicAdd(&h[vk_bin(vote_cert, vote_key, v0 + i, pre1, pre2, hdr_st, nkeys)], 1u);
   __syncthreads();
   for (uint32_t b = threadIdx.x; b <= nkeys; b += blockDim.x)
     if (h[b]) atomicAdd(&gh[b], h[b]);
@@ -420,6 +426,8 @@ __global__ __launch_bounds__(64) void k_vk_scan(uint32_t* __restrict__ gh, uint3
     acc += c;
   }
 }
+// Same chunks: count again, reserve the block's range in every bin (one atomic each), then
+// hand out positions inside the ranges with LDS cursors.
 __global__ __launch_bounds__(256) void k_vk_scatter(const uint32_t* __restrict__ vote_cert,
                                                     const uint32_t* __restrict__ vote_key,
                                                     uint64_t v0, uint64_t nv,
@@ -431,17 +439,18 @@ __global__ __launch_bounds__(256) void k_vk_scatter(const uint32_t* __restrict__
   __shared__ uint32_t h[kVkMaxBins];
   for (uint32_t b = threadIdx.x; b <= nkeys; b += blockDim.x) h[b] = 0;
   __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t b = 0, r = 0;
-  if (i < nv) {
-    b = vk_bin(vote_cert, vote_key, v0 + i, pre1, pre2, hdr_st, nkeys);
-    r = atomicAdd(&h[b], 1u);
-  }
+  const uint64_t c0 = (uint64_t)blockIdx.x * kVkChunk;
+  const uint64_t c1 = c0 + kVkChunk < nv ? c0 + kVkChunk : nv;
+  for (uint64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x)
+    atomicAdd(&h[vk_bin(vote_cert, vote_key, v0 + i, pre1, pre2, hdr_st, nkeys)], 1u);
   __syncthreads();
   for (uint32_t x = threadIdx.x; x <= nkeys; x += blockDim.x)
     if (h[x]) h[x] = atomicAdd(&cursor[x], h[x]);   // this block's range in bin x
   __syncthreads();
-  if (i < nv) perm[h[b] + r] = (uint32_t)i;
+  for (uint64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
+    const uint32_t b = vk_bin(vote_cert, vote_key, v0 + i, pre1, pre2, hdr_st, nkeys);
+    perm[atomicAdd(&h[b], 1u)] = (uint32_t)i;
+  }
 }
 
 #ifndef NW_KEYED_WAVES
@@ -693,7 +702,7 @@ static std::atomic<ge_niels_pad*> g_bcomb[kMaxDevIds];
 static_assert(kStrictKeyTables == (int)kKeyCombT && kStrictKeyN == kKeyN, "keyed comb tables");
 
 // Table set `which` of the current device (0: the ladder's 2 x kBtwPerHalf; 1: the keyed
-// comb's 16 x 32,769), built on first use.
+// comb's kBCombT x kBCombN: 11 x 8,388,609 = 11.8 GB at 24-bit digits), built on first use.
 static hipError_t btab_for_current_device(int which, const ge_niels_pad** out) {
   *out = nullptr;
   if (which == 0 && NW_BWIN == 8) return hipSuccess;
@@ -706,7 +715,7 @@ static hipError_t btab_for_current_device(int which, const ge_niels_pad** out) {
   std::lock_guard<std::mutex> lock(g_btw_mu[dev]);
   if ((*out = slot.load(std::memory_order_relaxed))) return hipSuccess;
   const uint32_t n = which ? kBCombN : kBtwPerHalf, ntab = which ? kBCombT : 2;
-  const uint32_t shift = which ? 16 : 128;
+  const uint32_t shift = which ? (uint32_t)kBCombW : 128;
   void* p = nullptr;
   const uint64_t entries = (uint64_t)ntab * n;
   e = hipMalloc(&p, entries * sizeof(ge_niels_pad));
@@ -839,10 +848,10 @@ hipError_t launch_votes_keyed(const uint32_t* cert_digest, const uint64_t* cvo, 
     if (sort) {
       hipError_t e = hipMemsetAsync(gh, 0, 4 * (nkeys + 1), stream);
       if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(k_vk_hist, dim3(grid_for(nv, 256)), dim3(256), 0, stream, vote_cert,
+      hipLaunchKernelGGL(k_vk_hist, dim3(grid_for(nv, kVkChunk)), dim3(256), 0, stream, vote_cert,
                          keys.vote_key, v0, nv, pre1, pre2, hdr_st, nkeys, gh);
       hipLaunchKernelGGL(k_vk_scan, dim3(1), dim3(64), 0, stream, gh, nkeys + 1);
-      hipLaunchKernelGGL(k_vk_scatter, dim3(grid_for(nv, 256)), dim3(256), 0, stream, vote_cert,
+      hipLaunchKernelGGL(k_vk_scatter, dim3(grid_for(nv, kVkChunk)), dim3(256), 0, stream, vote_cert,
                          keys.vote_key, v0, nv, pre1, pre2, hdr_st, nkeys, gh, perm);
     }
     hipLaunchKernelGGL(k_votes_keyed, dim3(grid_for(nv, 256)), dim3(256), 0, stream,

@@ -234,12 +234,18 @@ struct btab_lazy {
   }
 };
 
-// The B comb for keyed verifications: 16 tables j * 2^(16 m) * B (m = 0..15, j = 0..32,768),
-// so [s]B = sum_m T_m[d_m] over s's signed 16-bit digits with no doublings. bcomb_wide: the
+// The B comb for keyed verifications: kBCombT tables j * 2^(W m) * B (W = kBCombW), so
+// [s]B = sum_m T_m[d_m] over s's signed W-bit digits (bdigits) with no doublings. bcomb_wide: the
 // device copy (global memory, padded entries); bcomb_lazy: entries computed per lookup
 // (host self-check).
-constexpr int kBCombT = 16;
-constexpr uint32_t kBCombN = (1u << 15) + 1;
+// B comb width (NW_BCOMBW): 24-bit digits over 11 tables j * 2^(24 m) * B, j = 0..2^23
+// (11.8 GB per device, 11 additions for [s]B) or 16-bit over 16 tables (67 MB, 16 additions).
+#ifndef NW_BCOMBW
+#define NW_BCOMBW 24
+#endif
+constexpr int kBCombW = NW_BCOMBW;
+constexpr int kBCombT = bdigits<NW_BCOMBW>::NB;
+constexpr uint32_t kBCombN = bdigits<NW_BCOMBW>::ENTRIES;
 // Committee-key comb width (= nw_kernels.h kKeyW): 256 / W tables j * 2^(W t) A, j = 0..2^(W-1)
 #ifndef NW_KEYW
 #define NW_KEYW 16
@@ -265,7 +271,9 @@ struct bcomb_lazy {
     sc s;
 #pragma unroll
     for (int i = 0; i < 8; ++i) s.w[i] = 0;
-    s.w[m >> 1] = (uint32_t)ad << (16 * (m & 1));
+    const int bit = kBCombW * m, wi = bit >> 5, sh = bit & 31;
+    s.w[wi] = (uint32_t)ad << sh;
+    if (sh && wi < 7) s.w[wi + 1] = (uint32_t)ad >> (32 - sh);
     ge P;
     fixed_base_mul(P, s, btab8);
     ge_niels nb;
@@ -321,7 +329,7 @@ NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
                           const KeyTab& kt, const fe& d2) {
   uint32_t kd[8], sd[8];
   sc_recode(kd, k, kStrictKeyMask);   // k < l: 256 / W signed W-bit digits
-  sc_recode(sd, s, 0x80008000u);      // s < l: 16 signed 16-bit digits
+  bdigits<kBCombW>::recode(sd, s);    // s < l: kBCombT digits of kBCombW bits
   ge_identity(acc);
 #if NW_KEYED_SPLIT
   // two independent chains, one step of each per iteration: -[k]A in acc, [s]B in accB,
@@ -340,7 +348,7 @@ NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
       }
     }
     if (t < kBCombT) {
-      const int e = comb_digit<16>(sd, t);
+      const int e = bdigits<kBCombW>::digit(sd, t);
       if (e != 0) {
         ge_cached c;
         bc(t, e < 0 ? -e : e, c);
@@ -370,7 +378,7 @@ NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
   // +[s]B
 #pragma unroll 1
   for (int m = 0; m < kBCombT; ++m) {
-    const int d = comb_digit<16>(sd, m);
+    const int d = bdigits<kBCombW>::digit(sd, m);
     if (d != 0) {
       ge_cached e;
       bc(m, d < 0 ? -d : d, e);
