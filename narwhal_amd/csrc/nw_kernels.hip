@@ -242,6 +242,18 @@ struct strict_src_global {
   }
 };
 
+// Limb planes of the pending votes of a slice: X' limb k at planes[k S + i], Z' limb k at
+// planes[(10 + k) S + i] (coalesced in both kernels); state[i] = kVote* of vote v0 + i.
+struct vote_planes_t {
+  uint32_t* planes;
+  uint32_t* state;
+  uint64_t S;
+  const uint32_t* perm;   // slice position -> slice vote (key-major order), or nullptr
+};
+
+#ifndef NW_KEYED_WAVES
+#define NW_KEYED_WAVES 1
+#endif
 // The strict ladder's LDS prefetcher (nw_strict.hpp pf_none for the contract): one
 // 160-byte slot per lane (10 chunks of 16 B, chunk k of lane l at s_pf[k][l]: the lanes of a
 // wave write and read 16 consecutive bytes each, conflict-free), 40 KB per 256-thread block,
@@ -305,7 +317,11 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
                                                        ge_cached* __restrict__ tabs,
                                                        key_tables_t keys,
                                                        const ge_niels_pad* __restrict__ btw,
-                                                       const ge_niels_pad* __restrict__ bcomb) {
+                                                       const ge_niels_pad* __restrict__ bcomb,
+                                                       const uint32_t* __restrict__ list,
+                                                       const uint32_t* __restrict__ list_count) {
+  // list mode (keyed fast path's leftovers): items list[0 .. *list_count), no bitmap words
+  if (list) n = *list_count;
 #if NW_BWIN == 8
   __shared__ ge_niels s_btab[129];
   __shared__ ge_niels s_b128[129];
@@ -324,7 +340,7 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
        base += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t gi = base + threadIdx.x;
     const bool active = gi < n;
-    const uint64_t i = active ? gi : n - 1;
+    const uint64_t i = list ? list[active ? gi : n - 1] : active ? gi : n - 1;
     const strict_src_global src{pks + 8 * i, sigs + 16 * i, msgs + (uint64_t)msg_stride_words * i};
     const uint32_t kk = keys.vote_key ? keys.vote_key[i] : kNoKey;
     const ge_niels_pad* keytab = kk != kNoKey ? keys.tabs + kKeyTab * (uint64_t)kk : nullptr;
@@ -340,10 +356,118 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
                           : strict_verify_core<NW_BWIN>(src, g_consts.sk, bt, tabA, tabR,
                                                         WaveMax{});
 #endif
-    if (active) status[gi] = st;
+    if (active) status[i] = st;
+    if (list) continue;
     const uint64_t mask = __ballot(active && st == NW_OK);
     if ((threadIdx.x & 63) == 0 && gi < n) bitmap[gi >> 6] = mask;
   }
+}
+
+// Keyed fast path of launch_verify_strict (committee-key signers: Header::verify authors,
+// Vote::verify voters). k_strict_keyed runs the certificate votes' check (nw_strict.hpp
+// keyed_vote_check: [s]B - [k]A from the comb tables, compared with R in compressed form,
+// no square root) on every keyed item of a slice; a pass IS dalek's verify_strict Ok
+// (status 0), everything else — fails, non-committee signers, parity mismatches found by
+// k_strict_keyed_inv — is appended to a list (k_strict_keyed_list) and verified by
+// k_verify_strict in list mode, which names the exact failing check (status 1..7). With
+// honest streams the list is short, so the ~265-squaring decompression of R is skipped
+// for almost every signature.
+__global__ __launch_bounds__(256, NW_KEYED_WAVES) void k_strict_keyed(
+    const uint32_t* __restrict__ msgs, uint32_t msg_stride_words, const uint32_t* __restrict__ pks,
+    const uint32_t* __restrict__ sigs, uint64_t i0, uint64_t ns, int32_t* __restrict__ status,
+    key_tables_t keys, const ge_niels_pad* __restrict__ bcomb, vote_planes_t vp) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ns) return;
+  const uint64_t gi = i0 + i;
+  const uint32_t kk = keys.vote_key[gi];
+  uint32_t st = kVoteFail;
+  if (kk != kNoKey) {
+    const strict_src_global src{pks + 8 * gi, sigs + 16 * gi,
+                                msgs + (uint64_t)msg_stride_words * gi};
+    fe X, Z;
+    st = keyed_vote_check(src, g_consts.sk, bcomb_wide{bcomb},
+                          keytab_wide{keys.tabs + kKeyTab * (uint64_t)kk}, keys.ok[kk], X, Z);
+    if (st >= kVotePending) {
+#pragma unroll
+      for (int k = 0; k < 10; ++k) {
+        vp.planes[(uint64_t)k * vp.S + i] = X.v[k];
+        vp.planes[(uint64_t)(10 + k) * vp.S + i] = Z.v[k];
+      }
+    }
+  }
+  if (st == kVotePass) status[gi] = NW_OK;
+  vp.state[i] = st;
+}
+
+// Parity of the pending items (Montgomery's trick per strided chunk, as k_votes_keyed_inv):
+// a match is status 0, a mismatch goes to the list.
+__global__ __launch_bounds__(256) void k_strict_keyed_inv(uint64_t i0, uint64_t ns,
+                                                          uint64_t nchunks,
+                                                          int32_t* __restrict__ status,
+                                                          vote_planes_t vp) {
+  const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= nchunks) return;
+  auto load = [&](fe& f, int base, uint64_t i) {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) f.v[k] = vp.planes[(uint64_t)(base + k) * vp.S + i];
+  };
+  fe acc;
+  fe_1(acc);
+  uint64_t last = ~0ull;
+#pragma unroll 1
+  for (uint64_t i = lane; i < ns; i += nchunks) {
+    if (vp.state[i] < kVotePending) continue;
+    fe X, Z, W;
+    load(X, 0, i);
+    load(Z, 10, i);
+    fe_mul(W, X, acc);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) vp.planes[(uint64_t)k * vp.S + i] = W.v[k];
+    fe_mul(acc, acc, Z);
+    last = i;
+  }
+  if (last == ~0ull) return;
+  fe inv;
+  fe_invert(inv, acc);
+#pragma unroll 1
+  for (uint64_t i = last;; i -= nchunks) {
+    const uint32_t st = vp.state[i];
+    if (st >= kVotePending) {
+      fe W, Z, x;
+      load(W, 0, i);
+      load(Z, 10, i);
+      fe_mul(x, W, inv);
+      if (fe_isnegative(x) != (st & 1)) vp.state[i] = kVoteFail;
+      else status[i0 + i] = NW_OK;
+      fe_mul(inv, inv, Z);
+    }
+    if (i < nchunks) break;
+  }
+}
+
+// Failed / unkeyed items of the slice -> list (one atomic per wave).
+__global__ __launch_bounds__(256) void k_strict_keyed_list(uint64_t i0, uint64_t ns,
+                                                           const uint32_t* __restrict__ state,
+                                                           uint32_t* __restrict__ list,
+                                                           uint32_t* __restrict__ count) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool f = i < ns && state[i] == kVoteFail;
+  const uint64_t m = __ballot(f);
+  if (m == 0) return;
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t base = 0;
+  if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1))
+    base = atomicAdd(count, (uint32_t)__popcll(m));
+  base = (uint32_t)__shfl((int)base, __ffsll((unsigned long long)m) - 1);
+  if (f) list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint32_t)(i0 + i);
+}
+
+// Verdict bitmap from the statuses (bit i set iff status[i] == 0), 64 items per wave.
+__global__ __launch_bounds__(256) void k_status_bitmap(const int32_t* __restrict__ status,
+                                                       uint64_t n, uint64_t* __restrict__ bitmap) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t m = __ballot(i < n && status[i] == NW_OK);
+  if ((threadIdx.x & 63) == 0 && i < n) bitmap[i >> 6] = m;
 }
 
 // Certificate votes checked one by one with the keyed comb (Certificate::verify's
@@ -368,14 +492,6 @@ __global__ __launch_bounds__(256) void k_votes_keyed_init(const uint64_t* __rest
   if (c < ncert) cert_ok[c] = cvo[c + 1] > cvo[c] ? 1u : 0u;   // no votes: its own batch
 }
 
-// Limb planes of the pending votes of a slice: X' limb k at planes[k S + i], Z' limb k at
-// planes[(10 + k) S + i] (coalesced in both kernels); state[i] = kVote* of vote v0 + i.
-struct vote_planes_t {
-  uint32_t* planes;
-  uint32_t* state;
-  uint64_t S;
-  const uint32_t* perm;   // slice position -> slice vote (key-major order), or nullptr
-};
 
 // Key-major order of a slice's votes (k_vk_hist / k_vk_scan / k_vk_scatter: a counting sort
 // by committee key; the votes of already-decided certificates and non-members go to one
@@ -453,9 +569,6 @@ __global__ __launch_bounds__(256) void k_vk_scatter(const uint32_t* __restrict__
   }
 }
 
-#ifndef NW_KEYED_WAVES
-#define NW_KEYED_WAVES 1
-#endif
 __global__ __launch_bounds__(256, NW_KEYED_WAVES) void k_votes_keyed(
     const uint32_t* __restrict__ cert_digest, const uint32_t* __restrict__ vote_cert,
     uint64_t v0, uint64_t nv, const uint32_t* __restrict__ pks,
@@ -787,9 +900,11 @@ static unsigned strict_grid() {
   return (unsigned)cached[dev].load(std::memory_order_acquire);
 }
 
-size_t strict_workspace_bytes() {
-  return (size_t)strict_grid() * 256 * 16 * sizeof(ge_cached);
-}
+// The keyed fast path reuses the per-lane table region for its limb planes (84 B per item of
+// a slice) and keeps its list (4 B per item) and count in a tail after it.
+constexpr uint64_t kKeyedSliceMax = 1ull << 22;
+static size_t strict_tabs_bytes() { return (size_t)strict_grid() * 256 * 16 * sizeof(ge_cached); }
+size_t strict_workspace_bytes() { return strict_tabs_bytes() + 4 * kKeyedSliceMax + 256; }
 
 hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
                                 const uint32_t* pks, const uint32_t* sigs, uint64_t n,
@@ -803,9 +918,38 @@ hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
   hipError_t eb = btab_for_current_device(0, &btw);
   if (eb == hipSuccess && kt.vote_key) eb = btab_for_current_device(1, &bcomb);
   if (eb != hipSuccess) return eb;
-  hipLaunchKernelGGL(k_verify_strict, dim3(grid), dim3(256), 0, stream, msgs, msg_stride_words,
-                     pks, sigs, n, status, bitmap, static_cast<ge_cached*>(workspace), kt, btw,
-                     bcomb);
+  const char* kf = getenv("NW_STRICT_KEYED_FAST");
+  if (!kt.vote_key || (kf && kf[0] == '0')) {
+    hipLaunchKernelGGL(k_verify_strict, dim3(grid), dim3(256), 0, stream, msgs, msg_stride_words,
+                       pks, sigs, n, status, bitmap, static_cast<ge_cached*>(workspace), kt, btw,
+                       bcomb, nullptr, nullptr);
+    return hipGetLastError();
+  }
+  // keyed fast path (k_strict_keyed above), slice by slice through the workspace
+  const uint64_t S = std::min<uint64_t>(kKeyedSliceMax, strict_tabs_bytes() / (4 * 21)) & ~63ull;
+  uint32_t* base = static_cast<uint32_t*>(workspace);
+  uint32_t* list = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + strict_tabs_bytes());
+  uint32_t* count = list + kKeyedSliceMax;
+  const vote_planes_t vp{base, base + 20 * S, S, nullptr};
+  for (uint64_t i0 = 0; i0 < n; i0 += S) {
+    const uint64_t ns = std::min(S, n - i0);
+    hipError_t e = hipMemsetAsync(count, 0, 4, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_strict_keyed, dim3(grid_for(ns, 256)), dim3(256), 0, stream, msgs,
+                       msg_stride_words, pks, sigs, i0, ns, status, kt, bcomb, vp);
+    const uint64_t nchunks = std::min<uint64_t>(ns, 256ull * 4 * 2 * 64);
+    hipLaunchKernelGGL(k_strict_keyed_inv, dim3(grid_for(nchunks, 256)), dim3(256), 0, stream,
+                       i0, ns, nchunks, status, vp);
+    hipLaunchKernelGGL(k_strict_keyed_list, dim3(grid_for(ns, 256)), dim3(256), 0, stream, i0,
+                       ns, vp.state, list, count);
+    // the leftovers: full verification (exact status codes), the tables over the planes
+    hipLaunchKernelGGL(k_verify_strict, dim3(std::min<uint64_t>(strict_grid(), grid_for(ns, 256))),
+                       dim3(256), 0, stream, msgs, msg_stride_words, pks, sigs, ns, status,
+                       bitmap, static_cast<ge_cached*>(workspace), kt, btw, bcomb, list, count);
+  }
+  if (bitmap)
+    hipLaunchKernelGGL(k_status_bitmap, dim3(grid_for(n, 256)), dim3(256), 0, stream, status, n,
+                       bitmap);
   return hipGetLastError();
 }
 

@@ -76,6 +76,27 @@ def test_headers_vs_oracle():
                for a, c in zip(st, cls))
 
 
+def test_headers_and_votes_keyed_fast_path_vs_full(monkeypatch):
+    """The keyed fast path of the strict launches (compressed-R check, exact verification
+    only for the leftovers; NW_STRICT_KEYED_FAST=0 turns it off): header and vote statuses,
+    with every header-level failure class mixed into an honest stream, equal the full
+    path's and the oracle's."""
+    from cert_cases import pack, unpack
+    from narwhal_amd import crypto as C
+    com, ms, _, _, cls = mutated_stream(N=4, copies=6, seed=41)
+    honest = W.certificate_stream(700, O.keys(4), lambda sk, m: C.sign_many(sk, m),
+                                  oracle_digest_many, seed=43, n_votes=4)
+    hrec, mrec = unpack(honest), unpack(ms)
+    p = pack(hrec[:350] + mrec + hrec[350:])
+    ost, oix = O.certificates_verify_many(com, p, headers_only=True)
+    vcom, vp, vn, vexp = votes_case(N=8, seed=44, count=900)
+    for fast in ("1", "0"):
+        monkeypatch.setenv("NW_STRICT_KEYED_FAST", fast)
+        st, ix = M.verify_headers_many(_Com(com), p)
+        assert st.tolist() == ost.tolist() and ix.tolist() == oix.tolist(), fast
+        assert M.verify_votes_many(_Com(vcom), vp).tolist() == vexp.tolist(), fast
+
+
 def test_votes_vs_oracle():
     com, p, n, exp = votes_case()
     st = M.verify_votes_many(_Com(com), p)
