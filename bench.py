@@ -1006,9 +1006,9 @@ def main():
     ap.add_argument("--service-max-certs", type=float, default=400_000,
                     help="certificates per offered-load run at most (runs shorter than "
                          "--service-seconds at high rates)")
-    ap.add_argument("--service-max-items", type=int, default=1 << 18)
+    ap.add_argument("--service-max-items", type=int, default=1 << 20)
     ap.add_argument("--service-inflight", type=int, default=4)
-    ap.add_argument("--service-producers", type=int, default=2)
+    ap.add_argument("--service-producers", type=int, default=4)
     ap.add_argument("--service-delay", type=float, default=0.0005,
                     help="VerificationService max_delay (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

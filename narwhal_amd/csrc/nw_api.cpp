@@ -498,7 +498,8 @@ struct DevPolicies {
 };
 DevPolicies g_policies[kMaxDevices];
 
-// The latest failure-rate report for this committee size, and where this call's goes.
+// The latest failure-rate report for this committee (key hash, or size), and where this
+// call's goes.
 double group_failure_rate(int dev, uint64_t nkeys, hipStream_t s, uint32_t** fb_dev,
                           uint32_t** cnt) {
   DevPolicies& d = g_policies[dev];
@@ -543,10 +544,19 @@ size_t cert_workspace_bytes(size_t n, size_t nvotes) {
 }
 
 // The whole device pipeline; every pointer is a device pointer.
+uint64_t committee_hash(const nw_committee* com) {
+  uint64_t h = 1469598103934665603ull;
+  for (size_t i = 0; i < 32 * com->nauth; ++i) h = (h ^ com->pks[i]) * 1099511628211ull;
+  return h ? h : 1;
+}
+
 int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
                   const uint64_t* host_vote_offsets, int headers_only, const void* z16,
                   const uint8_t zkey32[32], void* workspace, int32_t* status, uint64_t* index,
-                  hipStream_t s) {
+                  hipStream_t s, uint64_t committee_tag) {
+  // the failure-rate policy is kept per committee: keyed by the committee's key
+  // hash when the caller knows it, else by the committee size
+  const uint64_t policy_key = committee_tag ? committee_tag : (uint64_t)com.nauth;
   const uint64_t n = cs.n;
   if (n == 0) return 0;
   nw::z_key_t key;
@@ -614,12 +624,12 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
     bool small = false;
     if (keyed) {
       // the reported failure rate only sizes the fallback batches' chunks
-      p_cert = group_failure_rate(dev, com.nauth, s, &fb_dev, &fb_cnt);
+      p_cert = group_failure_rate(dev, policy_key, s, &fb_dev, &fb_cnt);
     } else {
       K = nw::cert_group_size(host_vote_offsets, n, com.nauth, z16 != nullptr, kGroupDefault);
       small = getenv("NW_CERT_SMALL_K") != nullptr;
       if (!z16 && !small && !nw::cert_group_env_fixed()) {
-        p_cert = group_failure_rate(dev, com.nauth, s, &fb_dev, &fb_cnt);
+        p_cert = group_failure_rate(dev, policy_key, s, &fb_dev, &fb_cnt);
         // merging does not apply, or most big groups would fail at the measured rate
         if (!K || 1.0 - std::pow(1.0 - p_cert, (double)K) > 0.25) small = true;
       }

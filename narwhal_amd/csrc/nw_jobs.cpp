@@ -399,6 +399,7 @@ int submit_certs(int dev, const nw_committee* com, const nw_certificates* cs, in
   rc = job_reserve(j, out_end, P.off);
   if (rc) return job_abort(j, rc);
   const nw_committee dcom = stage_committee(j, oc, com);
+  const uint64_t ctag = nw::rt::committee_hash(com);
   put(j, o_hb, cs->header_bytes + hb0, hlen);
   uint64_t* ho = reinterpret_cast<uint64_t*>(j->hbuf + o_ho);
   for (size_t i = 0; i <= n; ++i) ho[i] = cs->header_offsets[i] - hb0;
@@ -429,7 +430,7 @@ int submit_certs(int dev, const nw_committee* com, const nw_certificates* cs, in
     return nw::rt::cert_pipeline(dev, dcom, d, hvo, headers_only, z16 ? j->dbuf + o_z : nullptr,
                                  nullptr, j->dbuf + o_ws,
                                  reinterpret_cast<int32_t*>(j->dbuf + o_st),
-                                 reinterpret_cast<uint64_t*>(j->dbuf + o_ix), j->stream);
+                                 reinterpret_cast<uint64_t*>(j->dbuf + o_ix), j->stream, ctag);
   });
   if (rc) return job_abort(j, rc);
   job_out(j, status_out, o_st, 4 * n);

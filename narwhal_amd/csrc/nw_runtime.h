@@ -41,10 +41,14 @@ int check_certificates(const nw_certificates* cs, int headers_only, size_t* nvot
 // device pointers, host_vote_offsets the vote offsets in host memory (read during the call
 // only). Queues the whole check on `s` and returns without waiting.
 size_t cert_workspace_bytes(size_t n, size_t nvotes);
+// committee_tag: identifies the committee for the failure-rate policy (committee_hash of
+// the host keys; 0 = unknown, the policy is then kept per committee size).
 int cert_pipeline(int dev, const nw_committee& dcom, const nw_certificates& dcs,
                   const uint64_t* host_vote_offsets, int headers_only, const void* z16,
                   const uint8_t zkey32[32], void* workspace, int32_t* status, uint64_t* index,
-                  hipStream_t s);
+                  hipStream_t s, uint64_t committee_tag = 0);
+// FNV-1a over a host committee's keys (never 0).
+uint64_t committee_hash(const nw_committee* com);
 // Vote::verify for n votes (device pointers), scratch = votes_workspace_bytes(n).
 size_t votes_workspace_bytes(size_t n);
 int votes_pipeline(int dev, const nw_committee& dcom, size_t n, const uint8_t* ids,
