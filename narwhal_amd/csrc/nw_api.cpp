@@ -485,6 +485,14 @@ size_t cert_ws_layout(size_t n, size_t nvotes, char* base, CertWs* w) {
 // keyed checks) off: every certificate's own verify_batch.
 constexpr uint32_t kGroupDefault = 32768;
 
+// The default certificate vote policy: the keyed vote checks (see above).
+bool keyed_policy(size_t nauth) {
+  const char* ke = getenv("NW_CERT_KEYED");
+  const char* me = getenv("NW_CERT_MERGE");
+  return nauth > 0 && !(ke && atoi(ke) == 0) && !(me && me[0] == '0') &&
+         !getenv("NW_CERT_SMALL_K") && !nw::cert_group_env_fixed();
+}
+
 struct GroupPolicy {
   uint32_t* fb = nullptr;       // host-mapped: seq, groups, failed, tag, counted, bad
   uint32_t* fb_dev = nullptr;
@@ -553,7 +561,7 @@ uint64_t committee_hash(const nw_committee* com) {
 int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
                   const uint64_t* host_vote_offsets, int headers_only, const void* z16,
                   const uint8_t zkey32[32], void* workspace, int32_t* status, uint64_t* index,
-                  hipStream_t s, uint64_t committee_tag) {
+                  hipStream_t s, uint64_t committee_tag, const Fork* fork) {
   // the failure-rate policy is kept per committee: keyed by the committee's key
   // hash when the caller knows it, else by the committee size
   const uint64_t policy_key = committee_tag ? committee_tag : (uint64_t)com.nauth;
@@ -598,9 +606,32 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
                                  headers_only ? nullptr : w.vote_cert, s),
          "k_cert_prepare");
   const nw::key_tables_t hk{ktabs, kok, w.author_key};
+  // With a fork stream (host-buffer jobs) and the keyed vote checks, the headers run on the
+  // fork stream while the votes run here: the votes then do not skip header-failed
+  // certificates (k_cert_ok_headers settles those after the join), and the two latency
+  // chains of a small call (each a keyed check and one batched inversion) overlap.
+  const bool fork_ok = fork && fork->s2 && !headers_only && keyed_policy(com.nauth);
+  if (fork_ok) {
+    NW_HIP(hipEventRecord(fork->ev_fork, s), "hipEventRecord (fork)");
+    NW_HIP(hipStreamWaitEvent(fork->s2, fork->ev_fork, 0), "hipStreamWaitEvent (fork)");
+  }
   NW_HIP(nw::launch_verify_strict(reinterpret_cast<const uint32_t*>(cs.ids), 8, w.authors,
                                   reinterpret_cast<const uint32_t*>(cs.header_sigs), n, w.hdr_st,
-                                  w.bitmap, sws, s, &hk), "k_verify_strict (headers)");
+                                  w.bitmap, sws, fork_ok ? fork->s2 : s, &hk),
+         "k_verify_strict (headers)");
+  if (fork_ok) NW_HIP(hipEventRecord(fork->ev_join, fork->s2), "hipEventRecord (join)");
+  // every exit (errors included) joins the fork stream back before the lease is released
+  struct JoinGuard {
+    hipStream_t s = nullptr;
+    hipEvent_t e = nullptr;
+    ~JoinGuard() {
+      if (s) (void)hipStreamWaitEvent(s, e, 0);
+    }
+  } join_guard;
+  if (fork_ok) {
+    join_guard.s = s;
+    join_guard.e = fork->ev_join;
+  }
   if (!headers_only) {
     const nw::key_tables_t kt{ktabs, kok, w.vote_key};
     // Default: the keyed vote checks (launch_votes_keyed): every vote of an undecided
@@ -613,10 +644,7 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
     // NW_CERT_KEYED=0 selects the merged-group policy instead (big Pippenger groups / small
     // keyed Straus groups, adaptive on the failure rate the previous calls reported),
     // NW_CERT_MERGE=0 every certificate's own verify_batch.
-    const char* ke = getenv("NW_CERT_KEYED");
-    const char* me = getenv("NW_CERT_MERGE");
-    const bool keyed = com.nauth > 0 && !(ke && atoi(ke) == 0) && !(me && me[0] == '0') &&
-                       !getenv("NW_CERT_SMALL_K") && !nw::cert_group_env_fixed();
+    const bool keyed = keyed_policy(com.nauth);
     uint32_t* fb_dev = nullptr;
     uint32_t* fb_cnt = nullptr;
     double p_cert = 0.0;
@@ -649,10 +677,15 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
       NW_HIP(nw::launch_votes_keyed(w.cert_digest, cs.vote_offsets, n, w.vote_cert,
                                     reinterpret_cast<const uint32_t*>(cs.vote_pks),
                                     reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
-                                    w.pre1, w.pre2, w.hdr_st, kt, (uint32_t)com.nauth,
-                                    group_ok, w.batch_ws,
+                                    w.pre1, w.pre2, fork_ok ? nullptr : w.hdr_st, kt,
+                                    (uint32_t)com.nauth, group_ok, w.batch_ws,
                                     w.batch_ws_bytes, s),
              "keyed vote checks");
+      if (fork_ok) {
+        join_guard.s = nullptr;   // joined here
+        NW_HIP(hipStreamWaitEvent(s, fork->ev_join, 0), "hipStreamWaitEvent (join)");
+        NW_HIP(nw::launch_cert_ok_headers(w.hdr_st, n, group_ok, s), "k_cert_ok_headers");
+      }
     } else if (K && !small)
       NW_HIP(nw::launch_cert_groups(w.cert_digest, cs.vote_offsets, host_vote_offsets, n,
                                     reinterpret_cast<const uint32_t*>(cs.vote_pks),

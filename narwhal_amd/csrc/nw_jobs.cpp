@@ -50,6 +50,7 @@ struct nw_job {
   int nouts = 0;
   bool pending = false;   // device work queued, outputs not yet delivered
   std::vector<nw_job*> parts;   // fan-out parent (dev = -1): one ordinary job per part
+  nw::rt::Fork fork{nullptr, nullptr, nullptr};   // certificate jobs: header checks' stream
 };
 
 namespace {
@@ -426,11 +427,24 @@ int submit_certs(int dev, const nw_committee* com, const nw_certificates* cs, in
     d.nvotes = nv;
     hvo = reinterpret_cast<const uint64_t*>(j->hbuf + o_vo);   // read while planning only
   }
+  if (!headers_only && !j->fork.s2) {   // created once per pooled job
+    hipStream_t s2 = nullptr;
+    hipEvent_t e1 = nullptr, e2 = nullptr;
+    if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) == hipSuccess &&
+        hipEventCreateWithFlags(&e1, hipEventDisableTiming) == hipSuccess &&
+        hipEventCreateWithFlags(&e2, hipEventDisableTiming) == hipSuccess) {
+      j->fork = nw::rt::Fork{s2, e1, e2};
+    } else {   // no fork: the sequential pipeline
+      if (e1) (void)hipEventDestroy(e1);
+      if (s2) (void)hipStreamDestroy(s2);
+    }
+  }
   rc = job_run(j, o_st, o_st, out_end - o_st, [&]() -> int {
     return nw::rt::cert_pipeline(dev, dcom, d, hvo, headers_only, z16 ? j->dbuf + o_z : nullptr,
                                  nullptr, j->dbuf + o_ws,
                                  reinterpret_cast<int32_t*>(j->dbuf + o_st),
-                                 reinterpret_cast<uint64_t*>(j->dbuf + o_ix), j->stream, ctag);
+                                 reinterpret_cast<uint64_t*>(j->dbuf + o_ix), j->stream, ctag,
+                                 j->fork.s2 ? &j->fork : nullptr);
   });
   if (rc) return job_abort(j, rc);
   job_out(j, status_out, o_st, 4 * n);

@@ -139,6 +139,10 @@ hipError_t launch_cert_sgroups(const uint32_t* cert_digest, const uint64_t* cvo,
 // cert_ok: ncert words; scratch: >= votes_keyed_fixed_bytes() + 64 x
 // votes_keyed_bytes_per_vote() bytes (slices of the votes go through it, each checked in
 // key-major order). keys.vote_key required; nkeys = committee size.
+// hdr_st may be NULL (votes checked concurrently with the headers); then follow the join
+// with launch_cert_ok_headers so header-failed certificates skip their verify_batch.
+hipError_t launch_cert_ok_headers(const int32_t* hdr_st, uint64_t ncert, uint32_t* cert_ok,
+                                  hipStream_t stream);
 size_t votes_keyed_bytes_per_vote();
 size_t votes_keyed_fixed_bytes();
 hipError_t launch_votes_keyed(const uint32_t* cert_digest, const uint64_t* cvo, uint64_t ncert,

@@ -261,7 +261,10 @@ struct vote_planes_t {
 #ifndef NW_STRICT_PF
 #define NW_STRICT_PF 1
 #endif
-#if NW_STRICT_PF && NW_BWIN != 8
+#ifndef NW_KEYED_PF
+#define NW_KEYED_PF 0   // 1: the keyed comb checks through the same LDS slots (measured slower)
+#endif
+#if (NW_STRICT_PF && NW_BWIN != 8) || NW_KEYED_PF
 __shared__ uint4 s_pf[10][256];
 struct pf_lds {
   static constexpr bool enabled = true;
@@ -386,7 +389,11 @@ __global__ __launch_bounds__(256, NW_KEYED_WAVES) void k_strict_keyed(
                                 msgs + (uint64_t)msg_stride_words * gi};
     fe X, Z;
     st = keyed_vote_check(src, g_consts.sk, bcomb_wide{bcomb},
-                          keytab_wide{keys.tabs + kKeyTab * (uint64_t)kk}, keys.ok[kk], X, Z);
+                          keytab_wide{keys.tabs + kKeyTab * (uint64_t)kk}, keys.ok[kk], X, Z
+#if NW_KEYED_PF
+                          , pf_lds{(uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)}
+#endif
+    );
     if (st >= kVotePending) {
 #pragma unroll
       for (int k = 0; k < 10; ++k) {
@@ -507,7 +514,7 @@ __device__ __forceinline__ uint32_t vk_bin(const uint32_t* __restrict__ vote_cer
                                            const int32_t* __restrict__ pre2,
                                            const int32_t* __restrict__ hdr_st, uint32_t nkeys) {
   const uint32_t c = vote_cert[v];
-  if (pre1[c] != 0 || hdr_st[c] != 0 || pre2[c] != 0) return nkeys;
+  if (pre1[c] != 0 || (hdr_st && hdr_st[c] != 0) || pre2[c] != 0) return nkeys;
   const uint32_t k = vote_key[v];
   return k < nkeys ? k : nkeys;
 }
@@ -580,7 +587,7 @@ __global__ __launch_bounds__(256, NW_KEYED_WAVES) void k_votes_keyed(
   const uint64_t v = v0 + (vp.perm ? vp.perm[i] : i);
   const uint32_t c = vote_cert[v];
   uint32_t st = kVotePass;
-  if (pre1[c] == 0 && hdr_st[c] == 0 && pre2[c] == 0) {
+  if (pre1[c] == 0 && (!hdr_st || hdr_st[c] == 0) && pre2[c] == 0) {
     const uint32_t kk = keys.vote_key[v];
     if (kk == kNoKey) {   // not a committee key (cannot happen for an undecided certificate)
       st = kVoteFail;
@@ -588,7 +595,11 @@ __global__ __launch_bounds__(256, NW_KEYED_WAVES) void k_votes_keyed(
       const strict_src_global src{pks + 8 * v, sigs + 16 * v, cert_digest + 8 * (uint64_t)c};
       fe X, Z;
       st = keyed_vote_check(src, g_consts.sk, bcomb_wide{bcomb},
-                            keytab_wide{keys.tabs + kKeyTab * (uint64_t)kk}, keys.ok[kk], X, Z);
+                            keytab_wide{keys.tabs + kKeyTab * (uint64_t)kk}, keys.ok[kk], X, Z
+#if NW_KEYED_PF
+                            , pf_lds{(uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)}
+#endif
+      );
       if (st >= kVotePending) {
 #pragma unroll
         for (int k = 0; k < 10; ++k) {
@@ -600,6 +611,16 @@ __global__ __launch_bounds__(256, NW_KEYED_WAVES) void k_votes_keyed(
     if (st == kVoteFail) cert_ok[c] = 0;   // same value from every failing lane
   }
   vp.state[i] = st;
+}
+
+// After votes were checked concurrently with the headers (hdr_st not yet known to them):
+// a certificate whose header failed is decided by its header, so it skips its own
+// verify_batch (cert_ok = 1 is the skip flag there).
+__global__ __launch_bounds__(256) void k_cert_ok_headers(const int32_t* __restrict__ hdr_st,
+                                                         uint64_t ncert,
+                                                         uint32_t* __restrict__ cert_ok) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < ncert && hdr_st[c] != 0) cert_ok[c] = 1u;
 }
 
 // One lane per chunk {i = j * nchunks + lane}: Montgomery's trick over the chunk's pending
@@ -1006,6 +1027,14 @@ hipError_t launch_votes_keyed(const uint32_t* cert_digest, const uint64_t* cvo, 
     hipLaunchKernelGGL(k_votes_keyed_inv, dim3(grid_for(nchunks, 256)), dim3(256), 0, stream,
                        vote_cert, v0, nv, nchunks, cert_ok, vp);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_cert_ok_headers(const int32_t* hdr_st, uint64_t ncert, uint32_t* cert_ok,
+                                  hipStream_t stream) {
+  if (ncert == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_cert_ok_headers, dim3(grid_for(ncert, 256)), dim3(256), 0, stream, hdr_st,
+                     ncert, cert_ok);
   return hipGetLastError();
 }
 

@@ -43,10 +43,16 @@ int check_certificates(const nw_certificates* cs, int headers_only, size_t* nvot
 size_t cert_workspace_bytes(size_t n, size_t nvotes);
 // committee_tag: identifies the committee for the failure-rate policy (committee_hash of
 // the host keys; 0 = unknown, the policy is then kept per committee size).
+// fork (optional): a second stream and two events of the caller's; the header checks then
+// run on fork->s2 concurrently with the vote checks on s (joined before the call returns).
+struct Fork {
+  hipStream_t s2;
+  hipEvent_t ev_fork, ev_join;
+};
 int cert_pipeline(int dev, const nw_committee& dcom, const nw_certificates& dcs,
                   const uint64_t* host_vote_offsets, int headers_only, const void* z16,
                   const uint8_t zkey32[32], void* workspace, int32_t* status, uint64_t* index,
-                  hipStream_t s, uint64_t committee_tag = 0);
+                  hipStream_t s, uint64_t committee_tag = 0, const Fork* fork = nullptr);
 // FNV-1a over a host committee's keys (never 0).
 uint64_t committee_hash(const nw_committee* com);
 // Vote::verify for n votes (device pointers), scratch = votes_workspace_bytes(n).

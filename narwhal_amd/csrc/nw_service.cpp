@@ -21,6 +21,8 @@
 // max_inflight jobs are queued on the device at once (backpressure on the flusher; requests
 // keep accumulating into the next, larger batch meanwhile, which is what keeps the device
 // efficient under load).
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <chrono>
@@ -133,6 +135,9 @@ struct nw_service {
   std::deque<std::unique_ptr<Batch>> inflight;
   bool force = false, stop = false, flusher_done = false;
   uint64_t accepted = 0, completed = 0, jobs = 0;
+  // NW_SERVICE_DEBUG: seconds the flusher spent submitting / blocked on max_inflight, the
+  // completer waiting for jobs / running callbacks (printed at destroy)
+  double t_submit = 0, t_backpressure = 0, t_wait = 0, t_callbacks = 0;
   size_t open_jobs = 0;   // submitted, callbacks not yet delivered
   std::thread flusher, completer;
 
@@ -234,7 +239,9 @@ struct nw_service {
       }
       // backpressure: at most max_inflight jobs queued; the open batch keeps growing
       if (inflight.size() >= max_inflight) {
+        const Clock::time_point w0 = Clock::now();
         cv_space.wait(lk);
+        t_backpressure += std::chrono::duration<double>(Clock::now() - w0).count();
         continue;
       }
       std::unique_ptr<Batch> fresh = take_spare(static_cast<Kind>(pick));
@@ -245,8 +252,11 @@ struct nw_service {
       std::unique_ptr<Batch> b = std::move(open[pick]);
       open[pick] = std::move(fresh);
       lk.unlock();
+      const Clock::time_point s0 = Clock::now();
       b->rc = submit(*b);
+      const double ds = std::chrono::duration<double>(Clock::now() - s0).count();
       lk.lock();
+      t_submit += ds;
       ++jobs;
       ++open_jobs;
       inflight.push_back(std::move(b));
@@ -267,15 +277,20 @@ struct nw_service {
       cv_space.notify_one();
       lk.unlock();
       int rc = b->rc;
+      const Clock::time_point w0 = Clock::now();
       if (b->job) {
         if (!rc) rc = nw_job_wait(b->job);
         nw_job_release(b->job);
         b->job = nullptr;
       }
+      const Clock::time_point c0 = Clock::now();
       const size_t n = b->reqs.size();
       for (size_t i = 0; i < n; ++i)
         b->reqs[i].fn(b->reqs[i].arg, rc ? rc : b->status[i], rc ? 0 : b->index[i]);
+      const Clock::time_point c1 = Clock::now();
       lk.lock();
+      t_wait += std::chrono::duration<double>(c0 - w0).count();
+      t_callbacks += std::chrono::duration<double>(c1 - c0).count();
       completed += n;
       if (--open_jobs == 0) cv_flush.notify_one();   // device idle: flush what has queued
       b->clear();
@@ -467,6 +482,12 @@ void nw_service_destroy(nw_service* s) {
   s->cv_space.notify_all();
   s->flusher.join();
   s->completer.join();
+  if (getenv("NW_SERVICE_DEBUG"))
+    fprintf(stderr,
+            "[narwhal_amd] service: %llu requests, %llu jobs; flusher submit %.3f s, "
+            "backpressure %.3f s; completer wait %.3f s, callbacks %.3f s\n",
+            (unsigned long long)s->accepted, (unsigned long long)s->jobs, s->t_submit,
+            s->t_backpressure, s->t_wait, s->t_callbacks);
   delete s;
 }
 

@@ -257,6 +257,9 @@ constexpr uint32_t kStrictKeyMask = kStrictKeyW == 16 ? 0x80008000u : 0x80808080
 static_assert(kStrictKeyW == 8 || kStrictKeyW == 16, "NW_KEYW must be 8 or 16");
 struct bcomb_wide {
   const ge_niels_pad* t;
+  NW_HD const ge_niels_pad* entry(int m, int ad) const {
+    return t + (uint32_t)m * kBCombN + (uint32_t)ad;
+  }
   NW_HD void operator()(int m, int ad, ge_cached& e) const {
     const ge_niels& nb = t[(uint32_t)m * kBCombN + (uint32_t)ad].n;
     fe_copy(e.YpX, nb.ypx);
@@ -284,11 +287,27 @@ struct bcomb_lazy {
   }
 };
 
+// Table-entry prefetch for the strict ladder. pf_none: each addition reads its entry from
+// its table when it runs (host self-check; NW_STRICT_PF=0). The device's LDS prefetcher
+// (nw_kernels.hip pf_lds) loads the NEXT addition's entry straight into LDS
+// (global_load_lds_dwordx4, no registers) while the current addition or the window's four
+// doublings run, so the ladder's ~77 dependent table loads per verification stop stalling
+// the wave. issue(src, chunks): 16-byte chunks at src (10 = ge_cached, 8 = ge_niels_pad);
+// get(e, niels): wait for it and read it (niels: Y+x, Y-x, xy2d into YpX, YmX, T2d).
+struct pf_none {
+  static constexpr bool enabled = false;
+  NW_HD void issue(const void*, int) const {}
+  NW_HD void get(ge_cached&, bool) const {}
+};
+
 // A committee key's comb tables: keytab_wide reads the device copy (keytab[kStrictKeyN t + j]
 // = j * 2^(W t) A, affine niels, built by k_key_tabs); keytab_lazy computes an entry per
 // lookup from A (host self-check: the full 16-bit tables are 67 MB per key).
 struct keytab_wide {
   const ge_niels_pad* t;
+  NW_HD const ge_niels_pad* entry(int tab, int j) const {
+    return t + (uint32_t)tab * kStrictKeyN + (uint32_t)j;
+  }
   NW_HD void operator()(int tab, int j, ge_niels& e) const {
     e = t[(uint32_t)tab * kStrictKeyN + (uint32_t)j].n;
   }
@@ -324,13 +343,49 @@ NW_HD int comb_digit(const uint32_t rd[8], int t) {
   constexpr uint32_t m = (W == 32) ? 0xffffffffu : ((1u << W) - 1u);
   return (int)((sel8(rd, t / per) >> ((t % per) * W)) & m) - (1 << (W - 1));
 }
-template <class BComb, class KeyTab>
+template <class BComb, class KeyTab, class PF = pf_none>
 NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
-                          const KeyTab& kt, const fe& d2) {
+                          const KeyTab& kt, const fe& d2, const PF& pf = PF{}) {
   uint32_t kd[8], sd[8];
   sc_recode(kd, k, kStrictKeyMask);   // k < l: 256 / W signed W-bit digits
   bdigits<kBCombW>::recode(sd, s);    // s < l: kBCombT digits of kBCombW bits
   ge_identity(acc);
+  if constexpr (PF::enabled) {
+    // the same additions in the same order, each entry requested one addition ahead
+    // (pf_lds: global_load_lds into a per-lane LDS slot while the current addition runs)
+    constexpr int KT = kStrictKeyTables, NS = kStrictKeyTables + kBCombT;
+    auto step_src = [&](int st, int& d) -> const void* {
+      if (st < KT) {
+        d = comb_digit<kStrictKeyW>(kd, st);
+        return d ? static_cast<const void*>(kt.entry(st, d < 0 ? -d : d)) : nullptr;
+      }
+      d = bdigits<kBCombW>::digit(sd, st - KT);
+      return d ? static_cast<const void*>(bc.entry(st - KT, d < 0 ? -d : d)) : nullptr;
+    };
+    {
+      int d0;
+      const void* s0 = step_src(0, d0);
+      if (s0) pf.issue(s0, 8);
+    }
+#pragma unroll 1
+    for (int st = 0; st < NS; ++st) {
+      int d;
+      const void* cur = step_src(st, d);
+      ge_cached e;
+      if (cur) pf.get(e, true);
+      if (st + 1 < NS) {
+        int dn;
+        const void* nx = step_src(st + 1, dn);
+        if (nx) pf.issue(nx, 8);
+      }
+      if (cur) {
+        ge_cached_cneg(e, st < KT ? d > 0 : d < 0);   // -[k]A: key digits negated
+        ge_add_any(acc, acc, e, true, true);
+      }
+    }
+    (void)d2;
+    return;
+  }
 #if NW_KEYED_SPLIT
   // two independent chains, one step of each per iteration: -[k]A in acc, [s]B in accB,
   // joined by one cached addition (T3 not needed by the callers' comparisons)
@@ -398,9 +453,10 @@ NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
 // X'/Z' equals the sign bit. Returns kVotePass / kVoteFail, or kVotePending (| sign) when
 // only that parity is left: the caller batches the inversions of Z' (k_votes_keyed_inv).
 constexpr uint32_t kVotePass = 0, kVoteFail = 1, kVotePending = 2;
-template <class BComb, class KeyTab, class Src>
+template <class BComb, class KeyTab, class Src, class PF = pf_none>
 NW_HD uint32_t keyed_vote_check(const Src& src, const strict_consts& K, const BComb& bc,
-                                const KeyTab& keytab, uint32_t keyflags, fe& X, fe& Z) {
+                                const KeyTab& keytab, uint32_t keyflags, fe& X, fe& Z,
+                                const PF& pf = PF{}) {
   const bool okA = (keyflags & 1) != 0, smallA = (keyflags & 2) != 0;
   uint32_t Sw[8];
   src.S(Sw);
@@ -420,7 +476,7 @@ NW_HD uint32_t keyed_vote_check(const Src& src, const strict_consts& K, const BC
 #pragma unroll
   for (int j = 0; j < 8; ++j) k.w[j] = kw[j];
   ge acc;
-  keyed_comb_sum(acc, k, s, bc, keytab, K.k.d2);
+  keyed_comb_sum(acc, k, s, bc, keytab, K.k.d2, pf);
   fe t;
   fe_mul(t, yR, acc.Z);
   if (!fe_eq(t, acc.Y)) return kVoteFail;
@@ -473,18 +529,6 @@ NW_HD int strict_keyed_comb(const Src& src, const strict_consts& K, const BComb&
   return ge_eq_affine(acc, R) ? NW_OK : NW_ERR_EQUATION;
 }
 
-// Table-entry prefetch for the strict ladder. pf_none: each addition reads its entry from
-// its table when it runs (host self-check; NW_STRICT_PF=0). The device's LDS prefetcher
-// (nw_kernels.hip pf_lds) loads the NEXT addition's entry straight into LDS
-// (global_load_lds_dwordx4, no registers) while the current addition or the window's four
-// doublings run, so the ladder's ~77 dependent table loads per verification stop stalling
-// the wave. issue(src, chunks): 16-byte chunks at src (10 = ge_cached, 8 = ge_niels_pad);
-// get(e, niels): wait for it and read it (niels: Y+x, Y-x, xy2d into YpX, YmX, T2d).
-struct pf_none {
-  static constexpr bool enabled = false;
-  NW_HD void issue(const void*, int) const {}
-  NW_HD void get(ge_cached&, bool) const {}
-};
 
 // Status of one strict verification. wave_max maps this lane's ladder length (in 4-bit
 // windows) to the wave's maximum (identity on the host). tabA/tabR: 8 entries each of

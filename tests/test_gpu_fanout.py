@@ -132,3 +132,30 @@ def test_fanout_rejects_device_pointer_calls():
         assert rc == -1 and b"one device" in L.nw_last_error()
     finally:
         assert L.nw_set_device(0) == 0
+
+
+def test_native_service_fans_out(fanout):
+    """A native aggregation service created under nw_set_device(NW_ALL_DEVICES) submits its
+    jobs fanned out (its threads take the creating thread's device choice): single
+    certificates from two threads, verdicts equal the oracle's."""
+    from narwhal_amd import service as S
+    from cert_cases import oracle_digest_many, oracle_sign_many
+    hon = W.certificate_stream(900, O.keys(10), oracle_sign_many, oracle_digest_many, seed=97)
+    m, est, eix = W.mutate_votes(hon, np.arange(3, 900, 50), seed=7)
+    from cert_cases import unpack
+    rows = [S.CertRow(r["hb"], r["np"], r["id"], r["sig"], b"".join(pk for pk, _ in r["votes"]),
+                      b"".join(sg for _, sg in r["votes"]), len(r["votes"])) for r in unpack(m)]
+    svc = S.NativeService(m["committee"], max_items=2000, max_delay=0.0005)
+    got = [None] * len(rows)
+
+    def worker(t):
+        for i in range(t, len(rows), 2):
+            svc.submit_certificate(rows[i], lambda st, ix, i=i: got.__setitem__(i, (st, ix)))
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    svc.drain()
+    svc.close()
+    assert got == [(int(a), int(b)) for a, b in zip(est, eix)]

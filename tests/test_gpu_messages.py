@@ -52,7 +52,7 @@ def test_appendix_b_fixture_through_mirror():
         bad.verify(committee)
 
 
-@pytest.mark.parametrize("N,copies", [(4, 3), (10, 2), (100, 1)])
+@pytest.mark.parametrize("N,copies", [(4, 3), (10, 2), (50, 1), (100, 1)])
 def test_certificates_vs_oracle(N, copies):
     com, s, exp_st, exp_ix, cls = mutated_stream(N=N, copies=copies, seed=N)
     z16 = np.random.Generator(np.random.PCG64(N)).integers(0, 256, size=(len(s["vote_pks"]), 16),
