@@ -267,6 +267,20 @@ def test_verify_wire_vs_oracle():
     assert not bad, bad
 
 
+@pytest.mark.gpu
+def test_verify_wire_multithreaded_decode():
+    """> 4096 frames per call: the decode splits over threads and merges the parts in place
+    (nw_wire.cpp decode_all). Tiling the small corpus must tile its statuses exactly."""
+    com, frames = _corpus(N=4, copies=2)
+    kind0, st0, _ = WI.verify_primary_messages(com, frames)
+    reps = -(-9000 // len(frames))
+    tiled = list(frames) * reps
+    for _ in range(2):   # second call reuses the per-thread buffers
+        kind, st, _ = WI.verify_primary_messages(com, tiled)
+        assert kind.tolist() == np.tile(kind0, reps).tolist()
+        assert st.tolist() == np.tile(st0, reps).tolist()
+
+
 def test_frames_from_stream_round_trip():
     """The bench's frame builder (wire.frames_from_stream) against the restatement."""
     from narwhal_amd import workloads as W

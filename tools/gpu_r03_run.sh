@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box helper (round 3): the -m gpu suite, then the bench legs named in LEGS
-# (cert, service, strict, batch, full), each step under its own time limit, stopping at the
+# (cert, service, strict, batch, wire, full), each step under its own time limit, stopping at the
 # first failure.   LEGS="cert service" bash tools/gpu_r03_run.sh OUTDIR
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -18,6 +18,7 @@ for L in $LEGS; do
     service) A="--workload service --no-cpu-baseline" ;;
     strict) A="--workload strict --no-sha --no-cert --no-batch --no-wire --no-service --no-cpu-baseline" ;;
     batch) A="--workload batch --no-cpu-baseline" ;;
+    wire) A="--workload strict --no-sha --no-cert --no-batch --no-service --no-cpu-baseline" ;;
     *) echo "unknown leg $L"; exit 2 ;;
   esac
   timeout -k 10 500 python -u bench.py $A > "$OUT/bench_$L.json" 2> "$OUT/bench_$L.log"
