@@ -1262,6 +1262,150 @@ __global__ __launch_bounds__(64) void k_pip_windows(const uint32_t* __restrict__
   }
 }
 
+// Latency form of k_pip_windows for few batches (npip <= kPipWinLpMax; config 1's one-call
+// path): sum_d d S_{d-1} = sum_j 2^j T_j with T_j = sum of the buckets whose digit has bit j,
+// every point operation limb-parallel (nw_lp.hpp), one wave per (window, part) on its own
+// SIMD. k_pip_windows_lp, grid (kPipWin + 1, kPipWinLpParts, npip), 64 threads; part
+// q = 2 j + h sums half h (entries 32 h .. 32 h + 31) of list j:
+//   j < 8: T_j (windows 0..30: digits 1..128, 64 buckets for j < 7 and bucket 127 for
+//     j = 7; window 31: digits 1..17 with their kPipTopSub sub-bins, j < 5);
+//   j = 8: the z-carry sub-bins of window 16 (weight 1);
+// and stores it (cached, lp layout) over the batch's point and entry arrays (contiguous,
+// dead after k_pip_buckets).
+// k_pip_wsum, grid (kPipWin, npip), one wave: the 7-doubling Horner over the parts.
+// A wave's chain is <= 32 additions of ~0.4 us instead of the one-wave form's 15
+// single-lane operations of ~5 us; in total instructions it is ~13x the one-wave form,
+// hence only for few batches. Block kPipWin: [-sum b_i]B as in k_pip_windows (part 0).
+constexpr uint32_t kPipWinLpMax = 8;
+constexpr int kPipWinLpParts = 18;
+uint32_t pip_win_lp_max() {   // NW_PIP_WIN_LP_MAX=0: always the one-wave form
+  static const uint32_t v = (uint32_t)env_u64("NW_PIP_WIN_LP_MAX", kPipWinLpMax);
+  return v;
+}
+// the parts live in the dead point + entry arrays (contiguous in pip_at)
+static_assert(2 * kPipFloor * sizeof(ge_niels) + 4 * kPipWinCap * kPipFloor >=
+                  4 * kPipWin * kPipWinLpParts * 64,
+              "window parts do not fit the point array");
+
+__device__ __forceinline__ uint32_t pip_lp_bucket(int w, int j, uint32_t i) {
+  // i-th bucket of list j of window w, or ~0u
+  if (j == 8) return (w == kPipZWin - 1 && i < (uint32_t)kPipCarryBins) ? kPipWin * 128 + i : ~0u;
+  if (w != kPipWin - 1) {
+    if (j == 7) return i == 0 ? (uint32_t)w * 128 + 127 : ~0u;
+    if (i >= 64) return ~0u;
+    const uint32_t d = ((i >> j) << (j + 1)) | (1u << j) | (i & ((1u << j) - 1));
+    return (uint32_t)w * 128 + d - 1;
+  }
+  // top window: digits d in 1..17 with bit j, each over kPipTopSub sub-bins
+  const uint32_t dd = i / kPipTopSub, k = i % kPipTopSub;
+  uint32_t seen = 0;
+  for (uint32_t d = 1; d <= (uint32_t)kPipTopStride; ++d) {
+    if (!((d >> j) & 1)) continue;
+    if (seen++ == dd) return (uint32_t)w * 128 + kPipTopStride * k + d - 1;
+  }
+  return ~0u;
+}
+
+// Extended point in lp layout (row r = coordinate r of X, Y, Z, T), identity for ~0u;
+// branch-free, so the prefetched loads stay in flight across the additions.
+__device__ __forceinline__ uint32_t pip_lp_load(const lp_ctx& L, const ge* S, uint32_t b) {
+  const uint32_t x = reinterpret_cast<const uint32_t*>(S + (b == ~0u ? 0u : b))
+      [10 * L.row + (L.k < 10 ? L.k : 9u)];
+  return b == ~0u ? lp_identity(L) : L.k < 10 ? x : 0u;
+}
+
+__global__ __launch_bounds__(64) void k_pip_windows_lp(const uint32_t* __restrict__ pip_list,
+                                                       const uint64_t* __restrict__ offsets,
+                                                       uint64_t b0, uint64_t i0, uint32_t extra,
+                                                       uint32_t pmin,
+                                                       ge_cached* __restrict__ tabs) {
+  const uint64_t bidx = b0 + pip_list[blockIdx.z];
+  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
+  if (n < pmin) return;
+  const pip_region reg = pip_at(tabs, bs - i0, n + extra);
+  const int w = blockIdx.x, q = blockIdx.y, lane = (int)threadIdx.x;
+  const lp_ctx L = lp_init((uint32_t)lane);
+  const fe& d2 = g_bc.k.d2;
+  const uint32_t d2l = L.k < 10 ? d2.v[L.k] : 0u;
+  if (w == kPipWin) {
+    if (q != 0) return;
+    uint32_t bb[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) bb[m] = reg.bb[m];
+    uint32_t v = lp_identity(L);
+#pragma unroll 1
+    for (int m = 0; m < kPipWin; ++m) {
+      const int e = digit8(bb, m);
+      v = lp_add(L, v, lp_niels_component(L, g_comb[129 * m + (e < 0 ? -e : e)], e < 0));
+    }
+    const uint32_t c = lp_to_cached(L, v, d2l);
+    if (L.k < 10) reinterpret_cast<uint32_t*>(reg.Bc)[10 * (L.row ^ 1u) + L.k] = c;
+    return;
+  }
+  // this part's bucket list, lane i < 32 holding entry i (additions in whole groups of 8,
+  // identities past the end)
+  const int j = q >> 1;
+  const uint32_t mine = lane < 32 ? pip_lp_bucket(w, j, 32u * (uint32_t)(q & 1) + lane) : ~0u;
+  const uint32_t cnt = (uint32_t)__builtin_popcountll(__ballot(mine != ~0u));
+  uint32_t v = lp_identity(L);
+  if (cnt) {
+    uint32_t buf[8];   // point i + 8 is loaded while point i is added
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      buf[u] = pip_lp_load(L, reg.S, (uint32_t)__builtin_amdgcn_readlane((int)mine, u));
+#pragma unroll 1
+    for (uint32_t i = 0; i < cnt; i += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t x = buf[u];
+        const uint32_t nx = i + 8 + u;
+        buf[u] = pip_lp_load(
+            L, reg.S, nx < 32 ? (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)nx) : ~0u);
+        v = lp_add(L, v, lp_to_cached(L, x, d2l));
+      }
+    }
+  }
+  reinterpret_cast<uint32_t*>(reg.pts)[(w * kPipWinLpParts + q) * 64 + lane] =
+      lp_to_cached(L, v, d2l);
+}
+
+__global__ __launch_bounds__(64) void k_pip_wsum(const uint32_t* __restrict__ pip_list,
+                                                 const uint64_t* __restrict__ offsets,
+                                                 uint64_t b0, uint64_t i0, uint32_t extra,
+                                                 uint32_t pmin, ge_cached* __restrict__ tabs) {
+  const uint64_t bidx = b0 + pip_list[blockIdx.y];
+  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
+  if (n < pmin) return;
+  const pip_region reg = pip_at(tabs, bs - i0, n + extra);
+  const int w = blockIdx.x, lane = (int)threadIdx.x;
+  const lp_ctx L = lp_init((uint32_t)lane);
+  const uint32_t* part = reinterpret_cast<const uint32_t*>(reg.pts) +
+                         (size_t)w * kPipWinLpParts * 64 + lane;
+  uint32_t t[kPipWinLpParts];
+#pragma unroll
+  for (int q = 0; q < kPipWinLpParts; ++q) t[q] = part[64 * q];
+  uint32_t r = lp_add(L, lp_identity(L), t[14]);
+  r = lp_add(L, r, t[15]);
+#pragma unroll 1
+  for (int j = 6; j >= 0; --j) {
+    r = lp_dbl(L, r);
+    // 2 j and 2 j + 1 by a runtime index would put t in scratch: select instead
+    uint32_t a = t[0], b = t[1];
+#pragma unroll
+    for (int k = 1; k < 7; ++k)
+      if (j == k) a = t[2 * k], b = t[2 * k + 1];
+    r = lp_add(L, r, a);
+    r = lp_add(L, r, b);
+  }
+  if (w == kPipZWin - 1) {
+    r = lp_add(L, r, t[16]);
+    r = lp_add(L, r, t[17]);
+  }
+  const fe& d2 = g_bc.k.d2;
+  const uint32_t c = lp_to_cached(L, r, L.k < 10 ? d2.v[L.k] : 0u);
+  if (L.k < 10) reinterpret_cast<uint32_t*>(reg.W + w)[10 * (L.row ^ 1u) + L.k] = c;
+}
+
 __global__ __launch_bounds__(64) void k_pip_final(const uint32_t* __restrict__ pip_list,
                                                   const uint64_t* __restrict__ offsets,
                                                   uint64_t b0, uint64_t i0,
@@ -1535,8 +1679,14 @@ void launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t b, ui
   const dim3 gb = xcd ? dim3((unsigned)(8 * bpb * ((npip + 7) / 8))) : dim3(bpb, (unsigned)npip);
   hipLaunchKernelGGL(k_pip_buckets, gb, dim3(256), 0, stream, w.pip_list, offsets, b, i0, lg,
                      (uint32_t)npip, bpb, xcd, extra, pmin, w.tabs);
-  hipLaunchKernelGGL(k_pip_windows, dim3(kPipWin + 1, (unsigned)npip), dim3(64), 0, stream,
-                     w.pip_list, offsets, b, i0, extra, pmin, w.tabs);
+  if (npip <= pip_win_lp_max()) {
+    hipLaunchKernelGGL(k_pip_windows_lp, dim3(kPipWin + 1, kPipWinLpParts, (unsigned)npip),
+                       dim3(64), 0, stream, w.pip_list, offsets, b, i0, extra, pmin, w.tabs);
+    hipLaunchKernelGGL(k_pip_wsum, dim3(kPipWin, (unsigned)npip), dim3(64), 0, stream,
+                       w.pip_list, offsets, b, i0, extra, pmin, w.tabs);
+  } else
+    hipLaunchKernelGGL(k_pip_windows, dim3(kPipWin + 1, (unsigned)npip), dim3(64), 0, stream,
+                       w.pip_list, offsets, b, i0, extra, pmin, w.tabs);
   hipLaunchKernelGGL(k_pip_final, dim3((unsigned)npip), dim3(64), 0, stream, w.pip_list,
                      offsets, b, i0, w.tabs, status, fail_index, extra, pmin, grp.group_ok);
 }

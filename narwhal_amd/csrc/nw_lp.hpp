@@ -8,14 +8,25 @@
 // holds limb k (radix 2^25.5, the same limbs as nw_field.hpp; lanes 10..15 hold 0). Limb-
 // wise additions are then ONE instruction, and a product is 10 multiply-accumulates per
 // lane: lane k accumulates column k = sum_j f_j g_{(k - j) mod 10} (x19 when wrapped, x2
-// for odd j with even k), with f_j broadcast by DPP row_newbcast and g rotated by
-// ds_bpermute. The four independent products of each formula stage run in the four rows.
+// for odd j with even k), with f_j broadcast by DPP row_newbcast. The four independent
+// products of each formula stage run in the four rows.
+//
+// Cross-lane moves stay in the VALU (NW_LP_XLANE=1, the default): g_{k-j} is DPP row_shr:j
+// of g and the wrapped g_{k+10-j} is row_shl:(10-j) of 19 g (lanes 10..15 hold 0, so each
+// shift contributes exactly its own lanes), the x2 of odd x odd limbs is folded into g's odd
+// source lanes for odd j; a coordinate is broadcast to all four rows by gfx950's
+// v_permlane16_swap + v_permlane32_swap (three instructions for all four rows). NW_LP_XLANE=0
+// is the earlier ds_bpermute form (an LDS-path round trip per move, 0.52 us per doubling).
 //
 // Operand discipline is nw_point.hpp's (same products, same first/second operand roles:
 // the second operand is the one scaled by 19, the first by 2); lp_carry64 leaves limbs in
 // the T_LP bound, for which tests/test_field_bounds.py checks every operand pair.
 #pragma once
 #include "nw_point.hpp"
+
+#ifndef NW_LP_XLANE
+#define NW_LP_XLANE 1
+#endif
 
 namespace nw {
 
@@ -27,6 +38,8 @@ struct lp_ctx {
   uint32_t c0;         // incoming-carry factor: 19 in limb 0 (wrapped from limb 9), 1 in
                        // limbs 1..9, 0 above (lanes 10..15 stay 0)
   uint32_t p4;         // limb k of 4p (0 above limb 9)
+  uint32_t odd;        // 1 in odd limbs (the source side of the x2 of odd x odd limbs)
+  uint32_t m1, m2;     // ~0 in rows with bit 0 / bit 1 of the row index set (lp_sel masks)
   uint32_t rot[10];    // ds_bpermute address of limb (k - j) mod 10 of this row
   uint32_t c19[10];    // 19 where column k wraps past limb 9 (k < j), else 1
   uint32_t s2[10];     // 1 for odd j with even k (the x2 of odd x odd limbs), else 0
@@ -41,6 +54,9 @@ __device__ __forceinline__ lp_ctx lp_init(uint32_t lane) {
   c.sh = (c.k & 1) ? 25u : 26u;
   c.c0 = c.k == 0 ? 19u : live ? 1u : 0u;
   c.p4 = !live ? 0u : c.k == 0 ? 0xfffffb4u : (c.k & 1) ? 0x7fffffcu : 0xffffffcu;
+  c.odd = c.k & 1;
+  c.m1 = (c.row & 1) ? ~0u : 0u;
+  c.m2 = (c.row & 2) ? ~0u : 0u;
   const uint32_t base = 16 * c.row;
 #pragma unroll
   for (int j = 0; j < 10; ++j) {
@@ -98,6 +114,29 @@ __device__ __forceinline__ uint64_t lp_mac(const lp_ctx& c, uint64_t acc, uint32
   return acc + (uint64_t)fj * (gj * c.c19[J]);
 }
 
+#if NW_LP_XLANE
+// term j of column k: f_j (row_newbcast:j) x [g_{k-j} (row_shr:j) + 19 g_{k+10-j} (row_shl:
+// (10-j))]; odd j reads the operand whose odd limbs are doubled.
+template <int J>
+__device__ __forceinline__ uint64_t lp_mac2(uint64_t acc, uint32_t f, uint32_t g,
+                                            uint32_t g19) {
+  const uint32_t gj = J == 0 ? g : lp_dpp<0x110 + J>(g) + lp_dpp<0x100 + 10 - J>(g19);
+  return acc + (uint64_t)lp_dpp<0x150 + J>(f) * gj;
+}
+
+// h = f g (fe_mul's operand roles: f first, g second; g's limbs x 38 / x 19 stay in 32 bits,
+// tests/test_field_bounds.py).
+__device__ __forceinline__ uint32_t lp_mul(const lp_ctx& c, uint32_t f, uint32_t g) {
+  const uint32_t go = g << c.odd, ge19 = g * 19u, go19 = go * 19u;
+  uint64_t a = 0, b = 0;   // two chains
+  a = lp_mac2<0>(a, f, g, ge19);  b = lp_mac2<1>(b, f, go, go19);
+  a = lp_mac2<2>(a, f, g, ge19);  b = lp_mac2<3>(b, f, go, go19);
+  a = lp_mac2<4>(a, f, g, ge19);  b = lp_mac2<5>(b, f, go, go19);
+  a = lp_mac2<6>(a, f, g, ge19);  b = lp_mac2<7>(b, f, go, go19);
+  a = lp_mac2<8>(a, f, g, ge19);  b = lp_mac2<9>(b, f, go, go19);
+  return lp_carry64(c, a + b);
+}
+#else
 // h = f g (fe_mul's operand roles: f first, g second).
 __device__ __forceinline__ uint32_t lp_mul(const lp_ctx& c, uint32_t f, uint32_t g) {
   uint32_t gr[10];
@@ -111,14 +150,38 @@ __device__ __forceinline__ uint32_t lp_mul(const lp_ctx& c, uint32_t f, uint32_t
   a = lp_mac<8>(c, a, f, gr[8]); b = lp_mac<9>(c, b, f, gr[9]);
   return lp_carry64(c, a + b);
 }
+#endif
 
 // Limb k of row q, in every row.
 __device__ __forceinline__ uint32_t lp_row(const lp_ctx& c, uint32_t q, uint32_t x) {
   return lp_perm(4 * (16 * q + c.k), x);
 }
+// Limb k of rows 0..3, each in every row.
+struct lp_rows {
+  uint32_t r0, r1, r2, r3;
+};
+__device__ __forceinline__ lp_rows lp_rows_of(const lp_ctx& c, uint32_t x) {
+#if NW_LP_XLANE
+  // permlane16_swap(x, x): odd rows of the first copy <-> even rows of the second, giving
+  // rows (0, 0, 2, 2) and (1, 1, 3, 3); permlane32_swap of each with itself: upper half of
+  // the first copy <-> lower half of the second, giving (0, 0, 0, 0) / (2, 2, 2, 2) etc.
+  (void)c;
+  const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  const auto e = __builtin_amdgcn_permlane32_swap(p[0], p[0], false, false);
+  const auto o = __builtin_amdgcn_permlane32_swap(p[1], p[1], false, false);
+  return {e[0], o[0], e[1], o[1]};
+#else
+  return {lp_row(c, 0, x), lp_row(c, 1, x), lp_row(c, 2, x), lp_row(c, 3, x)};
+#endif
+}
+// Row-wise select as three bitfield inserts (v_bfi_b32): a ternary chain on the row index
+// is compiled into divergent branches with every operand sunk into its own arm.
+__device__ __forceinline__ uint32_t lp_bfi(uint32_t m, uint32_t a, uint32_t b) {
+  return (a & m) | (b & ~m);
+}
 __device__ __forceinline__ uint32_t lp_sel(const lp_ctx& c, uint32_t a0, uint32_t a1,
                                            uint32_t a2, uint32_t a3) {
-  return c.row == 0 ? a0 : c.row == 1 ? a1 : c.row == 2 ? a2 : a3;
+  return lp_bfi(c.m2, lp_bfi(c.m1, a3, a2), lp_bfi(c.m1, a1, a0));
 }
 // a + 4p - b uncarried (fe_sub_nc) and carried (fe_sub).
 __device__ __forceinline__ uint32_t lp_sub_nc(const lp_ctx& c, uint32_t a, uint32_t b) {
@@ -136,11 +199,11 @@ __device__ __forceinline__ uint32_t lp_stage2(const lp_ctx& c, uint32_t E, uint3
 
 // 2P (ge_dbl with T): A = X^2, B = Y^2, C = Z^2, t = (X + Y)^2 in rows 0..3, then stage 2.
 __device__ __forceinline__ uint32_t lp_dbl(const lp_ctx& c, uint32_t v) {
-  const uint32_t X = lp_row(c, 0, v), Y = lp_row(c, 1, v);
-  const uint32_t in = c.row == 3 ? X + Y : v;
+  const lp_rows P = lp_rows_of(c, v);
+  const uint32_t in = lp_sel(c, v, v, v, P.r0 + P.r1);
   const uint32_t s = lp_mul(c, in, in);
-  const uint32_t A = lp_row(c, 0, s), B = lp_row(c, 1, s), C = lp_row(c, 2, s),
-                 t = lp_row(c, 3, s);
+  const lp_rows S = lp_rows_of(c, s);
+  const uint32_t A = S.r0, B = S.r1, C = S.r2, t = S.r3;
   const uint32_t H = A + B;
   const uint32_t E = lp_sub_nc(c, H, t);
   const uint32_t G = lp_sub(c, A, B);
@@ -151,24 +214,25 @@ __device__ __forceinline__ uint32_t lp_dbl(const lp_ctx& c, uint32_t v) {
 // P + Q, row q of tab holding component q of Q in the order (YmX, YpX, T2d, Z2)
 // (ge_add_cached with T; an affine niels Q has Z2 = 2).
 __device__ __forceinline__ uint32_t lp_add(const lp_ctx& c, uint32_t v, uint32_t tab) {
-  const uint32_t X = lp_row(c, 0, v), Y = lp_row(c, 1, v);
-  const uint32_t sw = lp_row(c, c.row ^ (c.row >> 1), v);   // rows 2 and 3 swapped: T, Z
+  const lp_rows P = lp_rows_of(c, v);
+  const uint32_t X = P.r0, Y = P.r1;
+  const uint32_t sw = lp_sel(c, X, Y, P.r3, P.r2);   // rows 2 and 3 swapped: T, Z
   const uint32_t ymx = lp_sub_nc(c, Y, X), ypx = Y + X;
   // a = (Y - X) YmX, b = (Y + X) YpX, c = T2d T, d = Z Z2 (operand order as ge_add_cached)
   const uint32_t m = lp_mul(c, lp_sel(c, ymx, ypx, tab, sw), lp_sel(c, tab, tab, sw, tab));
-  const uint32_t A = lp_row(c, 0, m), B = lp_row(c, 1, m), C = lp_row(c, 2, m),
-                 D = lp_row(c, 3, m);
+  const lp_rows M = lp_rows_of(c, m);
+  const uint32_t A = M.r0, B = M.r1, C = M.r2, D = M.r3;
   return lp_stage2(c, lp_sub_nc(c, B, A), lp_sub(c, D, C), D + C, B + A);
 }
 
 // Cached form (YpX, YmX, Z2, T2d; carried) of the point, row r producing the component
 // that lp_cached_component reads back for row r: YmX, YpX, T2d, Z2. d2l: limb k of 2d.
 __device__ __forceinline__ uint32_t lp_to_cached(const lp_ctx& c, uint32_t v, uint32_t d2l) {
-  const uint32_t X = lp_row(c, 0, v), Y = lp_row(c, 1, v), Z = lp_row(c, 2, v),
-                 T = lp_row(c, 3, v);
+  const lp_rows P = lp_rows_of(c, v);
+  const uint32_t X = P.r0, Y = P.r1, Z = P.r2, T = P.r3;
   const uint32_t prod = lp_mul(c, T, d2l);                       // T 2d (row 2 keeps it)
-  const uint32_t sum = lp_carry32(c, c.row == 0 ? Y + c.p4 - X : c.row == 1 ? Y + X : Z + Z);
-  return c.row == 2 ? prod : sum;
+  const uint32_t sum = lp_carry32(c, lp_sel(c, Y + c.p4 - X, Y + X, Z + Z, Z + Z));
+  return lp_sel(c, sum, sum, prod, sum);
 }
 
 __device__ __forceinline__ uint32_t lp_identity(const lp_ctx& c) {
@@ -178,8 +242,8 @@ __device__ __forceinline__ uint32_t lp_identity(const lp_ctx& c) {
 // Component (row) of a cached point in memory, in lp_add's order.
 __device__ __forceinline__ uint32_t lp_cached_component(const lp_ctx& c, const ge_cached& p) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(&p);   // YpX, YmX, Z2, T2d
-  const uint32_t field = c.row == 0 ? 1u : c.row == 1 ? 0u : c.row == 2 ? 3u : 2u;
-  return c.k < 10 ? w[10 * field + c.k] : 0u;
+  const uint32_t x = w[10 * (c.row ^ 1u) + (c.k < 10 ? c.k : 9u)];   // rows 0..3: 1, 0, 3, 2
+  return c.k < 10 ? x : 0u;
 }
 
 // Component of sign * n for an affine niels point n (Z2 = 2), in lp_add's order.

@@ -99,7 +99,8 @@ def test_limb_parallel_bounds():
     for F, G in pairs:
         c = colmax(F, G)
         assert c < 2**64
-        assert max(G) * 19 < 2**32 and max(F[1::2]) * 2 < 2**32
+        assert max(G) * 19 < 2**32 and max(F[1::2]) * 2 < 2**32   # NW_LP_XLANE=0
+        assert max(G[0::2]) * 19 < 2**32 and max(G[1::2]) * 38 < 2**32   # NW_LP_XLANE=1: x2 on g
     # first pass: carries < 2^39 (x19 < 2^43.3 into limb 0); second: < 2^18.3 into limb 0
     assert (2**64 >> 25) * 19 < 2**44
     assert 19 * (((2**25 + 2**39) >> 25) + 1) < 2**18.3
