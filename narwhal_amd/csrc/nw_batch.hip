@@ -1164,8 +1164,11 @@ __global__ __launch_bounds__(256) void k_pip_buckets(const uint32_t* __restrict_
                  e = e0 + (uint32_t)((uint64_t)ne * (g + 1) >> lg);
   ge acc;
   ge_identity(acc);
-  // the next entry's point is fetched while the current one is added
+  // two-stage prefetch: entry k + 2's index and entry k + 1's point (whose index is already
+  // here) are fetched while entry k is added, so the dependent index -> point loads never
+  // stall the chain
   uint32_t x = a < e ? reg.ent[a] : 0u;
+  uint32_t x2 = a + 1 < e ? reg.ent[a + 1] : 0u;
   ge_niels nx;
   if (a < e) nx = reg.pts[x & 0x7fffffffu];
 #pragma unroll 1
@@ -1173,9 +1176,10 @@ __global__ __launch_bounds__(256) void k_pip_buckets(const uint32_t* __restrict_
     ge_niels q = nx;
     const bool neg = (x >> 31) != 0;
     if (k + 1 < e) {
-      x = reg.ent[k + 1];
+      x = x2;
       nx = reg.pts[x & 0x7fffffffu];
     }
+    if (k + 2 < e) x2 = reg.ent[k + 2];
     ge_niels_cneg(q, neg);
     ge_add_niels(acc, acc, q, true);
   }
