@@ -321,40 +321,8 @@ int32_t decode_frame(const uint8_t* f, size_t len, uint64_t i, Decoded& d, uint6
   return NW_MSG_CERTIFICATES_REQUEST;
 }
 
-void merge_header(HeaderSoA& dst, const HeaderSoA& src) {
-  const uint64_t base = dst.bytes.size();
-  dst.bytes.insert(dst.bytes.end(), src.bytes.begin(), src.bytes.end());
-  for (size_t k = 1; k < src.offsets.size(); ++k) dst.offsets.push_back(base + src.offsets[k]);
-  dst.payload_counts.insert(dst.payload_counts.end(), src.payload_counts.begin(),
-                            src.payload_counts.end());
-  dst.ids.insert(dst.ids.end(), src.ids.begin(), src.ids.end());
-  dst.sigs.insert(dst.sigs.end(), src.sigs.begin(), src.sigs.end());
-}
-
-template <class T>
-void cat(std::vector<T>& dst, const std::vector<T>& src) {
-  dst.insert(dst.end(), src.begin(), src.end());
-}
-
-void merge(Decoded& d, const Decoded& s) {
-  merge_header(d.hdr, s.hdr);
-  merge_header(d.cert, s.cert);
-  cat(d.hdr_of, s.hdr_of);
-  cat(d.cert_of, s.cert_of);
-  cat(d.vote_of, s.vote_of);
-  const uint64_t vb = d.cvo.back();
-  for (size_t k = 1; k < s.cvo.size(); ++k) d.cvo.push_back(vb + s.cvo[k]);
-  cat(d.cvpk, s.cvpk);
-  cat(d.cvsig, s.cvsig);
-  cat(d.v_ids, s.v_ids);
-  cat(d.v_origins, s.v_origins);
-  cat(d.v_authors, s.v_authors);
-  cat(d.v_sigs, s.v_sigs);
-  cat(d.v_rounds, s.v_rounds);
-}
-
 // Decodes all frames, in parallel over contiguous ranges (host threads; the per-range
-// results are concatenated in frame order).
+// results are merged in frame order, in place and in parallel).
 void decode_all(const uint8_t* frames, const uint64_t* offsets, size_t n, Decoded& d,
                 int32_t* kind_out, uint64_t* counts_out) {
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
