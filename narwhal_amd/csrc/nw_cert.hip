@@ -74,9 +74,30 @@ __device__ void digest_72(uint32_t out[8], const uint32_t x[8], uint64_t round,
   }
 }
 
+// The committee's sorted keys and stakes staged in LDS for committees of up to
+// kLdsAuth members (8.5 KB): the per-vote binary searches then chain LDS reads instead of
+// ~6 dependent global loads per vote (k_cert_prepare at N = 50: ~140 us per small job,
+// a lane walks its certificate's 50 votes).
+constexpr uint32_t kLdsAuth = 256;
+__device__ __forceinline__ cert_committee_t committee_to_lds(const cert_committee_t& com,
+                                                            uint32_t* s_pks,
+                                                            uint32_t* s_stakes) {
+  cert_committee_t c = com;
+  if (com.nauth <= kLdsAuth) {
+    for (uint32_t k = threadIdx.x; k < 8 * (uint32_t)com.nauth; k += blockDim.x)
+      s_pks[k] = com.pks[k];
+    for (uint32_t k = threadIdx.x; k < (uint32_t)com.nauth; k += blockDim.x)
+      s_stakes[k] = com.stakes[k];
+    c.pks = s_pks;
+    c.stakes = s_stakes;
+  }
+  __syncthreads();
+  return c;
+}
+
 }  // namespace
 
-__global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com, cert_stream_t cs,
+__global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com_g, cert_stream_t cs,
                                                       int headers_only,
                                                       const uint32_t* __restrict__ hdr_digest,
                                                       uint32_t* __restrict__ authors,
@@ -88,6 +109,8 @@ __global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com, cert
                                                       uint32_t* __restrict__ vote_key,
                                                       uint32_t* __restrict__ author_key,
                                                       uint32_t* __restrict__ vote_cert) {
+  __shared__ uint32_t s_pks[8 * kLdsAuth], s_stakes[kLdsAuth];
+  const cert_committee_t com = committee_to_lds(com_g, s_pks, s_stakes);
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cs.n) return;
   const uint8_t* h = cs.header_bytes + cs.header_offsets[i];
@@ -224,7 +247,7 @@ __global__ __launch_bounds__(256) void k_cert_finalize(uint64_t n, int headers_o
   if (index) index[i] = ix;
 }
 
-__global__ __launch_bounds__(256) void k_vote_prepare(cert_committee_t com, uint64_t n,
+__global__ __launch_bounds__(256) void k_vote_prepare(cert_committee_t com_g, uint64_t n,
                                                       const uint32_t* __restrict__ ids,
                                                       const uint64_t* __restrict__ rounds,
                                                       const uint32_t* __restrict__ origins,
@@ -232,6 +255,8 @@ __global__ __launch_bounds__(256) void k_vote_prepare(cert_committee_t com, uint
                                                       uint32_t* __restrict__ digests,
                                                       int32_t* __restrict__ pre,
                                                       uint32_t* __restrict__ author_key) {
+  __shared__ uint32_t s_pks[8 * kLdsAuth], s_stakes[kLdsAuth];
+  const cert_committee_t com = committee_to_lds(com_g, s_pks, s_stakes);
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t id[8], org[8], au[8], d[8];
