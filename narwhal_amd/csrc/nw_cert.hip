@@ -173,10 +173,28 @@ __global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com_g, ce
     // up to 256; pairwise key comparison above that).
     uint32_t seen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const bool small_com = com.nauth <= 256;
+    // the votes' keys are fetched kVoteChunk at a time (one load latency per chunk instead of
+    // one per vote: a lane walks all of its certificate's votes); the checks themselves run
+    // vote by vote, in order, exactly as before
+    constexpr int kVoteChunk = 4;
+    uint32_t pkc[kVoteChunk][8];
     for (uint64_t v = vb; v < ve && p2 == 0; ++v) {
+      const int u = (int)((v - vb) % kVoteChunk);
+      if (u == 0) {
+#pragma unroll
+        for (int c = 0; c < kVoteChunk; ++c)
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            pkc[c][j] = v + c < ve ? cs.vote_pks[8 * (v + c) + j] : 0u;
+      }
       uint32_t pk[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) pk[j] = cs.vote_pks[8 * v + j];
+      for (int j = 0; j < 8; ++j) {
+        uint32_t x = pkc[0][j];
+#pragma unroll
+        for (int c = 1; c < kVoteChunk; ++c) x = u == c ? pkc[c][j] : x;
+        pk[j] = x;
+      }
       const int av = committee_find(com, pk);
       bool reuse = false;
       if (small_com) {
