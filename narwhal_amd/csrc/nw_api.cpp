@@ -603,7 +603,8 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
   NW_HIP(nw::launch_cert_prepare(dc, ds, headers_only, w.hdr_digest, w.authors, w.cert_digest,
                                  w.pre1, w.pre2, w.idx1, w.idx2,
                                  headers_only ? nullptr : w.vote_key, w.author_key,
-                                 headers_only ? nullptr : w.vote_cert, s),
+                                 headers_only ? nullptr : w.vote_cert,
+                                 headers_only ? 0 : cs.nvotes, s),
          "k_cert_prepare");
   const nw::key_tables_t hk{ktabs, kok, w.author_key};
   // With a fork stream (host-buffer jobs) and the keyed vote checks, the headers run on the

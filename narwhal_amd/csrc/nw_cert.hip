@@ -97,6 +97,27 @@ __device__ __forceinline__ cert_committee_t committee_to_lds(const cert_committe
 
 }  // namespace
 
+// One lane per vote: the committee index of the vote's key (vote_key, kNoKey when absent),
+// so that k_cert_prepare's lanes, which walk their certificate's votes in order, read one
+// word per vote instead of running a dependent binary search per vote (committees of up to
+// kLdsAuth; larger ones keep the in-loop lookup). Every vote gets its index, also votes
+// after a certificate's first failed check: those certificates are settled by that check
+// (Certificate::verify returns at the first failure, messages.rs:199-215), so their votes'
+// signature verdicts are never read.
+__global__ __launch_bounds__(256) void k_vote_keys(cert_committee_t com_g, uint64_t nv,
+                                                   const uint32_t* __restrict__ vote_pks,
+                                                   uint32_t* __restrict__ vote_key) {
+  __shared__ uint32_t s_pks[8 * kLdsAuth], s_stakes[kLdsAuth];
+  const cert_committee_t com = committee_to_lds(com_g, s_pks, s_stakes);
+  const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= nv) return;
+  uint32_t pk[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) pk[j] = vote_pks[8 * v + j];
+  const int a = committee_find(com, pk);
+  vote_key[v] = a >= 0 ? (uint32_t)a : kNoKey;
+}
+
 __global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com_g, cert_stream_t cs,
                                                       int headers_only,
                                                       const uint32_t* __restrict__ hdr_digest,
@@ -108,7 +129,8 @@ __global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com_g, ce
                                                       uint64_t* __restrict__ idx2,
                                                       uint32_t* __restrict__ vote_key,
                                                       uint32_t* __restrict__ author_key,
-                                                      uint32_t* __restrict__ vote_cert) {
+                                                      uint32_t* __restrict__ vote_cert,
+                                                      int keys_pre) {
   __shared__ uint32_t s_pks[8 * kLdsAuth], s_stakes[kLdsAuth];
   const cert_committee_t com = committee_to_lds(com_g, s_pks, s_stakes);
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -163,7 +185,7 @@ __global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com_g, ce
     const uint64_t vb = cs.vote_offsets[i], ve = cs.vote_offsets[i + 1];
     // committee index of each vote's key (for the batch's pre-decompressed key tables);
     // votes the loop below does not reach keep kNoKey (decompressed in the batch kernel)
-    if (vote_key)
+    if (vote_key && !keys_pre)
       for (uint64_t v = vb; v < ve; ++v) vote_key[v] = kNoKey;
     if (vote_cert)   // each vote's certificate (the keyed vote checks run one lane per vote)
       for (uint64_t v = vb; v < ve; ++v) vote_cert[v] = (uint32_t)i;
@@ -178,7 +200,35 @@ __global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com_g, ce
     // vote by vote, in order, exactly as before
     constexpr int kVoteChunk = 4;
     uint32_t pkc[kVoteChunk][8];
-    for (uint64_t v = vb; v < ve && p2 == 0; ++v) {
+    if (keys_pre) {   // k_vote_keys ran (small committee): one word per vote, 8 at a time
+      uint32_t kc[8];
+      for (uint64_t v = vb; v < ve && p2 == 0; ++v) {
+        const int u = (int)((v - vb) % 8);
+        if (u == 0) {
+#pragma unroll
+          for (int c = 0; c < 8; ++c) kc[c] = v + c < ve ? vote_key[v + c] : kNoKey;
+        }
+        uint32_t k = kc[0];
+#pragma unroll
+        for (int c = 1; c < 8; ++c) k = u == c ? kc[c] : k;
+        const int av = k == kNoKey ? -1 : (int)k;
+        bool reuse = false;
+        if (av >= 0) {
+          const uint32_t bit = 1u << (av & 31);
+          uint32_t word = 0;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) word = (av >> 5) == q ? seen[q] : word;
+          reuse = (word & bit) != 0;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) seen[q] |= (av >> 5) == q ? bit : 0u;
+        }
+        if (reuse) { p2 = NW_DAG_AUTHORITY_REUSE; x2 = v - vb; break; }
+        const uint32_t st = committee_stake(com, av);
+        if (st == 0) { p2 = NW_DAG_UNKNOWN_AUTHORITY; x2 = v - vb; break; }
+        weight += st;
+      }
+    }
+    for (uint64_t v = vb; !keys_pre && v < ve && p2 == 0; ++v) {
       const int u = (int)((v - vb) % kVoteChunk);
       if (u == 0) {
 #pragma unroll
@@ -307,11 +357,16 @@ hipError_t launch_cert_prepare(const cert_committee_t& com, const cert_stream_t&
                                int headers_only, const uint32_t* hdr_digest, uint32_t* authors,
                                uint32_t* cert_digest, int32_t* pre1, int32_t* pre2,
                                uint64_t* idx1, uint64_t* idx2, uint32_t* vote_key,
-                               uint32_t* author_key, uint32_t* vote_cert, hipStream_t stream) {
+                               uint32_t* author_key, uint32_t* vote_cert, uint64_t nvotes,
+                               hipStream_t stream) {
   if (cs.n == 0) return hipSuccess;
+  const int keys_pre = !headers_only && vote_key && com.nauth <= kLdsAuth && nvotes;
+  if (keys_pre)
+    hipLaunchKernelGGL(k_vote_keys, dim3(blocks_for(nvotes)), dim3(256), 0, stream, com,
+                       nvotes, cs.vote_pks, vote_key);
   hipLaunchKernelGGL(k_cert_prepare, dim3(blocks_for(cs.n)), dim3(256), 0, stream, com, cs,
                      headers_only, hdr_digest, authors, cert_digest, pre1, pre2, idx1, idx2,
-                     vote_key, author_key, vote_cert);
+                     vote_key, author_key, vote_cert, keys_pre);
   return hipGetLastError();
 }
 

@@ -175,7 +175,8 @@ hipError_t launch_cert_prepare(const cert_committee_t& com, const cert_stream_t&
                                int headers_only, const uint32_t* hdr_digest, uint32_t* authors,
                                uint32_t* cert_digest, int32_t* pre1, int32_t* pre2,
                                uint64_t* idx1, uint64_t* idx2, uint32_t* vote_key,
-                               uint32_t* author_key, uint32_t* vote_cert, hipStream_t stream);
+                               uint32_t* author_key, uint32_t* vote_cert, uint64_t nvotes,
+                               hipStream_t stream);
 hipError_t launch_cert_finalize(uint64_t n, int headers_only, const int32_t* pre1,
                                 const int32_t* pre2, const uint64_t* idx1, const uint64_t* idx2,
                                 const int32_t* hdr_status, const int32_t* batch_status,
