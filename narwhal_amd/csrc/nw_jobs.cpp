@@ -26,7 +26,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <mutex>
+#include <thread>
 #include <new>
 #include <vector>
 
@@ -766,6 +769,91 @@ void countdown_tick(void* p) {
     delete c;
   }
 }
+
+// Completion callbacks. A host function on the job's stream (hipLaunchHostFunc) is run by
+// the HIP runtime's own thread some hundreds of microseconds after the stream reaches it
+// and holds the stream until it returns; instead one watcher thread polls a marker event
+// recorded behind each armed job and calls fn(arg) as soon as that event completes, in
+// whatever order jobs finish. The stream never waits on the callback. Marker events are
+// pooled; the watcher spins briefly, then naps 20 us, while anything is armed, and sleeps
+// on a condition variable otherwise.
+struct Armed {
+  int dev;
+  hipEvent_t ev;
+  void (*fn)(void*);
+  void* arg;
+};
+struct Watcher {
+  std::mutex m;
+  std::condition_variable cv;
+  std::vector<Armed> armed;        // guarded by m
+  std::vector<hipEvent_t> pool[kMaxDev];   // per device, guarded by m
+  bool started = false;
+
+  int arm(int dev, hipStream_t s, void (*fn)(void*), void* arg) {
+    int rc = nw::rt::use_device(dev);
+    if (rc) return rc;
+    hipEvent_t ev = nullptr;
+    {
+      std::lock_guard<std::mutex> g(m);
+      if (!pool[dev].empty()) {
+        ev = pool[dev].back();
+        pool[dev].pop_back();
+      }
+      if (!started) {
+        std::thread(&Watcher::run, this).detach();
+        started = true;
+      }
+    }
+    hipError_t e = hipSuccess;
+    if (!ev) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(ev, s);
+    if (e != hipSuccess) {
+      if (ev) {
+        std::lock_guard<std::mutex> g(m);
+        pool[dev].push_back(ev);
+      }
+      return set_err(NW_E_DEVICE, "notify marker event", e);
+    }
+    {
+      std::lock_guard<std::mutex> g(m);
+      armed.push_back({dev, ev, fn, arg});
+    }
+    cv.notify_one();
+    return 0;
+  }
+
+  void run() {
+    std::vector<Armed> mine, ready;
+    int idle = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(m);
+        for (const Armed& a : ready) pool[a.dev].push_back(a.ev);
+        ready.clear();
+        mine.insert(mine.end(), armed.begin(), armed.end());
+        armed.clear();
+        if (mine.empty()) cv.wait(g, [&] { return !armed.empty(); });
+        mine.insert(mine.end(), armed.begin(), armed.end());
+        armed.clear();
+      }
+      size_t keep = 0;
+      for (const Armed& a : mine) {
+        // a device error also ends the wait: the caller's poll / wait reports it
+        if (hipEventQuery(a.ev) == hipErrorNotReady) mine[keep++] = a;
+        else ready.push_back(a);
+      }
+      mine.resize(keep);
+      for (const Armed& a : ready) a.fn(a.arg);
+      if (!ready.empty()) idle = 0;
+      else if (++idle > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+      else std::this_thread::yield();
+    }
+  }
+};
+// never destroyed: a static destructor would destroy the condition variable the detached
+// watcher waits on (pthread_cond_destroy blocks on waiters: a hang at process exit)
+Watcher& g_watcher = *new Watcher;
 }  // namespace
 
 int nw_job_notify(nw_job* job, void (*fn)(void*), void* arg) {
@@ -794,8 +882,7 @@ int nw_job_notify(nw_job* job, void (*fn)(void*), void* arg) {
     fn(arg);
     return 0;
   }
-  JOB_HIP(hipLaunchHostFunc(job->stream, fn, arg), "hipLaunchHostFunc");
-  return 0;
+  return g_watcher.arm(job->dev, job->stream, fn, arg);
 }
 
 void nw_job_release(nw_job* job) { job_recycle(job); }
