@@ -29,6 +29,7 @@
 #include "nw_consts.hpp"
 #include "nw_strict.hpp"
 #include "nw_lp.hpp"
+#include "nw_chacha.hpp"
 
 #include <stdlib.h>
 
@@ -45,6 +46,8 @@ struct batch_consts {
   curve_consts k;
   ge_niels btab[129];   // j * B
   ge_niels b128[129];   // j * 2^128 B (short ladders of keyed chunks)
+  torsion_consts tor;   // [j] T8 (k_key_base: a committee key's lambda)
+  uint32_t l[8];        // the group order l, little-endian words
 };
 __constant__ batch_consts g_bc;
 // j * 2^(8 w) * B (nw_consts.hpp compute_comb): [-sum b_i]B in 32 additions, no doublings
@@ -118,36 +121,6 @@ __device__ __forceinline__ void hram96(uint32_t x[16], const uint32_t R[8], cons
   for (int i = 0; i < 8; ++i) {
     x[2 * i] = bswap((uint32_t)(st[i] >> 32));
     x[2 * i + 1] = bswap((uint32_t)st[i]);
-  }
-}
-
-__device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
-
-// z_i = ChaCha20(key, nonce, block i/4) bytes [16 (i%4), 16 (i%4) + 16) (DJB layout).
-__device__ void chacha20_z(uint32_t z[4], const uint32_t key[8], uint64_t nonce, uint64_t i) {
-  const uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key[0], key[1],
-                          key[2], key[3], key[4], key[5], key[6], key[7], (uint32_t)(i >> 2),
-                          (uint32_t)(i >> 34), (uint32_t)nonce, (uint32_t)(nonce >> 32)};
-  uint32_t x[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) x[j] = s[j];
-#define NW_QR(a, b, c, d)                                                   \
-  x[a] += x[b]; x[d] ^= x[a]; x[d] = rotl32(x[d], 16); x[c] += x[d];        \
-  x[b] ^= x[c]; x[b] = rotl32(x[b], 12); x[a] += x[b]; x[d] ^= x[a];        \
-  x[d] = rotl32(x[d], 8); x[c] += x[d]; x[b] ^= x[c]; x[b] = rotl32(x[b], 7);
-#pragma unroll 1
-  for (int r = 0; r < 10; ++r) {
-    NW_QR(0, 4, 8, 12) NW_QR(1, 5, 9, 13) NW_QR(2, 6, 10, 14) NW_QR(3, 7, 11, 15)
-    NW_QR(0, 5, 10, 15) NW_QR(1, 6, 11, 12) NW_QR(2, 7, 8, 13) NW_QR(3, 4, 9, 14)
-  }
-#undef NW_QR
-  const int q = (int)(i & 3) * 4;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    uint32_t v = x[0] + s[0];
-#pragma unroll
-    for (int t = 1; t < 16; ++t) v = (q + j == t) ? x[t] + s[t] : v;
-    z[j] = v;
   }
 }
 
@@ -1492,6 +1465,8 @@ hipError_t upload_batch_consts() {
     compute_consts(host.k, host.btab);
     strict_consts sk;
     compute_strict_consts(sk, host.b128);
+    compute_torsion(host.tor);
+    for (int i = 0; i < 8; ++i) host.l[i] = L_W[i];
   });
   static std::vector<ge_niels> comb(32 * 129);
   static std::once_flag once_comb;
@@ -1545,7 +1520,24 @@ __global__ __launch_bounds__(256) void k_key_base(const uint32_t* __restrict__ p
   for (int j = 0; j < 8; ++j) Aw[j] = pks[8 * i + j];
   ge P;
   const bool dec = ge_frombytes(P, Aw, g_bc.k);
-  ok[i] = (dec ? 1u : 0u) | (dec && ge_is_small_order(P) ? 2u : 0u);   // bit 1: 8A == 0
+  // lambda: [l] A == [lambda] T8 (l A lies in E[8] for every curve point), by
+  // double-and-add over the 253 bits of l — once per key per committee
+  uint32_t lam = 0;
+  if (dec) {
+    ge_cached Pc;
+    ge_to_cached(Pc, P, g_bc.k.d2);
+    ge acc;
+    ge_identity(acc);
+#pragma unroll 1
+    for (int bit = 252; bit >= 0; --bit) {
+      ge_dbl(acc, acc, true);
+      if ((g_bc.l[bit >> 5] >> (bit & 31)) & 1u) ge_add_cached(acc, acc, Pc, true);
+    }
+    const int j = torsion_index(acc, g_bc.tor);
+    lam = j > 0 ? (uint32_t)j : 0u;
+  }
+  ok[i] = (dec ? kKeyDecoded : 0u) | (dec && ge_is_small_order(P) ? kKeySmall : 0u) |
+          (lam << kKeyLambdaShift);
   base[2 * i] = P;
 #pragma unroll 1
   for (int t = 0; t < (int)kKeyCombT; ++t) {

@@ -16,86 +16,9 @@
 // arithmetic lives in nw_kernels.hip.
 #include "nw_kernels.h"
 #include "nw_sha512.hpp"
+#include "nw_committee.hpp"
 
 namespace nw {
-
-namespace {
-
-__device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {
-  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-}
-
-// Committee lookup (BTreeMap<PublicKey, Authority>::get): binary search over the sorted
-// 32-byte keys; -1 if absent. key = 8 little-endian words of the public key bytes.
-__device__ int committee_find(const cert_committee_t& c, const uint32_t key[8]) {
-  uint32_t kb[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) kb[j] = __builtin_bswap32(key[j]);   // lexicographic order
-  int lo = 0, hi = (int)c.nauth - 1;
-  while (lo <= hi) {
-    const int mid = (lo + hi) >> 1;
-    const uint32_t* m = c.pks + 8 * (size_t)mid;
-    int cmp = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t mb = __builtin_bswap32(m[j]);
-      if (cmp == 0 && mb != kb[j]) cmp = mb < kb[j] ? -1 : 1;
-    }
-    if (cmp == 0) return mid;
-    if (cmp < 0) lo = mid + 1; else hi = mid - 1;
-  }
-  return -1;
-}
-
-__device__ __forceinline__ uint32_t committee_stake(const cert_committee_t& c, int a) {
-  return a < 0 ? 0u : c.stakes[a];
-}
-
-// Sha512(x32 || u64 LE || y32)[..32]: Vote::digest / Certificate::digest (72 bytes, 1 block).
-__device__ void digest_72(uint32_t out[8], const uint32_t x[8], uint64_t round,
-                          const uint32_t y[8]) {
-  uint64_t w[16], st[8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    w[i] = ((uint64_t)__builtin_bswap32(x[2 * i]) << 32) | __builtin_bswap32(x[2 * i + 1]);
-    w[5 + i] = ((uint64_t)__builtin_bswap32(y[2 * i]) << 32) | __builtin_bswap32(y[2 * i + 1]);
-  }
-  w[4] = __builtin_bswap64(round);
-  w[9] = 0x8000000000000000ULL;
-#pragma unroll
-  for (int i = 10; i < 15; ++i) w[i] = 0;
-  w[15] = 72 * 8;
-  sha512_init(st);
-  sha512_compress(st, w);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    out[2 * i] = __builtin_bswap32((uint32_t)(st[i] >> 32));
-    out[2 * i + 1] = __builtin_bswap32((uint32_t)st[i]);
-  }
-}
-
-// The committee's sorted keys and stakes staged in LDS for committees of up to
-// kLdsAuth members (8.5 KB): the per-vote binary searches then chain LDS reads instead of
-// ~6 dependent global loads per vote (k_cert_prepare at N = 50: ~140 us per small job,
-// a lane walks its certificate's 50 votes).
-constexpr uint32_t kLdsAuth = 256;
-__device__ __forceinline__ cert_committee_t committee_to_lds(const cert_committee_t& com,
-                                                            uint32_t* s_pks,
-                                                            uint32_t* s_stakes) {
-  cert_committee_t c = com;
-  if (com.nauth <= kLdsAuth) {
-    for (uint32_t k = threadIdx.x; k < 8 * (uint32_t)com.nauth; k += blockDim.x)
-      s_pks[k] = com.pks[k];
-    for (uint32_t k = threadIdx.x; k < (uint32_t)com.nauth; k += blockDim.x)
-      s_stakes[k] = com.stakes[k];
-    c.pks = s_pks;
-    c.stakes = s_stakes;
-  }
-  __syncthreads();
-  return c;
-}
-
-}  // namespace
 
 // One lane per vote: the committee index of the vote's key (vote_key, kNoKey when absent),
 // so that k_cert_prepare's lanes, which walk their certificate's votes in order, read one
@@ -273,7 +196,7 @@ __global__ __launch_bounds__(256) void k_cert_prepare(cert_committee_t com_g, ce
     }
     if (p2 == 0 && weight < quorum) p2 = NW_DAG_REQUIRES_QUORUM;
     uint32_t cd[8];
-    digest_72(cd, id, round, author);
+    sha512_digest72(cd, id, round, author);
 #pragma unroll
     for (int j = 0; j < 8; ++j) cert_digest[8 * i + j] = cd[j];
   }
@@ -334,7 +257,7 @@ __global__ __launch_bounds__(256) void k_vote_prepare(cert_committee_t com_g, ui
     org[j] = origins[8 * i + j];
     au[j] = authors[8 * i + j];
   }
-  digest_72(d, id, rounds[i], org);
+  sha512_digest72(d, id, rounds[i], org);
 #pragma unroll
   for (int j = 0; j < 8; ++j) digests[8 * i + j] = d[j];
   const int a = committee_find(com, au);

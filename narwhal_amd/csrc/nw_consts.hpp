@@ -102,6 +102,37 @@ inline void compute_strict_consts(strict_consts& sk, ge_niels b128[129]) {
   niels_multiples(b128, B, sk.k.d2);
 }
 
+// torsion_consts (nw_strict.hpp): affine [j] T8, j = 0..7, T8 = decompress(y8, sign 0).
+inline void compute_torsion(torsion_consts& tc) {
+  curve_consts k;
+  ge_niels btab[129];
+  compute_consts(k, btab);
+  static const uint8_t y8_enc[32] = {0x26, 0xe8, 0x95, 0x8f, 0xc2, 0xb2, 0x27, 0xb0,
+                                     0x45, 0xc3, 0xf4, 0x89, 0xf2, 0xef, 0x98, 0xf0,
+                                     0xd5, 0xdf, 0xac, 0x05, 0xd3, 0xc6, 0x33, 0x39,
+                                     0xb1, 0x38, 0x02, 0x88, 0x6d, 0x53, 0xfc, 0x05};
+  uint32_t w[8];
+  for (int i = 0; i < 8; ++i)
+    w[i] = (uint32_t)y8_enc[4 * i] | ((uint32_t)y8_enc[4 * i + 1] << 8) |
+           ((uint32_t)y8_enc[4 * i + 2] << 16) | ((uint32_t)y8_enc[4 * i + 3] << 24);
+  ge T8, acc;
+  ge_frombytes(T8, w, k);
+  ge_cached c8;
+  ge_to_cached(c8, T8, k.d2);
+  ge_identity(acc);
+  for (int j = 0; j < 8; ++j) {
+    fe zi, t;
+    fe_invert(zi, acc.Z);
+    fe_mul(t, acc.X, zi);
+    fe_canonical(tc.x[j], t);
+    fe_mul(t, acc.Y, zi);
+    fe_canonical(tc.y[j], t);
+    ge nxt;
+    ge_add_cached(nxt, acc, c8, true);
+    acc = nxt;
+  }
+}
+
 }  // namespace nw
 
 namespace nw {

@@ -123,4 +123,148 @@ __device__ __forceinline__ void sha512_init(uint64_t st[8]) {
   for (int i = 0; i < 8; ++i) st[i] = SHA512_H0[i];
 }
 
+// Tail block(s): message bytes [base, len) followed by 0x80, zeros, and (if last) the
+// 128-bit big-endian bit length in the final 16 bytes. Reads only the aligned dwords that
+// hold a message byte (such a dword never crosses a page, so nothing past the buffer can
+// fault) and masks the bytes at or beyond len.
+__device__ __forceinline__ void load_block_tail(uint64_t w[16], const uint8_t* msg, uint64_t base,
+                                                uint64_t len, bool last) {
+  const uintptr_t a0 = (uintptr_t)(msg + base);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(a0 & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a0 & 3) * 8;
+  // message bytes in this block; negative for a padding-only block after the 0x80 block
+  const int64_t rem = (int64_t)len - (int64_t)base;
+  // dword q[i] covers block bytes [4 i - sh/8, 4 i - sh/8 + 4)
+  uint32_t prev = 0;
+#pragma unroll 1
+  for (int i = 0; i < 33; ++i) {
+    const int64_t first = 4 * (int64_t)i - (int64_t)(sh >> 3);   // block byte of q[i]'s byte 0
+    const uint32_t cur = first < rem ? q[i] : 0u;
+    if (i > 0) {
+      // block dword i-1 = bytes [4(i-1), 4i): LE word realigned from q[i-1], q[i]
+      uint32_t lo = __builtin_amdgcn_alignbit(cur, prev, sh);
+      const int64_t k0 = 4 * (int64_t)(i - 1);                 // its first block byte
+      // keep bytes < rem, put 0x80 at byte rem
+      uint32_t keep = 0, pad = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int64_t pos = k0 + b;
+        keep |= (pos < rem ? 0xffu : 0u) << (8 * b);
+        pad |= (pos == rem ? 0x80u : 0u) << (8 * b);
+      }
+      lo = (lo & keep) | pad;
+      const int wi = (i - 1) >> 1;
+      const uint64_t be = (uint64_t)__builtin_bswap32(lo);
+      if ((i - 1) & 1) w[wi] = (w[wi] & 0xffffffff00000000ull) | be;
+      else w[wi] = be << 32;
+    }
+    prev = cur;
+  }
+  if (last) {
+    w[14] = len >> 61;
+    w[15] = len << 3;
+  }
+}
+
+// The 33 aligned dwords covering the 128-byte block at p (the 33rd only when p is not
+// 4-byte aligned; only dwords that contain message bytes), and their realignment by the
+// byte offset into 16 big-endian words — two halves, so the next block's loads can be issued
+// before this block's compression.
+__device__ __forceinline__ void load_block_raw(uint32_t d[33], const uint8_t* p) {
+  // The integer round trip makes these flat_load_dwordx4; keeping the global address space
+  // (global_load_dwordx4) measured 4 % slower (1,231 vs 1,279 GB/s, different schedule).
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+#pragma unroll
+  for (int i = 0; i < 32; ++i) d[i] = q[i];
+  d[32] = (a & 3) ? q[32] : 0u;
+}
+__device__ __forceinline__ void block_from_raw(uint64_t w[16], const uint32_t d[33], uint32_t sh) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint32_t lo = __builtin_amdgcn_alignbit(d[2 * i + 1], d[2 * i], sh);
+    const uint32_t hi = __builtin_amdgcn_alignbit(d[2 * i + 2], d[2 * i + 1], sh);
+    w[i] = ((uint64_t)__builtin_bswap32(lo) << 32) | __builtin_bswap32(hi);
+  }
+}
+
+
+// Digest(Sha512(msg[0..len))[..32]) on one lane into out[8] (LE words). Full blocks are
+// double-buffered: block k + 1's loads are issued before block k's 80 rounds, so a lone
+// wave per SIMD does not stall on each block's memory latency (HBM, or pinned host memory
+// for the small-job kernel, nw_small.hip).
+__device__ __forceinline__ void sha512_digest32_lane(const uint8_t* msg, uint64_t len,
+                                                     uint32_t* out) {
+  const uint64_t nblocks = (len + 17 + 127) / 128;
+  const uint64_t nfull = len / 128;   // blocks entirely inside the message
+  const uint32_t sh = (uint32_t)((uintptr_t)msg & 3) * 8;
+  uint64_t st[8], w[16];
+  sha512_init(st);
+  uint32_t d[33];
+  if (nfull) load_block_raw(d, msg);
+#pragma unroll 1
+  for (uint64_t k = 0; k < nfull; ++k) {
+    block_from_raw(w, d, sh);
+    if (k + 1 < nfull) load_block_raw(d, msg + 128 * (k + 1));
+    sha512_compress(st, w);
+  }
+#pragma unroll 1
+  for (uint64_t k = nfull; k < nblocks; ++k) {
+    load_block_tail(w, msg, 128 * k, len, k + 1 == nblocks);
+    sha512_compress(st, w);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    out[2 * j] = __builtin_bswap32((uint32_t)(st[j] >> 32));
+    out[2 * j + 1] = __builtin_bswap32((uint32_t)st[j]);
+  }
+}
+
+// SHA-512 of the 96-byte R || A || M (one block) -> 16 LE words of the digest.
+__device__ __forceinline__ void sha512_hram96(uint32_t x[16], const uint32_t R[8],
+                                              const uint32_t A[8], const uint32_t M[8]) {
+  uint64_t w[16], st[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    w[i] = ((uint64_t)__builtin_bswap32(R[2 * i]) << 32) | __builtin_bswap32(R[2 * i + 1]);
+    w[4 + i] = ((uint64_t)__builtin_bswap32(A[2 * i]) << 32) | __builtin_bswap32(A[2 * i + 1]);
+    w[8 + i] = ((uint64_t)__builtin_bswap32(M[2 * i]) << 32) | __builtin_bswap32(M[2 * i + 1]);
+  }
+  w[12] = 0x8000000000000000ULL;
+  w[13] = 0;
+  w[14] = 0;
+  w[15] = 96 * 8;
+  sha512_init(st);
+  sha512_compress(st, w);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    x[2 * i] = __builtin_bswap32((uint32_t)(st[i] >> 32));
+    x[2 * i + 1] = __builtin_bswap32((uint32_t)st[i]);
+  }
+}
+
+// Digest(Sha512(x32 || u64 LE || y32)[..32]): Vote::digest / Certificate::digest
+// (primary/src/messages.rs:145-153, 226-234; 72 bytes, one block).
+__device__ __forceinline__ void sha512_digest72(uint32_t out[8], const uint32_t x[8],
+                                                uint64_t round, const uint32_t y[8]) {
+  uint64_t w[16], st[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    w[i] = ((uint64_t)__builtin_bswap32(x[2 * i]) << 32) | __builtin_bswap32(x[2 * i + 1]);
+    w[5 + i] = ((uint64_t)__builtin_bswap32(y[2 * i]) << 32) | __builtin_bswap32(y[2 * i + 1]);
+  }
+  w[4] = __builtin_bswap64(round);
+  w[9] = 0x8000000000000000ULL;
+#pragma unroll
+  for (int i = 10; i < 15; ++i) w[i] = 0;
+  w[15] = 72 * 8;
+  sha512_init(st);
+  sha512_compress(st, w);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    out[2 * i] = __builtin_bswap32((uint32_t)(st[i] >> 32));
+    out[2 * i + 1] = __builtin_bswap32((uint32_t)st[i]);
+  }
+}
+
 }  // namespace nw

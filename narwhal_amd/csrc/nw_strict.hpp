@@ -55,6 +55,33 @@ NW_HD bool small_order_by_y(const fe& y, const fe small_y[5]) {
   return hit;
 }
 
+// The torsion subgroup E[8] of edwards25519 is cyclic of order 8: x[j], y[j] = the affine
+// (canonical) coordinates of [j] T8, j = 0..7, for the order-8 point T8 with y = y8 and
+// x >= 0 (nw_consts.hpp compute_torsion). torsion_index names a point of E[8] by its j, so
+// sums of torsion points become sums of indices mod 8.
+struct torsion_consts {
+  fe x[8], y[8];
+};
+// j with P == [j] T8 (projective compare), or -1 when P is not a torsion point.
+NW_HD int torsion_index(const ge& P, const torsion_consts& tc) {
+  int r = -1;
+#pragma unroll 1
+  for (int j = 0; j < 8; ++j) {
+    fe a, b;
+    fe_mul(a, tc.x[j], P.Z);
+    fe_mul(b, tc.y[j], P.Z);
+    if (fe_eq(a, P.X) && fe_eq(b, P.Y)) r = j;
+  }
+  return r;
+}
+
+// Committee-key flag word (nw_kernels.h key_tables_t::ok): bit 0 = the key decodes, bit 1 =
+// small order (8A == identity), bits 2..4 = lambda with [l] A == [lambda] T8 (the image of the
+// key's torsion component; 0 iff A lies in the prime-order subgroup). dalek's verify_batch
+// weights A by (z k mod l), not z k, so a key with lambda != 0 adds [-(z k div l) lambda] T8
+// to the batch sum even for a vote that passes its strict check.
+constexpr uint32_t kKeyDecoded = 1u, kKeySmall = 2u, kKeyLambdaShift = 2u, kKeyLambdaMask = 0x1cu;
+
 NW_HD int digit4_of(const uint32_t* w, int nwords, int j) {
   uint32_t word = w[0];
   for (int t = 1; t < 8; ++t) word = (t < nwords && (j >> 3) == t) ? w[t] : word;
@@ -457,13 +484,16 @@ template <class BComb, class KeyTab, class Src, class PF = pf_none>
 NW_HD uint32_t keyed_vote_check(const Src& src, const strict_consts& K, const BComb& bc,
                                 const KeyTab& keytab, uint32_t keyflags, fe& X, fe& Z,
                                 const PF& pf = PF{}) {
-  const bool okA = (keyflags & 1) != 0, smallA = (keyflags & 2) != 0;
+  const bool okA = (keyflags & kKeyDecoded) != 0, smallA = (keyflags & kKeySmall) != 0;
+  // a key with a torsion component: a strict pass does not make its batch term vanish
+  // (dalek weights A by z k mod l), so its votes take the certificate's own verify_batch
+  const bool torsionA = (keyflags & kKeyLambdaMask) != 0;
   uint32_t Sw[8];
   src.S(Sw);
   sc s;
 #pragma unroll
   for (int j = 0; j < 8; ++j) s.w[j] = Sw[j];
-  if ((Sw[7] >> 29) != 0 || !okA || smallA || !sc_is_canonical(s)) return kVoteFail;
+  if ((Sw[7] >> 29) != 0 || !okA || smallA || torsionA || !sc_is_canonical(s)) return kVoteFail;
   uint32_t Rw[8];
   src.R(Rw);
   const uint32_t sign = Rw[7] >> 31;
@@ -495,7 +525,7 @@ NW_HD uint32_t keyed_vote_check(const Src& src, const strict_consts& K, const BC
 template <class BComb, class KeyTab, class Src>
 NW_HD int strict_keyed_comb(const Src& src, const strict_consts& K, const BComb& bc,
                             const KeyTab& keytab, uint32_t keyflags) {
-  const bool okA = (keyflags & 1) != 0, smallA = (keyflags & 2) != 0;
+  const bool okA = (keyflags & kKeyDecoded) != 0, smallA = (keyflags & kKeySmall) != 0;
   ge R;
   bool okR, smallR;
   {

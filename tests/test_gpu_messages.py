@@ -202,6 +202,76 @@ def test_committee_key_classes_vs_oracle():
     assert {int(x) for x in hst} >= {0, 32 + 5, 32 + 3}         # Ok, A small order, A decode
 
 
+def mixed_order_committee_certs(count: int = 16, seed: int = 77):
+    """A committee of the 4 fixture keys plus a MIXED-ORDER member A = aB + T8 (decodes, not
+    small order, [l]A = [lambda]T8 != 0). Certificates whose header is by a fixture key or by
+    A, with votes by every member; A's signatures are made with its scalar a and a nonce
+    chosen so that k = H(R||A||M) is 0 mod 8 (dalek's verify_strict ACCEPTS: R == [s]B - [k]A)
+    or not (strict rejects). dalek's verify_batch weights A by (z k mod l), so even A's
+    strict-valid votes leave [(z k mod l)]T8 in the batch sum: the certificate's verdict
+    depends on z (tested with injected z). Returns (Committee, certificates)."""
+    import hashlib
+    import struct
+    rng = np.random.Generator(np.random.PCG64(seed))
+    L = 2**252 + 27742317777372353535851937790883648493
+    keys = O.keys(4)
+    t8 = bytes.fromhex("26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05")
+    a = (int.from_bytes(rng.bytes(32), "little") % L).to_bytes(32, "little")
+    A = O.point_add(O.scalarmult_base(a), t8)
+    assert O.is_small_order(A) == 0
+
+    def sign_A(msg: bytes, k_zero: bool) -> bytes:
+        for _ in range(200):
+            sig = O.sign_raw(a, rng.bytes(32), A, msg)
+            k = int.from_bytes(O.hram(sig[:32], A, msg), "little")
+            if (k % 8 == 0) == k_zero:
+                return sig
+        raise AssertionError("no nonce found")
+
+    sk_of = dict(keys)
+    members = [pk for pk, _ in keys] + [A]
+    com = M.Committee({PublicKey(pk): M.Authority(1) for pk in members})
+    d32 = lambda b: hashlib.sha512(b).digest()[:32]
+    certs = []
+    for i in range(count):
+        author = A if i % 3 == 0 else keys[i % 4][0]
+        h = M.Header(author=PublicKey(author), round=5 + i)
+        h.id = M.Digest(d32(h.digest_bytes()))
+        hs = sign_A(h.id.value, i % 2 == 0) if author == A else O.sign(sk_of[author], h.id.value)
+        h.signature = Signature.from_bytes(hs)
+        c = M.Certificate(h)
+        cd = d32(h.id.value + struct.pack("<Q", h.round) + author)   # Certificate::digest
+        votes = []
+        for pk in members:
+            s = sign_A(cd, (i // 2) % 2 == 0) if pk == A else O.sign(sk_of[pk], cd)
+            votes.append((PublicKey(pk), Signature.from_bytes(s)))
+        c.votes = votes[i % 5:] + votes[:i % 5]            # A's vote at every position
+        certs.append(c)
+    return com, certs
+
+
+def test_committee_mixed_order_key_vs_oracle():
+    """Certificate::verify with a mixed-order committee key (mixed_order_committee_certs):
+    with injected batch coefficients every status and index equals the oracle's dalek
+    restatement, including certificates whose only irregular vote passes verify_strict
+    (k = 0 mod 8) yet fails the batch equation for most z; Header::verify too."""
+    com, certs = mixed_order_committee_certs()
+    p = M.pack_certificates(certs)
+    seen = set()
+    for zs in range(3):
+        z16 = np.random.Generator(np.random.PCG64(zs)).integers(
+            0, 256, size=(len(p["vote_pks"]), 16), dtype=np.uint8)
+        st, ix = M.verify_certificates_many(com, p, z16)
+        ost, oix = O.certificates_verify_many(com.packed(), p, z16)
+        assert st.tolist() == ost.tolist() and ix.tolist() == oix.tolist(), zs
+        seen |= {int(x) for x in ost}
+    assert seen >= {0, 32 + 7, 48 + 7}
+    hst, hix = M.verify_headers_many(com, p)
+    ohst, ohix = O.certificates_verify_many(com.packed(), p, headers_only=True)
+    assert hst.tolist() == ohst.tolist() and hix.tolist() == ohix.tolist()
+    assert {int(x) for x in ohst} >= {0, 32 + 7}
+
+
 # ---- merged certificate groups (launch_cert_groups) ------------------------------------
 def test_certificate_groups_vs_per_certificate(monkeypatch):
     """With random coefficients, Certificate::verify's vote batches are checked as one random

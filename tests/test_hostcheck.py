@@ -226,11 +226,14 @@ def test_keyed_vote_check_compressed_r(hc, golden):
     signatures by the key's owner with [s]B - [k]A == -R (same y, other x sign: dalek
     rejects them, so must the parity check)."""
     hc.hc_keyed_vote_check.restype = ctypes.c_int
+    hc.hc_key_lambda.restype = ctypes.c_int
     for it in golden["edge_corpus"]["items"]:
         m, pk, sig = (bytes.fromhex(it[k]) for k in ("msg", "pk", "sig"))
         k = O.hram(sig[:32], pk, m)
-        assert hc.hc_keyed_vote_check(_b(pk), _b(sig), _b(k)) == int(it["status"] != 0), \
-            it["class"]
+        # keys with a torsion component always fail the keyed vote check (their votes take
+        # the certificate's own verify_batch: a strict pass does not cancel their batch term)
+        want = int(it["status"] != 0 or hc.hc_key_lambda(_b(pk)) > 0)
+        assert hc.hc_keyed_vote_check(_b(pk), _b(sig), _b(k)) == want, it["class"]
     rng = np.random.Generator(np.random.PCG64(16))
     for i in range(36):
         seed = rng.bytes(32)
@@ -260,6 +263,31 @@ def test_keyed_vote_check_compressed_r(hc, golden):
         sig = R + s_ok.to_bytes(32, "little")
         assert O.verify_strict(m, pk, sig) == 0
         assert hc.hc_keyed_vote_check(_b(pk), _b(sig), _b(O.hram(R, pk, m))) == 0
+
+
+def test_key_lambda_vs_oracle(hc, golden):
+    """A committee key's lambda ([l] A == [lambda] T8, k_key_base's definition) against the
+    oracle's own scalar multiplication by l, for every decodable key of the edge corpus (the
+    eight small-order points, mixed-order keys A = aB + T8, non-canonical encodings) and
+    prime-order keys (lambda 0)."""
+    hc.hc_key_lambda.restype = ctypes.c_int
+    t8 = bytes.fromhex("26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05")
+    tors = [bytes.fromhex("01" + "00" * 31)]
+    for _ in range(7):
+        tors.append(O.point_add(tors[-1], t8))
+    l_bytes = L_ORDER.to_bytes(32, "little")
+    seen = set()
+    pks = {bytes.fromhex(it["pk"]) for it in golden["edge_corpus"]["items"]}
+    pks |= {O.keypair_from_seed(bytes([i]) * 32)[0] for i in range(4)}
+    for pk in sorted(pks):
+        lam = hc.hc_key_lambda(_b(pk))
+        if O.decompress(pk) is None:
+            assert lam == -1, pk.hex()
+            continue
+        lA = O.scalarmult(l_bytes, pk)
+        assert lA == tors[lam], (pk.hex(), lam)
+        seen.add(lam)
+    assert 0 in seen and len(seen) >= 3, seen
 
 
 def test_strict_half_random_and_tampered(hc):

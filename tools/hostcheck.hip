@@ -151,7 +151,34 @@ int hc_verify_strict_half(const uint8_t pk[32], const uint8_t sig[64], const uin
 // key flags exactly as the device does (status 3).
 static uint32_t keyed_key(ge& A, const uint32_t Aw[8]) {
   const bool dec = ge_frombytes(A, Aw, K);
-  return (dec ? 1u : 0u) | (dec && ge_is_small_order(A) ? 2u : 0u);
+  uint32_t lam = 0;
+  if (dec) {   // [l] A == [lambda] T8, as k_key_base computes it
+    static torsion_consts tc;
+    static bool have = false;
+    if (!have) { compute_torsion(tc); have = true; }
+    ge_cached Pc;
+    ge_to_cached(Pc, A, K.d2);
+    ge acc;
+    ge_identity(acc);
+    for (int bit = 252; bit >= 0; --bit) {
+      ge_dbl(acc, acc, true);
+      if ((L_W[bit >> 5] >> (bit & 31)) & 1u) ge_add_cached(acc, acc, Pc, true);
+    }
+    const int j = torsion_index(acc, tc);
+    lam = j > 0 ? (uint32_t)j : 0u;
+  }
+  return (dec ? kKeyDecoded : 0u) | (dec && ge_is_small_order(A) ? kKeySmall : 0u) |
+         (lam << kKeyLambdaShift);
+}
+
+// lambda of a key (bits 2..4 of the flag word): [l] A == [lambda] T8; -1 if A does not decode.
+int hc_key_lambda(const uint8_t pk[32]) {
+  init();
+  uint32_t Aw[8];
+  load8(Aw, pk);
+  ge A;
+  const uint32_t f = keyed_key(A, Aw);
+  return (f & kKeyDecoded) ? (int)((f & kKeyLambdaMask) >> kKeyLambdaShift) : -1;
 }
 
 int hc_verify_strict_keyed(const uint8_t pk[32], const uint8_t sig[64], const uint8_t k32[32]) {
