@@ -22,6 +22,10 @@ $(BUILD)/nw_cert.o: $(CSRC)/nw_cert.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(BUILD)/nw_small.o: $(CSRC)/nw_small.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(BUILD)/nw_jobs.o: $(CSRC)/nw_jobs.cpp $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
@@ -38,7 +42,7 @@ $(BUILD)/nw_api.o: $(CSRC)/nw_api.cpp $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-$(LIB): $(BUILD)/nw_kernels.o $(BUILD)/nw_batch.o $(BUILD)/nw_cert.o $(BUILD)/nw_api.o $(BUILD)/nw_jobs.o $(BUILD)/nw_wire.o $(BUILD)/nw_service.o
+$(LIB): $(BUILD)/nw_kernels.o $(BUILD)/nw_batch.o $(BUILD)/nw_cert.o $(BUILD)/nw_small.o $(BUILD)/nw_api.o $(BUILD)/nw_jobs.o $(BUILD)/nw_wire.o $(BUILD)/nw_service.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 oracle:

@@ -192,6 +192,9 @@ int nw_job_wait(nw_job* job);
 int nw_job_notify(nw_job* job, void (*fn)(void*), void* arg);
 /* Return the job's buffers to the pool (waits first if it is still running). */
 void nw_job_release(nw_job* job);
+/* Diagnostics: Header / Vote / Certificate host-buffer jobs submitted so far by path, the
+ * small-job launch (one kernel, no copies) and the bulk pipeline. Either pointer may be NULL. */
+int nw_path_stats(uint64_t* small_jobs, uint64_t* pipeline_jobs);
 
 /* ---- aggregation service: one request per message, coalesced into device jobs ------- */
 /* The front end a crypto-gpu crate puts behind the primary's per-message checks: Core

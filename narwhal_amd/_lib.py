@@ -83,6 +83,7 @@ def lib() -> ctypes.CDLL:
         "nw_submit_votes_verify_many": ([P, P, P, P, P, P, S, P, ctypes.POINTER(P)], I),
         "nw_job_poll": ([P], I), "nw_job_wait": ([P], I),
         "nw_job_notify": ([P, NOTIFY_FN, P], I), "nw_job_release": ([P], None),
+        "nw_path_stats": ([P, P], I),
         "nw_primary_messages_verify_wire": ([P, P, P, S, P, P, P], I),
         "nw_primary_messages_scan": ([P, P, S, P, P], I),
         "nw_service_create": ([P, S, ctypes.c_uint32, S, ctypes.POINTER(P)], I),
@@ -100,6 +101,14 @@ def lib() -> ctypes.CDLL:
         fn.restype = res
     _lib = L
     return L
+
+
+def path_stats() -> tuple[int, int]:
+    """(small-job launches, bulk-pipeline jobs) of Header / Vote / Certificate host calls so
+    far (nw_path_stats)."""
+    a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    lib().nw_path_stats(ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
 
 
 def check(rc: int, what: str) -> int:

@@ -51,6 +51,9 @@ struct SharedDev {
   size_t ksaved_n = 0;         // their count; 0 = none
   hipEvent_t last = nullptr;   // completion of the last leased launch sequence
   bool last_valid = false;
+  std::vector<uint8_t> khost;  // host copy of the keys the tables hold (empty = unknown)
+  std::vector<hipEvent_t> readers;   // small jobs (ReadLease) queued since the last Lease
+  std::vector<hipEvent_t> rpool;     // recycled reader events
 };
 SharedDev g_shared[kMaxDevices];
 
@@ -561,7 +564,8 @@ uint64_t committee_hash(const nw_committee* com) {
 int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
                   const uint64_t* host_vote_offsets, int headers_only, const void* z16,
                   const uint8_t zkey32[32], void* workspace, int32_t* status, uint64_t* index,
-                  hipStream_t s, uint64_t committee_tag, const Fork* fork) {
+                  hipStream_t s, uint64_t committee_tag, const Fork* fork,
+                  const uint8_t* host_pks) {
   // the failure-rate policy is kept per committee: keyed by the committee's key
   // hash when the caller knows it, else by the committee size
   const uint64_t policy_key = committee_tag ? committee_tag : (uint64_t)com.nauth;
@@ -599,7 +603,7 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
   NW_HIP(nw::launch_key_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth, ktabs, kok,
                                s, ksaved, kflag, kforce),
          "k_key_tables");
-  lease.keys_built(com.nauth);
+  lease.keys_built(com.nauth, host_pks);
   NW_HIP(nw::launch_cert_prepare(dc, ds, headers_only, w.hdr_digest, w.authors, w.cert_digest,
                                  w.pre1, w.pre2, w.idx1, w.idx2,
                                  headers_only ? nullptr : w.vote_key, w.author_key,
@@ -733,7 +737,8 @@ size_t votes_workspace_bytes(size_t n) {
 
 int votes_pipeline(int dev, const nw_committee& com, size_t n, const uint8_t* ids,
                    const uint64_t* rounds, const uint8_t* origins, const uint8_t* authors,
-                   const uint8_t* sigs, void* workspace, int32_t* status, hipStream_t s) {
+                   const uint8_t* sigs, void* workspace, int32_t* status, hipStream_t s,
+                   const uint8_t* host_pks) {
   if (n == 0) return 0;
   char* p = static_cast<char*>(workspace);
   uint32_t* d_dig = reinterpret_cast<uint32_t*>(p); p += a256(32 * n);
@@ -764,7 +769,7 @@ int votes_pipeline(int dev, const nw_committee& com, size_t n, const uint8_t* id
                                static_cast<nw::ge_niels_pad*>(ktabs), kok, s, ksaved, kflag,
                                kforce),
          "k_key_tables");
-  lease.keys_built(com.nauth);
+  lease.keys_built(com.nauth, host_pks);
   const nw::key_tables_t kt{static_cast<nw::ge_niels_pad*>(ktabs), kok, d_key};
   NW_HIP(nw::launch_verify_strict(d_dig, 8, reinterpret_cast<const uint32_t*>(authors),
                                   reinterpret_cast<const uint32_t*>(sigs), n, d_sst, d_bm, sws, s,
@@ -919,10 +924,76 @@ int Lease::acquire(int dev_index, hipStream_t stream) {
   hipError_t e = hipSuccess;
   if (!d.last) e = hipEventCreateWithFlags(&d.last, hipEventDisableTiming);
   if (e == hipSuccess && d.last_valid) e = hipStreamWaitEvent(stream, d.last, 0);
+  // and after every small job queued since (they read the tables this holder may rewrite);
+  // a wait binds to the event's current record, so the events can be recycled at once
+  for (size_t i = 0; e == hipSuccess && i < d.readers.size(); ++i)
+    e = hipStreamWaitEvent(stream, d.readers[i], 0);
   if (e != hipSuccess) {
     held_ = false;
     d.m.unlock();
     return ::set_err(NW_E_DEVICE, "lease: event chain", e);
+  }
+  d.rpool.insert(d.rpool.end(), d.readers.begin(), d.readers.end());
+  d.readers.clear();
+  return 0;
+}
+
+int ReadLease::acquire(int dev_index, hipStream_t stream, const uint8_t* pks, size_t nkeys,
+                       const void** tabs, const uint32_t** ok) {
+  if (held_) return ::set_err(NW_E_INVALID_ARG, "read lease already held");
+  if (dev_index < 0 || dev_index >= kMaxDevices) return ::set_err(NW_E_INVALID_ARG, "bad device");
+  SharedDev& d = g_shared[dev_index];
+  d.m.lock();
+  if (!pks || !nkeys || d.ksaved_n != nkeys || !d.ktabs || d.khost.size() != 32 * nkeys ||
+      memcmp(d.khost.data(), pks, 32 * nkeys) != 0) {
+    d.m.unlock();
+    return 1;
+  }
+  hipError_t e = hipSuccess;
+  if (d.last_valid) e = hipStreamWaitEvent(stream, d.last, 0);
+  if (e != hipSuccess) {
+    d.m.unlock();
+    return ::set_err(NW_E_DEVICE, "read lease: event chain", e);
+  }
+  dev_ = dev_index;
+  stream_ = stream;
+  held_ = true;
+  *tabs = d.ktabs;
+  *ok = d.kok;
+  return 0;
+}
+
+int ReadLease::release() {
+  if (!held_) return 0;
+  SharedDev& d = g_shared[dev_];
+  hipEvent_t ev = nullptr;
+  hipError_t e = hipSuccess;
+  if (!d.rpool.empty()) {
+    ev = d.rpool.back();
+    d.rpool.pop_back();
+  } else {
+    e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  }
+  if (e == hipSuccess) e = hipEventRecord(ev, stream_);
+  if (e == hipSuccess) {
+    d.readers.push_back(ev);
+    if (d.readers.size() > 32) {   // keep the list short: drop readers that have finished
+      size_t keep = 0;
+      for (hipEvent_t r : d.readers) {
+        if (hipEventQuery(r) == hipErrorNotReady) d.readers[keep++] = r;
+        else d.rpool.push_back(r);
+      }
+      d.readers.resize(keep);
+    }
+  } else if (ev) {
+    d.rpool.push_back(ev);
+  }
+  held_ = false;
+  d.m.unlock();
+  // without its event a later Lease could overwrite the tables under the launch: wait
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(stream_);
+    return ::set_err(NW_E_DEVICE, "read lease: hipEventRecord", e);
   }
   return 0;
 }
@@ -953,6 +1024,7 @@ int Lease::key_tables(size_t nkeys, void** tabs, uint32_t** ok, uint32_t** saved
     d.ktabs = nullptr;
     d.kok = d.ksaved = d.kflag = nullptr;
     d.kcap = d.ksaved_n = 0;
+    d.khost.clear();
     const size_t cap = nkeys < 16 ? 16 : nkeys;   // 528 KB of comb tables per key
     hipError_t e = hipMalloc(&d.ktabs, nw::key_tables_bytes(cap));
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.kok), 4 * cap);
@@ -967,10 +1039,16 @@ int Lease::key_tables(size_t nkeys, void** tabs, uint32_t** ok, uint32_t** saved
   if (flag) *flag = d.kflag;
   if (force) *force = d.ksaved_n != nkeys;
   d.ksaved_n = 0;   // until keys_built: a failed launch leaves no tables to keep
+  d.khost.clear();
   return 0;
 }
 
-void Lease::keys_built(size_t nkeys) { g_shared[dev_].ksaved_n = nkeys; }
+void Lease::keys_built(size_t nkeys, const uint8_t* host_pks) {
+  SharedDev& d = g_shared[dev_];
+  d.ksaved_n = nkeys;
+  if (host_pks) d.khost.assign(host_pks, host_pks + 32 * nkeys);
+  else d.khost.clear();
+}
 
 int Lease::release() {
   if (!held_) return 0;

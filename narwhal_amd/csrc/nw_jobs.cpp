@@ -22,6 +22,7 @@
 // wait / notify / release act on every part, and each part delivers straight into its slice
 // of the caller's outputs.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -45,6 +46,9 @@ struct nw_job {
   size_t hcap = 0;
   char* dbuf = nullptr;   // device: same layout (+ workspace)
   size_t dcap = 0;
+  char* hdev = nullptr;   // the device's address of hbuf (small jobs read it directly)
+  uint32_t* dcnt = nullptr;   // small jobs' per-message arrival counters (kept zero)
+  size_t ccap = 0;
   struct Out {
     void* dst;
     size_t off;
@@ -134,9 +138,16 @@ int job_reserve(nw_job* j, size_t hbytes, size_t dbytes) {
     j->hbuf = nullptr;
     j->hcap = 0;
     const size_t cap = hbytes < (1u << 20) ? (1u << 20) : hbytes + hbytes / 4;
-    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&j->hbuf), cap, hipHostMallocDefault);
+    // coherent (fine-grained): small jobs' kernels read their inputs from it and write their
+    // outputs into it directly, and a recycled buffer must never be served from a GPU cache
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&j->hbuf), cap,
+                                 hipHostMallocMapped | hipHostMallocCoherent);
     if (e != hipSuccess) return set_err(NW_E_OUT_OF_MEMORY, "hipHostMalloc (job staging)", e);
     j->hcap = cap;
+    void* dp = nullptr;
+    e = hipHostGetDevicePointer(&dp, j->hbuf, 0);
+    if (e != hipSuccess) return set_err(NW_E_DEVICE, "hipHostGetDevicePointer (job staging)", e);
+    j->hdev = static_cast<char*>(dp);
   }
   if (dbytes > j->dcap) {
     if (j->dbuf) (void)hipFree(j->dbuf);
@@ -367,6 +378,209 @@ nw_committee stage_committee(nw_job* j, const CommitteeOffs& o, const nw_committ
   return d;
 }
 
+// ---- small jobs: one launch (nw_small.hip) ----------------------------------------------
+// NW_SMALL=0 turns the small-job path off, NW_SMALL=1 takes it whenever it applies whatever
+// the size (test hook); NW_SMALL_MAX_SLOTS = the largest job (signatures) it takes by default.
+int small_mode() {
+  const char* e = getenv("NW_SMALL");
+  return e && *e ? atoi(e) : -1;
+}
+uint64_t small_max_slots() {
+  const char* e = getenv("NW_SMALL_MAX_SLOTS");
+  const long long v = e && *e ? atoll(e) : 0;
+  return v > 0 ? (uint64_t)v : 4096;
+}
+// Slots per workgroup: the fewest (shortest comb chains) that keep the grid within ~2
+// workgroups per CU.
+uint32_t small_slots_per_wg(uint64_t nslots) {
+  const char* e = getenv("NW_SMALL_S");   // test hook: a fixed S (4, 8, 16, 32 or 64)
+  if (e && *e) {
+    const int s = atoi(e);
+    if (s == 4 || s == 8 || s == 16 || s == 32 || s == 64) return (uint32_t)s;
+  }
+  uint32_t S = 4;
+  while (S < 64 && (nslots + S - 1) / S > 512) S *= 2;
+  return S;
+}
+
+// Message jobs by path (nw_path_stats).
+std::atomic<uint64_t> g_small_jobs{0}, g_pipeline_jobs{0};
+
+// The per-message arrival counters of a job (device, zero; kernels leave them zero).
+int job_counters(nw_job* j, size_t n) {
+  if (n <= j->ccap) return 0;
+  if (j->dcnt) (void)hipFree(j->dcnt);
+  j->dcnt = nullptr;
+  j->ccap = 0;
+  const size_t cap = n < 4096 ? 4096 : n + n / 4;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&j->dcnt), 4 * cap);
+  if (e == hipSuccess) e = hipMemsetAsync(j->dcnt, 0, 4 * cap, j->stream);
+  if (e != hipSuccess) return set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (job counters)", e);
+  j->ccap = cap;
+  return 0;
+}
+
+// Header / Vote / Certificate checks of a small job in one launch. Returns 0 with *job set
+// when it took the job, 1 when the job does not qualify (size, committee, key tables not
+// built for this committee yet: the caller runs the ordinary pipeline, which builds them),
+// or a negative NW_E_*. cs: certificates / headers; for votes the vote arrays.
+struct VoteArrays {
+  const uint8_t *ids, *origins, *authors, *sigs;
+  const uint64_t* rounds;
+  size_t n;
+};
+int submit_small(int dev, uint32_t kind, const nw_committee* com, const nw_certificates* cs,
+                 const VoteArrays* va, const uint8_t* z16, int32_t* status_out,
+                 uint64_t* index_out, nw_job** job) {
+  const int mode = small_mode();
+  if (mode == 0) return 1;
+  const size_t na = com->nauth;
+  if (na == 0 || na > 256) return 1;
+  const size_t n = kind == nw::kSmallVotes ? va->n : cs->n;
+  if (n == 0 || n >= (1ull << 31)) return 1;
+  size_t nv = 0;
+  if (kind == nw::kSmallCerts) {
+    nv = cs->vote_offsets[n];
+    for (size_t i = 0; i < n; ++i)
+      if (cs->vote_offsets[i + 1] - cs->vote_offsets[i] > 128) return 1;   // quorum pass limit
+  }
+  const uint64_t nslots = n + nv;
+  if (mode != 1 && nslots > small_max_slots()) return 1;
+  if (nslots >= (1ull << 31)) return 1;
+  const nw::ge_niels_pad* bcomb = nullptr;
+  {
+    int rc = nw::rt::use_device(dev);
+    if (rc) return rc;
+    hipError_t e = nw::bcomb_table(&bcomb);
+    if (e != hipSuccess) return 1;   // the ordinary pipeline reports what failed
+  }
+  nw_job* j;
+  int rc = job_acquire(dev, &j);
+  if (rc) return rc;
+  Packer P;
+  const size_t nwk = com->worker_offsets[na];
+  const size_t o_pk = P.add(32 * na), o_stk = P.add(4 * na), o_wo = P.add(8 * (na + 1)),
+               o_wi = P.add(4 * nwk);
+  size_t o_hb = 0, o_ho = 0, o_pc = 0, o_id = 0, o_hs = 0, o_vp = 0, o_vs = 0, o_z = 0;
+  size_t o_rd = 0, o_or = 0, o_au = 0, o_sg = 0;
+  uint64_t hb0 = 0, hlen = 0;
+  if (kind == nw::kSmallVotes) {
+    o_id = P.add(32 * n); o_rd = P.add(8 * n); o_or = P.add(32 * n); o_au = P.add(32 * n);
+    o_sg = P.add(64 * n);
+  } else {
+    hb0 = cs->header_offsets[0];
+    hlen = cs->header_offsets[n] - hb0;
+    o_hb = P.add(hlen); o_ho = P.add(8 * (n + 1)); o_pc = P.add(4 * n); o_id = P.add(32 * n);
+    o_hs = P.add(64 * n);
+    if (kind == nw::kSmallCerts) {
+      o_vp = P.add(32 * nv); o_vs = P.add(64 * nv);
+      if (z16) o_z = P.add(16 * nv);
+    }
+  }
+  const size_t o_sl = P.add(sizeof(nw::small_slot_t) * nslots);
+  const size_t o_st = P.add(4 * n), o_ix = P.add(8 * n), hend = P.off;
+  Packer D;
+  const size_t d_mi = D.add(sizeof(nw::small_msg_info_t) * n), d_sr = D.add(4 * nslots);
+  rc = job_reserve(j, hend, D.off);
+  if (!rc) rc = job_counters(j, n);
+  if (rc) return job_abort(j, rc);
+  char* H = j->hbuf;
+  put(j, o_pk, com->pks, 32 * na);
+  put(j, o_stk, com->stakes, 4 * na);
+  put(j, o_wo, com->worker_offsets, 8 * (na + 1));
+  put(j, o_wi, com->worker_ids, 4 * nwk);
+  nw::small_slot_t* sl = reinterpret_cast<nw::small_slot_t*>(H + o_sl);
+  if (kind == nw::kSmallVotes) {
+    put(j, o_id, va->ids, 32 * n);
+    put(j, o_rd, va->rounds, 8 * n);
+    put(j, o_or, va->origins, 32 * n);
+    put(j, o_au, va->authors, 32 * n);
+    put(j, o_sg, va->sigs, 64 * n);
+    for (size_t i = 0; i < n; ++i) sl[i] = {(uint32_t)i, 0u, 0u, 1u};
+  } else {
+    put(j, o_hb, cs->header_bytes + hb0, hlen);
+    uint64_t* ho = reinterpret_cast<uint64_t*>(H + o_ho);
+    for (size_t i = 0; i <= n; ++i) ho[i] = cs->header_offsets[i] - hb0;
+    put(j, o_pc, cs->payload_counts, 4 * n);
+    put(j, o_id, cs->ids, 32 * n);
+    put(j, o_hs, cs->header_sigs, 64 * n);
+    if (kind == nw::kSmallCerts) {
+      put(j, o_vp, cs->vote_pks, 32 * nv);
+      put(j, o_vs, cs->vote_sigs, 64 * nv);
+      if (z16) put(j, o_z, z16, 16 * nv);
+      size_t s = 0;
+      for (size_t i = 0; i < n; ++i) {
+        const uint32_t v0 = (uint32_t)cs->vote_offsets[i];
+        const uint32_t q = (uint32_t)(cs->vote_offsets[i + 1] - v0);
+        for (uint32_t t = 0; t <= q; ++t) sl[s++] = {(uint32_t)i, t, v0 + (t ? t - 1 : 0), q + 1};
+      }
+    } else {
+      for (size_t i = 0; i < n; ++i) sl[i] = {(uint32_t)i, 0u, 0u, 1u};
+    }
+  }
+  char* X = j->hdev;   // the device's view of the staging buffer
+  nw::small_job_t J{};
+  J.kind = kind;
+  J.slots_per_wg = small_slots_per_wg(nslots);
+  J.nmsg = n;
+  J.nslots = nslots;
+  J.com = nw::cert_committee_t{na, reinterpret_cast<const uint32_t*>(X + o_pk),
+                               reinterpret_cast<const uint32_t*>(X + o_stk),
+                               reinterpret_cast<const uint64_t*>(X + o_wo),
+                               reinterpret_cast<const uint32_t*>(X + o_wi)};
+  if (kind == nw::kSmallVotes) {
+    J.ids = reinterpret_cast<const uint32_t*>(X + o_id);
+    J.rounds = reinterpret_cast<const uint64_t*>(X + o_rd);
+    J.origins = reinterpret_cast<const uint32_t*>(X + o_or);
+    J.authors = reinterpret_cast<const uint32_t*>(X + o_au);
+    J.sigs = reinterpret_cast<const uint32_t*>(X + o_sg);
+  } else {
+    J.hb = reinterpret_cast<const uint8_t*>(X + o_hb);
+    J.ho = reinterpret_cast<const uint64_t*>(X + o_ho);
+    J.pc = reinterpret_cast<const uint32_t*>(X + o_pc);
+    J.ids = reinterpret_cast<const uint32_t*>(X + o_id);
+    J.hsig = reinterpret_cast<const uint32_t*>(X + o_hs);
+    if (kind == nw::kSmallCerts) {
+      J.vpk = reinterpret_cast<const uint32_t*>(X + o_vp);
+      J.vsig = reinterpret_cast<const uint32_t*>(X + o_vs);
+      J.z16 = z16 ? reinterpret_cast<const uint32_t*>(X + o_z) : nullptr;
+    }
+  }
+  J.slots = reinterpret_cast<const nw::small_slot_t*>(X + o_sl);
+  J.bcomb = bcomb;
+  if (!z16) {
+    rc = nw::rt::os_random(J.zkey, 32);
+    if (rc) return job_abort(j, rc);
+  }
+  J.minfo = reinterpret_cast<nw::small_msg_info_t*>(j->dbuf + d_mi);
+  J.srec = reinterpret_cast<uint32_t*>(j->dbuf + d_sr);
+  J.mcount = j->dcnt;
+  J.status = reinterpret_cast<int32_t*>(X + o_st);
+  J.index = kind == nw::kSmallVotes ? nullptr : reinterpret_cast<uint64_t*>(X + o_ix);
+  nw::rt::ReadLease rl;
+  const void* tabs = nullptr;
+  const uint32_t* ok = nullptr;
+  rc = rl.acquire(dev, j->stream, com->pks, na, &tabs, &ok);
+  if (rc) {   // 1: no tables for this committee yet (or an error): not taken here
+    job_recycle(j);
+    return rc;
+  }
+  J.ktabs = static_cast<const nw::ge_niels_pad*>(tabs);
+  J.kok = ok;
+  hipError_t e = nw::launch_small(J, j->stream);
+  const int rrc = rl.release();
+  if (e != hipSuccess) return job_abort(j, set_err(NW_E_DEVICE, "k_small launch", e));
+  if (rrc) return job_abort(j, rrc);
+  e = hipEventRecord(j->done, j->stream);
+  if (e != hipSuccess) return job_abort(j, set_err(NW_E_DEVICE, "hipEventRecord", e));
+  j->pending = true;
+  job_out(j, status_out, o_st, 4 * n);
+  if (kind != nw::kSmallVotes) job_out(j, index_out, o_ix, 8 * n);
+  g_small_jobs.fetch_add(1, std::memory_order_relaxed);
+  *job = j;
+  return 0;
+}
+
 // Header::verify / Certificate::verify over one device: the committee and the stream are
 // packed into the job's pinned buffer (one H2D copy), then the device pipeline
 // (nw::rt::cert_pipeline: shared lease, committee key tables kept across calls, adaptive
@@ -378,6 +592,12 @@ int submit_certs(int dev, const nw_committee* com, const nw_certificates* cs, in
   if (!rc) rc = nw::rt::check_certificates(cs, headers_only, &nv);
   if (rc) return rc;
   if (cs->n && !status_out) return set_err(NW_E_INVALID_ARG, "null status_out");
+  if (cs->n) {   // a small job: one launch (nw_small.hip), when it qualifies
+    rc = submit_small(dev, headers_only ? nw::kSmallHeaders : nw::kSmallCerts, com, cs, nullptr,
+                      z16, status_out, index_out, job);
+    if (rc <= 0) return rc;
+    g_pipeline_jobs.fetch_add(1, std::memory_order_relaxed);
+  }
   nw_job* j;
   rc = job_acquire(dev, &j);
   if (rc) return rc;
@@ -447,7 +667,7 @@ int submit_certs(int dev, const nw_committee* com, const nw_certificates* cs, in
                                  nullptr, j->dbuf + o_ws,
                                  reinterpret_cast<int32_t*>(j->dbuf + o_st),
                                  reinterpret_cast<uint64_t*>(j->dbuf + o_ix), j->stream, ctag,
-                                 j->fork.s2 ? &j->fork : nullptr);
+                                 j->fork.s2 ? &j->fork : nullptr, com->pks);
   });
   if (rc) return job_abort(j, rc);
   job_out(j, status_out, o_st, 4 * n);
@@ -465,6 +685,12 @@ int submit_votes(int dev, const nw_committee* com, const uint8_t* ids, const uin
   if (rc) return rc;
   if (n && (!ids || !rounds || !origins || !authors || !sigs || !status_out))
     return set_err(NW_E_INVALID_ARG, "null pointer");
+  if (n) {   // a small job: one launch (nw_small.hip), when it qualifies
+    const VoteArrays va{ids, origins, authors, sigs, rounds, n};
+    rc = submit_small(dev, nw::kSmallVotes, com, nullptr, &va, nullptr, status_out, nullptr, job);
+    if (rc <= 0) return rc;
+    g_pipeline_jobs.fetch_add(1, std::memory_order_relaxed);
+  }
   nw_job* j;
   rc = job_acquire(dev, &j);
   if (rc) return rc;
@@ -491,7 +717,8 @@ int submit_votes(int dev, const nw_committee* com, const uint8_t* ids, const uin
     return nw::rt::votes_pipeline(dev, dcom, n, b + o_id,
                                   reinterpret_cast<const uint64_t*>(b + o_rd), b + o_or,
                                   b + o_au, b + o_sg, j->dbuf + o_ws,
-                                  reinterpret_cast<int32_t*>(j->dbuf + o_st), j->stream);
+                                  reinterpret_cast<int32_t*>(j->dbuf + o_st), j->stream,
+                                  com->pks);
   });
   if (rc) return job_abort(j, rc);
   job_out(j, status_out, o_st, 4 * n);
@@ -886,6 +1113,12 @@ int nw_job_notify(nw_job* job, void (*fn)(void*), void* arg) {
 }
 
 void nw_job_release(nw_job* job) { job_recycle(job); }
+
+int nw_path_stats(uint64_t* small_jobs, uint64_t* pipeline_jobs) {
+  if (small_jobs) *small_jobs = g_small_jobs.load(std::memory_order_relaxed);
+  if (pipeline_jobs) *pipeline_jobs = g_pipeline_jobs.load(std::memory_order_relaxed);
+  return 0;
+}
 
 // ---- blocking host-buffer entry points = submit + wait ------------------------------
 static int run_blocking(int rc, nw_job* j) {

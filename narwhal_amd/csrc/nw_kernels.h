@@ -189,4 +189,58 @@ hipError_t launch_vote_prepare(const cert_committee_t& com, uint64_t n, const ui
 hipError_t launch_vote_finalize(uint64_t n, const int32_t* pre, const int32_t* sig_status,
                                 int32_t* status, hipStream_t stream);
 
+// ---- small jobs in one launch (nw_small.hip) --------------------------------------------
+// Header / Vote / Certificate checks of a small job (the aggregation service's latency
+// path): one launch, no copies (inputs read from and outputs written to the job's pinned
+// host buffer), only read access to the committee's key tables and the B comb.
+enum : uint32_t { kSmallCerts = 0, kSmallHeaders = 1, kSmallVotes = 2 };
+// One signature ("slot"): message m, j = 0 for the header signature (or the vote's own), j >= 1
+// for certificate vote j - 1; v = global index of that vote (for j = 0 of a certificate: of
+// its first vote); cnt = slots of the message (1 + votes for a certificate, else 1).
+struct small_slot_t {
+  uint32_t m, j, v, cnt;
+};
+struct small_msg_info_t {
+  int32_t p1, p2;   // pre-signature verdicts: header level (-1 = genesis) / quorum
+  uint64_t x1, x2;
+};
+struct small_job_t {
+  uint32_t kind;           // kSmall*
+  uint32_t slots_per_wg;   // S: 4, 8, 16, 32 or 64
+  uint64_t nmsg, nslots;
+  cert_committee_t com;    // 1..256 authorities
+  // headers / certificates (nw_certificates layout; header offsets rebased to 0)
+  const uint8_t* hb;
+  const uint64_t* ho;
+  const uint32_t* pc;
+  const uint32_t* ids;     // also the votes' header ids
+  const uint32_t* hsig;
+  const uint32_t* vpk;     // certificate votes
+  const uint32_t* vsig;
+  const uint32_t* z16;     // optional injected batch coefficients (per vote)
+  // votes (Vote::verify)
+  const uint64_t* rounds;
+  const uint32_t* origins;
+  const uint32_t* authors;
+  const uint32_t* sigs;
+  const small_slot_t* slots;
+  // device: the committee's key tables (built for exactly these keys) and the B comb
+  const struct ge_niels_pad* ktabs;
+  const uint32_t* kok;
+  const struct ge_niels_pad* bcomb;
+  uint32_t zkey[8];        // ChaCha20 key of the batch coefficients when z16 is null
+  // device scratch: message info and slot records of messages spanning workgroups, and
+  // the per-message arrival counters (zero before the launch, left zero after it)
+  small_msg_info_t* minfo;
+  uint32_t* srec;
+  uint32_t* mcount;
+  // outputs (pinned host memory)
+  int32_t* status;
+  uint64_t* index;
+};
+hipError_t upload_small_consts();
+hipError_t launch_small(const small_job_t& job, hipStream_t stream);
+// The keyed comb's B tables of the current device (built on first use).
+hipError_t bcomb_table(const struct ge_niels_pad** out);
+
 }  // namespace nw

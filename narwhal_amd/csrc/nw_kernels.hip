@@ -782,6 +782,8 @@ static hipError_t btab_for_current_device(int which, const ge_niels_pad** out) {
   return hipSuccess;
 }
 
+hipError_t bcomb_table(const ge_niels_pad** out) { return btab_for_current_device(1, out); }
+
 hipError_t prepare_strict_tables() {
   const ge_niels_pad* p = nullptr;
   hipError_t e = btab_for_current_device(0, &p);
@@ -797,7 +799,8 @@ hipError_t upload_consts() {
   });
   hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_consts), &host, sizeof(host), 0,
                                    hipMemcpyHostToDevice);
-  return e != hipSuccess ? e : upload_batch_consts();
+  if (e == hipSuccess) e = upload_batch_consts();
+  return e != hipSuccess ? e : upload_small_consts();
 }
 
 static inline unsigned grid_for(uint64_t n, unsigned block) {

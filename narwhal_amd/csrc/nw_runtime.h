@@ -42,7 +42,9 @@ int check_certificates(const nw_certificates* cs, int headers_only, size_t* nvot
 // only). Queues the whole check on `s` and returns without waiting.
 size_t cert_workspace_bytes(size_t n, size_t nvotes);
 // committee_tag: identifies the committee for the failure-rate policy (committee_hash of
-// the host keys; 0 = unknown, the policy is then kept per committee size).
+// the host keys; 0 = unknown, the policy is then kept per committee size). host_pks
+// (optional): the committee's keys in host memory; the key tables built by this call are
+// then marked as theirs, for small jobs (ReadLease).
 // fork (optional): a second stream and two events of the caller's; the header checks then
 // run on fork->s2 concurrently with the vote checks on s (joined before the call returns).
 struct Fork {
@@ -52,14 +54,16 @@ struct Fork {
 int cert_pipeline(int dev, const nw_committee& dcom, const nw_certificates& dcs,
                   const uint64_t* host_vote_offsets, int headers_only, const void* z16,
                   const uint8_t zkey32[32], void* workspace, int32_t* status, uint64_t* index,
-                  hipStream_t s, uint64_t committee_tag = 0, const Fork* fork = nullptr);
+                  hipStream_t s, uint64_t committee_tag = 0, const Fork* fork = nullptr,
+                  const uint8_t* host_pks = nullptr);
 // FNV-1a over a host committee's keys (never 0).
 uint64_t committee_hash(const nw_committee* com);
 // Vote::verify for n votes (device pointers), scratch = votes_workspace_bytes(n).
 size_t votes_workspace_bytes(size_t n);
 int votes_pipeline(int dev, const nw_committee& dcom, size_t n, const uint8_t* ids,
                    const uint64_t* rounds, const uint8_t* origins, const uint8_t* authors,
-                   const uint8_t* sigs, void* workspace, int32_t* status, hipStream_t s);
+                   const uint8_t* sigs, void* workspace, int32_t* status, hipStream_t s,
+                   const uint8_t* host_pks = nullptr);
 
 // Per-device buffers shared by every caller of the library (host-buffer jobs, blocking
 // calls and nw_dev_* calls on caller streams): the strict kernel's per-lane table workspace
@@ -83,9 +87,33 @@ class Lease {
   // built from, the rebuild flag word, and whether a rebuild is forced (new size/buffers).
   int key_tables(size_t nkeys, void** tabs, uint32_t** ok, uint32_t** saved = nullptr,
                  uint32_t** flag = nullptr, bool* force = nullptr);
-  // After a successful launch_key_tables: the saved keys now describe the tables.
-  void keys_built(size_t nkeys);
+  // After a successful launch_key_tables: the saved keys now describe the tables; host_pks
+  // (nkeys x 32 bytes, optional) are those keys in host memory (small jobs compare them).
+  void keys_built(size_t nkeys, const uint8_t* host_pks = nullptr);
   // Record the chain event on the stream and unlock (idempotent). 0 or NW_E_DEVICE.
+  int release();
+
+ private:
+  int dev_ = -1;
+  hipStream_t stream_ = nullptr;
+  bool held_ = false;
+};
+
+// Read-only use of the key tables by a small job (nw_small.hip), which writes none of the
+// shared buffers: readers do not wait for each other, only for the last Lease holder (whose
+// launches may have built the tables), and every Lease holder waits for the readers queued
+// before it (their completion events). acquire() returns 0 with the tables when they hold
+// exactly the nkeys keys pks (host memory), 1 when they do not (the caller then
+// runs the ordinary pipeline, which builds them), or a negative NW_E_*. The device stays
+// locked between acquire() and release() (a launch's host time).
+class ReadLease {
+ public:
+  ReadLease() = default;
+  ReadLease(const ReadLease&) = delete;
+  ReadLease& operator=(const ReadLease&) = delete;
+  ~ReadLease() { (void)release(); }
+  int acquire(int dev_index, hipStream_t stream, const uint8_t* pks, size_t nkeys,
+              const void** tabs, const uint32_t** ok);
   int release();
 
  private:

@@ -1,0 +1,609 @@
+// nw_small.hip — Header::verify / Vote::verify / Certificate::verify of a SMALL job in one
+// launch: the latency path of the aggregation service (nw_service.cpp).
+//
+// Narwhal's primary checks one message at a time on its Core task (primary/src/core.rs:
+// 306-346: sanitize_header / sanitize_vote / sanitize_certificate call
+// primary/src/messages.rs:48-67, 131-142, 189-215 inline), so the service's jobs are mostly a
+// handful of messages. The bulk pipeline (nw_api.cpp cert_pipeline) spends a one-certificate
+// job in ~20 launches whose work is single-lane chains (keyed checks, batched inversions,
+// verify_batch planning): ~0.3 ms of device time, and every job serialises on the device
+// lease. Here one launch does the whole check, each independent chain in its own wave:
+//
+//   slot   one signature: a certificate's header signature (j = 0) and its votes (j = 1..q),
+//          a header's signature, a vote's signature. Slots are numbered in message order;
+//          workgroup w takes slots [w S, w S + S), S = 4 .. 64 (the host picks S for the
+//          job size: small S = short comb chains, large S = fewer workgroups).
+//   wave 0 decompresses R of every slot (curve25519-dalek decompress, a lane per slot): the
+//          ~255-squaring chain starts at once and runs beside everything else.
+//   wave 1 the messages whose first slot is here: Sha512(header bytes) == id, author stake,
+//          worker ids, genesis; then each certificate's vote quorum (reuse / stake / weight,
+//          lanes over its votes); a vote's author stake.
+//   wave 2 per slot: the committee index of A, the signed message M (the claimed header id,
+//          Certificate::digest, Vote::digest), k = H(R || A || M) mod l, the s checks and the
+//          comb digits of k and s.
+//   waves 2-3  R' = [s]B - [k]A: 27 table entries per slot (16 from the committee key's
+//          16-bit comb tables, 11 from the 24-bit B comb; both built once per device and
+//          committee), 128 / S lanes per slot, summed as a tree across the lanes.
+//   then   per slot: R == R' projectively and the strict status, or for a certificate vote
+//          its verify_batch record (below); the workgroup that completes a message (an
+//          arrival counter when its slots span workgroups) combines its slots in the
+//          reference's order and writes status and index straight into the job's pinned
+//          host buffer: no copies before or after the launch.
+//
+// Certificate::verify's verify_batch with no multi-scalar multiplication. dalek's equation is
+//   E = sum_i z_i R_i + (z_i k_i mod l) A_i - (sum_i z_i s_i mod l) B == identity.
+// With Delta_i = R_i - ([s_i]B - [k_i]A_i) (every vote's own residual, computed here) and
+// z_i k_i mod l = z_i k_i - q_i l:  E = sum_i z_i Delta_i - q_i [l]A_i, and [l]A_i =
+// [lambda_i]T8 is the key's torsion image (k_key_base). A Delta_i with a prime-order part
+// (8 Delta_i != 0) and z_i != 0 makes E != identity except with probability 2^-128 (the
+// reference's own soundness bound): Err. Otherwise every Delta_i = [delta_i]T8 and
+// E = [sum_i z_i delta_i - q_i lambda_i mod 8] T8 exactly, with q_i = 5 (z_i k_i - c_i) mod 8
+// (l = 5 mod 8, 5^-1 = 5 mod 8). So a certificate's status and index equal dalek's for the
+// coefficients used: injected z16, or ChaCha20 keyed from the OS CSPRNG.
+#include "nw_kernels.h"
+#include "nw_point.hpp"
+#include "nw_scalar.hpp"
+#include "nw_sha512.hpp"
+#include "nw_strict.hpp"
+#include "nw_consts.hpp"
+#include "nw_committee.hpp"
+#include "nw_chacha.hpp"
+
+#include <mutex>
+
+namespace nw {
+
+namespace {
+
+struct small_consts {
+  strict_consts sk;      // curve constants, small-order y values
+  torsion_consts tor;    // [j] T8
+};
+__constant__ small_consts g_sc;
+
+constexpr int kSlotsMax = 64;
+constexpr int kDigits = kStrictKeyTables + kBCombT;   // 16 + 11 comb entries per slot
+static_assert(kDigits == 27, "16 key-comb + 11 B-comb digits");
+
+// Per-slot record (slot_rec, s_rec).
+enum : uint32_t {
+  SR_S_HIGH = 1u,       // s has bits 253..255 set (ed25519 Signature::from_bytes)
+  SR_A_FAIL = 2u,       // the key does not decode
+  SR_S_NONCANON = 4u,   // s >= l
+  SR_R_FAIL = 8u,       // R does not decode
+  SR_PRIME = 16u,       // residual with a prime-order part (and z != 0): the batch fails
+  SR_TOR_SHIFT = 5u,    // 3 bits: z delta - q lambda mod 8
+  SR_ST_SHIFT = 8u,     // strict status (header / vote signatures)
+};
+
+struct slot_src {
+  const uint32_t* A;   // public key, 8 words
+  const uint32_t* sig; // R || s, 16 words
+};
+
+__device__ __forceinline__ void load8w(uint32_t o[8], const uint32_t* p) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = p[i];
+}
+
+__device__ __forceinline__ ge shfl_down_ge(const ge& p, int off) {
+  ge r;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    r.X.v[i] = (uint32_t)__shfl_down((int)p.X.v[i], off);
+    r.Y.v[i] = (uint32_t)__shfl_down((int)p.Y.v[i], off);
+    r.Z.v[i] = (uint32_t)__shfl_down((int)p.Z.v[i], off);
+    r.T.v[i] = (uint32_t)__shfl_down((int)p.T.v[i], off);
+  }
+  return r;
+}
+
+__device__ __forceinline__ void release_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_small(small_job_t J) {
+  __shared__ uint32_t s_pks[8 * kLdsAuth], s_stakes[kLdsAuth], s_first[kLdsAuth];
+  __shared__ small_slot_t s_slot[kSlotsMax];
+  __shared__ fe s_Rx[kSlotsMax], s_Ry[kSlotsMax];
+  __shared__ ge s_P[kSlotsMax];
+  __shared__ int32_t s_dig[kSlotsMax][kDigits + 1];
+  __shared__ uint32_t s_k[kSlotsMax][8];
+  __shared__ uint32_t s_key[kSlotsMax], s_kf[kSlotsMax], s_sfl[kSlotsMax], s_rfl[kSlotsMax];
+  __shared__ uint32_t s_rec[kSlotsMax];
+  __shared__ small_msg_info_t s_minfo[kSlotsMax];
+  __shared__ uint32_t s_ready;
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+  const uint64_t S = J.slots_per_wg;
+  const uint64_t first = (uint64_t)blockIdx.x * S;
+  const uint32_t ns = (uint32_t)(J.nslots - first < S ? J.nslots - first : S);
+  const bool certs = J.kind == kSmallCerts;
+
+  // ---- phase 0: the committee (sorted keys, stakes) and the slot table into LDS
+  const uint32_t na = (uint32_t)J.com.nauth;   // <= kLdsAuth (host check)
+  for (uint32_t k = tid; k < 8 * na; k += 256) s_pks[k] = J.com.pks[k];
+  for (uint32_t k = tid; k < na; k += 256) s_stakes[k] = J.com.stakes[k];
+  for (uint32_t k = tid; k < kLdsAuth; k += 256) s_first[k] = 0xffffffffu;
+  if (tid < ns) s_slot[tid] = J.slots[first + tid];
+  if (tid == 0) s_ready = 0;
+  __syncthreads();
+  cert_committee_t com = J.com;
+  com.pks = s_pks;
+  com.stakes = s_stakes;
+
+  if (wave == 0) {
+    // ---- wave 0: R of every slot (dalek decompress; x sign, y taken unreduced)
+    if (lane < ns) {
+      const small_slot_t sl = s_slot[lane];
+      const uint32_t* sig = certs ? (sl.j ? J.vsig + 16 * (uint64_t)sl.v : J.hsig + 16 * (uint64_t)sl.m)
+                                  : (J.kind == kSmallHeaders ? J.hsig : J.sigs) + 16 * (uint64_t)sl.m;
+      uint32_t Rw[8];
+      load8w(Rw, sig);
+      ge R;
+      const bool okR = ge_frombytes(R, Rw, g_sc.sk.k);
+      const bool smallR = small_order_by_y(R.Y, g_sc.sk.small_y);
+      s_Rx[lane] = R.X;
+      s_Ry[lane] = R.Y;
+      s_rfl[lane] = (okR ? 1u : 0u) | (smallR ? 2u : 0u);
+    }
+  } else if (wave == 1) {
+    // ---- wave 1: message-level checks of the messages whose first slot is here
+    const bool own = lane < ns && s_slot[lane].j == 0;
+    int32_t p1 = 0, p2 = 0;
+    uint64_t x1 = 0, x2 = 0;
+    uint32_t mown = own ? s_slot[lane].m : 0u;
+    if (own) {
+      const uint64_t m = mown;
+      if (J.kind == kSmallVotes) {
+        uint32_t au[8];
+        load8w(au, J.authors + 8 * m);
+        if (committee_stake(com, committee_find(com, au)) == 0) p1 = NW_DAG_UNKNOWN_AUTHORITY;
+      } else {
+        const uint8_t* h = J.hb + J.ho[m];
+        const uint64_t len = J.ho[m + 1] - J.ho[m];
+        uint32_t author[8], id[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          author[t] = ld_le32(h + 4 * t);
+          id[t] = J.ids[8 * m + t];
+        }
+        const uint64_t round = (uint64_t)ld_le32(h + 32) | ((uint64_t)ld_le32(h + 36) << 32);
+        const int a = committee_find(com, author);
+        uint32_t idor = 0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) idor |= id[t];
+        // Certificate::verify: genesis(committee).contains(self) (messages.rs:190-193)
+        if (certs && idor == 0 && round == 0 && a >= 0) {
+          p1 = -1;
+        } else {
+          // Header::verify (messages.rs:48-67), in order: id, stake, worker ids
+          uint32_t dg[8];
+          sha512_digest32_lane(h, len, dg);
+          bool id_ok = true;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) id_ok &= dg[t] == id[t];
+          if (!id_ok) {
+            p1 = NW_DAG_INVALID_HEADER_ID;
+          } else if (committee_stake(com, a) == 0) {
+            p1 = NW_DAG_UNKNOWN_AUTHORITY;
+            x1 = ~0ull;
+          } else {
+            const uint32_t np = J.pc[m];
+            const uint64_t wb = J.com.worker_offsets[a], we = J.com.worker_offsets[a + 1];
+            for (uint32_t e = 0; e < np && p1 == 0; ++e) {
+              const uint32_t wid = ld_le32(h + 40 + 36 * (uint64_t)e + 32);
+              bool found = false;
+              for (uint64_t w = wb; w < we; ++w) found |= J.com.worker_ids[w] == wid;
+              if (!found) { p1 = NW_DAG_MALFORMED_HEADER; x1 = e; }
+            }
+          }
+        }
+      }
+    }
+    if (certs) {
+      // Certificate::verify's quorum (messages.rs:196-211), per owned certificate whose
+      // header passed, lanes over its votes: reuse, then stake, first failure in vote
+      // order; else the u32 weight against 2 total / 3 + 1 (config/src/lib.rs:167-173).
+      uint32_t total = 0;
+      for (uint32_t a = lane; a < na; a += 64) total += s_stakes[a];
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) total += (uint32_t)__shfl_xor((int)total, off);
+      const uint32_t quorum = 2u * total / 3u + 1u;
+      uint64_t todo = __ballot(own && p1 == 0);
+      while (todo) {
+        const int o = __ffsll((unsigned long long)todo) - 1;
+        todo &= todo - 1;
+        const uint32_t sv = s_slot[o].v;          // the certificate's first vote
+        const uint32_t q = s_slot[o].cnt - 1;     // its votes
+        int kv[2] = {-1, -1};
+        uint32_t st[2] = {0, 0};
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+          const uint32_t v = 64u * pass + lane;
+          if (v < q) {
+            uint32_t pk[8];
+            load8w(pk, J.vpk + 8 * ((uint64_t)sv + v));
+            kv[pass] = committee_find(com, pk);
+            st[pass] = committee_stake(com, kv[pass]);
+            if (kv[pass] >= 0) atomicMin(&s_first[kv[pass]], v);
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        int32_t cp2 = 0;
+        uint64_t cx2 = 0;
+        uint32_t weight = 0;
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+          const uint32_t v = 64u * pass + lane;
+          const bool reuse = v < q && kv[pass] >= 0 && s_first[kv[pass]] < v;
+          const bool fail = v < q && (reuse || st[pass] == 0);
+          const uint64_t fm = __ballot(fail);
+          if (fm && cp2 == 0) {
+            const int f = __ffsll((unsigned long long)fm) - 1;
+            cp2 = __shfl((int)reuse, f) ? NW_DAG_AUTHORITY_REUSE : NW_DAG_UNKNOWN_AUTHORITY;
+            cx2 = 64u * pass + (uint32_t)f;
+          }
+          weight += v < q ? st[pass] : 0u;
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) weight += (uint32_t)__shfl_xor((int)weight, off);
+        if (cp2 == 0 && weight < quorum) cp2 = NW_DAG_REQUIRES_QUORUM;
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass)
+          if (64u * pass + lane < q && kv[pass] >= 0) s_first[kv[pass]] = 0xffffffffu;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        if ((int)lane == o) {
+          p2 = cp2;
+          x2 = cx2;
+        }
+      }
+    }
+    if (own) {
+      const small_msg_info_t info{p1, p2, x1, x2};
+      s_minfo[lane] = info;
+      const small_slot_t sl = s_slot[lane];
+      if ((first + lane) / S != (first + lane + sl.cnt - 1) / S) J.minfo[sl.m] = info;   // spans
+    }
+    release_vm();
+  } else {
+    // ---- wave 2: per slot, the signed message, k and the comb digits
+    if (wave == 2 && lane < ns) {
+      const small_slot_t sl = s_slot[lane];
+      const uint64_t m = sl.m;
+      const uint32_t *A, *sig;
+      uint32_t M[8];
+      if (J.kind == kSmallVotes) {
+        A = J.authors + 8 * m;
+        sig = J.sigs + 16 * m;
+        uint32_t id[8], org[8];
+        load8w(id, J.ids + 8 * m);
+        load8w(org, J.origins + 8 * m);
+        sha512_digest72(M, id, J.rounds[m], org);            // Vote::digest
+      } else {
+        const uint8_t* h = J.hb + J.ho[m];
+        A = reinterpret_cast<const uint32_t*>(h);            // header author (4-aligned)
+        if (sl.j == 0) {
+          sig = J.hsig + 16 * m;
+          load8w(M, J.ids + 8 * m);                          // Header::verify signs the id
+        } else {
+          A = J.vpk + 8 * (uint64_t)sl.v;
+          sig = J.vsig + 16 * (uint64_t)sl.v;
+          uint32_t id[8], au[8];
+          load8w(id, J.ids + 8 * m);
+#pragma unroll
+          for (int t = 0; t < 8; ++t) au[t] = ld_le32(h + 4 * t);
+          const uint64_t round = (uint64_t)ld_le32(h + 32) | ((uint64_t)ld_le32(h + 36) << 32);
+          sha512_digest72(M, id, round, au);                 // Certificate::digest
+        }
+      }
+      uint32_t Aw[8], Rw[8], Sw[8];
+      if (J.kind != kSmallVotes && sl.j == 0) {
+        const uint8_t* h = J.hb + J.ho[m];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) Aw[t] = ld_le32(h + 4 * t);
+      } else {
+        load8w(Aw, A);
+      }
+      load8w(Rw, sig);
+      load8w(Sw, sig + 8);
+      const int a = committee_find(com, Aw);
+      const uint32_t kk = a >= 0 ? (uint32_t)a : kNoKey;
+      const uint32_t kf = a >= 0 ? J.kok[a] : 0u;
+      sc s;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) s.w[t] = Sw[t];
+      const bool s_high = (Sw[7] >> 29) != 0;
+      const bool canon = sc_is_canonical(s);
+      const bool doc = a >= 0 && (kf & kKeyDecoded) && !s_high && canon;
+      if (doc) {
+        uint32_t hx[16];
+        sha512_hram96(hx, Rw, Aw, M);
+        sc k;
+        sc_reduce512(k, hx);
+        uint32_t kd[8], sd[8];
+        sc_recode(kd, k, kStrictKeyMask);
+        bdigits<kBCombW>::recode(sd, s);
+#pragma unroll
+        for (int t = 0; t < kStrictKeyTables; ++t) s_dig[lane][t] = comb_digit<kStrictKeyW>(kd, t);
+#pragma unroll
+        for (int t = 0; t < kBCombT; ++t)
+          s_dig[lane][kStrictKeyTables + t] = bdigits<kBCombW>::digit(sd, t);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) s_k[lane][t] = k.w[t];
+      }
+      s_key[lane] = kk;
+      s_kf[lane] = kf;
+      s_sfl[lane] = (s_high ? 1u : 0u) | (canon ? 0u : 2u) | (doc ? 4u : 0u);
+    }
+    if (wave == 2) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&s_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      while (__hip_atomic_load(&s_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+        __builtin_amdgcn_s_sleep(1);
+    }
+    // ---- waves 2-3: R' = [s]B - [k]A, G = 128 / S lanes per slot
+    const uint32_t G = 128u / (uint32_t)S;
+    const uint32_t c = tid - 128u, sl = c / G, g = c % G;
+    const bool live = sl < ns && (s_sfl[sl] & 4u);
+    ge acc;
+    ge_identity(acc);
+    if (live) {
+      const uint32_t kk = s_key[sl];
+      const ge_niels_pad* kt = J.ktabs + (uint64_t)kKeyTab * kk;
+#pragma unroll 1
+      for (uint32_t e = g; e < (uint32_t)kDigits; e += G) {
+        const int d = s_dig[sl][e];
+        if (d == 0) continue;
+        const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+        const bool isA = e < (uint32_t)kStrictKeyTables;
+        const ge_niels_pad* ent = isA ? kt + e * kStrictKeyN + ad
+                                      : J.bcomb + (e - kStrictKeyTables) * kBCombN + ad;
+        ge_niels nb = ent->n;
+        ge_niels_cneg(nb, isA ? d > 0 : d < 0);   // -[k]A: key digits negated
+        ge_add_niels(acc, acc, nb, true);
+      }
+    }
+    // tree over the slot's G lanes (every lane adds; a lane is read once, at the level of
+    // its lowest set bit, when it still holds its subtree's sum)
+#pragma unroll 1
+    for (uint32_t off = G >> 1; off >= 1; off >>= 1) {
+      const ge o = shfl_down_ge(acc, (int)off);
+      ge_cached oc;
+      ge_to_cached(oc, o, g_sc.sk.k.d2);
+      ge_add_cached(acc, acc, oc, true);
+    }
+    if (live && g == 0) s_P[sl] = acc;
+  }
+  __syncthreads();
+
+  // ---- per slot: R == R', the strict status or the certificate vote's batch record
+  if (wave == 2 && lane < ns) {
+    const small_slot_t sl = s_slot[lane];
+    const uint32_t kf = s_kf[lane], sfl = s_sfl[lane], rfl = s_rfl[lane];
+    const bool s_high = sfl & 1u, canon = !(sfl & 2u), doc = sfl & 4u;
+    const bool okA = kf & kKeyDecoded, smallA = kf & kKeySmall;
+    const bool okR = rfl & 1u, smallR = rfl & 2u;
+    ge R;
+    R.X = s_Rx[lane];
+    R.Y = s_Ry[lane];
+    fe_1(R.Z);
+    fe_mul(R.T, R.X, R.Y);
+    bool eq = false;
+    ge P;
+    if (doc) {
+      P = s_P[lane];
+      if (okR) eq = ge_eq_affine(P, R);
+    }
+    uint32_t rec;
+    if (certs && sl.j != 0) {
+      rec = (s_high ? SR_S_HIGH : 0u) | (okA ? 0u : SR_A_FAIL) | (canon ? 0u : SR_S_NONCANON) |
+            (okR ? 0u : SR_R_FAIL);
+      const uint32_t lam = (kf & kKeyLambdaMask) >> kKeyLambdaShift;
+      if (rec == 0 && doc && (!eq || lam != 0)) {
+        uint32_t z[4];
+        if (J.z16) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) z[t] = J.z16[4 * (uint64_t)sl.v + t];
+        } else {
+          chacha20_z(z, J.zkey, 0, sl.v);
+        }
+        if ((z[0] | z[1] | z[2] | z[3]) != 0) {
+          uint32_t delta = 0;
+          bool prime = false;
+          if (!eq) {
+            ge D, t;
+            ge_cached Pc;
+            ge_to_cached(Pc, P, g_sc.sk.k.d2);
+            ge_sub_cached(D, R, Pc, true);     // Delta = R - R'
+            ge_dbl(t, D, false);
+            ge_dbl(t, t, false);
+            ge_dbl(t, t, false);
+            if (!ge_is_identity(t)) {
+              prime = true;
+            } else {
+              const int j8 = torsion_index(D, g_sc.tor);
+              delta = j8 > 0 ? (uint32_t)j8 : 0u;
+            }
+          }
+          if (prime) {
+            rec |= SR_PRIME;
+          } else {
+            sc zs, kx, cz;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              zs.w[t] = t < 4 ? z[t] : 0u;
+              kx.w[t] = s_k[lane][t];
+            }
+            sc_mul(cz, zs, kx);                 // c = z k mod l
+            const uint32_t q = (5u * ((z[0] & 7u) * (kx.w[0] & 7u) + 8u - (cz.w[0] & 7u))) & 7u;
+            const uint32_t term = ((z[0] & 7u) * delta + 8u * 8u - q * lam) & 7u;
+            rec |= term << SR_TOR_SHIFT;
+          }
+        }
+      }
+    } else {
+      // crypto/src/lib.rs:200-204 order: s high bits, A decode, s < l, R decode, R small,
+      // A small, equation
+      const int st = s_high ? NW_ERR_S_HIGH_BITS : !okA ? NW_ERR_A_DECODE
+                   : !canon ? NW_ERR_S_NONCANONICAL : !okR ? NW_ERR_R_DECODE
+                   : smallR ? NW_ERR_R_SMALL_ORDER : smallA ? NW_ERR_A_SMALL_ORDER
+                   : eq ? NW_OK : NW_ERR_EQUATION;
+      rec = (uint32_t)st << SR_ST_SHIFT;
+    }
+    s_rec[lane] = rec;
+    const uint64_t base = first + lane - sl.j;
+    if (base / S != (base + sl.cnt - 1) / S) J.srec[first + lane] = rec;   // message spans
+    release_vm();
+  }
+  __syncthreads();
+
+  // ---- messages: the workgroup that completes one combines its slots
+  if (wave != 2) return;
+  const bool live = lane < ns;
+  const small_slot_t sl = live ? s_slot[lane] : small_slot_t{0, 0, 0, 1};
+  if (!certs) {
+    // one slot per message, always here
+    if (!live) return;
+    const small_msg_info_t info = s_minfo[lane];
+    const int st = (int)(s_rec[lane] >> SR_ST_SHIFT);
+    int32_t status = 0;
+    uint64_t index = 0;
+    if (info.p1 != 0) {
+      status = info.p1;
+      index = info.x1;
+    } else if (st != 0) {
+      status = NW_DAG_INVALID_SIGNATURE + st;
+    }
+    J.status[sl.m] = status;
+    if (J.index) J.index[sl.m] = index;
+    __threadfence_system();
+    return;
+  }
+  const uint64_t base = first + lane - sl.j;            // the message's first slot
+  const bool start = live && (lane == 0 || s_slot[lane - 1].m != sl.m);
+  const uint64_t wlo = base / S, whi = (base + sl.cnt - 1) / S;
+  const bool spans = wlo != whi;
+  if (__ballot(start && spans)) {
+    if (lane == 0) {
+      __threadfence();
+      release_vm();
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  bool last = start && !spans;
+  if (start && spans) {
+    const uint32_t expect = (uint32_t)(whi - wlo + 1);
+    const uint32_t old = atomicAdd(&J.mcount[sl.m], 1u);
+    last = old == expect - 1;
+    if (last) J.mcount[sl.m] = 0;   // no other arrival can follow: ready for the next job
+  }
+  if (__ballot(last && spans)) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    release_vm();
+  }
+  uint64_t todo = __ballot(last);
+  while (todo) {
+    const int o = __ffsll((unsigned long long)todo) - 1;
+    todo &= todo - 1;
+    const uint32_t m = s_slot[o].m;
+    const uint64_t mb = first + (uint32_t)o - s_slot[o].j;
+    const uint32_t cnt = s_slot[o].cnt;
+    auto rec_of = [&](uint64_t slot) -> uint32_t {
+      return (slot >= first && slot < first + ns) ? s_rec[slot - first] : J.srec[slot];
+    };
+    const small_msg_info_t info = (mb >= first) ? s_minfo[mb - first] : J.minfo[m];
+    int32_t status = 0;
+    uint64_t index = 0;
+    if (info.p1 < 0) {
+      status = 0;                                        // genesis
+    } else if (info.p1 > 0) {
+      status = info.p1;
+      index = info.x1;
+    } else {
+      const int hst = (int)(rec_of(mb) >> SR_ST_SHIFT);
+      if (hst != 0) {
+        status = NW_DAG_INVALID_SIGNATURE + hst;
+      } else if (info.p2 != 0) {
+        status = info.p2;
+        index = info.x2;
+      } else {
+        // verify_batch (crypto/src/lib.rs:206-219): per vote in order s high bits / A
+        // decode (first failure), then s < l over all, then R decode, then the equation
+        const uint32_t q = cnt - 1;
+        uint32_t r[2];
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+          const uint32_t v = 64u * pass + lane;
+          r[pass] = v < q ? rec_of(mb + 1 + v) : 0u;
+        }
+        int b = 0;
+        uint64_t bi = q;
+        const uint32_t cls[3] = {SR_S_HIGH | SR_A_FAIL, SR_S_NONCANON, SR_R_FAIL};
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+#pragma unroll
+          for (int pass = 0; pass < 2; ++pass) {
+            const uint64_t fm = __ballot((r[pass] & cls[c]) != 0);
+            if (fm && b == 0) {
+              const int f = __ffsll((unsigned long long)fm) - 1;
+              const uint32_t rf = (uint32_t)__shfl((int)r[pass], f);
+              b = c == 0 ? ((rf & SR_S_HIGH) ? NW_ERR_S_HIGH_BITS : NW_ERR_A_DECODE)
+                         : c == 1 ? NW_ERR_S_NONCANONICAL : NW_ERR_R_DECODE;
+              bi = 64u * pass + (uint32_t)f;
+            }
+          }
+        }
+        if (b == 0) {
+          uint32_t tor = ((r[0] >> SR_TOR_SHIFT) & 7u) + ((r[1] >> SR_TOR_SHIFT) & 7u);
+#pragma unroll
+          for (int off = 32; off >= 1; off >>= 1) tor += (uint32_t)__shfl_xor((int)tor, off);
+          if (__ballot(((r[0] | r[1]) & SR_PRIME) != 0) || (tor & 7u) != 0) {
+            b = NW_ERR_EQUATION;
+            bi = q;
+          }
+        }
+        if (b != 0) {
+          status = NW_DAG_INVALID_VOTES + b;
+          index = bi;
+        }
+      }
+    }
+    if (lane == 0) {
+      J.status[m] = status;
+      if (J.index) J.index[m] = index;
+      __threadfence_system();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------------------
+hipError_t upload_small_consts() {
+  static small_consts host;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    ge_niels b128[129];
+    compute_strict_consts(host.sk, b128);
+    compute_torsion(host.tor);
+  });
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_sc), &host, sizeof(host), 0, hipMemcpyHostToDevice);
+}
+
+hipError_t launch_small(const small_job_t& job, hipStream_t stream) {
+  if (job.nslots == 0) return hipSuccess;
+  const uint64_t S = job.slots_per_wg;
+  if (S < 4 || S > (uint64_t)kSlotsMax || (S & (S - 1)) || job.com.nauth > kLdsAuth ||
+      job.com.nauth == 0)
+    return hipErrorInvalidValue;
+  const uint64_t nwg = (job.nslots + S - 1) / S;
+  hipLaunchKernelGGL(k_small, dim3((unsigned)nwg), dim3(256), 0, stream, job);
+  return hipGetLastError();
+}
+
+}  // namespace nw
