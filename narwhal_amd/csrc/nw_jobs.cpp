@@ -22,6 +22,7 @@
 // wait / notify / release act on every part, and each part delivers straight into its slice
 // of the caller's outputs.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -388,7 +389,7 @@ int small_mode() {
 uint64_t small_max_slots() {
   const char* e = getenv("NW_SMALL_MAX_SLOTS");
   const long long v = e && *e ? atoll(e) : 0;
-  return v > 0 ? (uint64_t)v : 4096;
+  return v > 0 ? (uint64_t)v : 65536;
 }
 // Slots per workgroup: the fewest (shortest comb chains) that keep the grid within ~2
 // workgroups per CU.
@@ -567,10 +568,40 @@ int submit_small(int dev, uint32_t kind, const nw_committee* com, const nw_certi
   }
   J.ktabs = static_cast<const nw::ge_niels_pad*>(tabs);
   J.kok = ok;
+  const char* se = getenv("NW_SMALL_STAMPS");   // diagnostics: per-phase times of this launch
+  const uint64_t nwg = (nslots + J.slots_per_wg - 1) / J.slots_per_wg;
+  if (se && *se && *se != '0') (void)hipMalloc(reinterpret_cast<void**>(&J.stamps), 64 * nwg);
   hipError_t e = nw::launch_small(J, j->stream);
   const int rrc = rl.release();
   if (e != hipSuccess) return job_abort(j, set_err(NW_E_DEVICE, "k_small launch", e));
   if (rrc) return job_abort(j, rrc);
+  if (J.stamps) {
+    std::vector<uint64_t> st(8 * nwg);
+    if (hipMemcpyAsync(st.data(), J.stamps, 64 * nwg, hipMemcpyDeviceToHost, j->stream) ==
+            hipSuccess &&
+        hipStreamSynchronize(j->stream) == hipSuccess) {
+      // per phase: median over workgroups of (stamp - the workgroup's start), microseconds
+      double med[8];
+      for (int p = 0; p < 8; ++p) {
+        std::vector<double> v;
+        for (uint64_t w = 0; w < nwg; ++w)
+          if (st[8 * w + p] >= st[8 * w]) v.push_back((double)(st[8 * w + p] - st[8 * w]) * 0.01);
+        std::sort(v.begin(), v.end());
+        med[p] = v.empty() ? -1.0 : v[v.size() / 2];
+      }
+      uint64_t t0 = ~0ull, t1 = 0;
+      for (uint64_t w = 0; w < nwg; ++w) {
+        t0 = std::min(t0, st[8 * w]);
+        t1 = std::max(t1, st[8 * w + 7]);
+      }
+      fprintf(stderr, "[narwhal_amd] k_small kind=%u slots=%llu S=%u wgs=%llu: decomp %.1f msg %.1f "
+              "digits %.1f comb %.1f sync %.1f slots %.1f end %.1f us (median per workgroup); "
+              "first start -> last end %.1f us\n", kind, (unsigned long long)nslots,
+              J.slots_per_wg, (unsigned long long)nwg, med[1], med[2], med[3], med[4], med[5],
+              med[6], med[7], (double)(t1 - t0) * 0.01);
+    }
+    (void)hipFree(J.stamps);
+  }
   e = hipEventRecord(j->done, j->stream);
   if (e != hipSuccess) return job_abort(j, set_err(NW_E_DEVICE, "hipEventRecord", e));
   j->pending = true;

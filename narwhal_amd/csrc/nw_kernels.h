@@ -237,6 +237,7 @@ struct small_job_t {
   // outputs (pinned host memory)
   int32_t* status;
   uint64_t* index;
+  uint64_t* stamps;        // diagnostics (NW_SMALL_STAMPS): 8 phase times per workgroup, or null
 };
 hipError_t upload_small_consts();
 hipError_t launch_small(const small_job_t& job, hipStream_t stream);

@@ -106,6 +106,9 @@ struct Batch {
 };
 
 uint8_t g_dummy[64];
+
+// The completer polls a job this long before it blocks on it.
+constexpr int kSpinUs = 2000;
 template <class T>
 const T* nz(const std::vector<T>& v) {
   return v.empty() ? reinterpret_cast<const T*>(g_dummy) : v.data();
@@ -279,7 +282,15 @@ struct nw_service {
       int rc = b->rc;
       const Clock::time_point w0 = Clock::now();
       if (b->job) {
-        if (!rc) rc = nw_job_wait(b->job);
+        // poll first (a small job finishes in ~0.1 ms; a blocking event wait adds the
+        // runtime's wake-up latency to every verdict), then block
+        if (!rc) {
+          int done = 0;
+          const Clock::time_point spin_end = w0 + std::chrono::microseconds(kSpinUs);
+          while (!(done = nw_job_poll(b->job)) && Clock::now() < spin_end)
+            std::this_thread::yield();
+          rc = done < 0 ? done : done ? 0 : nw_job_wait(b->job);
+        }
         nw_job_release(b->job);
         b->job = nullptr;
       }

@@ -100,6 +100,15 @@ __device__ __forceinline__ ge shfl_down_ge(const ge& p, int off) {
 
 __device__ __forceinline__ void release_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// Diagnostic phase stamps (NW_SMALL_STAMPS, small_job_t::stamps): s_memrealtime (100 MHz)
+// per workgroup at the phase boundaries below, written by one lane of the wave that ends
+// the phase; no output depends on them.
+enum { ST_START = 0, ST_DECOMP, ST_MSG, ST_DIGITS, ST_COMB, ST_SYNC, ST_SLOTS, ST_END, ST_N };
+__device__ __forceinline__ void stamp(const small_job_t& J, int which) {
+  if (J.stamps && (threadIdx.x & 63) == 0)
+    J.stamps[(uint64_t)blockIdx.x * ST_N + which] = __builtin_amdgcn_s_memrealtime();
+}
+
 }  // namespace
 
 __global__ __launch_bounds__(256) void k_small(small_job_t J) {
@@ -128,6 +137,7 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
   for (uint32_t k = tid; k < kLdsAuth; k += 256) s_first[k] = 0xffffffffu;
   if (tid < ns) s_slot[tid] = J.slots[first + tid];
   if (tid == 0) s_ready = 0;
+  if (tid == 0) stamp(J, ST_START);
   __syncthreads();
   cert_committee_t com = J.com;
   com.pks = s_pks;
@@ -148,6 +158,7 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
       s_Ry[lane] = R.Y;
       s_rfl[lane] = (okR ? 1u : 0u) | (smallR ? 2u : 0u);
     }
+    stamp(J, ST_DECOMP);
   } else if (wave == 1) {
     // ---- wave 1: message-level checks of the messages whose first slot is here
     const bool own = lane < ns && s_slot[lane].j == 0;
@@ -268,6 +279,7 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
       const small_slot_t sl = s_slot[lane];
       if ((first + lane) / S != (first + lane + sl.cnt - 1) / S) J.minfo[sl.m] = info;   // spans
     }
+    stamp(J, ST_MSG);
     release_vm();
   } else {
     // ---- wave 2: per slot, the signed message, k and the comb digits
@@ -340,6 +352,7 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
       s_sfl[lane] = (s_high ? 1u : 0u) | (canon ? 0u : 2u) | (doc ? 4u : 0u);
     }
     if (wave == 2) {
+      stamp(J, ST_DIGITS);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&s_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else {
@@ -378,8 +391,10 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
       ge_add_cached(acc, acc, oc, true);
     }
     if (live && g == 0) s_P[sl] = acc;
+    if (wave == 2) stamp(J, ST_COMB);
   }
   __syncthreads();
+  if (tid == 0) stamp(J, ST_SYNC);
 
   // ---- per slot: R == R', the strict status or the certificate vote's batch record
   if (wave == 2 && lane < ns) {
@@ -460,6 +475,7 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
     if (base / S != (base + sl.cnt - 1) / S) J.srec[first + lane] = rec;   // message spans
     release_vm();
   }
+  if (wave == 2) stamp(J, ST_SLOTS);
   __syncthreads();
 
   // ---- messages: the workgroup that completes one combines its slots
@@ -482,6 +498,7 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
     J.status[sl.m] = status;
     if (J.index) J.index[sl.m] = index;
     __threadfence_system();
+    stamp(J, ST_END);
     return;
   }
   const uint64_t base = first + lane - sl.j;            // the message's first slot
@@ -579,6 +596,7 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
       __threadfence_system();
     }
   }
+  stamp(J, ST_END);
 }
 
 // ---------------------------------------------------------------------------------------
