@@ -866,6 +866,97 @@ def run_service_latency(args, rank, world, N: int, cache=None):
     return res
 
 
+def run_worker_latency(args, rank, world):
+    """the worker Processor (worker/src/processor.rs:36-54, here
+    narwhal_amd/worker.py over the aggregating VerificationService) hashing 508,052-B batches
+    that arrive at a fixed offered rate (open loop; latency = the digest message's arrival on
+    tx_digest - the batch's scheduled arrival), next to the host's SHA-512 on the same batches
+    (OpenSSL via hashlib = sha2-equivalent: one batch on 1 thread; 16 batches at once on 16
+    threads). A GPU digest is one lane walking the batch's ~3,970 blocks, so a
+    lone batch takes ~26 ms against ~0.6 ms on one core: the GPU path only pays for itself
+    when the host's cores cannot keep up."""
+    import asyncio
+    from concurrent.futures import ThreadPoolExecutor
+    from narwhal_amd import service as SV
+    from narwhal_amd import worker as WK
+    uniq = 32
+    ub = [W.worker_batch(i, seed=11 + rank).tobytes() for i in range(uniq)]
+    expect = [hashlib.sha512(b).digest()[:32] for b in ub]
+
+    async def load(rate: float, total: int):
+        svc = SV.VerificationService(max_delay=args.worker_delay)
+        store, rx, tx = WK.Store(), asyncio.Queue(), asyncio.Queue()
+        task = WK.Processor.spawn(0, store, rx, tx, True, svc)
+        loop = asyncio.get_running_loop()
+        for i in range(4):                                   # warm: pool, first job
+            await rx.put(ub[i])
+            await tx.get()
+        jobs0 = svc.jobs_submitted
+        due, lat, bad = [], [], [0]
+
+        async def produce():
+            t0 = loop.time() + 0.002
+            for i in range(total):
+                d = t0 + i / rate - loop.time()
+                if d > 0:
+                    await asyncio.sleep(d)
+                due.append(t0 + i / rate)
+                await rx.put(ub[i % uniq])
+            await rx.put(None)
+
+        async def consume():
+            for i in range(total):
+                msg = await tx.get()
+                lat.append(loop.time() - due[i])
+                if msg[4:36] != expect[i % uniq]:
+                    bad[0] += 1
+        t_start = loop.time()
+        await asyncio.gather(produce(), consume(), task)
+        el = loop.time() - t_start
+        a = np.array(lat) * 1e3
+        return {"offered_batches_per_s": rate, "batches": total,
+                "achieved_batches_per_s": total / el,
+                "p50_ms": float(np.percentile(a, 50)), "p99_ms": float(np.percentile(a, 99)),
+                "max_ms": float(a.max()), "jobs": svc.jobs_submitted - jobs0,
+                "batches_per_job": total / max(1, svc.jobs_submitted - jobs0),
+                "parity": "ok" if bad[0] == 0 else f"FAIL ({bad[0]} digests differ)"}
+
+    rates = [float(x) for x in args.worker_rates.split(",") if x]
+    loads = [asyncio.run(load(r, max(20, int(min(args.worker_seconds,
+                                                   args.worker_max_batches / r) * r))))
+             for r in rates]
+    res = {"batch_bytes": W.BATCH_BYTES, "max_delay_ms": args.worker_delay * 1e3, "loads": loads,
+           "path": "worker.Processor -> VerificationService.digest -> "
+                   "nw_submit_sha512_digest32_many (one lane per batch)",
+           "parity": "ok" if all(x["parity"] == "ok" for x in loads) else "FAIL"}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        one = []
+        for i in range(100):
+            t = time.perf_counter()
+            hashlib.sha512(ub[i % uniq]).digest()
+            one.append(time.perf_counter() - t)
+        T = 16
+
+        def timed(b):
+            t = time.perf_counter()
+            hashlib.sha512(b).digest()
+            return time.perf_counter() - t
+        with ThreadPoolExecutor(T) as ex:
+            list(ex.map(timed, ub[:T]))
+            per, t0, n = [], time.perf_counter(), 0
+            while time.perf_counter() - t0 < 1.0:
+                per += list(ex.map(timed, ub[:T]))
+                n += T
+            dt = time.perf_counter() - t0
+        res["cpu_sha2_equivalent"] = {
+            "one_thread_p50_ms": float(np.percentile(one, 50) * 1e3),
+            "one_thread_p99_ms": float(np.percentile(one, 99) * 1e3),
+            "threads16_batch_p50_ms": float(np.percentile(per, 50) * 1e3),
+            "threads16_batches_per_s": n / dt, "kind": "OpenSSL SHA-512 (hashlib)",
+            "sample": "100 single batches on 1 thread; 16 batches at a time on 16 threads for 1 s"}
+    return res
+
+
 def cpu_baseline_batch(sample, seconds: float):
     """Config 1 on the host: the oracle's verify_batch (the
     dalek-equivalent restatement, crypto/src/lib.rs:206-219) on the same 10k batch --
@@ -961,6 +1052,14 @@ def summary(r: dict) -> dict:
                                                   and g(b, "cpu_baseline", "one_thread", "value") / 1e3, 1)}
     if "wire_ingest" in r:
         out["wire_Mcerts_s"] = rnd(r["wire_ingest"].get("certs_per_s", 0) / 1e6, 2)
+    if r.get("worker_latency"):
+        wl = r["worker_latency"]
+        out["worker"] = {"offered_achieved_p50ms_p99ms": [
+                             [int(x["offered_batches_per_s"]), int(x["achieved_batches_per_s"]),
+                              rnd(x["p50_ms"], 2), rnd(x["p99_ms"], 2)] for x in wl["loads"]],
+                         "cpu_1thread_ms": rnd(g(wl, "cpu_sha2_equivalent", "one_thread_p50_ms"), 3),
+                         "cpu16_batches_s": rnd(g(wl, "cpu_sha2_equivalent",
+                                                  "threads16_batches_per_s"), 0)}
     if r.get("service_latency"):
         out["service"] = {k: {"offered_achieved_p50ms_p99ms": [
                                   [int(x["offered_certs_per_s"]),
@@ -976,7 +1075,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["strict", "sha", "cert", "batch", "service"],
+    ap.add_argument("--workload", choices=["strict", "sha", "cert", "batch", "service", "worker"],
                     default="strict")
     ap.add_argument("--items-per-gpu", type=int, default=12_500_000)
     ap.add_argument("--unique", type=int, default=1 << 18)
@@ -1011,6 +1110,13 @@ def main():
     ap.add_argument("--service-producers", type=int, default=4)
     ap.add_argument("--service-delay", type=float, default=0.0005,
                     help="VerificationService max_delay (s)")
+    ap.add_argument("--no-worker", action="store_true",
+                    help="skip the worker Processor latency leg")
+    ap.add_argument("--worker-rates", default="50,500,5000")
+    ap.add_argument("--worker-seconds", type=float, default=2.0)
+    ap.add_argument("--worker-max-batches", type=float, default=2000)
+    ap.add_argument("--worker-delay", type=float, default=0.0005,
+                    help="VerificationService max_delay (s) for the worker leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -1151,6 +1257,11 @@ def main():
             result["wire_ingest"] = rw
             if rw["parity"] != "ok":
                 result["parity"] = "FAIL"
+        if not args.no_worker:
+            rwk = run_worker_latency(args, rank, world)
+            result["worker_latency"] = rwk
+            if rwk["parity"] != "ok":
+                result["parity"] = "FAIL"
         if not args.no_service:
             result["service_latency"] = {}
             for N in [int(x) for x in args.service_committees.split(",") if x]:
@@ -1200,6 +1311,16 @@ def main():
                              "parallelism": f"shard{world}"},
                   "service_latency": res,
                   "parity": "ok" if all(r["parity"] == "ok" for r in res.values()) else "FAIL"}
+    elif args.workload == "worker":
+        rw = run_worker_latency(args, rank, world)
+        last = rw["loads"][0]
+        result = {"metric": METRIC, "value": last["achieved_batches_per_s"], "unit": "batches/s",
+                  "n_gpus": world, "steps": 1, "warmup": 1, "ms_per_step": None,
+                  "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                  "dtype": "u64", "data": "synthetic",
+                  "config": {"workload": "worker_processor_latency",
+                             "parallelism": f"shard{world}"},
+                  "worker_latency": rw, "parity": rw["parity"]}
     elif args.workload == "batch":
         r1, bsample = run_batch10k(args, dev, stream, rank, world)
         result = {"metric": METRIC, "value": r1["verifies_per_s_resident"], "unit": "verifies/s",

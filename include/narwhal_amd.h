@@ -84,9 +84,16 @@ const char* nw_last_error(void);
 const char* nw_version(void);
 /* Wait for all work this thread queued on its device stream. */
 int nw_synchronize(void);
-/* Build, now, the per-device tables the engine otherwise builds on first use (the strict
- * kernel's B tables, 2.15 GB, ~0.2 s; the keyed comb's B tables, 67 MB) on the calling
- * thread's device, or on every device under NW_ALL_DEVICES. Optional: keeps the first
+/* Build, now, the per-device tables the engine otherwise builds on first use, on the
+ * calling thread's device, or on every device under NW_ALL_DEVICES: the strict kernel's B
+ * tables (2 x 8,388,609 entries of 128 B = 2.15 GB, ~0.2 s) and the keyed comb's B tables
+ * (11 x 8,388,609 entries = 11.8 GB, ~0.7 s). Besides these a device holds, per committee
+ * in use, its key tables (16 x 32,769 entries = 67 MB per key: 6.7 GB at 100 authorities,
+ * built by the first Header / Vote / Certificate call with that committee, ~0.4 s at
+ * N = 100) and the strict workspace (~0.5 GB): ~21 GB in all at N = 100. Returns 0, or
+ * NW_E_OUT_OF_MEMORY when a table does not fit; without the keyed comb or a committee's key
+ * tables, Header / Vote / Certificate calls still run, unkeyed (the strict ladder and
+ * per-certificate verify_batch: same verdicts, lower throughput). Optional: keeps the first
  * verification's latency low. hipGraph capture: nw_dev_sha512_digest32_many,
  * nw_dev_keypair_from_seed_many and nw_dev_sign_many may be captured (after one
  * uncaptured call on the device); strict / Header / Vote / Certificate launches share
@@ -166,10 +173,13 @@ int nw_submit_sha512_digest32_many(const uint8_t* data, const uint64_t* offsets,
 /* Header::verify / Vote::verify / Certificate::verify (as nw_headers_verify_many /
  * nw_votes_verify_many / nw_certificates_verify_many below; the committee and every array
  * are copied at submit). The non-blocking form of the primary's sanitize_header /
- * sanitize_vote / sanitize_certificate (primary/src/core.rs:306-346), with the same device
- * pipeline as the blocking and device entry points: the per-device committee key tables
- * (kept across jobs while the committee is unchanged), certificate grouping and the shared
- * strict workspace, all ordered by the device's lease. status_out is required. */
+ * sanitize_vote / sanitize_certificate (primary/src/core.rs:306-346). A job of up to
+ * NW_SMALL_MAX_SLOTS (default 65,536) signatures whose committee's key tables are built
+ * (1..256 authorities, <= 128 votes per certificate) is ONE kernel launch reading its
+ * inputs from the job's pinned buffer, only reading the shared tables, so such jobs run
+ * concurrently; larger jobs (or a committee's first) run the bulk pipeline: per-device
+ * committee key tables (kept across jobs while the committee is unchanged) and the shared
+ * strict workspace, ordered by the device's lease. status_out is required. */
 int nw_submit_certificates_verify_many(const struct nw_committee* committee,
                                        const struct nw_certificates* certs, const uint8_t* z16,
                                        int32_t* status_out, uint64_t* index_out, nw_job** job);
@@ -184,11 +194,13 @@ int nw_submit_votes_verify_many(const struct nw_committee* committee, const uint
 int nw_job_poll(nw_job* job);
 /* Block until done (outputs written): 0 or a runtime error. */
 int nw_job_wait(nw_job* job);
-/* Call fn(arg) from a HIP runtime thread once the job's device work has finished (e.g. to
- * wake an async task, which then calls nw_job_poll). fn must not call into this library.
- * fn runs exactly once whenever this returns 0, and never when it returns an error (on a
- * fanned-out job: one part could not be armed; the parts already armed are disarmed), so
- * the caller may free arg and fall back to nw_job_wait. */
+/* Call fn(arg) once the job's device work has finished (e.g. to wake an async task, which
+ * then calls nw_job_poll). fn runs on the library's own watcher thread, which polls a marker
+ * event recorded behind the job (the job's stream never waits for fn); the callbacks of all
+ * jobs run one after another on that thread, so fn must be short, and must not call into
+ * this library. fn runs exactly once whenever this returns 0, and never when it returns an
+ * error (on a fanned-out job: one part could not be armed; the parts already armed are
+ * disarmed), so the caller may free arg and fall back to nw_job_wait. */
 int nw_job_notify(nw_job* job, void (*fn)(void*), void* arg);
 /* Return the job's buffers to the pool (waits first if it is still running). */
 void nw_job_release(nw_job* job);
@@ -206,8 +218,11 @@ int nw_path_stats(uint64_t* small_jobs, uint64_t* pipeline_jobs);
  * nw_submit_* calls above, so the committee's key tables stay on the device across jobs)
  * once it holds max_items units (certificate = 1 + votes, batch = its votes, else 1),
  * max_delay_us after its first request, or at once while no job is in flight (an idle
- * device gains nothing from waiting); at most max_inflight jobs are queued at once (the
- * next batch keeps filling meanwhile). A second service thread waits for the jobs in
+ * device gains nothing from waiting: the submitting caller's thread then submits the job
+ * itself); among ready batches the one whose first request is oldest goes first; at most
+ * max_inflight jobs are on the device at once (the next batch keeps filling meanwhile).
+ * Small jobs (up to ~64k signatures) are single launches that do not wait for one another
+ * (nw_path_stats). A second service thread waits for the jobs in
  * order and calls fn(arg, status, index) once per accepted request: status / index as the
  * corresponding bulk call returns them (NW_DAG_* for messages, NW_ERR_* for verify /
  * verify_batch, index = the batch's fail index), or a negative NW_E_* if the job failed.

@@ -171,10 +171,11 @@ int os_random(void* buf, size_t n) {
   return 0;
 }
 
-#define NW_HIP(call, what)                                        \
-  do {                                                            \
-    hipError_t e_ = (call);                                       \
-    if (e_ != hipSuccess) return set_err(NW_E_DEVICE, what, e_);  \
+#define NW_HIP(call, what)                                                              \
+  do {                                                                                  \
+    hipError_t e_ = (call);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return set_err(e_ == hipErrorOutOfMemory ? NW_E_OUT_OF_MEMORY : NW_E_DEVICE, what, e_); \
   } while (0)
 
 hipStream_t pick_stream(void* s, DevCtx* c) {
@@ -220,7 +221,13 @@ int nw_prepare(void) {
        ++d) {
     rc = activate(d);
     if (rc) return rc;
-    NW_HIP(nw::prepare_strict_tables(), "strict table build");
+    const hipError_t e = nw::prepare_strict_tables();
+    if (e == hipErrorOutOfMemory)
+      return set_err(NW_E_OUT_OF_MEMORY,
+                     "device memory for the strict B tables (2.15 GB) or the keyed B comb "
+                     "(11.8 GB); without the comb, committee checks run without key tables",
+                     e);
+    NW_HIP(e, "strict table build");
   }
   return 0;
 }
@@ -554,6 +561,26 @@ size_t cert_workspace_bytes(size_t n, size_t nvotes) {
   return cert_ws_layout(n, nvotes, nullptr, nullptr);
 }
 
+// Key tables for a keyed pipeline, or (out of device memory for them or for the keyed B
+// comb) *use_keys = false and 0: the caller then runs unkeyed.
+static int keyed_tables_or_fallback(Lease& lease, size_t nauth, void** tabs, uint32_t** ok,
+                                    uint32_t** saved, uint32_t** flag, bool* force,
+                                    bool* use_keys) {
+  const nw::ge_niels_pad* bc = nullptr;
+  const hipError_t eb = nw::bcomb_table(&bc);
+  if (eb == hipErrorOutOfMemory) {
+    *use_keys = false;
+    return 0;
+  }
+  if (eb != hipSuccess) return ::set_err(NW_E_DEVICE, "keyed B comb build", eb);
+  const int rc = lease.key_tables(nauth, tabs, ok, saved, flag, force);
+  if (rc == NW_E_OUT_OF_MEMORY) {
+    *use_keys = false;
+    return 0;
+  }
+  return rc;
+}
+
 // The whole device pipeline; every pointer is a device pointer.
 uint64_t committee_hash(const nw_committee* com) {
   uint64_t h = 1469598103934665603ull;
@@ -596,14 +623,21 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
   uint32_t* ksaved = nullptr;
   uint32_t* kflag = nullptr;
   bool kforce = true;
-  if (!rc) rc = lease.key_tables(com.nauth, &ktabs_v, &kok, &ksaved, &kflag, &kforce);
+  // Without device memory for the keyed B comb (11.8 GB) or the committee's key tables
+  // (67 MB per key) every check still runs, unkeyed: headers through the strict ladder,
+  // votes through each certificate's own verify_batch (same statuses).
+  bool use_keys = com.nauth > 0;
+  if (!rc && use_keys) rc = keyed_tables_or_fallback(lease, com.nauth, &ktabs_v, &kok, &ksaved,
+                                                     &kflag, &kforce, &use_keys);
   if (!rc) rc = lease.strict_ws(&sws);
   if (rc) return rc;
   nw::ge_niels_pad* ktabs = static_cast<nw::ge_niels_pad*>(ktabs_v);
-  NW_HIP(nw::launch_key_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth, ktabs, kok,
-                               s, ksaved, kflag, kforce),
-         "k_key_tables");
-  lease.keys_built(com.nauth, host_pks);
+  if (use_keys) {
+    NW_HIP(nw::launch_key_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth, ktabs,
+                                 kok, s, ksaved, kflag, kforce),
+           "k_key_tables");
+    lease.keys_built(com.nauth, host_pks);
+  }
   NW_HIP(nw::launch_cert_prepare(dc, ds, headers_only, w.hdr_digest, w.authors, w.cert_digest,
                                  w.pre1, w.pre2, w.idx1, w.idx2,
                                  headers_only ? nullptr : w.vote_key, w.author_key,
@@ -615,14 +649,14 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
   // fork stream while the votes run here: the votes then do not skip header-failed
   // certificates (k_cert_ok_headers settles those after the join), and the two latency
   // chains of a small call (each a keyed check and one batched inversion) overlap.
-  const bool fork_ok = fork && fork->s2 && !headers_only && keyed_policy(com.nauth);
+  const bool fork_ok = fork && fork->s2 && !headers_only && use_keys && keyed_policy(com.nauth);
   if (fork_ok) {
     NW_HIP(hipEventRecord(fork->ev_fork, s), "hipEventRecord (fork)");
     NW_HIP(hipStreamWaitEvent(fork->s2, fork->ev_fork, 0), "hipStreamWaitEvent (fork)");
   }
   NW_HIP(nw::launch_verify_strict(reinterpret_cast<const uint32_t*>(cs.ids), 8, w.authors,
                                   reinterpret_cast<const uint32_t*>(cs.header_sigs), n, w.hdr_st,
-                                  w.bitmap, sws, fork_ok ? fork->s2 : s, &hk),
+                                  w.bitmap, sws, fork_ok ? fork->s2 : s, use_keys ? &hk : nullptr),
          "k_verify_strict (headers)");
   if (fork_ok) NW_HIP(hipEventRecord(fork->ev_join, fork->s2), "hipEventRecord (join)");
   // every exit (errors included) joins the fork stream back before the lease is released
@@ -649,7 +683,7 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
     // NW_CERT_KEYED=0 selects the merged-group policy instead (big Pippenger groups / small
     // keyed Straus groups, adaptive on the failure rate the previous calls reported),
     // NW_CERT_MERGE=0 every certificate's own verify_batch.
-    const bool keyed = keyed_policy(com.nauth);
+    const bool keyed = use_keys && keyed_policy(com.nauth);
     uint32_t* fb_dev = nullptr;
     uint32_t* fb_cnt = nullptr;
     double p_cert = 0.0;
@@ -658,6 +692,8 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
     if (keyed) {
       // the reported failure rate only sizes the fallback batches' chunks
       p_cert = group_failure_rate(dev, policy_key, s, &fb_dev, &fb_cnt);
+    } else if (!use_keys) {
+      K = 0;   // no key tables: every certificate's own verify_batch, unkeyed
     } else {
       K = nw::cert_group_size(host_vote_offsets, n, com.nauth, z16 != nullptr, kGroupDefault);
       small = getenv("NW_CERT_SMALL_K") != nullptr;
@@ -712,8 +748,8 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
                                      reinterpret_cast<const uint32_t*>(cs.vote_pks),
                                      reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
                                      static_cast<const uint32_t*>(z16), key, w.batch_ws,
-                                     w.batch_st, w.batch_idx, s, &kt, group_ok, K,
-                                     keyed ? std::max(p_cert, 1e-3) : 1.0),
+                                     w.batch_st, w.batch_idx, s, use_keys ? &kt : nullptr,
+                                     group_ok, K, keyed ? std::max(p_cert, 1e-3) : 1.0),
              "verify_batch (votes)");
     if (fb_dev)
       NW_HIP(nw::launch_group_feedback(group_ok, n, K,
@@ -762,18 +798,23 @@ int votes_pipeline(int dev, const nw_committee& com, size_t n, const uint8_t* id
   bool kforce = true;
   void* sws = nullptr;
   int rc = lease.acquire(dev, s);
-  if (!rc) rc = lease.key_tables(com.nauth, &ktabs, &kok, &ksaved, &kflag, &kforce);
+  bool use_keys = com.nauth > 0;
+  if (!rc && use_keys)
+    rc = keyed_tables_or_fallback(lease, com.nauth, &ktabs, &kok, &ksaved, &kflag, &kforce,
+                                  &use_keys);
   if (!rc) rc = lease.strict_ws(&sws);
   if (rc) return rc;
-  NW_HIP(nw::launch_key_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth,
-                               static_cast<nw::ge_niels_pad*>(ktabs), kok, s, ksaved, kflag,
-                               kforce),
-         "k_key_tables");
-  lease.keys_built(com.nauth, host_pks);
+  if (use_keys) {
+    NW_HIP(nw::launch_key_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth,
+                                 static_cast<nw::ge_niels_pad*>(ktabs), kok, s, ksaved, kflag,
+                                 kforce),
+           "k_key_tables");
+    lease.keys_built(com.nauth, host_pks);
+  }
   const nw::key_tables_t kt{static_cast<nw::ge_niels_pad*>(ktabs), kok, d_key};
   NW_HIP(nw::launch_verify_strict(d_dig, 8, reinterpret_cast<const uint32_t*>(authors),
                                   reinterpret_cast<const uint32_t*>(sigs), n, d_sst, d_bm, sws, s,
-                                  &kt),
+                                  use_keys ? &kt : nullptr),
          "k_verify_strict (votes)");
   rc = lease.release();
   if (rc) return rc;
@@ -1001,7 +1042,7 @@ int ReadLease::release() {
 int Lease::strict_ws(void** out) {
   SharedDev& d = g_shared[dev_];
   if (!d.strict_ws) {
-    hipError_t e = hipMalloc(&d.strict_ws, nw::strict_workspace_bytes());
+    hipError_t e = nw::table_malloc(&d.strict_ws, nw::strict_workspace_bytes());
     if (e != hipSuccess) {
       d.strict_ws = nullptr;
       return ::set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (strict workspace)", e);
@@ -1026,7 +1067,7 @@ int Lease::key_tables(size_t nkeys, void** tabs, uint32_t** ok, uint32_t** saved
     d.kcap = d.ksaved_n = 0;
     d.khost.clear();
     const size_t cap = nkeys < 16 ? 16 : nkeys;   // 528 KB of comb tables per key
-    hipError_t e = hipMalloc(&d.ktabs, nw::key_tables_bytes(cap));
+    hipError_t e = nw::table_malloc(&d.ktabs, nw::key_tables_bytes(cap));
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.kok), 4 * cap);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.ksaved), 32 * cap);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.kflag), 4);

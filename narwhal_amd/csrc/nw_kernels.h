@@ -17,6 +17,11 @@ struct z_key_t {
 // copies them to the current device's constant memory.
 hipError_t upload_consts();
 
+// hipMalloc for the large per-device tables (strict B tables, keyed B comb, committee key
+// tables, strict workspace). Test hook: NW_DEVICE_MEM_LIMIT=bytes makes any such allocation
+// above that size fail with hipErrorOutOfMemory, as on a device without the memory.
+hipError_t table_malloc(void** p, size_t bytes);
+
 // lengths == nullptr: offsets has n + 1 entries and message i = [offsets[i], offsets[i+1]).
 hipError_t launch_sha512_digest32(const uint8_t* data, const uint64_t* offsets,
                                   const uint64_t* lengths, uint64_t n, uint32_t* out,
@@ -66,7 +71,8 @@ constexpr uint32_t kKeyCombT = 256 / kKeyW;               // comb tables per key
 constexpr uint32_t kKeyN = (1u << (kKeyW - 1)) + 1;       // entries per table, j = 0..2^(W-1)
 constexpr uint32_t kKeyTab = kKeyCombT * kKeyN;           // entries per key
 constexpr uint32_t kKeyHalf = (128 / kKeyW) * kKeyN;      // offset of the j * 2^128 A table
-// ok[key]: bit 0 = decompressed, bit 1 = small order (8A == identity)
+// ok[key]: bit 0 = decompressed, bit 1 = small order (8A == identity), bits 2..4 = lambda
+// with [l]A == [lambda]T8 (nw_strict.hpp kKeyLambdaShift: the key's torsion image)
 size_t key_tables_bytes(uint64_t nkeys);
 // tabs: key_tables_bytes(nkeys) of device memory; ok: nkeys words. saved (nkeys x 8 words)
 // and flag (1 word), optional: the keys the tables were last built from; the tables are

@@ -745,6 +745,15 @@ static std::mutex g_btw_mu[kMaxDevIds];   // per device: devices build in parall
 static constexpr uint32_t kBtwPerHalf = bdigits<NW_BWIN>::ENTRIES;
 
 static std::atomic<ge_niels_pad*> g_bcomb[kMaxDevIds];
+
+hipError_t table_malloc(void** p, size_t bytes) {
+  *p = nullptr;
+  if (const char* e = getenv("NW_DEVICE_MEM_LIMIT")) {
+    const unsigned long long lim = strtoull(e, nullptr, 10);
+    if (lim && bytes > lim) return hipErrorOutOfMemory;
+  }
+  return hipMalloc(p, bytes);
+}
 static_assert(kStrictKeyTables == (int)kKeyCombT && kStrictKeyN == kKeyN, "keyed comb tables");
 
 // Table set `which` of the current device (0: the ladder's 2 x kBtwPerHalf; 1: the keyed
@@ -764,7 +773,7 @@ static hipError_t btab_for_current_device(int which, const ge_niels_pad** out) {
   const uint32_t shift = which ? (uint32_t)kBCombW : 128;
   void* p = nullptr;
   const uint64_t entries = (uint64_t)ntab * n;
-  e = hipMalloc(&p, entries * sizeof(ge_niels_pad));
+  e = table_malloc(&p, entries * sizeof(ge_niels_pad));
   if (e != hipSuccess) return e;
   hipStream_t s = nullptr;
   e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);

@@ -141,14 +141,19 @@ struct nw_service {
   // NW_SERVICE_DEBUG: seconds the flusher spent submitting / blocked on max_inflight, the
   // completer waiting for jobs / running callbacks (printed at destroy)
   double t_submit = 0, t_backpressure = 0, t_wait = 0, t_callbacks = 0;
-  size_t open_jobs = 0;   // submitted, callbacks not yet delivered
+  size_t open_jobs = 0;   // submitted (or being submitted), callbacks not yet delivered
+  size_t submitting = 0;  // submits in progress outside the lock
+  bool inline_submit = true;   // NW_SERVICE_INLINE=0: only the flusher submits
   std::thread flusher, completer;
 
   // Adds one request to its kind's open batch (fill copies the inputs); 0 or NW_E_*.
+  // On an idle device (no job in flight, none being submitted) the caller's thread submits
+  // the batch itself: the request reaches the device without waking the flusher thread
+  // (a futex wake-up is tens of microseconds, a third of a small job).
   template <class Fill>
   int add(Kind k, size_t units, nw_verdict_fn fn, void* arg, Fill fill) {
     if (!fn) return set_err(NW_E_INVALID_ARG, "null verdict callback");
-    std::lock_guard<std::mutex> g(m);
+    std::unique_lock<std::mutex> lk(m);
     if (stop) return set_err(NW_E_INVALID_ARG, "service is shutting down");
     Batch& b = *open[k];
     const bool first_req = b.reqs.empty();
@@ -158,9 +163,39 @@ struct nw_service {
     const size_t before = b.units;
     b.units += units;
     ++accepted;
+    if (inline_submit && open_jobs == 0 && submitting == 0 && inflight.size() < max_inflight) {
+      std::unique_ptr<Batch> fresh = take_spare(k);
+      if (fresh) {
+        std::unique_ptr<Batch> own = std::move(open[k]);
+        open[k] = std::move(fresh);
+        launch(lk, std::move(own));
+        return 0;
+      }
+    }
     // wake the flusher to arm its timer (first request) or because the batch just filled
     if (first_req || (before < max_items && b.units >= max_items)) cv_flush.notify_one();
     return 0;
+  }
+
+  // Submits b as one device job outside the lock (held on entry and on return) and queues it
+  // for the completer. The flusher and idle-device requests both come through here.
+  void launch(std::unique_lock<std::mutex>& lk, std::unique_ptr<Batch> b) {
+    ++open_jobs;
+    ++submitting;
+    lk.unlock();
+    const Clock::time_point s0 = Clock::now();
+    // the service's device choice, also when a producer's thread submits (restored after)
+    const int prev = nw_get_device();
+    if (prev != device) nw_set_device(device);
+    b->rc = submit(*b);
+    if (prev != device) nw_set_device(prev);
+    const double ds = std::chrono::duration<double>(Clock::now() - s0).count();
+    lk.lock();
+    --submitting;
+    t_submit += ds;
+    ++jobs;
+    inflight.push_back(std::move(b));
+    cv_inflight.notify_one();
   }
 
   std::unique_ptr<Batch> take_spare(Kind k) {
@@ -223,13 +258,16 @@ struct nw_service {
         const Batch& b = *open[k];
         if (b.reqs.empty()) continue;
         // flush: stopping / forced, full, its delay is over, or the device is idle (no job
-        // in flight: waiting would only add latency, nothing is gained by a bigger batch)
+        // in flight: waiting would only add latency, nothing is gained by a bigger batch).
+        // Among the ready kinds the one whose first request is oldest goes first, so a
+        // saturating certificate load cannot starve a trickle of votes or headers (the
+        // primary's Core interleaves all three, primary/src/core.rs:349-411).
         if (stop || force || b.units >= max_items || now >= b.first + delay ||
             open_jobs == 0) {
-          pick = k;
-          break;
+          if (pick < 0 || b.first < open[pick]->first) pick = k;
+        } else if (b.first + delay < wake) {
+          wake = b.first + delay;
         }
-        if (b.first + delay < wake) wake = b.first + delay;
       }
       if (pick < 0) {
         force = false;
@@ -254,16 +292,7 @@ struct nw_service {
       }
       std::unique_ptr<Batch> b = std::move(open[pick]);
       open[pick] = std::move(fresh);
-      lk.unlock();
-      const Clock::time_point s0 = Clock::now();
-      b->rc = submit(*b);
-      const double ds = std::chrono::duration<double>(Clock::now() - s0).count();
-      lk.lock();
-      t_submit += ds;
-      ++jobs;
-      ++open_jobs;
-      inflight.push_back(std::move(b));
-      cv_inflight.notify_one();
+      launch(lk, std::move(b));
     }
     flusher_done = true;
     cv_inflight.notify_all();
@@ -275,9 +304,9 @@ struct nw_service {
     for (;;) {
       cv_inflight.wait(lk, [&] { return !inflight.empty() || flusher_done; });
       if (inflight.empty()) break;
-      std::unique_ptr<Batch> b = std::move(inflight.front());
-      inflight.pop_front();
-      cv_space.notify_one();
+      // the job stays counted in `inflight` until it has finished (max_inflight jobs on the
+      // device at most); deque::push_back keeps references to existing elements valid
+      Batch* const b = inflight.front().get();
       lk.unlock();
       int rc = b->rc;
       const Clock::time_point w0 = Clock::now();
@@ -300,12 +329,15 @@ struct nw_service {
         b->reqs[i].fn(b->reqs[i].arg, rc ? rc : b->status[i], rc ? 0 : b->index[i]);
       const Clock::time_point c1 = Clock::now();
       lk.lock();
+      std::unique_ptr<Batch> own = std::move(inflight.front());
+      inflight.pop_front();
+      cv_space.notify_one();
       t_wait += std::chrono::duration<double>(c0 - w0).count();
       t_callbacks += std::chrono::duration<double>(c1 - c0).count();
       completed += n;
       if (--open_jobs == 0) cv_flush.notify_one();   // device idle: flush what has queued
-      b->clear();
-      spare[b->kind].push_back(std::move(b));
+      own->clear();
+      spare[own->kind].push_back(std::move(own));
       cv_idle.notify_all();
     }
   }
@@ -329,6 +361,7 @@ int nw_service_create(const nw_committee* committee, size_t max_items, uint32_t 
   s->max_items = max_items ? max_items : 1;
   s->delay = std::chrono::duration_cast<Clock::duration>(std::chrono::microseconds(max_delay_us));
   s->max_inflight = max_inflight ? max_inflight : 1;
+  if (const char* e = getenv("NW_SERVICE_INLINE")) s->inline_submit = atoi(e) != 0;
   if (committee) {
     const size_t na = committee->nauth, nwk = na ? committee->worker_offsets[na] : 0;
     s->has_committee = true;

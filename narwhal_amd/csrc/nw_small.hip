@@ -48,6 +48,7 @@
 #include "nw_consts.hpp"
 #include "nw_committee.hpp"
 #include "nw_chacha.hpp"
+#include "nw_lp.hpp"
 
 #include <mutex>
 
@@ -76,11 +77,6 @@ enum : uint32_t {
   SR_ST_SHIFT = 8u,     // strict status (header / vote signatures)
 };
 
-struct slot_src {
-  const uint32_t* A;   // public key, 8 words
-  const uint32_t* sig; // R || s, 16 words
-};
-
 __device__ __forceinline__ void load8w(uint32_t o[8], const uint32_t* p) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) o[i] = p[i];
@@ -99,6 +95,33 @@ __device__ __forceinline__ ge shfl_down_ge(const ge& p, int off) {
 }
 
 __device__ __forceinline__ void release_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// z^((p-5)/8) for the four field elements of a wave's rows (nw_lp.hpp: row r = one element,
+// limb k in lane 16 r + k), the addition chain of fe_pow22523: 252 squarings and 11
+// multiplications, each a limb-parallel product (a dependent chain of ~75 VALU instructions
+// instead of a 10-limb serial product on one lane). Every operand is a limb-parallel
+// product's output (the T_LP bound, tests/test_field_bounds.py) or the canonical input.
+__device__ __forceinline__ uint32_t lp_sqn(const lp_ctx& c, uint32_t x, int n) {
+#pragma unroll 1
+  for (int i = 0; i < n; ++i) x = lp_mul(c, x, x);
+  return x;
+}
+__device__ __forceinline__ uint32_t lp_pow22523(const lp_ctx& c, uint32_t z) {
+  const uint32_t z2 = lp_mul(c, z, z);                          // 2
+  uint32_t t = lp_sqn(c, z2, 2);                                // 8
+  const uint32_t z9 = lp_mul(c, t, z);                          // 9
+  const uint32_t z11 = lp_mul(c, z9, z2);                       // 11
+  t = lp_mul(c, z11, z11);                                      // 22
+  const uint32_t z5 = lp_mul(c, t, z9);                         // 2^5 - 1
+  const uint32_t z10 = lp_mul(c, lp_sqn(c, z5, 5), z5);         // 2^10 - 1
+  const uint32_t z20 = lp_mul(c, lp_sqn(c, z10, 10), z10);      // 2^20 - 1
+  t = lp_mul(c, lp_sqn(c, z20, 20), z20);                       // 2^40 - 1
+  const uint32_t z50 = lp_mul(c, lp_sqn(c, t, 10), z10);        // 2^50 - 1
+  const uint32_t z100 = lp_mul(c, lp_sqn(c, z50, 50), z50);     // 2^100 - 1
+  t = lp_mul(c, lp_sqn(c, z100, 100), z100);                    // 2^200 - 1
+  t = lp_mul(c, lp_sqn(c, t, 50), z50);                         // 2^250 - 1
+  return lp_mul(c, lp_sqn(c, t, 2), z);                         // 2^252 - 3
+}
 
 // Diagnostic phase stamps (NW_SMALL_STAMPS, small_job_t::stamps): s_memrealtime (100 MHz)
 // per workgroup at the phase boundaries below, written by one lane of the wave that ends
@@ -122,6 +145,7 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
   __shared__ uint32_t s_rec[kSlotsMax];
   __shared__ small_msg_info_t s_minfo[kSlotsMax];
   __shared__ uint32_t s_ready;
+  __shared__ uint32_t s_lp[64];   // wave 0: the limb-parallel power's rows, gathered
 
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
@@ -145,12 +169,50 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
 
   if (wave == 0) {
     // ---- wave 0: R of every slot (dalek decompress; x sign, y taken unreduced)
-    if (lane < ns) {
-      const small_slot_t sl = s_slot[lane];
-      const uint32_t* sig = certs ? (sl.j ? J.vsig + 16 * (uint64_t)sl.v : J.hsig + 16 * (uint64_t)sl.m)
-                                  : (J.kind == kSmallHeaders ? J.hsig : J.sigs) + 16 * (uint64_t)sl.m;
+    auto sig_of = [&](const small_slot_t& sl) -> const uint32_t* {
+      return certs ? (sl.j ? J.vsig + 16 * (uint64_t)sl.v : J.hsig + 16 * (uint64_t)sl.m)
+                   : (J.kind == kSmallHeaders ? J.hsig : J.sigs) + 16 * (uint64_t)sl.m;
+    };
+    if (S == 4) {
+      // four slots, one per row: the (p-5)/8 power limb-parallel (lp_pow22523), the
+      // prologue and the final step (sqrt_ratio_i's checks, x's sign) per row as usual
+      const lp_ctx c = lp_init(lane);
+      const uint32_t r = c.row;
+      uint32_t Rw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (r < ns) load8w(Rw, sig_of(s_slot[r]));
+      const curve_consts& K = g_sc.sk.k;
+      fe y, u, v, t, v3, v7, uv7, zc;
+      fe_frombytes(y, Rw);
+      ge_decomp_uv(u, v, y, K);
+      fe_sq(t, v);  fe_mul(v3, t, v);
+      fe_sq(t, v3); fe_mul(v7, t, v);
+      fe_mul(uv7, u, v7);
+      fe_canonical(zc, uv7);
+      uint32_t zl = 0;
+#pragma unroll
+      for (int i = 0; i < 10; ++i) zl = c.k == (uint32_t)i ? zc.v[i] : zl;
+      const uint32_t tl = lp_pow22523(c, zl);
+      s_lp[lane] = tl;
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      fe tp;
+#pragma unroll
+      for (int i = 0; i < 10; ++i) tp.v[i] = s_lp[16 * r + i];
+      fe_canonical(t, tp);
+      ge R;
+      R.Y = y;
+      const bool okR = fe_sqrt_ratio_finish(R.X, u, v, t, K);
+      fe_neg(t, R.X);
+      fe_cmov(R.X, t, (Rw[7] >> 31) != 0);
+      const bool smallR = small_order_by_y(R.Y, g_sc.sk.small_y);
+      if (r < ns && c.k == 0) {
+        s_Rx[r] = R.X;
+        s_Ry[r] = R.Y;
+        s_rfl[r] = (okR ? 1u : 0u) | (smallR ? 2u : 0u);
+      }
+    } else if (lane < ns) {
       uint32_t Rw[8];
-      load8w(Rw, sig);
+      load8w(Rw, sig_of(s_slot[lane]));
       ge R;
       const bool okR = ge_frombytes(R, Rw, g_sc.sk.k);
       const bool smallR = small_order_by_y(R.Y, g_sc.sk.small_y);

@@ -499,3 +499,68 @@ def test_native_service_all_kinds_asyncio_vs_oracle():
     bsg = np.array([np.frombuffer(q, np.uint8) for _, q in bad])
     assert got[-3:] == [0, int(O.verify_batch(dig, bpk, bsg)[0]), 0]
     assert got[-2] != 0
+
+
+@pytest.mark.gpu
+def test_native_service_votes_not_starved_by_certificates():
+    """Fairness of the service flusher (nw_service.cpp): a saturating stream of certificates
+    (N = 100, two producer threads, one job in flight at a time, jobs longer than max_delay)
+    plus a trickle of votes. The ready batch whose first request is oldest goes first, so
+    every vote's verdict arrives within max_delay plus a few jobs' time, not after the
+    certificate flood (enum-order picking starved them: the certificate batch is always
+    ready when a slot frees). Every verdict equals the oracle's / the construction."""
+    import threading
+    import time
+    from cert_cases import oracle_digest_many, votes_case
+    from narwhal_amd import workloads as W
+    keys = O.keys(100)
+    s = W.certificate_stream(1500, keys, lambda sk, m: C.sign_many(sk, m), oracle_digest_many,
+                             seed=61)
+    m, mst, mix = W.mutate_votes(s, np.arange(3, 1500, 100), seed=6)
+    vcom, vp, vn, vexp = votes_case(N=100, seed=62, count=60, keys=keys)
+    for k in ("pks", "stakes", "worker_offsets", "worker_ids"):
+        assert np.array_equal(vcom[k], m["committee"][k]), k
+    rows = _rows(m)
+    expect = [(int(a), int(b)) for a, b in zip(mst, mix)]
+    svc = S.NativeService(m["committee"], max_items=1 << 16, max_delay=0.0002, max_inflight=1)
+    stop = threading.Event()
+    bad_certs = []
+    done_certs = [0]
+    lock = threading.Lock()
+
+    def flood(t):
+        i = t
+        while not stop.is_set():
+            r = i % len(rows)
+
+            def cb(st, ix, r=r):
+                with lock:
+                    done_certs[0] += 1
+                    if (st, ix) != expect[r]:
+                        bad_certs.append(r)
+            svc.submit_certificate(rows[r], cb)
+            i += 2
+    lat, got = [None] * vn, [None] * vn
+    th = [threading.Thread(target=flood, args=(t,)) for t in range(2)]
+    for t in th:
+        t.start()
+    time.sleep(0.2)                                   # the flood is in full swing
+    for i in range(vn):
+        v = (vp["ids"][i].tobytes(), int(vp["rounds"][i]), vp["origins"][i].tobytes(),
+             vp["authors"][i].tobytes(), vp["sigs"][i].tobytes())
+        t0 = time.perf_counter()
+
+        def vcb(st, ix, i=i, t0=t0):
+            lat[i] = time.perf_counter() - t0
+            got[i] = st
+        svc.submit_vote(v, vcb)
+        time.sleep(0.01)
+    time.sleep(0.1)
+    stop.set()
+    for t in th:
+        t.join()
+    svc.drain()
+    svc.close()
+    assert got == [int(x) for x in vexp]
+    assert not bad_certs and done_certs[0] > 2000
+    assert max(lat) < 0.05, sorted(lat)[-5:]
