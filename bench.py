@@ -408,19 +408,23 @@ def cpu_baseline_sha(sample, seconds: float):
                 parity="ok" if ok else "FAIL")
 
 
-def cert_stream_for(args, rank, N: int, stream_cache=None):
-    """65,536 unique honest certificates for committee N (signed on the GPU), cached."""
+def cert_stream_for(args, rank, N: int, stream_cache=None, payload: int = 0):
+    """65,536 unique honest certificates for committee N (signed on the GPU), cached;
+    payload = (digest, worker id) entries per header (SURVEY 8(d) config 2's P = 32 variant:
+    +1,152 header bytes, primary/src/messages.rs:70-84)."""
     uniq = min(args.cert_unique, args.certs)
-    if stream_cache is not None and N in stream_cache:
-        return stream_cache[N]
+    key = N if payload == 0 else (N, payload)
+    if stream_cache is not None and key in stream_cache:
+        return stream_cache[key]
     keys = [(bytes(pk), bytes(sd) + bytes(pk)) for sd, pk in
             zip(W.fixture_seeds(N), C.keypair_from_seed_many(W.fixture_seeds(N)))]
-    log(f"cert stream N={N}: building {uniq} unique certificates, tiled to {args.certs}")
+    log(f"cert stream N={N} P={payload}: building {uniq} unique certificates, tiled to "
+        f"{args.certs}")
     s = W.certificate_stream(uniq, keys, lambda sk, m: C.sign_many(sk, m),
                              lambda d, o: C.sha512_digest32_many(d, o[:-1], np.diff(o)),
-                             seed=rank)
+                             payload=payload, seed=rank)
     if stream_cache is not None:
-        stream_cache[N] = s
+        stream_cache[key] = s
     return s
 
 
@@ -442,7 +446,7 @@ class ResidentCerts:
                   "ids": dev_tile(s["ids"], n), "header_sigs": dev_tile(s["header_sigs"], n),
                   "vote_pks": dev_tile(s["vote_pks"].reshape(uniq, q * 32), n).view(-1, 32),
                   "vote_sigs": dev_tile(s["vote_sigs"].reshape(uniq, q * 64), n).view(-1, 64),
-                  "payload_counts": torch.zeros(n, dtype=torch.int32, device=dev),
+                  "payload_counts": dev_tile(s["payload_counts"].astype(np.int32), n),
                   "header_offsets": torch.arange(n + 1, dtype=torch.int64, device=dev) * Lh,
                   "vote_offsets": torch.arange(n + 1, dtype=torch.int64, device=dev) * q}
         self.Cm = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
@@ -475,7 +479,8 @@ class ResidentCerts:
         return bool(torch.equal(self.st, self.exp_st) and torch.equal(self.ix, self.exp_ix))
 
 
-def run_cert(args, dev, stream, rank, world, N: int, invalid: float = 0.0, stream_cache=None):
+def run_cert(args, dev, stream, rank, world, N: int, invalid: float = 0.0, stream_cache=None,
+             payload: int = 0):
     """Config 2: Certificate::verify stream, committee N, q = 2N/3 + 1 votes per cert.
     65,536 unique certificates (signed on the GPU), tiled to --certs; no dedup/caching.
     invalid > 0: that fraction of the unique certificates (evenly spaced, so every merged
@@ -483,7 +488,7 @@ def run_cert(args, dev, stream, rank, world, N: int, invalid: float = 0.0, strea
     bits, R not on the curve); statuses AND indices are checked against the construction
     for every certificate of the tiled stream."""
     L = _lib.lib()
-    s = cert_stream_for(args, rank, N, stream_cache)
+    s = cert_stream_for(args, rank, N, stream_cache, payload)
     uniq = len(s["header_offsets"]) - 1
     exp_st_u = np.zeros(uniq, np.int32)
     exp_ix_u = np.zeros(uniq, np.uint64)
@@ -499,7 +504,8 @@ def run_cert(args, dev, stream, rank, world, N: int, invalid: float = 0.0, strea
     mac_survey = MAC_PER_STRICT_VERIFY + q * MAC_PER_BATCH_ITEM_SMALL
     mac_keyed = MAC_PER_KEYED_STRICT + q * MAC_PER_KEYED_VOTE
     ach = n * mac_keyed / (kernel_ms * 1e-3) / 1e12
-    res = {"committee": N, "quorum": q, "certs_per_gpu": n, "unique_certs": uniq,
+    res = {"committee": N, "quorum": q, "payload_entries": payload,
+           "header_bytes": int(s["header_offsets"][1]), "certs_per_gpu": n, "unique_certs": uniq,
            "invalid_fraction": float((exp_st_u != 0).mean()),
            "certs_per_s": n * world / sec, "sig_checks_per_s": n * (q + 1) * world / sec,
            "ms_per_step": sec * 1e3,
@@ -1031,7 +1037,7 @@ def summary(r: dict) -> dict:
                          "hbm_frac": rnd(g(r, "sha512", "hbm_frac")),
                          "issue_frac": rnd(g(r, "sha512", "issue_frac")),
                          "cpu_GB_s": rnd(g(r, "sha512", "cpu_baseline", "value"), 2)}
-    for leg in ("cert_stream", "cert_stream_invalid"):
+    for leg in ("cert_stream", "cert_stream_invalid", "cert_stream_p32"):
         if r.get(leg):
             out[leg + "_Mcerts_s"] = {k: rnd(v.get("certs_per_s", 0) / 1e6, 2)
                                       for k, v in r[leg].items()}
@@ -1090,6 +1096,10 @@ def main():
                     help="extra config-2 leg with this fraction of certificates carrying a bad "
                          "vote (0 = skip)")
     ap.add_argument("--committees", default="4,10,50,100")
+    ap.add_argument("--cert-payload", type=int, default=32,
+                    help="payload entries per header of the config-2 P variant")
+    ap.add_argument("--cert-payload-committees", default="4,100",
+                    help="committees of the P variant leg (empty = skip)")
     ap.add_argument("--no-cert", action="store_true", help="skip the config-2 certificate leg")
     ap.add_argument("--no-batch", action="store_true", help="skip the config-1 verify_batch leg")
     ap.add_argument("--batch-many", type=int, default=64)
@@ -1245,6 +1255,13 @@ def main():
                     if r4["parity"] != "ok":
                         result["parity"] = "FAIL"
                 cache.pop(N, None)
+            for N in [int(x) for x in args.cert_payload_committees.split(",") if x]:
+                rp, _ = run_cert(args, dev, stream, rank, world, N, stream_cache=cache,
+                                 payload=args.cert_payload)
+                result.setdefault("cert_stream_p32", {})[f"N{N}"] = rp
+                if rp["parity"] != "ok":
+                    result["parity"] = "FAIL"
+                cache.pop((N, args.cert_payload), None)
         if not args.no_batch:
             r1, bsample = run_batch10k(args, dev, stream, rank, world)
             result["verify_batch_10k"] = r1
@@ -1287,6 +1304,11 @@ def main():
                 res_alt[f"N{N}"] = run_cert_alternating(args, dev, stream, rank, world, N,
                                                         args.cert_invalid, stream_cache=cache)
             cache.pop(N, None)
+        res_p = {}
+        for N in [int(x) for x in args.cert_payload_committees.split(",") if x]:
+            res_p[f"N{N}"] = run_cert(args, dev, stream, rank, world, N, stream_cache=cache,
+                                      payload=args.cert_payload)[0]
+            cache.pop((N, args.cert_payload), None)
         last = list(res.values())[-1]
         result = {"metric": METRIC, "value": last["sig_checks_per_s"], "unit": "verifies/s",
                   "n_gpus": world, "steps": args.cert_steps, "warmup": 1,
@@ -1295,10 +1317,11 @@ def main():
                   "config": {"workload": "config2_certificate_stream",
                              "certs_per_gpu": args.certs, "parallelism": f"shard{world}"},
                   "cert_stream": res, "cert_stream_invalid": res_bad,
-                  "cert_stream_alternating": res_alt,
+                  "cert_stream_alternating": res_alt, "cert_stream_p32": res_p,
                   "parity": "ok" if all(r["parity"] == "ok" for r in
                                         list(res.values()) + list(res_bad.values()) +
-                                        list(res_alt.values())) else "FAIL"}
+                                        list(res_alt.values()) + list(res_p.values()))
+                  else "FAIL"}
     elif args.workload == "service":
         res = {f"N{N}": run_service_latency(args, rank, world, N)
                for N in [int(x) for x in args.service_committees.split(",") if x]}

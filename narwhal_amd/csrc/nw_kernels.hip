@@ -223,6 +223,11 @@ struct pf_lds {
 #ifndef NW_STRICT_WAVES
 #define NW_STRICT_WAVES 3
 #endif
+// KEYED = false: arbitrary keys only, every item through the half-size ladder (config 4,
+// nw_verify_strict_many): the instance carries neither the keyed comb branch nor the list
+// mode, so their registers and code do not weigh on the ladder. KEYED = true: committee
+// keys take the keyed comb, and `list` (the keyed fast path's leftovers) is honoured.
+template <bool KEYED>
 __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const uint32_t* __restrict__ msgs,
                                                        uint32_t msg_stride_words,
                                                        const uint32_t* __restrict__ pks,
@@ -236,6 +241,7 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
                                                        const uint32_t* __restrict__ list,
                                                        const uint32_t* __restrict__ list_count) {
   // list mode (keyed fast path's leftovers): items list[0 .. *list_count), no bitmap words
+  if (!KEYED) list = nullptr;
   if (list) n = *list_count;
 #if NW_BWIN == 8
   __shared__ ge_niels s_btab[129];
@@ -257,20 +263,21 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
     const bool active = gi < n;
     const uint64_t i = list ? list[active ? gi : n - 1] : active ? gi : n - 1;
     const strict_src_global src{pks + 8 * i, sigs + 16 * i, msgs + (uint64_t)msg_stride_words * i};
-    const uint32_t kk = keys.vote_key ? keys.vote_key[i] : kNoKey;
+    const uint32_t kk = KEYED && keys.vote_key ? keys.vote_key[i] : kNoKey;
     const ge_niels_pad* keytab = kk != kNoKey ? keys.tabs + kKeyTab * (uint64_t)kk : nullptr;
     // committee keys: [s]B - [k]A from comb tables, no ladder; others: the half-size ladder
-    const int st = keytab ? strict_keyed_comb(src, g_consts.sk, bcomb_wide{bcomb},
-                                              keytab_wide{keytab}, keys.ok[kk])
+    int st;
+    if (KEYED && keytab) {
+      st = strict_keyed_comb(src, g_consts.sk, bcomb_wide{bcomb}, keytab_wide{keytab}, keys.ok[kk]);
+    } else {
 #if NW_STRICT_PF && NW_BWIN != 8
-                          : strict_verify_core<NW_BWIN>(src, g_consts.sk, bt, tabA, tabR,
-                                                        WaveMax{},
-                                                        pf_lds{(uint32_t)__builtin_amdgcn_readfirstlane(
-                                                            threadIdx.x >> 6)});
+      st = strict_verify_core<NW_BWIN>(src, g_consts.sk, bt, tabA, tabR, WaveMax{},
+                                       pf_lds{(uint32_t)__builtin_amdgcn_readfirstlane(
+                                           threadIdx.x >> 6)});
 #else
-                          : strict_verify_core<NW_BWIN>(src, g_consts.sk, bt, tabA, tabR,
-                                                        WaveMax{});
+      st = strict_verify_core<NW_BWIN>(src, g_consts.sk, bt, tabA, tabR, WaveMax{});
 #endif
+    }
     if (active) status[i] = st;
     if (list) continue;
     const uint64_t mask = __ballot(active && st == NW_OK);
@@ -834,7 +841,7 @@ static unsigned strict_grid() {
   if (dev < 0 || dev >= 64) dev = 0;
   if (!cached[dev].load(std::memory_order_acquire)) {
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_verify_strict, 256, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_verify_strict<false>, 256, 0) !=
             hipSuccess || per_cu <= 0)
       per_cu = 1;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -864,10 +871,16 @@ hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
   if (eb == hipSuccess && kt.vote_key) eb = btab_for_current_device(1, &bcomb);
   if (eb != hipSuccess) return eb;
   const char* kf = getenv("NW_STRICT_KEYED_FAST");
-  if (!kt.vote_key || (kf && kf[0] == '0')) {
-    hipLaunchKernelGGL(k_verify_strict, dim3(grid), dim3(256), 0, stream, msgs, msg_stride_words,
-                       pks, sigs, n, status, bitmap, static_cast<ge_cached*>(workspace), kt, btw,
-                       bcomb, nullptr, nullptr);
+  if (!kt.vote_key) {
+    hipLaunchKernelGGL(k_verify_strict<false>, dim3(grid), dim3(256), 0, stream, msgs,
+                       msg_stride_words, pks, sigs, n, status, bitmap,
+                       static_cast<ge_cached*>(workspace), kt, btw, bcomb, nullptr, nullptr);
+    return hipGetLastError();
+  }
+  if (kf && kf[0] == '0') {
+    hipLaunchKernelGGL(k_verify_strict<true>, dim3(grid), dim3(256), 0, stream, msgs,
+                       msg_stride_words, pks, sigs, n, status, bitmap,
+                       static_cast<ge_cached*>(workspace), kt, btw, bcomb, nullptr, nullptr);
     return hipGetLastError();
   }
   // keyed fast path (k_strict_keyed above), slice by slice through the workspace
@@ -888,7 +901,7 @@ hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
     hipLaunchKernelGGL(k_strict_keyed_list, dim3(grid_for(ns, 256)), dim3(256), 0, stream, i0,
                        ns, vp.state, list, count);
     // the leftovers: full verification (exact status codes), the tables over the planes
-    hipLaunchKernelGGL(k_verify_strict, dim3(std::min<uint64_t>(strict_grid(), grid_for(ns, 256))),
+    hipLaunchKernelGGL(k_verify_strict<true>, dim3(std::min<uint64_t>(strict_grid(), grid_for(ns, 256))),
                        dim3(256), 0, stream, msgs, msg_stride_words, pks, sigs, ns, status,
                        bitmap, static_cast<ge_cached*>(workspace), kt, btw, bcomb, list, count);
   }
