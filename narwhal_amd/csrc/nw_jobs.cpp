@@ -1033,8 +1033,12 @@ void countdown_tick(void* p) {
 // and holds the stream until it returns; instead one watcher thread polls a marker event
 // recorded behind each armed job and calls fn(arg) as soon as that event completes, in
 // whatever order jobs finish. The stream never waits on the callback. Marker events are
-// pooled; the watcher spins briefly, then naps 20 us, while anything is armed, and sleeps
-// on a condition variable otherwise.
+// pooled. While anything is armed the watcher yields for a few polls, then naps 20 us, and
+// 200 us once nothing has completed for ~2 ms (long bulk jobs: a wakeup a tenth of a
+// millisecond late is noise, a core spinning for seconds is not); with nothing armed it
+// sleeps on a condition variable. Callbacks of all jobs run one after another on this one
+// thread. At process exit (atexit, registered after the HIP runtime's own teardown handlers
+// so it runs before them) the watcher is stopped: callbacks still armed then never run.
 struct Armed {
   int dev;
   hipEvent_t ev;
@@ -1047,6 +1051,7 @@ struct Watcher {
   std::vector<Armed> armed;        // guarded by m
   std::vector<hipEvent_t> pool[kMaxDev];   // per device, guarded by m
   bool started = false;
+  bool stopping = false, stopped = false;   // guarded by m
 
   int arm(int dev, hipStream_t s, void (*fn)(void*), void* arg) {
     int rc = nw::rt::use_device(dev);
@@ -1058,9 +1063,11 @@ struct Watcher {
         ev = pool[dev].back();
         pool[dev].pop_back();
       }
+      if (stopping) return set_err(NW_E_DEVICE, "notify during process exit");
       if (!started) {
         std::thread(&Watcher::run, this).detach();
         started = true;
+        atexit(quiesce_at_exit);
       }
     }
     hipError_t e = hipSuccess;
@@ -1091,9 +1098,14 @@ struct Watcher {
         ready.clear();
         mine.insert(mine.end(), armed.begin(), armed.end());
         armed.clear();
-        if (mine.empty()) cv.wait(g, [&] { return !armed.empty(); });
+        if (mine.empty()) cv.wait(g, [&] { return !armed.empty() || stopping; });
         mine.insert(mine.end(), armed.begin(), armed.end());
         armed.clear();
+        if (stopping) {
+          stopped = true;
+          cv.notify_all();
+          return;
+        }
       }
       size_t keep = 0;
       for (const Armed& a : mine) {
@@ -1104,14 +1116,26 @@ struct Watcher {
       mine.resize(keep);
       for (const Armed& a : ready) a.fn(a.arg);
       if (!ready.empty()) idle = 0;
-      else if (++idle > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+      else if (++idle > 64 + 100) std::this_thread::sleep_for(std::chrono::microseconds(200));
+      else if (idle > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
       else std::this_thread::yield();
     }
   }
+
+  // stop polling before the HIP runtime tears down; bounded, so a callback stuck in a
+  // finalising interpreter cannot hang the exit
+  void quiesce() {
+    std::unique_lock<std::mutex> g(m);
+    stopping = true;
+    cv.notify_all();
+    cv.wait_for(g, std::chrono::milliseconds(200), [&] { return stopped; });
+  }
+  static void quiesce_at_exit();
 };
 // never destroyed: a static destructor would destroy the condition variable the detached
 // watcher waits on (pthread_cond_destroy blocks on waiters: a hang at process exit)
 Watcher& g_watcher = *new Watcher;
+void Watcher::quiesce_at_exit() { g_watcher.quiesce(); }
 }  // namespace
 
 int nw_job_notify(nw_job* job, void (*fn)(void*), void* arg) {

@@ -13,8 +13,9 @@ rank 1), written against asyncio because the image has no Rust toolchain:
   as one device job when ``max_items`` is reached or ``max_delay`` has passed since the
   first queued request.
 * Submission never blocks the event loop on the device: inputs are staged into pinned
-  memory by ``nw_submit_*`` and completion arrives through ``nw_job_notify`` (a HIP host
-  callback that only schedules the future on the loop), the same shape as the reference's
+  memory by ``nw_submit_*`` and completion arrives through ``nw_job_notify`` (a callback on
+  the library's watcher thread, serialised with every other job's, that only schedules the
+  future on the loop; the job's stream never waits for it), the same shape as the reference's
   ``SignatureService`` (crypto/src/lib.rs:222-250: requests over a channel, replies over
   oneshot channels).
 
@@ -88,7 +89,8 @@ class Job:
                 fut.set_result(None)
 
         def _fire(_arg):
-            # HIP runtime thread: only hand the wake-up to the loop
+            # the library's watcher thread (shared by every job): only hand the wake-up
+            # to the loop
             if not loop.is_closed():
                 loop.call_soon_threadsafe(_finish)
 
