@@ -879,8 +879,9 @@ def run_worker_latency(args, rank, world):
     tx_digest - the batch's scheduled arrival), next to the host's SHA-512 on the same batches
     (OpenSSL via hashlib = sha2-equivalent: one batch on 1 thread; 16 batches at once on 16
     threads). A GPU digest is one lane walking the batch's ~3,970 blocks, so a
-    lone batch takes ~26 ms against ~0.6 ms on one core: the GPU path only pays for itself
-    when the host's cores cannot keep up."""
+    lone batch takes ~30 ms against ~0.35 ms on one core: the GPU path loses on latency at
+    every rate and on throughput unless hundreds of batches are in flight (the --worker-deep
+    load)."""
     import asyncio
     from concurrent.futures import ThreadPoolExecutor
     from narwhal_amd import service as SV
@@ -889,10 +890,10 @@ def run_worker_latency(args, rank, world):
     ub = [W.worker_batch(i, seed=11 + rank).tobytes() for i in range(uniq)]
     expect = [hashlib.sha512(b).digest()[:32] for b in ub]
 
-    async def load(rate: float, total: int):
+    async def load(rate: float, total: int, lookahead: int):
         svc = SV.VerificationService(max_delay=args.worker_delay)
         store, rx, tx = WK.Store(), asyncio.Queue(), asyncio.Queue()
-        task = WK.Processor.spawn(0, store, rx, tx, True, svc)
+        task = WK.Processor.spawn(0, store, rx, tx, True, svc, max_in_flight=lookahead)
         loop = asyncio.get_running_loop()
         for i in range(4):                                   # warm: pool, first job
             await rx.put(ub[i])
@@ -920,7 +921,7 @@ def run_worker_latency(args, rank, world):
         await asyncio.gather(produce(), consume(), task)
         el = loop.time() - t_start
         a = np.array(lat) * 1e3
-        return {"offered_batches_per_s": rate, "batches": total,
+        return {"offered_batches_per_s": rate, "batches": total, "lookahead": lookahead,
                 "achieved_batches_per_s": total / el,
                 "p50_ms": float(np.percentile(a, 50)), "p99_ms": float(np.percentile(a, 99)),
                 "max_ms": float(a.max()), "jobs": svc.jobs_submitted - jobs0,
@@ -928,9 +929,16 @@ def run_worker_latency(args, rank, world):
                 "parity": "ok" if bad[0] == 0 else f"FAIL ({bad[0]} digests differ)"}
 
     rates = [float(x) for x in args.worker_rates.split(",") if x]
+    plan = [(r, WK.Processor.MAX_IN_FLIGHT) for r in rates]
+    # the GPU's capacity needs hundreds of batches in flight (one lane per batch): one load
+    # with a deep lookahead shows the throughput the device can take, at its latency
+    for x in args.worker_deep.split(","):
+        if x:
+            r, la = x.split(":")
+            plan.append((float(r), int(la)))
     loads = [asyncio.run(load(r, max(20, int(min(args.worker_seconds,
-                                                   args.worker_max_batches / r) * r))))
-             for r in rates]
+                                                   args.worker_max_batches / r) * r)), la))
+             for r, la in plan]
     res = {"batch_bytes": W.BATCH_BYTES, "max_delay_ms": args.worker_delay * 1e3, "loads": loads,
            "path": "worker.Processor -> VerificationService.digest -> "
                    "nw_submit_sha512_digest32_many (one lane per batch)",
@@ -1125,6 +1133,8 @@ def main():
     ap.add_argument("--worker-rates", default="50,500,5000")
     ap.add_argument("--worker-seconds", type=float, default=2.0)
     ap.add_argument("--worker-max-batches", type=float, default=2000)
+    ap.add_argument("--worker-deep", default="10000:1024",
+                    help="extra worker loads rate:lookahead (Processor max_in_flight)")
     ap.add_argument("--worker-delay", type=float, default=0.0005,
                     help="VerificationService max_delay (s) for the worker leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -10,9 +10,12 @@
 // channels. A Rust crypto-gpu crate binds these entry points and completes a oneshot
 // channel from the verdict callback, so its tokio tasks never block.
 //
-// Structure: one service per committee. A request is copied into the open batch of its
-// kind under the service mutex (a few hundred bytes, no allocation in the steady state:
-// batches are recycled). A flusher thread submits a batch as ONE device job
+// Structure: one service per committee. A request reserves its place in the open batch of
+// its kind under the service mutex (offsets and its callback; no allocation in the steady
+// state: batches are recycled) and copies its signatures, keys and header bytes there after
+// releasing it, so producers copy in parallel (an N = 50 certificate is ~3.4 KB; at 10^6 per
+// second copying under the mutex was the service's limit). A batch taken for submission
+// waits for its writers to finish. A flusher thread submits a batch as ONE device job
 // (nw_submit_*: the committee-aware pipeline with its key tables kept on the device) when it
 // holds max_items units, max_delay has passed since its first request, or no job is in
 // flight (an idle device gains nothing from a bigger batch, so a lone request goes at once
@@ -25,6 +28,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -56,24 +61,54 @@ void append(std::vector<T>& v, const void* src, size_t count) {
   if (count) memcpy(v.data() + o, src, count * sizeof(T));
 }
 
+// A byte array that grows only while nobody writes into it (under the mutex, no writers):
+// requests reserve ranges under the mutex and fill them after releasing it. Not
+// zero-initialised (std::vector::resize writes every byte twice).
+struct Buf {
+  uint8_t* p = nullptr;
+  size_t n = 0, cap = 0;
+  Buf() = default;
+  Buf(const Buf&) = delete;
+  Buf& operator=(const Buf&) = delete;
+  ~Buf() { free(p); }
+  bool fits(size_t k) const { return n + k <= cap; }
+  bool grow(size_t k) {
+    const size_t c = std::max<size_t>({2 * cap, n + k, 4096});
+    void* q = realloc(p, c);
+    if (!q) return false;
+    p = static_cast<uint8_t*>(q);
+    cap = c;
+    return true;
+  }
+  uint8_t* take(size_t k) {
+    uint8_t* d = p + n;
+    n += k;
+    return d;
+  }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  const uint8_t* data() const { return p; }
+};
+
 // One kind's requests in the SoA form of its nw_submit_* entry point.
 struct Batch {
   Kind kind;
   size_t units = 0;
   Clock::time_point first;
   std::vector<Req> reqs;
+  std::atomic<int> writers{0};   // requests copying into the Bufs outside the mutex
   // Header / Certificate (nw_certificates)
-  std::vector<uint8_t> header_bytes;
+  Buf header_bytes;
   std::vector<uint64_t> header_offsets{0};
   std::vector<uint32_t> payload_counts;
-  std::vector<uint8_t> ids, header_sigs;
+  Buf ids, header_sigs;
   std::vector<uint64_t> vote_offsets{0};
-  std::vector<uint8_t> vote_pks, vote_sigs;
+  Buf vote_pks, vote_sigs;
   // Vote (nw_submit_votes_verify_many): ids and signatures reuse ids / header_sigs
   std::vector<uint64_t> rounds;
-  std::vector<uint8_t> origins, authors;
+  Buf origins, authors;
   // Signature::verify / verify_batch: digests (n x 32), keys, signatures, batch offsets
-  std::vector<uint8_t> digests, pks, sigs;
+  Buf digests, pks, sigs;
   std::vector<uint64_t> batch_offsets{0};
   // outputs and the job
   std::vector<int32_t> status;
@@ -85,25 +120,30 @@ struct Batch {
   void clear() {
     units = 0;
     reqs.clear();
-    header_bytes.clear();
+    for (Buf* b : {&header_bytes, &ids, &header_sigs, &vote_pks, &vote_sigs, &origins, &authors,
+                   &digests, &pks, &sigs})
+      b->n = 0;
     header_offsets.assign(1, 0);
     payload_counts.clear();
-    ids.clear();
-    header_sigs.clear();
     vote_offsets.assign(1, 0);
-    vote_pks.clear();
-    vote_sigs.clear();
     rounds.clear();
-    origins.clear();
-    authors.clear();
-    digests.clear();
-    pks.clear();
-    sigs.clear();
     batch_offsets.assign(1, 0);
     job = nullptr;
     rc = 0;
   }
+  // a batch taken for submission: every request that reserved a range has filled it
+  void wait_writers() const {
+    while (writers.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+  }
 };
+
+// One input range of a request: len bytes from src into the batch's Buf `buf`.
+struct Piece {
+  Buf Batch::*buf;
+  const void* src;
+  size_t len;
+};
+constexpr int kMaxPieces = 5;
 
 uint8_t g_dummy[64];
 
@@ -113,6 +153,7 @@ template <class T>
 const T* nz(const std::vector<T>& v) {
   return v.empty() ? reinterpret_cast<const T*>(g_dummy) : v.data();
 }
+const uint8_t* nz(const Buf& v) { return v.empty() ? g_dummy : v.data(); }
 
 }  // namespace
 
@@ -146,34 +187,72 @@ struct nw_service {
   bool inline_submit = true;   // NW_SERVICE_INLINE=0: only the flusher submits
   std::thread flusher, completer;
 
-  // Adds one request to its kind's open batch (fill copies the inputs); 0 or NW_E_*.
+  // Adds one request to its kind's open batch; 0 or NW_E_*. Under the mutex: room in the
+  // batch's Bufs for the request's pieces (growing them waits until no request is still
+  // copying into the batch), its callback, and the small per-request fields (fill: offsets,
+  // counts, rounds); then, with the mutex released, the pieces are copied in.
   // On an idle device (no job in flight, none being submitted) the caller's thread submits
-  // the batch itself: the request reaches the device without waking the flusher thread
-  // (a futex wake-up is tens of microseconds, a third of a small job).
+  // the oldest batch itself: the request reaches the device without waking the flusher
+  // thread (a futex wake-up is tens of microseconds, a third of a small job).
   template <class Fill>
-  int add(Kind k, size_t units, nw_verdict_fn fn, void* arg, Fill fill) {
+  int add(Kind k, size_t units, nw_verdict_fn fn, void* arg, const Piece* pc, int npc,
+          Fill fill) {
     if (!fn) return set_err(NW_E_INVALID_ARG, "null verdict callback");
     std::unique_lock<std::mutex> lk(m);
     if (stop) return set_err(NW_E_INVALID_ARG, "service is shutting down");
+    for (;;) {
+      Batch& b = *open[k];
+      bool fits = true;
+      for (int i = 0; i < npc; ++i) fits = fits && (b.*pc[i].buf).fits(pc[i].len);
+      if (fits) break;
+      if (b.writers.load(std::memory_order_acquire) != 0) {
+        lk.unlock();   // let them finish; the batch may be flushed meanwhile
+        b.wait_writers();
+        lk.lock();
+        continue;
+      }
+      for (int i = 0; i < npc; ++i)
+        if (!(b.*pc[i].buf).fits(pc[i].len) && !(b.*pc[i].buf).grow(pc[i].len))
+          return set_err(NW_E_OUT_OF_MEMORY, "service batch");
+    }
     Batch& b = *open[k];
     const bool first_req = b.reqs.empty();
     if (first_req) b.first = Clock::now();
+    uint8_t* dst[kMaxPieces];
+    for (int i = 0; i < npc; ++i) dst[i] = (b.*pc[i].buf).take(pc[i].len);
     fill(b);
     b.reqs.push_back({fn, arg});
+    b.writers.fetch_add(1, std::memory_order_relaxed);
     const size_t before = b.units;
     b.units += units;
     ++accepted;
-    if (inline_submit && open_jobs == 0 && submitting == 0 && inflight.size() < max_inflight) {
-      std::unique_ptr<Batch> fresh = take_spare(k);
+    const bool idle =
+        inline_submit && open_jobs == 0 && submitting == 0 && inflight.size() < max_inflight;
+    // wake the flusher to arm its timer (first request) or because the batch just filled
+    if (!idle && (first_req || (before < max_items && b.units >= max_items)))
+      cv_flush.notify_one();
+    lk.unlock();
+    for (int i = 0; i < npc; ++i)
+      if (pc[i].len) memcpy(dst[i], pc[i].src, pc[i].len);
+    b.writers.fetch_sub(1, std::memory_order_release);
+    if (!idle) return 0;
+    lk.lock();
+    if (open_jobs == 0 && submitting == 0 && inflight.size() < max_inflight && !stop) {
+      // every non-empty batch is ready on an idle device: the oldest goes, as in the flusher
+      // (taking always the caller's own kind let a flood of one kind starve the others)
+      int pick = -1;
+      for (int j = 0; j < K_COUNT; ++j)
+        if (!open[j]->reqs.empty() && (pick < 0 || open[j]->first < open[pick]->first))
+          pick = j;
+      std::unique_ptr<Batch> fresh = pick < 0 ? nullptr : take_spare(static_cast<Kind>(pick));
       if (fresh) {
-        std::unique_ptr<Batch> own = std::move(open[k]);
-        open[k] = std::move(fresh);
+        std::unique_ptr<Batch> own = std::move(open[pick]);
+        open[pick] = std::move(fresh);
         launch(lk, std::move(own));
-        return 0;
+        if (open[k]->reqs.empty()) return 0;
       }
     }
-    // wake the flusher to arm its timer (first request) or because the batch just filled
-    if (first_req || (before < max_items && b.units >= max_items)) cv_flush.notify_one();
+    cv_flush.notify_one();   // whatever is left waits for the flusher
     return 0;
   }
 
@@ -183,6 +262,7 @@ struct nw_service {
     ++open_jobs;
     ++submitting;
     lk.unlock();
+    b->wait_writers();
     const Clock::time_point s0 = Clock::now();
     // the service's device choice, also when a producer's thread submits (restored after)
     const int prev = nw_get_device();
@@ -424,14 +504,14 @@ int nw_service_certificate(nw_service* s, const uint8_t* header_bytes, size_t he
   if (!rc) rc = check_header(header_bytes, header_len, payload_count, id, header_sig);
   if (rc) return rc;
   if (nvotes && (!vote_pks || !vote_sigs)) return set_err(NW_E_INVALID_ARG, "null votes");
-  return s->add(K_CERT, 1 + nvotes, fn, arg, [&](Batch& b) {
-    append(b.header_bytes, header_bytes, header_len);
+  const Piece pc[] = {{&Batch::header_bytes, header_bytes, header_len},
+                      {&Batch::ids, id, 32},
+                      {&Batch::header_sigs, header_sig, 64},
+                      {&Batch::vote_pks, vote_pks, 32 * nvotes},
+                      {&Batch::vote_sigs, vote_sigs, 64 * nvotes}};
+  return s->add(K_CERT, 1 + nvotes, fn, arg, pc, 5, [&](Batch& b) {
     b.header_offsets.push_back(b.header_bytes.size());
     b.payload_counts.push_back(payload_count);
-    append(b.ids, id, 32);
-    append(b.header_sigs, header_sig, 64);
-    append(b.vote_pks, vote_pks, 32 * nvotes);
-    append(b.vote_sigs, vote_sigs, 64 * nvotes);
     b.vote_offsets.push_back(b.vote_offsets.back() + nvotes);
   });
 }
@@ -442,12 +522,12 @@ int nw_service_header(nw_service* s, const uint8_t* header_bytes, size_t header_
   int rc = need_committee(s);
   if (!rc) rc = check_header(header_bytes, header_len, payload_count, id, sig);
   if (rc) return rc;
-  return s->add(K_HEADER, 1, fn, arg, [&](Batch& b) {
-    append(b.header_bytes, header_bytes, header_len);
+  const Piece pc[] = {{&Batch::header_bytes, header_bytes, header_len},
+                      {&Batch::ids, id, 32},
+                      {&Batch::header_sigs, sig, 64}};
+  return s->add(K_HEADER, 1, fn, arg, pc, 3, [&](Batch& b) {
     b.header_offsets.push_back(b.header_bytes.size());
     b.payload_counts.push_back(payload_count);
-    append(b.ids, id, 32);
-    append(b.header_sigs, sig, 64);
   });
 }
 
@@ -456,34 +536,29 @@ int nw_service_vote(nw_service* s, const uint8_t* id, uint64_t round, const uint
   int rc = need_committee(s);
   if (rc) return rc;
   if (!id || !origin || !author || !sig) return set_err(NW_E_INVALID_ARG, "null pointer");
-  return s->add(K_VOTE, 1, fn, arg, [&](Batch& b) {
-    append(b.ids, id, 32);
-    b.rounds.push_back(round);
-    append(b.origins, origin, 32);
-    append(b.authors, author, 32);
-    append(b.header_sigs, sig, 64);
-  });
+  const Piece pc[] = {{&Batch::ids, id, 32},
+                      {&Batch::origins, origin, 32},
+                      {&Batch::authors, author, 32},
+                      {&Batch::header_sigs, sig, 64}};
+  return s->add(K_VOTE, 1, fn, arg, pc, 4, [&](Batch& b) { b.rounds.push_back(round); });
 }
 
 int nw_service_verify(nw_service* s, const uint8_t* digest, const uint8_t* pk,
                       const uint8_t* sig, nw_verdict_fn fn, void* arg) {
   if (!s) return set_err(NW_E_INVALID_ARG, "null service");
   if (!digest || !pk || !sig) return set_err(NW_E_INVALID_ARG, "null pointer");
-  return s->add(K_STRICT, 1, fn, arg, [&](Batch& b) {
-    append(b.digests, digest, 32);
-    append(b.pks, pk, 32);
-    append(b.sigs, sig, 64);
-  });
+  const Piece pc[] = {{&Batch::digests, digest, 32}, {&Batch::pks, pk, 32},
+                      {&Batch::sigs, sig, 64}};
+  return s->add(K_STRICT, 1, fn, arg, pc, 3, [](Batch&) {});
 }
 
 int nw_service_verify_batch(nw_service* s, const uint8_t* digest, const uint8_t* pks,
                             const uint8_t* sigs, size_t n, nw_verdict_fn fn, void* arg) {
   if (!s) return set_err(NW_E_INVALID_ARG, "null service");
   if (!digest || (n && (!pks || !sigs))) return set_err(NW_E_INVALID_ARG, "null pointer");
-  return s->add(K_BATCH, n ? n : 1, fn, arg, [&](Batch& b) {
-    append(b.digests, digest, 32);
-    append(b.pks, pks, 32 * n);
-    append(b.sigs, sigs, 64 * n);
+  const Piece pc[] = {{&Batch::digests, digest, 32}, {&Batch::pks, pks, 32 * n},
+                      {&Batch::sigs, sigs, 64 * n}};
+  return s->add(K_BATCH, n ? n : 1, fn, arg, pc, 3, [&](Batch& b) {
     b.batch_offsets.push_back(b.batch_offsets.back() + n);
   });
 }
