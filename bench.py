@@ -730,6 +730,9 @@ def loadgen_lib():
                                           ctypes.c_size_t, ctypes.c_uint32, ctypes.c_size_t,
                                           ctypes.c_uint32, P, P]
     L.nw_loadgen_certificates.restype = ctypes.c_int
+    L.nw_loadgen_certificates_on.argtypes = [P, P, P, P, ctypes.c_double, ctypes.c_uint64,
+                                             ctypes.c_uint32, P, P]
+    L.nw_loadgen_certificates_on.restype = ctypes.c_int
     return L
 
 
@@ -773,7 +776,13 @@ def run_service_latency(args, rank, world, N: int, cache=None):
                                         ptr_np(lat), ptr_np(out3))
         check(rc, "nw_loadgen_certificates")
         el, jobs, bad = float(out3[0]), int(out3[1]), int(out3[2])
-        return {"offered_certs_per_s": rate, "certs": total,
+        inval = exp_st[np.arange(total) % uniq] != 0
+        slow = np.argsort(lat)[-max(1, total // 100):]   # the slowest 1 %: where in the run
+        diag = {"p99_valid_ms": float(np.percentile(lat[~inval], 99) * 1e3),
+                "p99_invalid_ms": float(np.percentile(lat[inval], 99) * 1e3) if inval.any() else None,
+                "slowest1pct_in_first_tenth": float(np.mean(slow < total // 10)),
+                "slowest1pct_invalid_frac": float(np.mean(inval[slow]))}
+        return {**diag, "offered_certs_per_s": rate, "certs": total,
                 "achieved_certs_per_s": total / el if el > 0 else None,
                 "p50_ms": float(np.percentile(lat, 50) * 1e3),
                 "p90_ms": float(np.percentile(lat, 90) * 1e3),

@@ -794,10 +794,10 @@ __global__ __launch_bounds__(256, 3) void k_pip_points(
     uint64_t b1, uint64_t i0, uint64_t i1, uint32_t pmin, const uint32_t* __restrict__ pks,
     const uint32_t* __restrict__ sigs, const uint32_t* __restrict__ z16, z_key_t zkey,
     bv_item* __restrict__ items, ge_cached* __restrict__ tabs, pip_group_t grp,
-    uint32_t roles) {
+    uint32_t roles, uint32_t role0) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t wave = g >> 6;
-  const int which = (int)(wave % roles);
+  const int which = (int)(role0 + wave % roles);
   const uint64_t li = (wave / roles) * 64 + (g & 63);
   const uint64_t gi = i0 + li;
   if (gi >= i1) return;
@@ -1057,7 +1057,8 @@ __global__ __launch_bounds__(1024) void k_pip_sort(const uint32_t* __restrict__ 
                                                    const uint64_t* __restrict__ offsets,
                                                    uint64_t b0, uint64_t i0, uint32_t extra,
                                                    uint32_t pmin, ge_cached* __restrict__ tabs,
-                                                   const bv_item* __restrict__ items) {
+                                                   const bv_item* __restrict__ items,
+                                                   uint32_t wbase) {
   constexpr int NL = 128 + kPipCarryBins;
   __shared__ uint32_t s_h[NL], s_c[NL];
   __shared__ uint32_t s_b[16][8];
@@ -1067,11 +1068,11 @@ __global__ __launch_bounds__(1024) void k_pip_sort(const uint32_t* __restrict__ 
   if (n0 < pmin) return;
   const uint64_t n = n0 + extra;   // votes + (group mode) key sums
   const pip_region reg = pip_at(tabs, bs - i0, n);
-  if (blockIdx.x == kPipWin) {     // the batch's b sum and first failures
+  const int w = (int)(blockIdx.x + wbase), tid = threadIdx.x;
+  if (w == kPipWin) {     // the batch's b sum and first failures
     pip_bsum_block(reg, n0, items + (bs - i0), s_b, s_f);
     return;
   }
-  const int w = blockIdx.x, tid = threadIdx.x;
   if (tid < NL) s_h[tid] = 0;
   __syncthreads();
   for (uint64_t t = tid; t < n; t += 1024)
@@ -1645,23 +1646,51 @@ namespace {
 
 // The Pippenger kernels over the pip_list batches of one slice (plain batches or, with
 // grp.cert_vote_offsets set, certificate groups).
-void launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t b, uint64_t e,
+hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t b, uint64_t e,
                 uint64_t i0, uint64_t i1, uint32_t pmin, uint64_t npip, uint64_t pmax,
                 const uint32_t* pks, const uint32_t* sigs, const uint32_t* z16,
                 const z_key_t& zkey, const bv_ws& w, int32_t* status, uint64_t* fail_index,
-                const pip_group_t& grp, hipStream_t stream) {
+                const pip_group_t& grp, hipStream_t stream, const batch_fork_t* fk) {
   const bool group = grp.cert_vote_offsets != nullptr;
   const uint32_t extra = group ? grp.nkeys : 0;   // key sums
   const uint32_t roles = group ? 2 : 3;
-  hipLaunchKernelGGL(k_pip_points,
-                     dim3((unsigned)((i1 - i0 + 63) / 64 * roles * 64 + 255) / 256),
-                     dim3(256), 0, stream, digests, offsets, b, e, i0, i1, pmin, pks, sigs, z16,
-                     zkey, w.items, w.tabs, grp, roles);
-  if (group)
-    hipLaunchKernelGGL(k_grp_keys, dim3((unsigned)npip), dim3(1024), 0, stream, offsets, b, i0,
-                       pmin, w.items, w.tabs, grp);
-  hipLaunchKernelGGL(k_pip_sort, dim3(kPipWin + 1, (unsigned)npip), dim3(1024), 0, stream,
-                     w.pip_list, offsets, b, i0, extra, pmin, w.tabs, w.items);
+  const uint64_t wv = (i1 - i0 + 63) / 64;   // waves per role
+  if (fk && fk->s2 && !group) {
+    // Forked (config 1's one call): the digit lanes (role 0: hash, scalars, digits) and the
+    // window sorts, which read only digits, run on `stream` while the R / A decompressions
+    // (roles 1, 2: the 255-squaring chains) run on s2; the b-sum / first-failure block of
+    // the sort needs both, so it joins on s2. The bucket pass waits for s2. The sort no
+    // longer sits between the decompressions and the buckets (~25 us of a 10k batch).
+    // (An event's wait takes the record made before it: `a` is recorded twice.)
+    hipError_t fe = hipEventRecord(fk->a, stream);
+    if (fe == hipSuccess) fe = hipStreamWaitEvent(fk->s2, fk->a, 0);
+    if (fe != hipSuccess) return fe;
+    hipLaunchKernelGGL(k_pip_points, dim3((unsigned)((wv * 2 * 64 + 255) / 256)), dim3(256), 0,
+                       fk->s2, digests, offsets, b, e, i0, i1, pmin, pks, sigs, z16, zkey,
+                       w.items, w.tabs, grp, 2u, 1u);
+    hipLaunchKernelGGL(k_pip_points, dim3((unsigned)((wv * 64 + 255) / 256)), dim3(256), 0,
+                       stream, digests, offsets, b, e, i0, i1, pmin, pks, sigs, z16, zkey,
+                       w.items, w.tabs, grp, 1u, 0u);
+    fe = hipEventRecord(fk->a, stream);
+    if (fe == hipSuccess) fe = hipStreamWaitEvent(fk->s2, fk->a, 0);
+    if (fe != hipSuccess) return fe;
+    hipLaunchKernelGGL(k_pip_sort, dim3(1, (unsigned)npip), dim3(1024), 0, fk->s2, w.pip_list,
+                       offsets, b, i0, extra, pmin, w.tabs, w.items, (uint32_t)kPipWin);
+    hipLaunchKernelGGL(k_pip_sort, dim3(kPipWin, (unsigned)npip), dim3(1024), 0, stream,
+                       w.pip_list, offsets, b, i0, extra, pmin, w.tabs, w.items, 0u);
+    fe = hipEventRecord(fk->b, fk->s2);
+    if (fe == hipSuccess) fe = hipStreamWaitEvent(stream, fk->b, 0);
+    if (fe != hipSuccess) return fe;
+  } else {
+    hipLaunchKernelGGL(k_pip_points, dim3((unsigned)((wv * roles * 64 + 255) / 256)), dim3(256),
+                       0, stream, digests, offsets, b, e, i0, i1, pmin, pks, sigs, z16, zkey,
+                       w.items, w.tabs, grp, roles, 0u);
+    if (group)
+      hipLaunchKernelGGL(k_grp_keys, dim3((unsigned)npip), dim3(1024), 0, stream, offsets, b,
+                         i0, pmin, w.items, w.tabs, grp);
+    hipLaunchKernelGGL(k_pip_sort, dim3(kPipWin + 1, (unsigned)npip), dim3(1024), 0, stream,
+                       w.pip_list, offsets, b, i0, extra, pmin, w.tabs, w.items, 0u);
+  }
   // G lanes per bucket: about 8 additions each at the largest batch's mean bucket size
   // (<= 49 digits per vote over kPipBins buckets); more lanes measured slower (the shuffle
   // tree's full additions cost more than the niels additions they replace: 10k batch,
@@ -1685,6 +1714,7 @@ void launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t b, ui
                        w.pip_list, offsets, b, i0, extra, pmin, w.tabs);
   hipLaunchKernelGGL(k_pip_final, dim3((unsigned)npip), dim3(64), 0, stream, w.pip_list,
                      offsets, b, i0, w.tabs, status, fail_index, extra, pmin, grp.group_ok);
+  return hipGetLastError();
 }
 
 uint32_t pip_min() {
@@ -1721,7 +1751,8 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                const uint32_t* z16, const z_key_t& zkey, void* workspace,
                                int32_t* status, uint64_t* fail_index, hipStream_t stream,
                                const key_tables_t* keys, const uint32_t* skip_group_ok,
-                               uint64_t skip_per_group, double active_frac) {
+                               uint64_t skip_per_group, double active_frac,
+                               const batch_fork_t* fork) {
   const key_tables_t kt = keys ? *keys : key_tables_t{nullptr, nullptr, nullptr};
   const batch_skip_t sk{skip_group_ok, skip_per_group ? skip_per_group : 1};
   if (nbatches == 0) return hipSuccess;
@@ -1795,9 +1826,11 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
       hipLaunchKernelGGL(k_bv_items, dim3((unsigned)((i1 - i0 + 255) / 256)), dim3(256), 0,
                          stream, digests, offsets, b, e, i0, i1, pmin, pks, sigs, z16, zkey,
                          w.items, w.tabs, kt, sk);
-    if (npip)
-      launch_pip(digests, offsets, b, e, i0, i1, pmin, npip, pmax, pks, sigs, z16, zkey, w,
-                 status, fail_index, nogrp, stream);
+    if (npip) {
+      const hipError_t pe = launch_pip(digests, offsets, b, e, i0, i1, pmin, npip, pmax, pks,
+                                       sigs, z16, zkey, w, status, fail_index, nogrp, stream, fork);
+      if (pe != hipSuccess) return pe;
+    }
     if (chunks)
       hipLaunchKernelGGL(k_bv_chunks, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
                          stream, w.chunks, (uint32_t)chunks, offsets, b, i0, w.items, w.tabs,
@@ -1944,9 +1977,12 @@ hipError_t launch_cert_groups(const uint32_t* cert_digest, const uint64_t* cvo,
     }
     if (votes > cap) return hipErrorInvalidValue;
     const uint64_t i0 = host_cvo[std::min(g * K, ncert)], i1 = host_cvo[std::min(e * K, ncert)];
-    if (i1 > i0)
-      launch_pip(cert_digest, gofs, g, e, i0, i1, pmin, e - g, pmax, pks, sigs, nullptr, zkey, w,
-                 nullptr, nullptr, grp, stream);
+    if (i1 > i0) {
+      const hipError_t pe = launch_pip(cert_digest, gofs, g, e, i0, i1, pmin, e - g, pmax, pks,
+                                       sigs, nullptr, zkey, w, nullptr, nullptr, grp, stream,
+                                       nullptr);
+      if (pe != hipSuccess) return pe;
+    }
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
     g = e;

@@ -189,6 +189,22 @@ int job_run(nw_job* j, size_t in_bytes, size_t out_off, size_t out_bytes, Launch
   return 0;
 }
 
+// The job's second stream and two events (created once per pooled job); without them the
+// callers run their sequential form.
+void ensure_fork(nw_job* j) {
+  if (j->fork.s2) return;
+  hipStream_t s2 = nullptr;
+  hipEvent_t e1 = nullptr, e2 = nullptr;
+  if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) == hipSuccess &&
+      hipEventCreateWithFlags(&e1, hipEventDisableTiming) == hipSuccess &&
+      hipEventCreateWithFlags(&e2, hipEventDisableTiming) == hipSuccess) {
+    j->fork = nw::rt::Fork{s2, e1, e2};
+  } else {
+    if (e1) (void)hipEventDestroy(e1);
+    if (s2) (void)hipStreamDestroy(s2);
+  }
+}
+
 int fill_key(nw::z_key_t& k) {
   int rc = nw::rt::os_random(k.key, 32);
   k.nonce = 0;
@@ -270,6 +286,14 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
   rc = fill_key(key);
   if (rc) return job_abort(j, rc);
   const uint64_t* h_off = reinterpret_cast<const uint64_t*>(j->hbuf + o_off);
+  ensure_fork(j);
+  const nw::batch_fork_t fk{j->fork.s2, j->fork.ev_fork, j->fork.ev_join};
+  // NW_BATCH_FORK=0: the single-stream form (A/B hook)
+  static const bool fork_on = [] {
+    const char* e = getenv("NW_BATCH_FORK");
+    return !(e && *e == '0');
+  }();
+  const bool fork = fork_on && j->fork.s2;
   rc = job_run(j, o_st, o_st, o_ws - o_st, [&]() -> int {
     JOB_HIP(nw::launch_verify_batch(reinterpret_cast<const uint32_t*>(j->dbuf + o_d),
                                     reinterpret_cast<const uint64_t*>(j->dbuf + o_off), h_off,
@@ -279,7 +303,8 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
                                         : nullptr,
                                     key, j->dbuf + o_ws,
                                     reinterpret_cast<int32_t*>(j->dbuf + o_st),
-                                    reinterpret_cast<uint64_t*>(j->dbuf + o_fi), j->stream),
+                                    reinterpret_cast<uint64_t*>(j->dbuf + o_fi), j->stream,
+                                    nullptr, nullptr, 0, 1.0, fork ? &fk : nullptr),
             "verify_batch launch");
     return 0;
   });
@@ -681,18 +706,7 @@ int submit_certs(int dev, const nw_committee* com, const nw_certificates* cs, in
     d.nvotes = nv;
     hvo = reinterpret_cast<const uint64_t*>(j->hbuf + o_vo);   // read while planning only
   }
-  if (!headers_only && !j->fork.s2) {   // created once per pooled job
-    hipStream_t s2 = nullptr;
-    hipEvent_t e1 = nullptr, e2 = nullptr;
-    if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) == hipSuccess &&
-        hipEventCreateWithFlags(&e1, hipEventDisableTiming) == hipSuccess &&
-        hipEventCreateWithFlags(&e2, hipEventDisableTiming) == hipSuccess) {
-      j->fork = nw::rt::Fork{s2, e1, e2};
-    } else {   // no fork: the sequential pipeline
-      if (e1) (void)hipEventDestroy(e1);
-      if (s2) (void)hipStreamDestroy(s2);
-    }
-  }
+  if (!headers_only) ensure_fork(j);
   rc = job_run(j, o_st, o_st, out_end - o_st, [&]() -> int {
     return nw::rt::cert_pipeline(dev, dcom, d, hvo, headers_only, z16 ? j->dbuf + o_z : nullptr,
                                  nullptr, j->dbuf + o_ws,

@@ -82,6 +82,12 @@ hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, struct ge_niel
                              uint32_t* ok, hipStream_t stream, uint32_t* saved = nullptr,
                              uint32_t* flag = nullptr, bool force = true);
 size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems);
+// Optional second stream for launch_verify_batch's Pippenger batches (decompressions beside
+// the digit lanes and sorts) and two events it records (reused per call).
+struct batch_fork_t {
+  hipStream_t s2;
+  hipEvent_t a, b;
+};
 // skip_group_ok (optional, device): batch b is settled (status Ok) when
 // skip_group_ok[b / skip_per_group] != 0 (launch_cert_groups, launch_votes_keyed);
 // active_frac: the caller's estimate of the fraction of votes not skipped (chunk sizing).
@@ -92,7 +98,8 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                int32_t* status, uint64_t* fail_index, hipStream_t stream,
                                const key_tables_t* keys = nullptr,
                                const uint32_t* skip_group_ok = nullptr,
-                               uint64_t skip_per_group = 0, double active_frac = 1.0);
+                               uint64_t skip_per_group = 0, double active_frac = 1.0,
+                               const batch_fork_t* fork = nullptr);
 
 // Certificate::verify vote batches merged over groups of certificates (nw_batch.hip):
 // cert_group_size() = certificates per group, 0 when the merge does not apply;

@@ -149,6 +149,9 @@ uint8_t g_dummy[64];
 
 // The completer polls a job this long before it blocks on it.
 constexpr int kSpinUs = 2000;
+// Largest batch (units) a request's own thread submits on an idle device (a few
+// certificates): anything bigger is the flusher's.
+constexpr size_t kInlineUnits = 256;
 template <class T>
 const T* nz(const std::vector<T>& v) {
   return v.empty() ? reinterpret_cast<const T*>(g_dummy) : v.data();
@@ -226,8 +229,11 @@ struct nw_service {
     const size_t before = b.units;
     b.units += units;
     ++accepted;
-    const bool idle =
-        inline_submit && open_jobs == 0 && submitting == 0 && inflight.size() < max_inflight;
+    // only a small batch goes from the caller's thread: a big one (the device just went idle
+    // under load) costs the caller its submit (~0.1 ms of staging and launches at a few
+    // hundred certificates), and callers that stall fall behind their own arrivals
+    const bool idle = inline_submit && open_jobs == 0 && submitting == 0 &&
+                      inflight.size() < max_inflight && b.units <= kInlineUnits;
     // wake the flusher to arm its timer (first request) or because the batch just filled
     if (!idle && (first_req || (before < max_items && b.units >= max_items)))
       cv_flush.notify_one();
@@ -244,6 +250,7 @@ struct nw_service {
       for (int j = 0; j < K_COUNT; ++j)
         if (!open[j]->reqs.empty() && (pick < 0 || open[j]->first < open[pick]->first))
           pick = j;
+      if (pick >= 0 && open[pick]->units > kInlineUnits) pick = -1;   // the flusher's
       std::unique_ptr<Batch> fresh = pick < 0 ? nullptr : take_spare(static_cast<Kind>(pick));
       if (fresh) {
         std::unique_ptr<Batch> own = std::move(open[pick]);

@@ -503,48 +503,52 @@ def test_native_service_all_kinds_asyncio_vs_oracle():
 
 @pytest.mark.gpu
 def test_native_service_votes_not_starved_by_certificates():
-    """Fairness of the service flusher (nw_service.cpp): a saturating stream of certificates
-    (N = 100, two producer threads, one job in flight at a time, jobs longer than max_delay)
-    plus a trickle of votes. The ready batch whose first request is oldest goes first, so
-    every vote's verdict arrives within max_delay plus a few jobs' time, not after the
-    certificate flood (enum-order picking starved them: the certificate batch is always
-    ready when a slot frees). Every verdict equals the oracle's / the construction."""
+    """Fairness of the service flusher (nw_service.cpp): a saturating stream of N = 100
+    certificates from the C load generator's threads (tools/nw_loadgen.cpp on this very
+    service: no Python, so the flood holds no interpreter lock), one job in flight at a time
+    (jobs much longer than max_delay), plus a trickle of votes from Python. The ready batch
+    whose first request is oldest goes first, also from an idle-device submit on a
+    producer's thread, so every vote's verdict arrives within max_delay plus a few jobs'
+    time, not after the flood (enum-order picking, or a producer always submitting its own
+    kind, starved them). Every verdict equals the oracle's / the construction."""
+    import ctypes
+    import os
+    import sys
     import threading
     import time
     from cert_cases import oracle_digest_many, votes_case
     from narwhal_amd import workloads as W
+    from narwhal_amd.messages import certificates_struct
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import loadgen_lib
     keys = O.keys(100)
     s = W.certificate_stream(1500, keys, lambda sk, m: C.sign_many(sk, m), oracle_digest_many,
                              seed=61)
     m, mst, mix = W.mutate_votes(s, np.arange(3, 1500, 100), seed=6)
-    vcom, vp, vn, vexp = votes_case(N=100, seed=62, count=60, keys=keys)
+    mst = np.ascontiguousarray(mst, np.int32)
+    mix = np.ascontiguousarray(mix, np.uint64)
+    vcom, vp, vn, vexp = votes_case(N=100, seed=62, count=40, keys=keys)
     for k in ("pks", "stakes", "worker_offsets", "worker_ids"):
         assert np.array_equal(vcom[k], m["committee"][k]), k
-    rows = _rows(m)
-    expect = [(int(a), int(b)) for a, b in zip(mst, mix)]
     svc = S.NativeService(m["committee"], max_items=1 << 16, max_delay=0.0002, max_inflight=1)
-    stop = threading.Event()
-    bad_certs = []
-    done_certs = [0]
-    lock = threading.Lock()
+    rows = _rows(m)
+    for r in rows[:8]:                                # warm: key tables, pools
+        svc.submit_certificate(r, lambda st, ix: None)
+    svc.drain()
+    LG = loadgen_lib()
+    cs = certificates_struct(m, len(rows))
+    total = 400_000
+    lat_c, out3 = np.zeros(total), np.zeros(3)
+    res = {}
 
-    def flood(t):
-        i = t
-        while not stop.is_set():
-            r = i % len(rows)
-
-            def cb(st, ix, r=r):
-                with lock:
-                    done_certs[0] += 1
-                    if (st, ix) != expect[r]:
-                        bad_certs.append(r)
-            svc.submit_certificate(rows[r], cb)
-            i += 2
+    def flood():
+        res["rc"] = LG.nw_loadgen_certificates_on(
+            svc._h, ctypes.byref(cs), mst.ctypes.data, mix.ctypes.data,
+            2e6, total, 2, lat_c.ctypes.data, out3.ctypes.data)
     lat, got = [None] * vn, [None] * vn
-    th = [threading.Thread(target=flood, args=(t,)) for t in range(2)]
-    for t in th:
-        t.start()
-    time.sleep(0.2)                                   # the flood is in full swing
+    th = threading.Thread(target=flood)
+    th.start()
+    time.sleep(0.1)                                   # the flood is in full swing
     for i in range(vn):
         v = (vp["ids"][i].tobytes(), int(vp["rounds"][i]), vp["origins"][i].tobytes(),
              vp["authors"][i].tobytes(), vp["sigs"][i].tobytes())
@@ -554,13 +558,12 @@ def test_native_service_votes_not_starved_by_certificates():
             lat[i] = time.perf_counter() - t0
             got[i] = st
         svc.submit_vote(v, vcb)
-        time.sleep(0.01)
-    time.sleep(0.1)
-    stop.set()
-    for t in th:
-        t.join()
+        time.sleep(0.005)
+    th.join()
     svc.drain()
     svc.close()
+    assert res["rc"] == 0 and out3[2] == 0, (res, out3)
+    flood_s = out3[0]
+    assert flood_s > 0.3, flood_s                     # the votes arrived during the flood
     assert got == [int(x) for x in vexp]
-    assert not bad_certs and done_certs[0] > 2000
     assert max(lat) < 0.05, sorted(lat)[-5:]

@@ -49,6 +49,9 @@ void on_verdict(void* arg, int32_t status, uint64_t index) {
   while (ns > prev && !run->last_ns.compare_exchange_weak(prev, ns)) {
   }
 }
+int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_status,
+              const uint64_t* exp_index, double rate, uint64_t total, uint32_t producers,
+              double* lat_out, double* out3);
 }  // namespace
 
 extern "C" {
@@ -66,27 +69,6 @@ int nw_loadgen_certificates(const nw_committee* com, const nw_certificates* corp
   nw_service* s = nullptr;
   int rc = nw_service_create(com, max_items, max_delay_us, max_inflight, &s);
   if (rc) return rc;
-  Run run;
-  run.exp_status = exp_status;
-  run.exp_index = exp_index;
-  run.nuniq = corpus->n;
-  run.lat = lat_out;
-  std::vector<Rec> recs(total);
-  std::atomic<int> first_err{0};
-  auto submit = [&](uint64_t i) {
-    const size_t u = i % corpus->n;
-    const uint64_t h0 = corpus->header_offsets[u], h1 = corpus->header_offsets[u + 1];
-    const uint64_t v0 = corpus->vote_offsets[u], v1 = corpus->vote_offsets[u + 1];
-    const int e = nw_service_certificate(s, corpus->header_bytes + h0, h1 - h0,
-                                         corpus->payload_counts[u], corpus->ids + 32 * u,
-                                         corpus->header_sigs + 64 * u, corpus->vote_pks + 32 * v0,
-                                         corpus->vote_sigs + 64 * v0, v1 - v0, on_verdict,
-                                         &recs[i]);
-    if (e) {
-      int z = 0;
-      first_err.compare_exchange_strong(z, e);
-    }
-  };
   // warm-up (untimed): the committee's key tables and the job pool
   {
     Run warm;
@@ -114,6 +96,48 @@ int nw_loadgen_certificates(const nw_committee* com, const nw_certificates* corp
       return rc;
     }
   }
+  rc = timed_run(s, corpus, exp_status, exp_index, rate, total, producers, lat_out, out3);
+  nw_service_destroy(s);
+  return rc;
+}
+
+int nw_loadgen_certificates_on(nw_service* s, const nw_certificates* corpus,
+                               const int32_t* exp_status, const uint64_t* exp_index, double rate,
+                               uint64_t total, uint32_t producers, double* lat_out,
+                               double* out3) {
+  if (!s || !corpus || !corpus->n || !exp_status || !exp_index || !lat_out || !out3 ||
+      rate <= 0 || !producers)
+    return NW_E_INVALID_ARG;
+  return timed_run(s, corpus, exp_status, exp_index, rate, total, producers, lat_out, out3);
+}
+
+}  // extern "C"
+
+namespace {
+int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_status,
+              const uint64_t* exp_index, double rate, uint64_t total, uint32_t producers,
+              double* lat_out, double* out3) {
+  Run run;
+  run.exp_status = exp_status;
+  run.exp_index = exp_index;
+  run.nuniq = corpus->n;
+  run.lat = lat_out;
+  std::vector<Rec> recs(total);
+  std::atomic<int> first_err{0};
+  auto submit = [&](uint64_t i) {
+    const size_t u = i % corpus->n;
+    const uint64_t h0 = corpus->header_offsets[u], h1 = corpus->header_offsets[u + 1];
+    const uint64_t v0 = corpus->vote_offsets[u], v1 = corpus->vote_offsets[u + 1];
+    const int e = nw_service_certificate(s, corpus->header_bytes + h0, h1 - h0,
+                                         corpus->payload_counts[u], corpus->ids + 32 * u,
+                                         corpus->header_sigs + 64 * u, corpus->vote_pks + 32 * v0,
+                                         corpus->vote_sigs + 64 * v0, v1 - v0, on_verdict,
+                                         &recs[i]);
+    if (e) {
+      int z = 0;
+      first_err.compare_exchange_strong(z, e);
+    }
+  };
   uint64_t jobs0 = 0;
   nw_service_stats(s, nullptr, &jobs0);
   run.t0 = Clock::now() + std::chrono::milliseconds(2);
@@ -138,11 +162,9 @@ int nw_loadgen_certificates(const nw_committee* com, const nw_certificates* corp
   nw_service_drain(s);
   uint64_t jobs1 = 0;
   nw_service_stats(s, nullptr, &jobs1);
-  nw_service_destroy(s);
   out3[0] = (double)run.last_ns.load() * 1e-9;
   out3[1] = (double)(jobs1 - jobs0);
   out3[2] = (double)run.mismatches.load();
   return first_err.load();
 }
-
-}  // extern "C"
+}  // namespace
