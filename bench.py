@@ -769,20 +769,22 @@ def run_service_latency(args, rank, world, N: int, cache=None):
     def native_load(rate: float, seconds: float):
         total = max(1, int(rate * seconds))
         lat = np.zeros(total)
-        out3 = np.zeros(3)
+        out3 = np.zeros(5)
         rc = LG.nw_loadgen_certificates(ctypes.byref(cc), ctypes.byref(cs), ptr_np(exp_st),
                                         ptr_np(exp_ix), rate, total, args.service_max_items,
                                         delay_us, args.service_inflight, args.service_producers,
                                         ptr_np(lat), ptr_np(out3))
         check(rc, "nw_loadgen_certificates")
         el, jobs, bad = float(out3[0]), int(out3[1]), int(out3[2])
+        lag = {"producer_lag_max_ms": float(out3[3] * 1e3),
+               "producer_lag_mean_ms": float(out3[4] * 1e3)}
         inval = exp_st[np.arange(total) % uniq] != 0
         slow = np.argsort(lat)[-max(1, total // 100):]   # the slowest 1 %: where in the run
         diag = {"p99_valid_ms": float(np.percentile(lat[~inval], 99) * 1e3),
                 "p99_invalid_ms": float(np.percentile(lat[inval], 99) * 1e3) if inval.any() else None,
                 "slowest1pct_in_first_tenth": float(np.mean(slow < total // 10)),
                 "slowest1pct_invalid_frac": float(np.mean(inval[slow]))}
-        return {**diag, "offered_certs_per_s": rate, "certs": total,
+        return {**diag, **lag, "offered_certs_per_s": rate, "certs": total,
                 "achieved_certs_per_s": total / el if el > 0 else None,
                 "p50_ms": float(np.percentile(lat, 50) * 1e3),
                 "p90_ms": float(np.percentile(lat, 90) * 1e3),

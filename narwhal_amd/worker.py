@@ -13,6 +13,18 @@ batch at a time on the tokio thread. Here every batch is handed to the aggregati
 ``VerificationService`` as soon as it arrives (several batches in flight share one
 SHA-512 device job), while a writer task stores and announces the digests strictly in
 arrival order — the store write of one batch overlaps the hashing of the next.
+
+Crossover (bench.py ``worker_latency``, 508,052-B batches, 1x MI355X,
+``profiles/r04b/worker.json``,
+``worker_deep.json``): SHA-512 is a serial chain per message, so a GPU digest is
+one lane walking the batch's ~3,970 blocks — ~31 ms per batch (p50 at 50 batches/s)
+against 0.36 ms on one host core (OpenSSL). The GPU path therefore loses on latency at
+EVERY offered rate, and on throughput to the host's cores too: with the default lookahead
+of 16 batches it sustains ~380 batches/s (one host core: ~2,800/s; 16 threads: ~19,900/s),
+and even with 1,024 batches in flight 4,700/s at 232 ms p50. The device only wins when
+tens of thousands of batches are hashed at once (config 3: 65,536 batches in 26 ms,
+1.28 TB/s). Keep the worker's ``Processor`` on the host's SHA-512, as the reference does,
+unless its cores are needed elsewhere and a ~30 ms digest latency is acceptable.
 """
 from __future__ import annotations
 

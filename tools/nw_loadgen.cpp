@@ -51,19 +51,21 @@ void on_verdict(void* arg, int32_t status, uint64_t index) {
 }
 int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_status,
               const uint64_t* exp_index, double rate, uint64_t total, uint32_t producers,
-              double* lat_out, double* out3);
+              double* lat_out, double* out);
 }  // namespace
 
 extern "C" {
 
 // Returns 0 or the first negative NW_E_* from the service. lat_out: total seconds;
-// out3: elapsed seconds (t0 .. last verdict), jobs, mismatches (as doubles).
+// out (5 doubles): elapsed seconds (t0 .. last verdict), jobs, mismatches, and the
+// producers' lateness: the largest and the mean (call time - due time) of a submit, seconds
+// (a producer that cannot keep its schedule shows here before it shows as latency).
 int nw_loadgen_certificates(const nw_committee* com, const nw_certificates* corpus,
                             const int32_t* exp_status, const uint64_t* exp_index, double rate,
                             uint64_t total, size_t max_items, uint32_t max_delay_us,
                             size_t max_inflight, uint32_t producers, double* lat_out,
-                            double* out3) {
-  if (!com || !corpus || !corpus->n || !exp_status || !exp_index || !lat_out || !out3 ||
+                            double* out) {
+  if (!com || !corpus || !corpus->n || !exp_status || !exp_index || !lat_out || !out ||
       rate <= 0 || !producers)
     return NW_E_INVALID_ARG;
   nw_service* s = nullptr;
@@ -96,7 +98,7 @@ int nw_loadgen_certificates(const nw_committee* com, const nw_certificates* corp
       return rc;
     }
   }
-  rc = timed_run(s, corpus, exp_status, exp_index, rate, total, producers, lat_out, out3);
+  rc = timed_run(s, corpus, exp_status, exp_index, rate, total, producers, lat_out, out);
   nw_service_destroy(s);
   return rc;
 }
@@ -104,11 +106,11 @@ int nw_loadgen_certificates(const nw_committee* com, const nw_certificates* corp
 int nw_loadgen_certificates_on(nw_service* s, const nw_certificates* corpus,
                                const int32_t* exp_status, const uint64_t* exp_index, double rate,
                                uint64_t total, uint32_t producers, double* lat_out,
-                               double* out3) {
-  if (!s || !corpus || !corpus->n || !exp_status || !exp_index || !lat_out || !out3 ||
+                               double* out) {
+  if (!s || !corpus || !corpus->n || !exp_status || !exp_index || !lat_out || !out ||
       rate <= 0 || !producers)
     return NW_E_INVALID_ARG;
-  return timed_run(s, corpus, exp_status, exp_index, rate, total, producers, lat_out, out3);
+  return timed_run(s, corpus, exp_status, exp_index, rate, total, producers, lat_out, out);
 }
 
 }  // extern "C"
@@ -116,7 +118,7 @@ int nw_loadgen_certificates_on(nw_service* s, const nw_certificates* corpus,
 namespace {
 int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_status,
               const uint64_t* exp_index, double rate, uint64_t total, uint32_t producers,
-              double* lat_out, double* out3) {
+              double* lat_out, double* out) {
   Run run;
   run.exp_status = exp_status;
   run.exp_index = exp_index;
@@ -147,14 +149,18 @@ int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_s
                run.t0 + std::chrono::duration_cast<Clock::duration>(
                             std::chrono::duration<double>(period * (double)i))};
   std::vector<std::thread> th;
+  std::vector<double> lag_max(producers, 0.0), lag_sum(producers, 0.0);
   for (uint32_t p = 0; p < producers; ++p)
     th.emplace_back([&, p] {
       for (uint64_t i = p; i < total; i += producers) {
         const Clock::time_point due = recs[i].due;
         Clock::time_point now = Clock::now();
         if (due - now > std::chrono::microseconds(100)) std::this_thread::sleep_until(due);
-        while (Clock::now() < due) {
+        while ((now = Clock::now()) < due) {
         }
+        const double lag = std::chrono::duration<double>(now - due).count();
+        lag_max[p] = std::max(lag_max[p], lag);
+        lag_sum[p] += lag;
         submit(i);
       }
     });
@@ -162,9 +168,16 @@ int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_s
   nw_service_drain(s);
   uint64_t jobs1 = 0;
   nw_service_stats(s, nullptr, &jobs1);
-  out3[0] = (double)run.last_ns.load() * 1e-9;
-  out3[1] = (double)(jobs1 - jobs0);
-  out3[2] = (double)run.mismatches.load();
+  out[0] = (double)run.last_ns.load() * 1e-9;
+  out[1] = (double)(jobs1 - jobs0);
+  out[2] = (double)run.mismatches.load();
+  double lm = 0, ls = 0;
+  for (uint32_t p = 0; p < producers; ++p) {
+    lm = std::max(lm, lag_max[p]);
+    ls += lag_sum[p];
+  }
+  out[3] = lm;
+  out[4] = ls / (double)(total ? total : 1);
   return first_err.load();
 }
 }  // namespace
