@@ -50,15 +50,15 @@ P_FIELD = 2**255 - 19
 MAC_PER_STRICT_VERIFY = 3200 * 64          # 204,800 32x32->64 MACs
 MAC_PER_BATCH_ITEM_LARGE = 1000 * 64       # batch item, n >= 10k (64,000 MACs)
 MAC_PER_BATCH_ITEM_SMALL = 2000 * 64       # batch item, small n (certificate votes)
-# Keyed vote check: 48 comb-table additions (~7.5 F_p mults each) + one
-# product for the y comparison + a share of the batched inversion ~ 370 F_p mults, no R
-# decompression; the SURVEY small-n constant above describes per-certificate Straus, not
-# this algorithm.
-MAC_PER_KEYED_VOTE = 370 * 64              # 23,680 MACs
+# Keyed vote check: 27 table additions (16 from the committee key's 16-bit
+# combs, 11 from the 24-bit B comb; ~7.5 F_p mults each) + one product for the y comparison
+# + a share of the batched inversion ~ 215 F_p mults, no R decompression; the SURVEY small-n
+# constant above describes per-certificate Straus, not this algorithm.
+MAC_PER_KEYED_VOTE = 215 * 64              # 13,760 MACs
 # Keyed strict verification (Header::verify by a committee key): R's
-# decompression (~265 F_p mults) + 48 comb-table additions (~7.5 each) ~ 650 F_p mults;
+# decompression (~265 F_p mults) + 27 table additions (~7.5 each) ~ 470 F_p mults;
 # SURVEY's 204,800 describes an unkeyed ladder verification.
-MAC_PER_KEYED_STRICT = 650 * 64            # 41,600 MACs
+MAC_PER_KEYED_STRICT = 470 * 64            # 30,080 MACs
 SHA_OPS_PER_BLOCK = 4800                   # int32 ops per 128-B block
 # Peaks (DESIGN.md "Measurement"): v_mad_u64_u32 issues at half rate on gfx950, so the spec
 # MAC peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz; the measured one is the microbenchmark's
@@ -89,6 +89,22 @@ def pmc_traffic(kernel: str, units: int):
     except (OSError, KeyError, ValueError):
         return None, None
     return e["hbm_bytes"] * units / e["units"], e["source"]
+
+
+def cert_traffic(N: int):
+    """HBM bytes per vote of one config-2 certificate call at committee size N (the call's
+    kernels, FETCH_SIZE x 2 + WRITE_SIZE from tools/pmc_cert.sh, summarised by
+    tools/pmc_cert_summary.py into profiles/cert_traffic.json). None when absent."""
+    try:
+        e = json.load(open(os.path.join(ROOT, "profiles", "cert_traffic.json")))[f"N{N}"]
+    except (OSError, KeyError, ValueError):
+        return None, None
+    return e["hbm_bytes_per_vote"], e["source"]
+
+
+# Algorithmic HBM bytes of one keyed vote check: the vote's key and signature (96 B) and its
+# 27 table entries (affine niels, 128-B slots: 16 from the key's combs, 11 from the B comb).
+ALG_BYTES_PER_KEYED_VOTE = 96 + 27 * 128
 
 
 def pmc_issue_peak():
@@ -511,8 +527,9 @@ def run_cert(args, dev, stream, rank, world, N: int, invalid: float = 0.0, strea
            "ms_per_step": sec * 1e3,
            "achieved_TMAC_s": ach, "frac": ach / PEAK_TMAC, "frac_measured": ach / PEAK_TMAC_MEASURED,
            "work_per_cert": f"{mac_keyed} MAC (keyed strict header {MAC_PER_KEYED_STRICT} + q x "
-                            f"{MAC_PER_KEYED_VOTE} per keyed vote check: 48 comb additions, no "
+                            f"{MAC_PER_KEYED_VOTE} per keyed vote check: 27 table additions, no "
                             f"R decompression)",
+           "roofline": cert_roofline(N, n, q, ach),
            "survey_TMAC_s": n * mac_survey / (kernel_ms * 1e-3) / 1e12,
            "survey_work_note": "SURVEY 8(d) small-n constant (per-certificate Straus, 128,000 "
                                "MAC/vote) overstates the keyed algorithm's work; not a roofline",
@@ -521,6 +538,21 @@ def run_cert(args, dev, stream, rank, world, N: int, invalid: float = 0.0, strea
     del rc
     torch.cuda.empty_cache()
     return res, (s, exp_st_u, exp_ix_u)
+
+
+def cert_roofline(N: int, n: int, q: int, ach: float):
+    """The certificate call's roofline: VALU-bound (integer field arithmetic), achieved
+    keyed-algorithm TMAC/s against the spec MAC peak, with the call's measured HBM traffic
+    (committed PMC, per vote x the call's votes) beside its algorithmic bytes."""
+    bpv, src = cert_traffic(N)
+    votes = n * q
+    return {"bound": "valu", "achieved": ach, "peak": PEAK_TMAC, "unit": "TMAC/s",
+            "frac": ach / PEAK_TMAC,
+            "traffic": bpv * votes if bpv is not None else None,
+            "traffic_per_vote": bpv, "traffic_unit": "HBM bytes per call",
+            "traffic_source": src,
+            "algorithmic_bytes": ALG_BYTES_PER_KEYED_VOTE * votes,
+            "algorithmic_bytes_per_vote": ALG_BYTES_PER_KEYED_VOTE}
 
 
 def run_cert_alternating(args, dev, stream, rank, world, N: int, invalid: float,

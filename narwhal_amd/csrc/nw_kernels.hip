@@ -24,6 +24,10 @@
 #include <atomic>
 #include <mutex>
 
+#ifndef NW_STRICT_PLAIN_KEYED
+#define NW_STRICT_PLAIN_KEYED 0
+#endif
+
 namespace nw {
 
 struct dev_consts {
@@ -872,7 +876,10 @@ hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
   if (eb != hipSuccess) return eb;
   const char* kf = getenv("NW_STRICT_KEYED_FAST");
   if (!kt.vote_key) {
-    hipLaunchKernelGGL(k_verify_strict<false>, dim3(grid), dim3(256), 0, stream, msgs,
+    // -DNW_STRICT_PLAIN_KEYED=1: the keyed/list instance here too (the A/B of the
+    // specialisation, tools/strict_variants.py)
+    hipLaunchKernelGGL(k_verify_strict<NW_STRICT_PLAIN_KEYED != 0>, dim3(grid), dim3(256), 0,
+                       stream, msgs,
                        msg_stride_words, pks, sigs, n, status, bitmap,
                        static_cast<ge_cached*>(workspace), kt, btw, bcomb, nullptr, nullptr);
     return hipGetLastError();

@@ -201,7 +201,8 @@ struct nw_service {
   int add(Kind k, size_t units, nw_verdict_fn fn, void* arg, const Piece* pc, int npc,
           Fill fill) {
     if (!fn) return set_err(NW_E_INVALID_ARG, "null verdict callback");
-    std::unique_lock<std::mutex> lk(m);
+    std::unique_lock<std::mutex> lk(m, std::defer_lock);
+    lock_spin(lk);
     if (stop) return set_err(NW_E_INVALID_ARG, "service is shutting down");
     for (;;) {
       Batch& b = *open[k];
@@ -229,20 +230,21 @@ struct nw_service {
     const size_t before = b.units;
     b.units += units;
     ++accepted;
-    // only a small batch goes from the caller's thread: a big one (the device just went idle
-    // under load) costs the caller its submit (~0.1 ms of staging and launches at a few
-    // hundred certificates), and callers that stall fall behind their own arrivals
-    const bool idle = inline_submit && open_jobs == 0 && submitting == 0 &&
+    // Only the first request of a batch goes from the caller's thread (a quiet service): a
+    // batch that filled while the device was busy is the flusher's (the completer wakes it
+    // when the device goes idle), since a submit costs the caller ~0.05-0.1 ms and callers
+    // that stall under load fall behind their own arrivals
+    const bool idle = inline_submit && first_req && open_jobs == 0 && submitting == 0 &&
                       inflight.size() < max_inflight && b.units <= kInlineUnits;
     // wake the flusher to arm its timer (first request) or because the batch just filled
-    if (!idle && (first_req || (before < max_items && b.units >= max_items)))
-      cv_flush.notify_one();
+    const bool wake = !idle && (first_req || (before < max_items && b.units >= max_items));
     lk.unlock();
+    if (wake) cv_flush.notify_one();
     for (int i = 0; i < npc; ++i)
       if (pc[i].len) memcpy(dst[i], pc[i].src, pc[i].len);
     b.writers.fetch_sub(1, std::memory_order_release);
     if (!idle) return 0;
-    lk.lock();
+    lock_spin(lk);
     if (open_jobs == 0 && submitting == 0 && inflight.size() < max_inflight && !stop) {
       // every non-empty batch is ready on an idle device: the oldest goes, as in the flusher
       // (taking always the caller's own kind let a flood of one kind starve the others)
@@ -259,8 +261,20 @@ struct nw_service {
         if (open[k]->reqs.empty()) return 0;
       }
     }
+    lk.unlock();
     cv_flush.notify_one();   // whatever is left waits for the flusher
     return 0;
+  }
+
+  // The service mutex is held for well under a microsecond at a time; a producer that finds
+  // it taken spins briefly instead of sleeping in the kernel (a futex wait and wake-up costs
+  // tens of microseconds, and at 10^6 requests per second producers collide constantly).
+  static void lock_spin(std::unique_lock<std::mutex>& lk) {
+    for (int i = 0; i < 256; ++i) {
+      if (lk.try_lock()) return;
+      __builtin_ia32_pause();
+    }
+    lk.lock();
   }
 
   // Submits b as one device job outside the lock (held on entry and on return) and queues it

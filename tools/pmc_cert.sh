@@ -13,7 +13,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/pmc_cert}; shift
 mkdir -p "$OUT"
-ARGS="--workload cert --no-sha --no-batch --no-wire --no-cpu-baseline --cert-steps 1 --cert-invalid 0"
+ARGS="--workload cert --no-sha --no-batch --no-wire --no-cpu-baseline --cert-steps 1 --cert-invalid 0 --cert-payload-committees="
 
 run() {  # run NAME N MODE [rocprofv3 args...]
   local name=$1 n=$2 mode=$3; shift 3

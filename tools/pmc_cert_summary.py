@@ -121,6 +121,22 @@ def main():
                     "kernels": kern}
     out = os.path.join(dst, "cert_pmc.json")
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
+    # per committee size: HBM bytes per vote of one certificate call (the call's kernels
+    # only), for bench.py's cert_stream roofline (profiles/cert_traffic.json)
+    setup = ("k_sign", "k_keypair", "k_btab_build", "k_key_", "direct_copy", "elementwise",
+             "vectorized", "__amd_rocclr")
+    tr = {}
+    for tag, r in res.items():
+        if r["mode"] != "keyed":
+            continue
+        per = [e for k, e in r["kernels"].items() if not k.startswith(setup)]
+        if not per or any("hbm_read_bytes" not in e for e in per):
+            continue
+        tr[f"N{r['committee']}"] = {
+            "hbm_bytes_per_vote": sum(e["hbm_bytes_per_vote"] for e in per),
+            "kernels": sorted(k for k in r["kernels"] if not k.startswith(setup)),
+            "source": os.path.join(dst, "cert_pmc.json")}
+    json.dump(tr, open(os.path.join(dst, "cert_traffic.json"), "w"), indent=1, sort_keys=True)
     for tag, r in res.items():
         print(f"== {tag}: {r['certs_per_s'] and r['certs_per_s'] / 1e6:.2f} M certs/s, "
               f"{r['ms_per_step']:.1f} ms/call")

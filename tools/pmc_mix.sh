@@ -7,7 +7,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/pmc_mix}
-ARGS="--items-per-gpu 4194304 --steps 1 --warmup 0 --no-cpu-baseline --no-sha --no-cert --no-batch --no-wire --no-service"
+ARGS="--items-per-gpu 4194304 --steps 1 --warmup 0 --no-cpu-baseline --no-sha --no-cert --no-batch --no-wire --no-service --no-worker"
 mkdir -p $OUT
 timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 \
   SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_BUSY_CYCLES SQ_CYCLES SQ_WAVE_CYCLES \

@@ -8,7 +8,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/pmc_stall}
 [ -n "$2" ] && export NW_LIB=$2
-ARGS="--items-per-gpu 4194304 --steps 1 --warmup 0 --no-cpu-baseline --no-sha --no-cert --no-batch --no-wire --no-service"
+ARGS="--items-per-gpu 4194304 --steps 1 --warmup 0 --no-cpu-baseline --no-sha --no-cert --no-batch --no-wire --no-service --no-worker"
 mkdir -p $OUT
 run() {
   local name=$1; shift
