@@ -56,12 +56,21 @@ loadgen: tools/libnw_loadgen.so
 tools/libnw_loadgen.so: tools/nw_loadgen.cpp include/narwhal_amd.h $(LIB)
 	g++ -O2 -std=c++17 -fPIC -shared -Iinclude $< -o $@ -Lnarwhal_amd -lnarwhal_amd -Wl,-rpath,'$$ORIGIN/../narwhal_amd' -pthread
 
+# CPU harness of the service's host logic over test doubles of the device entry points
+# (tests/test_service_stress.py); _tsan: the same under ThreadSanitizer
+STRESS_FLAGS := -std=c++17 -pthread -D__HIP_PLATFORM_AMD__ -Iinclude -I$(CSRC) -I/opt/rocm/include
+stress: tools/service_stress tools/service_stress_tsan
+tools/service_stress: tools/service_stress.cpp $(CSRC)/nw_service.cpp $(HDRS)
+	g++ -O2 $(STRESS_FLAGS) tools/service_stress.cpp $(CSRC)/nw_service.cpp -o $@
+tools/service_stress_tsan: tools/service_stress.cpp $(CSRC)/nw_service.cpp $(HDRS)
+	g++ -O1 -g -fsanitize=thread -DNW_SERVICE_SYSTEM_CLOCK_WAIT $(STRESS_FLAGS) tools/service_stress.cpp $(CSRC)/nw_service.cpp -o $@
+
 ubench: tools/ubench_valu
 tools/ubench_valu: tools/ubench_valu.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 $< -o $@
 
 clean:
-	rm -rf $(BUILD) $(LIB) tools/libnw_hostcheck.so tools/libnw_loadgen.so
+	rm -rf $(BUILD) $(LIB) tools/libnw_hostcheck.so tools/libnw_loadgen.so tools/service_stress tools/service_stress_tsan
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle hostcheck loadgen ubench clean
+.PHONY: all oracle hostcheck loadgen stress ubench clean

@@ -10,20 +10,31 @@
 // channels. A Rust crypto-gpu crate binds these entry points and completes a oneshot
 // channel from the verdict callback, so its tokio tasks never block.
 //
-// Structure: one service per committee. A request reserves its place in the open batch of
-// its kind under the service mutex (offsets and its callback; no allocation in the steady
-// state: batches are recycled) and copies its signatures, keys and header bytes there after
-// releasing it, so producers copy in parallel (an N = 50 certificate is ~3.4 KB; at 10^6 per
-// second copying under the mutex was the service's limit). A batch taken for submission
-// waits for its writers to finish. A flusher thread submits a batch as ONE device job
-// (nw_submit_*: the committee-aware pipeline with its key tables kept on the device) when it
-// holds max_items units, max_delay has passed since its first request, or no job is in
-// flight (an idle device gains nothing from a bigger batch, so a lone request goes at once
-// and batches grow only while the device is busy); a completer thread
-// waits for the jobs in submission order and calls every request's verdict callback. At most
-// max_inflight jobs are queued on the device at once (backpressure on the flusher; requests
-// keep accumulating into the next, larger batch meanwhile, which is what keeps the device
-// efficient under load).
+// Structure: one service per committee, one open batch per request kind, in the SoA form of
+// that kind's nw_submit_* entry point, in fixed-capacity arrays.
+//   ingest   lock-free: a request reserves its place with one compare-and-swap on the
+//            batch's cursor (request count, header bytes, votes packed in one word), then
+//            copies its signatures, keys, header bytes, offsets and callback into the
+//            reserved ranges. At 10^6 N = 50 certificates per second (~3.4 GB/s of requests
+//            from several threads) a mutex around that bookkeeping made producers queue on
+//            one lock and fall behind their arrivals, in runs that stayed slow once behind.
+//            The mutex is taken only by a batch's first request (to wake the flusher, or to
+//            submit the batch itself when the device is idle), when the arrays are full (the
+//            batch is sealed for submission and the next one gets twice the room), and at
+//            max_items.
+//   flusher  submits a batch as ONE device job (the committee-aware pipeline, or the
+//            one-launch small-job kernel) when it holds max_items units, max_delay has
+//            passed since its first request, it is full, or no job is in flight (an idle
+//            device gains nothing from a bigger batch, so a lone request goes at once and
+//            batches grow only while the device is busy). Taking a batch seals its cursor
+//            (later reservations fail and go to the next batch) and waits for the requests
+//            still copying into it. Among ready batches the oldest goes first.
+//   completer waits for the jobs in submission order and calls every request's verdict
+//            callback. At most max_inflight jobs are on the device at once (backpressure on
+//            the flusher; requests keep accumulating into the next, larger batch meanwhile,
+//            which is what keeps the device efficient under load).
+// Batches are recycled; a batch is never freed before the service (a request that loaded a
+// batch just before it was taken only touches its cursor and writer count, and fails).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -61,55 +72,64 @@ void append(std::vector<T>& v, const void* src, size_t count) {
   if (count) memcpy(v.data() + o, src, count * sizeof(T));
 }
 
-// A byte array that grows only while nobody writes into it (under the mutex, no writers):
-// requests reserve ranges under the mutex and fill them after releasing it. Not
-// zero-initialised (std::vector::resize writes every byte twice).
-struct Buf {
+// Cursor of a batch: requests (bits 0..19), var1 = header bytes (bits 20..43), var2 = votes
+// or verify_batch items (bits 44..62), sealed (bit 63).
+constexpr uint64_t kReqBits = 20, kVar1Bits = 24, kVar2Bits = 19;
+constexpr uint64_t kMaxReq = (1ull << kReqBits) - 1, kMaxVar1 = (1ull << kVar1Bits) - 1,
+                   kMaxVar2 = (1ull << kVar2Bits) - 1;
+constexpr uint64_t kSealed = 1ull << 63;
+inline uint64_t c_req(uint64_t c) { return c & kMaxReq; }
+inline uint64_t c_v1(uint64_t c) { return (c >> kReqBits) & kMaxVar1; }
+inline uint64_t c_v2(uint64_t c) { return (c >> (kReqBits + kVar1Bits)) & kMaxVar2; }
+inline uint64_t c_pack(uint64_t r, uint64_t v1, uint64_t v2) {
+  return r | (v1 << kReqBits) | (v2 << (kReqBits + kVar1Bits));
+}
+
+// A fixed-capacity array whose pages are touched when it is (re)allocated: a page fault on a
+// producer's copy costs more than the copy.
+struct Arr {
   uint8_t* p = nullptr;
-  size_t n = 0, cap = 0;
-  Buf() = default;
-  Buf(const Buf&) = delete;
-  Buf& operator=(const Buf&) = delete;
-  ~Buf() { free(p); }
-  bool fits(size_t k) const { return n + k <= cap; }
-  bool grow(size_t k) {
-    const size_t c = std::max<size_t>({2 * cap, n + k, 4096});
-    void* q = realloc(p, c);
-    if (!q) return false;
-    p = static_cast<uint8_t*>(q);
-    cap = c;
-    return true;
+  size_t cap = 0;
+  Arr() = default;
+  Arr(const Arr&) = delete;
+  Arr& operator=(const Arr&) = delete;
+  ~Arr() { free(p); }
+  bool ensure(size_t c) {
+    if (cap >= c) return true;
+    free(p);
+    p = static_cast<uint8_t*>(malloc(c));
+    cap = p ? c : 0;
+    if (p) memset(p, 0, c);
+    return p != nullptr;
   }
-  uint8_t* take(size_t k) {
-    uint8_t* d = p + n;
-    n += k;
-    return d;
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
   }
-  size_t size() const { return n; }
-  bool empty() const { return n == 0; }
-  const uint8_t* data() const { return p; }
+};
+
+// Room of a batch: requests, header bytes, votes / items.
+struct Caps {
+  uint64_t req, v1, v2;
 };
 
 // One kind's requests in the SoA form of its nw_submit_* entry point.
 struct Batch {
   Kind kind;
-  size_t units = 0;
-  Clock::time_point first;
-  std::vector<Req> reqs;
-  std::atomic<int> writers{0};   // requests copying into the Bufs outside the mutex
+  std::atomic<uint64_t> cursor{kSealed};   // sealed until installed as the open batch
+  std::atomic<int> writers{0};             // requests copying into the batch
+  std::atomic<int64_t> first_ns{0};        // arrival of request 0 (0: not yet stamped)
+  Caps caps{0, 0, 0};
+  uint64_t n = 0, nv1 = 0, nv2 = 0;        // final counts (from the cursor when taken)
+  bool full = false;                       // sealed for lack of room: ready at once
+  Arr reqs;
   // Header / Certificate (nw_certificates)
-  Buf header_bytes;
-  std::vector<uint64_t> header_offsets{0};
-  std::vector<uint32_t> payload_counts;
-  Buf ids, header_sigs;
-  std::vector<uint64_t> vote_offsets{0};
-  Buf vote_pks, vote_sigs;
-  // Vote (nw_submit_votes_verify_many): ids and signatures reuse ids / header_sigs
-  std::vector<uint64_t> rounds;
-  Buf origins, authors;
+  Arr header_bytes, header_offsets, payload_counts, ids, header_sigs, vote_offsets, vote_pks,
+      vote_sigs;
+  // Vote: ids and signatures reuse ids / header_sigs
+  Arr rounds, origins, authors;
   // Signature::verify / verify_batch: digests (n x 32), keys, signatures, batch offsets
-  Buf digests, pks, sigs;
-  std::vector<uint64_t> batch_offsets{0};
+  Arr digests, pks, sigs, batch_offsets;
   // outputs and the job
   std::vector<int32_t> status;
   std::vector<uint64_t> index;
@@ -117,33 +137,59 @@ struct Batch {
   int rc = 0;
 
   explicit Batch(Kind k) : kind(k) {}
-  void clear() {
-    units = 0;
-    reqs.clear();
-    for (Buf* b : {&header_bytes, &ids, &header_sigs, &vote_pks, &vote_sigs, &origins, &authors,
-                   &digests, &pks, &sigs})
-      b->n = 0;
-    header_offsets.assign(1, 0);
-    payload_counts.clear();
-    vote_offsets.assign(1, 0);
-    rounds.clear();
-    batch_offsets.assign(1, 0);
+
+  // arrays for caps c (only the ones this kind uses)
+  bool reserve(const Caps& c) {
+    const uint64_t r = c.req, r1 = c.req + 1;
+    bool ok = reqs.ensure(sizeof(Req) * r);
+    switch (kind) {
+      case K_CERT:
+        ok = ok && vote_offsets.ensure(8 * r1) && vote_pks.ensure(32 * c.v2) &&
+             vote_sigs.ensure(64 * c.v2);
+        [[fallthrough]];
+      case K_HEADER:
+        ok = ok && header_bytes.ensure(c.v1) && header_offsets.ensure(8 * r1) &&
+             payload_counts.ensure(4 * r) && ids.ensure(32 * r) && header_sigs.ensure(64 * r);
+        break;
+      case K_VOTE:
+        ok = ok && ids.ensure(32 * r) && rounds.ensure(8 * r) && origins.ensure(32 * r) &&
+             authors.ensure(32 * r) && header_sigs.ensure(64 * r);
+        break;
+      case K_STRICT:
+        ok = ok && digests.ensure(32 * r) && pks.ensure(32 * r) && sigs.ensure(64 * r);
+        break;
+      case K_BATCH:
+        ok = ok && digests.ensure(32 * r) && batch_offsets.ensure(8 * r1) &&
+             pks.ensure(32 * c.v2) && sigs.ensure(64 * c.v2);
+        break;
+      default:
+        break;
+    }
+    if (!ok) return false;
+    caps = c;
+    return true;
+  }
+  // an empty open batch (under the service mutex; the cursor is published last)
+  void open_empty() {
+    n = nv1 = nv2 = 0;
+    full = false;
     job = nullptr;
     rc = 0;
+    first_ns.store(0, std::memory_order_relaxed);
+    if (header_offsets.p) header_offsets.as<uint64_t>()[0] = 0;
+    if (vote_offsets.p) vote_offsets.as<uint64_t>()[0] = 0;
+    if (batch_offsets.p) batch_offsets.as<uint64_t>()[0] = 0;
+    cursor.store(0, std::memory_order_release);
   }
   // a batch taken for submission: every request that reserved a range has filled it
   void wait_writers() const {
     while (writers.load(std::memory_order_acquire) != 0) std::this_thread::yield();
   }
+  uint64_t units() const { return units_of(kind, n, nv2); }
+  static uint64_t units_of(Kind k, uint64_t r, uint64_t v2) {
+    return (k == K_CERT || k == K_BATCH) ? r + v2 : r;
+  }
 };
-
-// One input range of a request: len bytes from src into the batch's Buf `buf`.
-struct Piece {
-  Buf Batch::*buf;
-  const void* src;
-  size_t len;
-};
-constexpr int kMaxPieces = 5;
 
 uint8_t g_dummy[64];
 
@@ -152,11 +198,26 @@ constexpr int kSpinUs = 2000;
 // Largest batch (units) a request's own thread submits on an idle device (a few
 // certificates): anything bigger is the flusher's.
 constexpr size_t kInlineUnits = 256;
+const uint8_t* nz(const Arr& a, uint64_t count) { return count ? a.p : g_dummy; }
 template <class T>
 const T* nz(const std::vector<T>& v) {
   return v.empty() ? reinterpret_cast<const T*>(g_dummy) : v.data();
 }
-const uint8_t* nz(const Buf& v) { return v.empty() ? g_dummy : v.data(); }
+// Timed condition waits. -DNW_SERVICE_SYSTEM_CLOCK_WAIT (the ThreadSanitizer build of
+// tools/service_stress): on the system clock, because libstdc++ waits on the steady clock
+// with pthread_cond_clockwait, which this image's libtsan does not intercept (it then misses
+// the mutex release inside the wait and reports races under the mutex).
+void wait_ns(std::condition_variable& cv, std::unique_lock<std::mutex>& lk, int64_t ns) {
+#ifdef NW_SERVICE_SYSTEM_CLOCK_WAIT
+  cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::nanoseconds(ns));
+#else
+  cv.wait_for(lk, std::chrono::nanoseconds(ns));
+#endif
+}
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch())
+      .count();
+}
 
 }  // namespace
 
@@ -173,108 +234,184 @@ struct nw_service {
   size_t max_inflight = 4;
 
   std::mutex m;
-  std::condition_variable cv_flush;     // flusher: new request / flush / stop
+  std::condition_variable cv_flush;     // flusher: new batch / full / flush / stop
   std::condition_variable cv_inflight;  // completer: a job was submitted
   std::condition_variable cv_space;     // flusher: in-flight count dropped
   std::condition_variable cv_idle;      // drain: requests completed
+  // open[k] (owned, guarded by m) and cur[k] (its pointer, read lock-free by producers)
   std::unique_ptr<Batch> open[K_COUNT];
+  std::atomic<Batch*> cur[K_COUNT];
+  Caps caps[K_COUNT];                   // room of the next batch of each kind (grows)
+  std::deque<std::unique_ptr<Batch>> sealed;   // full batches waiting for the flusher
   std::vector<std::unique_ptr<Batch>> spare[K_COUNT];
   std::deque<std::unique_ptr<Batch>> inflight;
-  bool force = false, stop = false, flusher_done = false;
-  uint64_t accepted = 0, completed = 0, jobs = 0;
+  std::atomic<bool> stop{false};
+  bool force = false, flusher_done = false;
+  std::atomic<uint64_t> accepted{0};
+  uint64_t completed = 0, jobs = 0;
   // NW_SERVICE_DEBUG: seconds the flusher spent submitting / blocked on max_inflight, the
-  // completer waiting for jobs / running callbacks (printed at destroy)
+  // completer waiting for jobs / running callbacks, caller-thread submits and full batches
+  // (printed at destroy)
   double t_submit = 0, t_backpressure = 0, t_wait = 0, t_callbacks = 0;
+  uint64_t n_inline = 0, n_full = 0;
   size_t open_jobs = 0;   // submitted (or being submitted), callbacks not yet delivered
   size_t submitting = 0;  // submits in progress outside the lock
   bool inline_submit = true;   // NW_SERVICE_INLINE=0: only the flusher submits
   std::thread flusher, completer;
 
-  // Adds one request to its kind's open batch; 0 or NW_E_*. Under the mutex: room in the
-  // batch's Bufs for the request's pieces (growing them waits until no request is still
-  // copying into the batch), its callback, and the small per-request fields (fill: offsets,
-  // counts, rounds); then, with the mutex released, the pieces are copied in.
-  // On an idle device (no job in flight, none being submitted) the caller's thread submits
-  // the oldest batch itself: the request reaches the device without waking the flusher
-  // thread (a futex wake-up is tens of microseconds, a third of a small job).
-  template <class Fill>
-  int add(Kind k, size_t units, nw_verdict_fn fn, void* arg, const Piece* pc, int npc,
-          Fill fill) {
+  // One request of kind k with v1 header bytes and v2 votes / items: reserve its ranges in
+  // the open batch (write(b, i, v1_off, v2_off) fills them), then wake the flusher or submit.
+  template <class Write>
+  int add(Kind k, uint64_t v1, uint64_t v2, nw_verdict_fn fn, void* arg, Write write) {
     if (!fn) return set_err(NW_E_INVALID_ARG, "null verdict callback");
-    std::unique_lock<std::mutex> lk(m, std::defer_lock);
-    lock_spin(lk);
-    if (stop) return set_err(NW_E_INVALID_ARG, "service is shutting down");
+    if (v1 > kMaxVar1 / 2 || v2 > kMaxVar2 / 2)
+      return set_err(NW_E_INVALID_ARG, "request too large for the service");
+    Batch* b;
+    uint64_t c;
     for (;;) {
-      Batch& b = *open[k];
-      bool fits = true;
-      for (int i = 0; i < npc; ++i) fits = fits && (b.*pc[i].buf).fits(pc[i].len);
-      if (fits) break;
-      if (b.writers.load(std::memory_order_acquire) != 0) {
-        lk.unlock();   // let them finish; the batch may be flushed meanwhile
-        b.wait_writers();
-        lk.lock();
+      if (stop.load(std::memory_order_acquire))
+        return set_err(NW_E_INVALID_ARG, "service is shutting down");
+      b = cur[k].load(std::memory_order_acquire);
+      b->writers.fetch_add(1, std::memory_order_seq_cst);
+      c = b->cursor.load(std::memory_order_seq_cst);
+      bool retry = false, room = true;
+      for (;;) {
+        if (c & kSealed) {
+          retry = true;
+          break;
+        }
+        const uint64_t r = c_req(c), a = c_v1(c), z = c_v2(c);
+        if (r + 1 > b->caps.req || a + v1 > b->caps.v1 || z + v2 > b->caps.v2) {
+          room = false;
+          break;
+        }
+        if (b->cursor.compare_exchange_weak(c, c_pack(r + 1, a + v1, z + v2),
+                                            std::memory_order_seq_cst))
+          break;
+      }
+      if (!retry && room) break;
+      b->writers.fetch_sub(1, std::memory_order_release);
+      if (retry) {   // taken meanwhile: the next batch is (about to be) installed
+        std::this_thread::yield();
         continue;
       }
-      for (int i = 0; i < npc; ++i)
-        if (!(b.*pc[i].buf).fits(pc[i].len) && !(b.*pc[i].buf).grow(pc[i].len))
-          return set_err(NW_E_OUT_OF_MEMORY, "service batch");
+      const int rc = make_room(k, b, v1, v2);   // full: seal it, install a bigger one
+      if (rc) return rc;
     }
-    Batch& b = *open[k];
-    const bool first_req = b.reqs.empty();
-    if (first_req) b.first = Clock::now();
-    uint8_t* dst[kMaxPieces];
-    for (int i = 0; i < npc; ++i) dst[i] = (b.*pc[i].buf).take(pc[i].len);
-    fill(b);
-    b.reqs.push_back({fn, arg});
-    b.writers.fetch_add(1, std::memory_order_relaxed);
-    const size_t before = b.units;
-    b.units += units;
-    ++accepted;
-    // Only the first request of a batch goes from the caller's thread (a quiet service): a
-    // batch that filled while the device was busy is the flusher's (the completer wakes it
-    // when the device goes idle), since a submit costs the caller ~0.05-0.1 ms and callers
-    // that stall under load fall behind their own arrivals
-    const bool idle = inline_submit && first_req && open_jobs == 0 && submitting == 0 &&
-                      inflight.size() < max_inflight && b.units <= kInlineUnits;
-    // wake the flusher to arm its timer (first request) or because the batch just filled
-    const bool wake = !idle && (first_req || (before < max_items && b.units >= max_items));
-    lk.unlock();
-    if (wake) cv_flush.notify_one();
-    for (int i = 0; i < npc; ++i)
-      if (pc[i].len) memcpy(dst[i], pc[i].src, pc[i].len);
-    b.writers.fetch_sub(1, std::memory_order_release);
-    if (!idle) return 0;
-    lock_spin(lk);
-    if (open_jobs == 0 && submitting == 0 && inflight.size() < max_inflight && !stop) {
-      // every non-empty batch is ready on an idle device: the oldest goes, as in the flusher
-      // (taking always the caller's own kind let a flood of one kind starve the others)
-      int pick = -1;
-      for (int j = 0; j < K_COUNT; ++j)
-        if (!open[j]->reqs.empty() && (pick < 0 || open[j]->first < open[pick]->first))
-          pick = j;
-      if (pick >= 0 && open[pick]->units > kInlineUnits) pick = -1;   // the flusher's
-      std::unique_ptr<Batch> fresh = pick < 0 ? nullptr : take_spare(static_cast<Kind>(pick));
-      if (fresh) {
-        std::unique_ptr<Batch> own = std::move(open[pick]);
-        open[pick] = std::move(fresh);
-        launch(lk, std::move(own));
-        if (open[k]->reqs.empty()) return 0;
-      }
+    const uint64_t i = c_req(c);
+    write(*b, i, c_v1(c), c_v2(c));
+    b->reqs.as<Req>()[i] = {fn, arg};
+    if (i == 0) b->first_ns.store(now_ns(), std::memory_order_relaxed);
+    const uint64_t before = Batch::units_of(k, i, c_v2(c));
+    const uint64_t after = Batch::units_of(k, i + 1, c_v2(c) + v2);
+    b->writers.fetch_sub(1, std::memory_order_release);
+    accepted.fetch_add(1, std::memory_order_relaxed);
+    if (i == 0) return first_request(k, b);
+    if (before < max_items && after >= max_items) {   // the batch just filled: flush it
+      { std::lock_guard<std::mutex> g(m); }
+      cv_flush.notify_one();
     }
-    lk.unlock();
-    cv_flush.notify_one();   // whatever is left waits for the flusher
     return 0;
   }
 
-  // The service mutex is held for well under a microsecond at a time; a producer that finds
-  // it taken spins briefly instead of sleeping in the kernel (a futex wait and wake-up costs
-  // tens of microseconds, and at 10^6 requests per second producers collide constantly).
-  static void lock_spin(std::unique_lock<std::mutex>& lk) {
-    for (int i = 0; i < 256; ++i) {
-      if (lk.try_lock()) return;
-      __builtin_ia32_pause();
+  // The first request of batch b: the flusher arms its timer for it, or, on an idle device
+  // (no job in flight, none being submitted), the caller's thread submits the oldest
+  // non-empty batch itself — a lone request reaches the device without waking the flusher
+  // (a futex wake-up is tens of microseconds, a third of a small job).
+  int first_request(Kind k, Batch* b) {
+    std::unique_lock<std::mutex> lk(m);
+    (void)k;
+    (void)b;
+    if (inline_submit && open_jobs == 0 && submitting == 0 && inflight.size() < max_inflight &&
+        sealed.empty() && !stop.load(std::memory_order_relaxed)) {
+      int pick = -1;
+      int64_t oldest = 0;
+      for (int j = 0; j < K_COUNT; ++j) {
+        const uint64_t cj = open[j]->cursor.load(std::memory_order_acquire);
+        if (c_req(cj) == 0) continue;
+        int64_t f = open[j]->first_ns.load(std::memory_order_relaxed);
+        if (f == 0) f = now_ns();
+        if (pick < 0 || f < oldest) {
+          pick = j;
+          oldest = f;
+        }
+      }
+      if (pick >= 0) {
+        const uint64_t cp = open[pick]->cursor.load(std::memory_order_acquire);
+        if (Batch::units_of(static_cast<Kind>(pick), c_req(cp), c_v2(cp)) <= kInlineUnits) {
+          std::unique_ptr<Batch> own = take_open(static_cast<Kind>(pick));
+          if (own) {
+            ++n_inline;
+            launch(lk, std::move(own));
+            return 0;
+          }
+        }
+      }
     }
-    lk.lock();
+    lk.unlock();
+    cv_flush.notify_one();
+    return 0;
+  }
+
+  // b (kind k) has no room for a request of v1 / v2: if it is still the open batch, seal it
+  // as full (the flusher submits it next), grow the kind's room to fit, install a new batch.
+  int make_room(Kind k, Batch* b, uint64_t v1, uint64_t v2) {
+    std::unique_lock<std::mutex> lk(m);
+    if (open[k].get() != b) return 0;   // someone else did (retry on the new batch)
+    Caps& c = caps[k];
+    const uint64_t cur_c = b->cursor.load(std::memory_order_acquire);
+    const uint64_t r = c_req(cur_c);
+    // double what overflowed (twice this request at least), up to the cursor's fields
+    if (r + 1 > c.req) c.req = std::min<uint64_t>(kMaxReq, std::max<uint64_t>(2 * c.req, 64));
+    if (c_v1(cur_c) + v1 > c.v1)
+      c.v1 = std::min<uint64_t>(kMaxVar1, std::max<uint64_t>(2 * c.v1, 2 * v1 + 4096));
+    if (c_v2(cur_c) + v2 > c.v2)
+      c.v2 = std::min<uint64_t>(kMaxVar2, std::max<uint64_t>(2 * c.v2, 2 * v2 + 64));
+    std::unique_ptr<Batch> old = take_open(k);
+    if (!old) return set_err(NW_E_OUT_OF_MEMORY, "service batch");
+    if (old->n == 0) {   // empty and too small for this request: recycle it
+      spare[k].push_back(std::move(old));
+      return 0;
+    }
+    ++n_full;
+    old->full = true;
+    sealed.push_back(std::move(old));
+    lk.unlock();
+    cv_flush.notify_one();
+    return 0;
+  }
+
+  // Seals the open batch of kind k and installs a fresh one (under m); nullptr when no
+  // fresh batch could be made (the open batch stays). The sealed batch's final counts are
+  // taken from its cursor; its writers may still be copying (launch waits for them).
+  std::unique_ptr<Batch> take_open(Kind k) {
+    std::unique_ptr<Batch> fresh = take_spare(k);
+    if (!fresh) return nullptr;
+    std::unique_ptr<Batch> b = std::move(open[k]);
+    const uint64_t c = b->cursor.fetch_or(kSealed, std::memory_order_seq_cst);
+    b->n = c_req(c);
+    b->nv1 = c_v1(c);
+    b->nv2 = c_v2(c);
+    fresh->open_empty();
+    open[k] = std::move(fresh);
+    cur[k].store(open[k].get(), std::memory_order_release);
+    return b;
+  }
+
+  std::unique_ptr<Batch> take_spare(Kind k) {
+    std::unique_ptr<Batch> b;
+    if (!spare[k].empty()) {
+      b = std::move(spare[k].back());
+      spare[k].pop_back();
+    } else {
+      b.reset(new (std::nothrow) Batch(k));
+      if (!b) return b;
+    }
+    if (!b->reserve(caps[k])) {
+      spare[k].push_back(std::move(b));
+      return nullptr;
+    }
+    return b;
   }
 
   // Submits b as one device job outside the lock (held on entry and on return) and queues it
@@ -299,18 +436,8 @@ struct nw_service {
     cv_inflight.notify_one();
   }
 
-  std::unique_ptr<Batch> take_spare(Kind k) {
-    if (!spare[k].empty()) {
-      std::unique_ptr<Batch> b = std::move(spare[k].back());
-      spare[k].pop_back();
-      return b;
-    }
-    return std::unique_ptr<Batch>(new (std::nothrow) Batch(k));
-  }
-
-  // Flusher thread: one device job per batch.
   int submit(Batch& b) {
-    const size_t n = b.reqs.size();
+    const size_t n = b.n;
     b.status.assign(n, 0);
     b.index.assign(n, 0);
     switch (b.kind) {
@@ -318,65 +445,78 @@ struct nw_service {
       case K_HEADER: {
         nw_certificates c{};
         c.n = n;
-        c.header_bytes = nz(b.header_bytes);
-        c.header_offsets = b.header_offsets.data();
-        c.payload_counts = b.payload_counts.data();
-        c.ids = b.ids.data();
-        c.header_sigs = b.header_sigs.data();
+        c.header_bytes = nz(b.header_bytes, b.nv1);
+        c.header_offsets = b.header_offsets.as<uint64_t>();
+        c.payload_counts = b.payload_counts.as<uint32_t>();
+        c.ids = b.ids.p;
+        c.header_sigs = b.header_sigs.p;
         if (b.kind == K_CERT) {
-          c.vote_offsets = b.vote_offsets.data();
-          c.vote_pks = nz(b.vote_pks);
-          c.vote_sigs = nz(b.vote_sigs);
+          c.vote_offsets = b.vote_offsets.as<uint64_t>();
+          c.vote_pks = nz(b.vote_pks, b.nv2);
+          c.vote_sigs = nz(b.vote_sigs, b.nv2);
           return nw_submit_certificates_verify_many(&com, &c, nullptr, b.status.data(),
                                                     b.index.data(), &b.job);
         }
         return nw_submit_headers_verify_many(&com, &c, b.status.data(), b.index.data(), &b.job);
       }
       case K_VOTE:
-        return nw_submit_votes_verify_many(&com, b.ids.data(), b.rounds.data(), b.origins.data(),
-                                           b.authors.data(), b.header_sigs.data(), n,
-                                           b.status.data(), &b.job);
+        return nw_submit_votes_verify_many(&com, b.ids.p, b.rounds.as<uint64_t>(), b.origins.p,
+                                           b.authors.p, b.header_sigs.p, n, b.status.data(),
+                                           &b.job);
       case K_STRICT:
-        return nw_submit_verify_strict(b.digests.data(), 32, b.pks.data(), b.sigs.data(), n,
-                                       b.status.data(), nullptr, &b.job);
+        return nw_submit_verify_strict(b.digests.p, 32, b.pks.p, b.sigs.p, n, b.status.data(),
+                                       nullptr, &b.job);
       case K_BATCH:
-        return nw_submit_verify_batch_many(b.digests.data(), nz(b.pks), nz(b.sigs),
-                                           b.batch_offsets.data(), n, nullptr, b.status.data(),
-                                           b.index.data(), &b.job);
+        return nw_submit_verify_batch_many(b.digests.p, nz(b.pks, b.nv2), nz(b.sigs, b.nv2),
+                                           b.batch_offsets.as<uint64_t>(), n, nullptr,
+                                           b.status.data(), b.index.data(), &b.job);
       default:
         return set_err(NW_E_INVALID_ARG, "bad request kind");
     }
   }
 
+  // Flusher thread: one device job per batch.
   void flusher_main() {
     nw_set_device(device);
     std::unique_lock<std::mutex> lk(m);
     for (;;) {
-      const Clock::time_point now = Clock::now();
-      Clock::time_point wake = Clock::time_point::max();
+      const int64_t tnow = now_ns();
+      const int64_t dns = std::chrono::duration_cast<std::chrono::nanoseconds>(delay).count();
+      int64_t wake = INT64_MAX;
       int pick = -1;
-      for (int k = 0; k < K_COUNT; ++k) {
-        const Batch& b = *open[k];
-        if (b.reqs.empty()) continue;
-        // flush: stopping / forced, full, its delay is over, or the device is idle (no job
-        // in flight: waiting would only add latency, nothing is gained by a bigger batch).
-        // Among the ready kinds the one whose first request is oldest goes first, so a
-        // saturating certificate load cannot starve a trickle of votes or headers (the
-        // primary's Core interleaves all three, primary/src/core.rs:349-411).
-        if (stop || force || b.units >= max_items || now >= b.first + delay ||
-            open_jobs == 0) {
-          if (pick < 0 || b.first < open[pick]->first) pick = k;
-        } else if (b.first + delay < wake) {
-          wake = b.first + delay;
+      int64_t oldest = INT64_MAX;
+      // full batches first (oldest first), then the ready open batches, oldest first: a
+      // flood of one kind cannot starve a trickle of another (the primary's Core
+      // interleaves all three, primary/src/core.rs:349-411)
+      bool have_sealed = !sealed.empty();
+      if (!have_sealed) {
+        for (int k = 0; k < K_COUNT; ++k) {
+          const Batch& b = *open[k];
+          const uint64_t c = b.cursor.load(std::memory_order_acquire);
+          if (c_req(c) == 0) continue;
+          int64_t f = b.first_ns.load(std::memory_order_relaxed);
+          if (f == 0) f = tnow;
+          const bool ready = stop.load(std::memory_order_relaxed) || force ||
+                             Batch::units_of(static_cast<Kind>(k), c_req(c), c_v2(c)) >=
+                                 max_items ||
+                             tnow >= f + dns || open_jobs == 0;
+          if (ready) {
+            if (f < oldest) {
+              pick = k;
+              oldest = f;
+            }
+          } else if (f + dns < wake) {
+            wake = f + dns;
+          }
         }
       }
-      if (pick < 0) {
+      if (!have_sealed && pick < 0) {
         force = false;
-        if (stop) break;
-        if (wake == Clock::time_point::max())
+        if (stop.load(std::memory_order_relaxed)) break;
+        if (wake == INT64_MAX)
           cv_flush.wait(lk);
         else
-          cv_flush.wait_until(lk, wake);
+          wait_ns(cv_flush, lk, wake - tnow);
         continue;
       }
       // backpressure: at most max_inflight jobs queued; the open batch keeps growing
@@ -386,13 +526,17 @@ struct nw_service {
         t_backpressure += std::chrono::duration<double>(Clock::now() - w0).count();
         continue;
       }
-      std::unique_ptr<Batch> fresh = take_spare(static_cast<Kind>(pick));
-      if (!fresh) {   // out of memory: submit nothing new until something completes
-        cv_space.wait_for(lk, std::chrono::milliseconds(1));
-        continue;
+      std::unique_ptr<Batch> b;
+      if (have_sealed) {
+        b = std::move(sealed.front());
+        sealed.pop_front();
+      } else {
+        b = take_open(static_cast<Kind>(pick));
+        if (!b) {   // out of memory: submit nothing new until something completes
+          wait_ns(cv_space, lk, 1000000);
+          continue;
+        }
       }
-      std::unique_ptr<Batch> b = std::move(open[pick]);
-      open[pick] = std::move(fresh);
       launch(lk, std::move(b));
     }
     flusher_done = true;
@@ -425,9 +569,10 @@ struct nw_service {
         b->job = nullptr;
       }
       const Clock::time_point c0 = Clock::now();
-      const size_t n = b->reqs.size();
+      const size_t n = b->n;
+      const Req* reqs = b->reqs.as<Req>();
       for (size_t i = 0; i < n; ++i)
-        b->reqs[i].fn(b->reqs[i].arg, rc ? rc : b->status[i], rc ? 0 : b->index[i]);
+        reqs[i].fn(reqs[i].arg, rc ? rc : b->status[i], rc ? 0 : b->index[i]);
       const Clock::time_point c1 = Clock::now();
       lk.lock();
       std::unique_ptr<Batch> own = std::move(inflight.front());
@@ -437,8 +582,7 @@ struct nw_service {
       t_callbacks += std::chrono::duration<double>(c1 - c0).count();
       completed += n;
       if (--open_jobs == 0) cv_flush.notify_one();   // device idle: flush what has queued
-      own->clear();
-      spare[own->kind].push_back(std::move(own));
+      spare[own->kind].push_back(std::move(own));    // cursor stays sealed while spare
       cv_idle.notify_all();
     }
   }
@@ -478,11 +622,15 @@ int nw_service_create(const nw_committee* committee, size_t max_items, uint32_t 
     s->com.worker_ids = nz(s->com_wi);
   }
   for (int k = 0; k < K_COUNT; ++k) {
-    s->open[k].reset(new (std::nothrow) Batch(static_cast<Kind>(k)));
-    if (!s->open[k]) {
+    s->caps[k] = Caps{1024, 1 << 16, 1 << 14};
+    std::unique_ptr<Batch> b = s->take_spare(static_cast<Kind>(k));
+    if (!b) {
       delete s;
       return set_err(NW_E_OUT_OF_MEMORY, "service allocation");
     }
+    b->open_empty();
+    s->open[k] = std::move(b);
+    s->cur[k].store(s->open[k].get(), std::memory_order_release);
   }
   try {
     s->flusher = std::thread([s] { s->flusher_main(); });
@@ -525,16 +673,19 @@ int nw_service_certificate(nw_service* s, const uint8_t* header_bytes, size_t he
   if (!rc) rc = check_header(header_bytes, header_len, payload_count, id, header_sig);
   if (rc) return rc;
   if (nvotes && (!vote_pks || !vote_sigs)) return set_err(NW_E_INVALID_ARG, "null votes");
-  const Piece pc[] = {{&Batch::header_bytes, header_bytes, header_len},
-                      {&Batch::ids, id, 32},
-                      {&Batch::header_sigs, header_sig, 64},
-                      {&Batch::vote_pks, vote_pks, 32 * nvotes},
-                      {&Batch::vote_sigs, vote_sigs, 64 * nvotes}};
-  return s->add(K_CERT, 1 + nvotes, fn, arg, pc, 5, [&](Batch& b) {
-    b.header_offsets.push_back(b.header_bytes.size());
-    b.payload_counts.push_back(payload_count);
-    b.vote_offsets.push_back(b.vote_offsets.back() + nvotes);
-  });
+  return s->add(K_CERT, header_len, nvotes, fn, arg,
+                [&](Batch& b, uint64_t i, uint64_t h, uint64_t v) {
+                  memcpy(b.header_bytes.p + h, header_bytes, header_len);
+                  b.header_offsets.as<uint64_t>()[i + 1] = h + header_len;
+                  b.payload_counts.as<uint32_t>()[i] = payload_count;
+                  memcpy(b.ids.p + 32 * i, id, 32);
+                  memcpy(b.header_sigs.p + 64 * i, header_sig, 64);
+                  if (nvotes) {
+                    memcpy(b.vote_pks.p + 32 * v, vote_pks, 32 * nvotes);
+                    memcpy(b.vote_sigs.p + 64 * v, vote_sigs, 64 * nvotes);
+                  }
+                  b.vote_offsets.as<uint64_t>()[i + 1] = v + nvotes;
+                });
 }
 
 int nw_service_header(nw_service* s, const uint8_t* header_bytes, size_t header_len,
@@ -543,13 +694,14 @@ int nw_service_header(nw_service* s, const uint8_t* header_bytes, size_t header_
   int rc = need_committee(s);
   if (!rc) rc = check_header(header_bytes, header_len, payload_count, id, sig);
   if (rc) return rc;
-  const Piece pc[] = {{&Batch::header_bytes, header_bytes, header_len},
-                      {&Batch::ids, id, 32},
-                      {&Batch::header_sigs, sig, 64}};
-  return s->add(K_HEADER, 1, fn, arg, pc, 3, [&](Batch& b) {
-    b.header_offsets.push_back(b.header_bytes.size());
-    b.payload_counts.push_back(payload_count);
-  });
+  return s->add(K_HEADER, header_len, 0, fn, arg,
+                [&](Batch& b, uint64_t i, uint64_t h, uint64_t) {
+                  memcpy(b.header_bytes.p + h, header_bytes, header_len);
+                  b.header_offsets.as<uint64_t>()[i + 1] = h + header_len;
+                  b.payload_counts.as<uint32_t>()[i] = payload_count;
+                  memcpy(b.ids.p + 32 * i, id, 32);
+                  memcpy(b.header_sigs.p + 64 * i, sig, 64);
+                });
 }
 
 int nw_service_vote(nw_service* s, const uint8_t* id, uint64_t round, const uint8_t* origin,
@@ -557,30 +709,37 @@ int nw_service_vote(nw_service* s, const uint8_t* id, uint64_t round, const uint
   int rc = need_committee(s);
   if (rc) return rc;
   if (!id || !origin || !author || !sig) return set_err(NW_E_INVALID_ARG, "null pointer");
-  const Piece pc[] = {{&Batch::ids, id, 32},
-                      {&Batch::origins, origin, 32},
-                      {&Batch::authors, author, 32},
-                      {&Batch::header_sigs, sig, 64}};
-  return s->add(K_VOTE, 1, fn, arg, pc, 4, [&](Batch& b) { b.rounds.push_back(round); });
+  return s->add(K_VOTE, 0, 0, fn, arg, [&](Batch& b, uint64_t i, uint64_t, uint64_t) {
+    memcpy(b.ids.p + 32 * i, id, 32);
+    b.rounds.as<uint64_t>()[i] = round;
+    memcpy(b.origins.p + 32 * i, origin, 32);
+    memcpy(b.authors.p + 32 * i, author, 32);
+    memcpy(b.header_sigs.p + 64 * i, sig, 64);
+  });
 }
 
 int nw_service_verify(nw_service* s, const uint8_t* digest, const uint8_t* pk,
                       const uint8_t* sig, nw_verdict_fn fn, void* arg) {
   if (!s) return set_err(NW_E_INVALID_ARG, "null service");
   if (!digest || !pk || !sig) return set_err(NW_E_INVALID_ARG, "null pointer");
-  const Piece pc[] = {{&Batch::digests, digest, 32}, {&Batch::pks, pk, 32},
-                      {&Batch::sigs, sig, 64}};
-  return s->add(K_STRICT, 1, fn, arg, pc, 3, [](Batch&) {});
+  return s->add(K_STRICT, 0, 0, fn, arg, [&](Batch& b, uint64_t i, uint64_t, uint64_t) {
+    memcpy(b.digests.p + 32 * i, digest, 32);
+    memcpy(b.pks.p + 32 * i, pk, 32);
+    memcpy(b.sigs.p + 64 * i, sig, 64);
+  });
 }
 
 int nw_service_verify_batch(nw_service* s, const uint8_t* digest, const uint8_t* pks,
                             const uint8_t* sigs, size_t n, nw_verdict_fn fn, void* arg) {
   if (!s) return set_err(NW_E_INVALID_ARG, "null service");
   if (!digest || (n && (!pks || !sigs))) return set_err(NW_E_INVALID_ARG, "null pointer");
-  const Piece pc[] = {{&Batch::digests, digest, 32}, {&Batch::pks, pks, 32 * n},
-                      {&Batch::sigs, sigs, 64 * n}};
-  return s->add(K_BATCH, n ? n : 1, fn, arg, pc, 3, [&](Batch& b) {
-    b.batch_offsets.push_back(b.batch_offsets.back() + n);
+  return s->add(K_BATCH, 0, n, fn, arg, [&](Batch& b, uint64_t i, uint64_t, uint64_t v) {
+    memcpy(b.digests.p + 32 * i, digest, 32);
+    if (n) {
+      memcpy(b.pks.p + 32 * v, pks, 32 * n);
+      memcpy(b.sigs.p + 64 * v, sigs, 64 * n);
+    }
+    b.batch_offsets.as<uint64_t>()[i + 1] = v + n;
   });
 }
 
@@ -597,7 +756,7 @@ int nw_service_flush(nw_service* s) {
 int nw_service_drain(nw_service* s) {
   if (!s) return set_err(NW_E_INVALID_ARG, "null service");
   std::unique_lock<std::mutex> lk(s->m);
-  const uint64_t target = s->accepted;
+  const uint64_t target = s->accepted.load(std::memory_order_acquire);
   s->force = true;
   s->cv_flush.notify_one();
   s->cv_idle.wait(lk, [&] { return s->completed >= target; });
@@ -607,7 +766,7 @@ int nw_service_drain(nw_service* s) {
 int nw_service_stats(nw_service* s, uint64_t* requests, uint64_t* jobs) {
   if (!s) return set_err(NW_E_INVALID_ARG, "null service");
   std::lock_guard<std::mutex> g(s->m);
-  if (requests) *requests = s->accepted;
+  if (requests) *requests = s->accepted.load(std::memory_order_acquire);
   if (jobs) *jobs = s->jobs;
   return 0;
 }
@@ -624,9 +783,11 @@ void nw_service_destroy(nw_service* s) {
   s->completer.join();
   if (getenv("NW_SERVICE_DEBUG"))
     fprintf(stderr,
-            "[narwhal_amd] service: %llu requests, %llu jobs; flusher submit %.3f s, "
-            "backpressure %.3f s; completer wait %.3f s, callbacks %.3f s\n",
-            (unsigned long long)s->accepted, (unsigned long long)s->jobs, s->t_submit,
+            "[narwhal_amd] service: %llu requests, %llu jobs (%llu from callers' threads, "
+            "%llu full batches); submit %.3f s, backpressure %.3f s; completer wait %.3f s, "
+            "callbacks %.3f s\n",
+            (unsigned long long)s->accepted.load(), (unsigned long long)s->jobs,
+            (unsigned long long)s->n_inline, (unsigned long long)s->n_full, s->t_submit,
             s->t_backpressure, s->t_wait, s->t_callbacks);
   delete s;
 }

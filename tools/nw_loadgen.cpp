@@ -9,6 +9,7 @@
 // behind its schedule shows up as latency, not as a lower offered rate. Every verdict is
 // compared with the expected (status, index) of the corpus row it came from.
 #include <string.h>
+#include <sys/resource.h>
 
 #include <algorithm>
 #include <atomic>
@@ -57,9 +58,11 @@ int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_s
 extern "C" {
 
 // Returns 0 or the first negative NW_E_* from the service. lat_out: total seconds;
-// out (5 doubles): elapsed seconds (t0 .. last verdict), jobs, mismatches, and the
+// out (11 doubles): elapsed seconds (t0 .. last verdict), jobs, mismatches, and the
 // producers' lateness: the largest and the mean (call time - due time) of a submit, seconds
-// (a producer that cannot keep its schedule shows here before it shows as latency).
+// (a producer that cannot keep its schedule shows here before it shows as latency), then
+// the producers' CPU / wall time and their voluntary / involuntary context switches, and
+// the nw_service_certificate calls' mean and longest duration and the count above 20 us.
 int nw_loadgen_certificates(const nw_committee* com, const nw_certificates* corpus,
                             const int32_t* exp_status, const uint64_t* exp_index, double rate,
                             uint64_t total, size_t max_items, uint32_t max_delay_us,
@@ -126,6 +129,8 @@ int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_s
   run.lat = lat_out;
   std::vector<Rec> recs(total);
   std::atomic<int> first_err{0};
+  std::vector<double> call_sum(producers, 0.0), call_max(producers, 0.0);
+  std::vector<uint64_t> call_slow(producers, 0);
   auto submit = [&](uint64_t i) {
     const size_t u = i % corpus->n;
     const uint64_t h0 = corpus->header_offsets[u], h1 = corpus->header_offsets[u + 1];
@@ -150,8 +155,13 @@ int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_s
                             std::chrono::duration<double>(period * (double)i))};
   std::vector<std::thread> th;
   std::vector<double> lag_max(producers, 0.0), lag_sum(producers, 0.0);
+  std::vector<double> cpu_s(producers, 0.0), wall_s(producers, 0.0);
+  std::vector<long> vcsw(producers, 0), ivcsw(producers, 0);
   for (uint32_t p = 0; p < producers; ++p)
     th.emplace_back([&, p] {
+      const Clock::time_point w0 = Clock::now();
+      struct rusage r0, r1;
+      getrusage(RUSAGE_THREAD, &r0);
       for (uint64_t i = p; i < total; i += producers) {
         const Clock::time_point due = recs[i].due;
         Clock::time_point now = Clock::now();
@@ -162,7 +172,17 @@ int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_s
         lag_max[p] = std::max(lag_max[p], lag);
         lag_sum[p] += lag;
         submit(i);
+        const double c = std::chrono::duration<double>(Clock::now() - now).count();
+        call_sum[p] += c;
+        call_max[p] = std::max(call_max[p], c);
+        call_slow[p] += c > 20e-6;
       }
+      getrusage(RUSAGE_THREAD, &r1);
+      auto sec = [](const timeval& t) { return (double)t.tv_sec + 1e-6 * (double)t.tv_usec; };
+      cpu_s[p] = sec(r1.ru_utime) + sec(r1.ru_stime) - sec(r0.ru_utime) - sec(r0.ru_stime);
+      wall_s[p] = std::chrono::duration<double>(Clock::now() - w0).count();
+      vcsw[p] = r1.ru_nvcsw - r0.ru_nvcsw;
+      ivcsw[p] = r1.ru_nivcsw - r0.ru_nivcsw;
     });
   for (auto& t : th) t.join();
   nw_service_drain(s);
@@ -178,6 +198,25 @@ int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_s
   }
   out[3] = lm;
   out[4] = ls / (double)(total ? total : 1);
+  double cs = 0, ws = 0, v = 0, iv = 0;
+  for (uint32_t p = 0; p < producers; ++p) {
+    cs += cpu_s[p];
+    ws += wall_s[p];
+    v += (double)vcsw[p];
+    iv += (double)ivcsw[p];
+  }
+  out[5] = ws > 0 ? cs / ws : 0;   // producers' CPU time / wall time (1 = never off-CPU)
+  out[6] = v;                      // voluntary context switches (sleeps: futex, nanosleep)
+  out[7] = iv;                     // involuntary ones (preempted: CPU contention)
+  double cs2 = 0, cm = 0, sl = 0;
+  for (uint32_t p = 0; p < producers; ++p) {
+    cs2 += call_sum[p];
+    cm = std::max(cm, call_max[p]);
+    sl += (double)call_slow[p];
+  }
+  out[8] = cs2 / (double)(total ? total : 1);   // mean nw_service_certificate call, seconds
+  out[9] = cm;                                  // longest call
+  out[10] = sl;                                 // calls longer than 20 us
   return first_err.load();
 }
 }  // namespace
