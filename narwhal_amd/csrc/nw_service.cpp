@@ -20,15 +20,16 @@
 //            one lock and fall behind their arrivals, in runs that stayed slow once behind.
 //            The mutex is taken only by a batch's first request (to wake the flusher, or to
 //            submit the batch itself when the device is idle), when the arrays are full (the
-//            batch is sealed for submission and the next one gets twice the room), and at
-//            max_items.
+//            batch is sealed for submission and the next one gets twice the room), and when
+//            a batch reaches max_items units (sealed too: a job holds about max_items).
 //   flusher  submits a batch as ONE device job (the committee-aware pipeline, or the
-//            one-launch small-job kernel) when it holds max_items units, max_delay has
-//            passed since its first request, it is full, or no job is in flight (an idle
-//            device gains nothing from a bigger batch, so a lone request goes at once and
-//            batches grow only while the device is busy). Taking a batch seals its cursor
-//            (later reservations fail and go to the next batch) and waits for the requests
-//            still copying into it. Among ready batches the oldest goes first.
+//            one-launch small-job kernel) when it is sealed, max_delay has passed since its
+//            first request, or no job is in flight (an idle device gains nothing from a
+//            bigger batch, so a lone request goes at once and batches grow only while the
+//            device is busy). Taking an open batch seals its cursor (later reservations fail
+//            and go to the next batch) and waits for the requests still copying into it.
+//            Kinds with ready batches take turns, so a flood of certificates cannot starve
+//            a trickle of votes.
 //   completer waits for the jobs in submission order and calls every request's verdict
 //            callback. At most max_inflight jobs are on the device at once (backpressure on
 //            the flusher; requests keep accumulating into the next, larger batch meanwhile,
@@ -121,7 +122,6 @@ struct Batch {
   std::atomic<int64_t> first_ns{0};        // arrival of request 0 (0: not yet stamped)
   Caps caps{0, 0, 0};
   uint64_t n = 0, nv1 = 0, nv2 = 0;        // final counts (from the cursor when taken)
-  bool full = false;                       // sealed for lack of room: ready at once
   Arr reqs;
   // Header / Certificate (nw_certificates)
   Arr header_bytes, header_offsets, payload_counts, ids, header_sigs, vote_offsets, vote_pks,
@@ -172,7 +172,6 @@ struct Batch {
   // an empty open batch (under the service mutex; the cursor is published last)
   void open_empty() {
     n = nv1 = nv2 = 0;
-    full = false;
     job = nullptr;
     rc = 0;
     first_ns.store(0, std::memory_order_relaxed);
@@ -242,7 +241,10 @@ struct nw_service {
   std::unique_ptr<Batch> open[K_COUNT];
   std::atomic<Batch*> cur[K_COUNT];
   Caps caps[K_COUNT];                   // room of the next batch of each kind (grows)
-  std::deque<std::unique_ptr<Batch>> sealed;   // full batches waiting for the flusher
+  // per kind: batches sealed full (no room, or max_items reached) waiting for the flusher
+  std::deque<std::unique_ptr<Batch>> sealed[K_COUNT];
+  size_t nsealed = 0;
+  int last_kind = K_COUNT - 1;          // the flusher's round-robin position
   std::vector<std::unique_ptr<Batch>> spare[K_COUNT];
   std::deque<std::unique_ptr<Batch>> inflight;
   std::atomic<bool> stop{false};
@@ -307,11 +309,24 @@ struct nw_service {
     b->writers.fetch_sub(1, std::memory_order_release);
     accepted.fetch_add(1, std::memory_order_relaxed);
     if (i == 0) return first_request(k, b);
-    if (before < max_items && after >= max_items) {   // the batch just filled: flush it
-      { std::lock_guard<std::mutex> g(m); }
-      cv_flush.notify_one();
-    }
+    if (before < max_items && after >= max_items) seal_full(k, b);   // the batch is done
     return 0;
+  }
+
+  // b reached max_items: if it is still the open batch, seal it for the flusher and open the
+  // next (a job never holds much more than max_items units, however fast requests arrive).
+  void seal_full(Kind k, Batch* b) {
+    std::unique_lock<std::mutex> lk(m);
+    if (open[k].get() == b) {
+      std::unique_ptr<Batch> old = take_open(k);
+      if (old) {
+        ++n_full;
+        sealed[k].push_back(std::move(old));
+        ++nsealed;
+      }
+    }
+    lk.unlock();
+    cv_flush.notify_one();
   }
 
   // The first request of batch b: the flusher arms its timer for it, or, on an idle device
@@ -323,7 +338,7 @@ struct nw_service {
     (void)k;
     (void)b;
     if (inline_submit && open_jobs == 0 && submitting == 0 && inflight.size() < max_inflight &&
-        sealed.empty() && !stop.load(std::memory_order_relaxed)) {
+        nsealed == 0 && !stop.load(std::memory_order_relaxed)) {
       int pick = -1;
       int64_t oldest = 0;
       for (int j = 0; j < K_COUNT; ++j) {
@@ -374,8 +389,8 @@ struct nw_service {
       return 0;
     }
     ++n_full;
-    old->full = true;
-    sealed.push_back(std::move(old));
+    sealed[k].push_back(std::move(old));
+    ++nsealed;
     lk.unlock();
     cv_flush.notify_one();
     return 0;
@@ -484,33 +499,32 @@ struct nw_service {
       const int64_t dns = std::chrono::duration_cast<std::chrono::nanoseconds>(delay).count();
       int64_t wake = INT64_MAX;
       int pick = -1;
-      int64_t oldest = INT64_MAX;
-      // full batches first (oldest first), then the ready open batches, oldest first: a
-      // flood of one kind cannot starve a trickle of another (the primary's Core
-      // interleaves all three, primary/src/core.rs:349-411)
-      bool have_sealed = !sealed.empty();
-      if (!have_sealed) {
-        for (int k = 0; k < K_COUNT; ++k) {
-          const Batch& b = *open[k];
-          const uint64_t c = b.cursor.load(std::memory_order_acquire);
-          if (c_req(c) == 0) continue;
-          int64_t f = b.first_ns.load(std::memory_order_relaxed);
-          if (f == 0) f = tnow;
-          const bool ready = stop.load(std::memory_order_relaxed) || force ||
-                             Batch::units_of(static_cast<Kind>(k), c_req(c), c_v2(c)) >=
-                                 max_items ||
-                             tnow >= f + dns || open_jobs == 0;
-          if (ready) {
-            if (f < oldest) {
-              pick = k;
-              oldest = f;
-            }
-          } else if (f + dns < wake) {
-            wake = f + dns;
-          }
+      // Per kind: a sealed batch (full, or at max_items) is ready; an open one when its
+      // delay is over, the device is idle, or on flush / stop. Kinds with ready work take
+      // turns (round-robin): under a flood of one kind (sealed batches queueing faster than
+      // the device takes them) a trickle of another still goes within a job or two — the
+      // primary's Core interleaves all three (primary/src/core.rs:349-411).
+      bool ready[K_COUNT] = {};
+      for (int k = 0; k < K_COUNT; ++k) {
+        if (!sealed[k].empty()) {
+          ready[k] = true;
+          continue;
         }
+        const Batch& b = *open[k];
+        const uint64_t c = b.cursor.load(std::memory_order_acquire);
+        if (c_req(c) == 0) continue;
+        int64_t f = b.first_ns.load(std::memory_order_relaxed);
+        if (f == 0) f = tnow;
+        ready[k] = stop.load(std::memory_order_relaxed) || force ||
+                   Batch::units_of(static_cast<Kind>(k), c_req(c), c_v2(c)) >= max_items ||
+                   tnow >= f + dns || open_jobs == 0;
+        if (!ready[k] && f + dns < wake) wake = f + dns;
       }
-      if (!have_sealed && pick < 0) {
+      for (int d = 1; d <= K_COUNT && pick < 0; ++d) {
+        const int k = (last_kind + d) % K_COUNT;
+        if (ready[k]) pick = k;
+      }
+      if (pick < 0) {
         force = false;
         if (stop.load(std::memory_order_relaxed)) break;
         if (wake == INT64_MAX)
@@ -527,9 +541,10 @@ struct nw_service {
         continue;
       }
       std::unique_ptr<Batch> b;
-      if (have_sealed) {
-        b = std::move(sealed.front());
-        sealed.pop_front();
+      if (!sealed[pick].empty()) {
+        b = std::move(sealed[pick].front());
+        sealed[pick].pop_front();
+        --nsealed;
       } else {
         b = take_open(static_cast<Kind>(pick));
         if (!b) {   // out of memory: submit nothing new until something completes
@@ -537,6 +552,7 @@ struct nw_service {
           continue;
         }
       }
+      last_kind = pick;
       launch(lk, std::move(b));
     }
     flusher_done = true;
