@@ -129,12 +129,14 @@ def main():
     for tag, r in res.items():
         if r["mode"] != "keyed":
             continue
-        per = [e for k, e in r["kernels"].items() if not k.startswith(setup)]
+        call_k = {k: e for k, e in r["kernels"].items()
+                  if k.startswith("k_") and not k.startswith(setup)}   # library kernels
+        per = list(call_k.values())
         if not per or any("hbm_read_bytes" not in e for e in per):
             continue
         tr[f"N{r['committee']}"] = {
             "hbm_bytes_per_vote": sum(e["hbm_bytes_per_vote"] for e in per),
-            "kernels": sorted(k for k in r["kernels"] if not k.startswith(setup)),
+            "kernels": sorted(call_k),
             "source": os.path.join(dst, "cert_pmc.json")}
     json.dump(tr, open(os.path.join(dst, "cert_traffic.json"), "w"), indent=1, sort_keys=True)
     for tag, r in res.items():
