@@ -15,7 +15,7 @@ export TMPDIR=/tmp
 TAG=${1:-run}
 OUT=$PWD/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
-PMC_ARGS="--steps 1 --warmup 0 --no-cert --no-batch --no-wire --no-service --no-cpu-baseline"
+PMC_ARGS="--steps 1 --warmup 0 --no-cert --no-batch --no-wire --no-service --no-worker --no-cpu-baseline"
 
 timeout -s KILL 60 rocprofv3 -L > "$OUT/counters_available.txt" 2>&1
 echo "list rc=$?"
