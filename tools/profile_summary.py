@@ -34,6 +34,7 @@ KERNELS = {"k_verify_strict": ("config4 strict verify launch", 12_500_000, "veri
 def short(name):
     m = re.match(r"(?:void )?([\w:]+(?:\(anonymous namespace\)::)?\w+)\(", name)
     base = m.group(1) if m else name.split("(")[0]
+    base = re.sub(r"<[^<>]*>", "", base)   # k_verify_strict<false> -> k_verify_strict
     return base.split("::")[-1][:60]
 
 
