@@ -616,16 +616,28 @@ int submit_small(int dev, uint32_t kind, const nw_committee* com, const nw_certi
         std::sort(v.begin(), v.end());
         med[p] = v.empty() ? -1.0 : v[v.size() / 2];
       }
-      uint64_t t0 = ~0ull, t1 = 0;
+      uint64_t t0 = ~0ull, t1 = 0, s1 = 0, wl = 0;
       for (uint64_t w = 0; w < nwg; ++w) {
         t0 = std::min(t0, st[8 * w]);
-        t1 = std::max(t1, st[8 * w + 7]);
+        s1 = std::max(s1, st[8 * w]);
+        if (st[8 * w + 7] > t1) {
+          t1 = st[8 * w + 7];
+          wl = w;
+        }
       }
+      // the workgroup that ended last: its phases relative to its own start
+      double last[8];
+      for (int p = 0; p < 8; ++p)
+        last[p] = st[8 * wl + p] >= st[8 * wl] ? (double)(st[8 * wl + p] - st[8 * wl]) * 0.01 : -1.0;
       fprintf(stderr, "[narwhal_amd] k_small kind=%u slots=%llu S=%u wgs=%llu: decomp %.1f msg %.1f "
               "digits %.1f comb %.1f sync %.1f slots %.1f end %.1f us (median per workgroup); "
-              "first start -> last end %.1f us\n", kind, (unsigned long long)nslots,
+              "first start -> last end %.1f us, last start +%.1f us; last-ending wg %llu "
+              "(start +%.1f): decomp %.1f msg %.1f digits %.1f comb %.1f sync %.1f slots %.1f "
+              "end %.1f\n", kind, (unsigned long long)nslots,
               J.slots_per_wg, (unsigned long long)nwg, med[1], med[2], med[3], med[4], med[5],
-              med[6], med[7], (double)(t1 - t0) * 0.01);
+              med[6], med[7], (double)(t1 - t0) * 0.01, (double)(s1 - t0) * 0.01,
+              (unsigned long long)wl, (double)(st[8 * wl] - t0) * 0.01, last[1], last[2],
+              last[3], last[4], last[5], last[6], last[7]);
     }
     (void)hipFree(J.stamps);
   }

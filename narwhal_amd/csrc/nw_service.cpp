@@ -19,14 +19,15 @@
 //            from several threads) a mutex around that bookkeeping made producers queue on
 //            one lock and fall behind their arrivals, in runs that stayed slow once behind.
 //            The mutex is taken only by a batch's first request (to wake the flusher, or to
-//            submit the batch itself when the device is idle), when the arrays are full (the
+//            submit the batch itself when a job slot is free), when the arrays are full (the
 //            batch is sealed for submission and the next one gets twice the room), and when
 //            a batch reaches max_items units (sealed too: a job holds about max_items).
 //   flusher  submits a batch as ONE device job (the committee-aware pipeline, or the
 //            one-launch small-job kernel) when it is sealed, max_delay has passed since its
-//            first request, or no job is in flight (an idle device gains nothing from a
-//            bigger batch, so a lone request goes at once and batches grow only while the
-//            device is busy). Taking an open batch seals its cursor (later reservations fail
+//            first request, or fewer than eager_jobs (2) jobs are open (a device with a free
+//            slot gains nothing from a bigger batch: small-job launches only read the shared
+//            tables and run side by side, so a lone request goes at once and batches grow
+//            only while the device is busy). Taking an open batch seals its cursor (later reservations fail
 //            and go to the next batch) and waits for the requests still copying into it.
 //            Kinds with ready batches take turns, so a flood of certificates cannot starve
 //            a trickle of votes.
@@ -122,6 +123,7 @@ struct Batch {
   std::atomic<int64_t> first_ns{0};        // arrival of request 0 (0: not yet stamped)
   Caps caps{0, 0, 0};
   uint64_t n = 0, nv1 = 0, nv2 = 0;        // final counts (from the cursor when taken)
+  int64_t t_taken = 0, t_sub0 = 0, t_sub1 = 0;   // NW_SERVICE_DEBUG: taken, submit start / end
   Arr reqs;
   // Header / Certificate (nw_certificates)
   Arr header_bytes, header_offsets, payload_counts, ids, header_sigs, vote_offsets, vote_pks,
@@ -256,9 +258,20 @@ struct nw_service {
   // (printed at destroy)
   double t_submit = 0, t_backpressure = 0, t_wait = 0, t_callbacks = 0;
   uint64_t n_inline = 0, n_full = 0;
+  // NW_SERVICE_DEBUG: per job, microseconds from its first request to: taken, submit start,
+  // submitted, done seen by the completer, callbacks delivered (medians printed at destroy)
+  bool debug = false;
+  std::vector<float> d_taken, d_sub0, d_sub1, d_done, d_cb;
   size_t open_jobs = 0;   // submitted (or being submitted), callbacks not yet delivered
   size_t submitting = 0;  // submits in progress outside the lock
   bool inline_submit = true;   // NW_SERVICE_INLINE=0: only the flusher submits
+  // A batch goes at once (no max_delay wait) while fewer than eager_jobs jobs are open: one
+  // small-job launch only reads the shared tables, so a second one runs beside the first
+  // instead of after it (NW_SERVICE_EAGER; 1 = only on an idle device). A/B with the
+  // service leg (profiles/r04b/service_eager_ab.txt): p50 at N = 4 and 10^5..10^6 certs/s
+  // 0.09-0.10 vs 0.11-0.12 ms, N = 50 at 10^4 0.16 vs 0.22 ms; N = 50 at 10^5 0.26 vs
+  // 0.18 ms (smaller jobs, each paying the header digest's serial chain)
+  size_t eager_jobs = 2;
   std::thread flusher, completer;
 
   // One request of kind k with v1 header bytes and v2 votes / items: reserve its ranges in
@@ -329,15 +342,16 @@ struct nw_service {
     cv_flush.notify_one();
   }
 
-  // The first request of batch b: the flusher arms its timer for it, or, on an idle device
-  // (no job in flight, none being submitted), the caller's thread submits the oldest
+  // The first request of batch b: the flusher arms its timer for it, or, with a job slot
+  // free (fewer than eager_jobs open, none being submitted), the caller's thread submits the oldest
   // non-empty batch itself — a lone request reaches the device without waking the flusher
   // (a futex wake-up is tens of microseconds, a third of a small job).
   int first_request(Kind k, Batch* b) {
     std::unique_lock<std::mutex> lk(m);
     (void)k;
     (void)b;
-    if (inline_submit && open_jobs == 0 && submitting == 0 && inflight.size() < max_inflight &&
+    if (inline_submit && open_jobs < eager_jobs && submitting == 0 &&
+        inflight.size() < max_inflight &&
         nsealed == 0 && !stop.load(std::memory_order_relaxed)) {
       int pick = -1;
       int64_t oldest = 0;
@@ -435,14 +449,17 @@ struct nw_service {
     ++open_jobs;
     ++submitting;
     lk.unlock();
+    if (debug) b->t_taken = now_ns();
     b->wait_writers();
     const Clock::time_point s0 = Clock::now();
+    if (debug) b->t_sub0 = now_ns();
     // the service's device choice, also when a producer's thread submits (restored after)
     const int prev = nw_get_device();
     if (prev != device) nw_set_device(device);
     b->rc = submit(*b);
     if (prev != device) nw_set_device(prev);
     const double ds = std::chrono::duration<double>(Clock::now() - s0).count();
+    if (debug) b->t_sub1 = now_ns();
     lk.lock();
     --submitting;
     t_submit += ds;
@@ -517,7 +534,7 @@ struct nw_service {
         if (f == 0) f = tnow;
         ready[k] = stop.load(std::memory_order_relaxed) || force ||
                    Batch::units_of(static_cast<Kind>(k), c_req(c), c_v2(c)) >= max_items ||
-                   tnow >= f + dns || open_jobs == 0;
+                   tnow >= f + dns || open_jobs < eager_jobs;
         if (!ready[k] && f + dns < wake) wake = f + dns;
       }
       for (int d = 1; d <= K_COUNT && pick < 0; ++d) {
@@ -585,11 +602,22 @@ struct nw_service {
         b->job = nullptr;
       }
       const Clock::time_point c0 = Clock::now();
+      const int64_t tdone = debug ? now_ns() : 0;
       const size_t n = b->n;
       const Req* reqs = b->reqs.as<Req>();
       for (size_t i = 0; i < n; ++i)
         reqs[i].fn(reqs[i].arg, rc ? rc : b->status[i], rc ? 0 : b->index[i]);
       const Clock::time_point c1 = Clock::now();
+      if (debug && b->n && d_done.size() < (1u << 22)) {
+        const int64_t f = b->first_ns.load(std::memory_order_relaxed);
+        const int64_t tcb = now_ns();
+        auto us = [f](int64_t t) { return (float)((double)(t - f) * 1e-3); };
+        d_taken.push_back(us(b->t_taken));
+        d_sub0.push_back(us(b->t_sub0));
+        d_sub1.push_back(us(b->t_sub1));
+        d_done.push_back(us(tdone));
+        d_cb.push_back(us(tcb));
+      }
       lk.lock();
       std::unique_ptr<Batch> own = std::move(inflight.front());
       inflight.pop_front();
@@ -597,7 +625,8 @@ struct nw_service {
       t_wait += std::chrono::duration<double>(c0 - w0).count();
       t_callbacks += std::chrono::duration<double>(c1 - c0).count();
       completed += n;
-      if (--open_jobs == 0) cv_flush.notify_one();   // device idle: flush what has queued
+      // a job slot freed below eager_jobs: flush what has queued
+      if (--open_jobs < eager_jobs) cv_flush.notify_one();
       spare[own->kind].push_back(std::move(own));    // cursor stays sealed while spare
       cv_idle.notify_all();
     }
@@ -623,6 +652,8 @@ int nw_service_create(const nw_committee* committee, size_t max_items, uint32_t 
   s->delay = std::chrono::duration_cast<Clock::duration>(std::chrono::microseconds(max_delay_us));
   s->max_inflight = max_inflight ? max_inflight : 1;
   if (const char* e = getenv("NW_SERVICE_INLINE")) s->inline_submit = atoi(e) != 0;
+  s->debug = getenv("NW_SERVICE_DEBUG") != nullptr;
+  if (const char* e = getenv("NW_SERVICE_EAGER")) s->eager_jobs = std::max(1, atoi(e));
   if (committee) {
     const size_t na = committee->nauth, nwk = na ? committee->worker_offsets[na] : 0;
     s->has_committee = true;
@@ -805,6 +836,18 @@ void nw_service_destroy(nw_service* s) {
             (unsigned long long)s->accepted.load(), (unsigned long long)s->jobs,
             (unsigned long long)s->n_inline, (unsigned long long)s->n_full, s->t_submit,
             s->t_backpressure, s->t_wait, s->t_callbacks);
+  if (s->debug && !s->d_done.empty()) {
+    auto med = [](std::vector<float>& v) {
+      std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+      return v[v.size() / 2];
+    };
+    fprintf(stderr,
+            "[narwhal_amd] service job timeline, median us after the job's first request: "
+            "taken %.1f, submit start %.1f, submitted %.1f, done seen %.1f, callbacks %.1f "
+            "(%zu jobs)\n",
+            med(s->d_taken), med(s->d_sub0), med(s->d_sub1), med(s->d_done), med(s->d_cb),
+            s->d_done.size());
+  }
   delete s;
 }
 

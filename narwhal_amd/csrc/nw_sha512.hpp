@@ -134,12 +134,19 @@ __device__ __forceinline__ void load_block_tail(uint64_t w[16], const uint8_t* m
   const uint32_t sh = (uint32_t)(a0 & 3) * 8;
   // message bytes in this block; negative for a padding-only block after the 0x80 block
   const int64_t rem = (int64_t)len - (int64_t)base;
-  // dword q[i] covers block bytes [4 i - sh/8, 4 i - sh/8 + 4)
-  uint32_t prev = 0;
-#pragma unroll 1
+  // dword q[i] covers block bytes [4 i - sh/8, 4 i - sh/8 + 4). Every load is issued before
+  // any is used: from pinned host memory (the small-job kernel) a load is a ~1-2 us round
+  // trip, and 33 of them one after another cost a header's tail block ~40 us.
+  uint32_t qd[33];
+#pragma unroll
   for (int i = 0; i < 33; ++i) {
     const int64_t first = 4 * (int64_t)i - (int64_t)(sh >> 3);   // block byte of q[i]'s byte 0
-    const uint32_t cur = first < rem ? q[i] : 0u;
+    qd[i] = first < rem ? q[i] : 0u;
+  }
+  uint32_t prev = 0;
+#pragma unroll
+  for (int i = 0; i < 33; ++i) {
+    const uint32_t cur = qd[i];
     if (i > 0) {
       // block dword i-1 = bytes [4(i-1), 4i): LE word realigned from q[i-1], q[i]
       uint32_t lo = __builtin_amdgcn_alignbit(cur, prev, sh);
