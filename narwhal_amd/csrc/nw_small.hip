@@ -144,6 +144,10 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
   __shared__ uint32_t s_key[kSlotsMax], s_kf[kSlotsMax], s_sfl[kSlotsMax], s_rfl[kSlotsMax];
   __shared__ uint32_t s_rec[kSlotsMax];
   __shared__ small_msg_info_t s_minfo[kSlotsMax];
+  // a message whose first slot is here: wave 1's header verdict (s_p1, s_x1) and wave 0's
+  // quorum verdict (s_p2, s_x2), assembled into s_minfo after the first barrier
+  __shared__ int32_t s_p1[kSlotsMax], s_p2[kSlotsMax];
+  __shared__ uint64_t s_x1[kSlotsMax], s_x2[kSlotsMax];
   __shared__ uint32_t s_ready;
   __shared__ uint32_t s_lp[64];   // wave 0: the limb-parallel power's rows, gathered
 
@@ -221,70 +225,20 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
       s_rfl[lane] = (okR ? 1u : 0u) | (smallR ? 2u : 0u);
     }
     stamp(J, ST_DECOMP);
-  } else if (wave == 1) {
-    // ---- wave 1: message-level checks of the messages whose first slot is here
     const bool own = lane < ns && s_slot[lane].j == 0;
-    int32_t p1 = 0, p2 = 0;
-    uint64_t x1 = 0, x2 = 0;
-    uint32_t mown = own ? s_slot[lane].m : 0u;
-    if (own) {
-      const uint64_t m = mown;
-      if (J.kind == kSmallVotes) {
-        uint32_t au[8];
-        load8w(au, J.authors + 8 * m);
-        if (committee_stake(com, committee_find(com, au)) == 0) p1 = NW_DAG_UNKNOWN_AUTHORITY;
-      } else {
-        const uint8_t* h = J.hb + J.ho[m];
-        const uint64_t len = J.ho[m + 1] - J.ho[m];
-        uint32_t author[8], id[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          author[t] = ld_le32(h + 4 * t);
-          id[t] = J.ids[8 * m + t];
-        }
-        const uint64_t round = (uint64_t)ld_le32(h + 32) | ((uint64_t)ld_le32(h + 36) << 32);
-        const int a = committee_find(com, author);
-        uint32_t idor = 0;
-#pragma unroll
-        for (int t = 0; t < 8; ++t) idor |= id[t];
-        // Certificate::verify: genesis(committee).contains(self) (messages.rs:190-193)
-        if (certs && idor == 0 && round == 0 && a >= 0) {
-          p1 = -1;
-        } else {
-          // Header::verify (messages.rs:48-67), in order: id, stake, worker ids
-          uint32_t dg[8];
-          sha512_digest32_lane(h, len, dg);
-          bool id_ok = true;
-#pragma unroll
-          for (int t = 0; t < 8; ++t) id_ok &= dg[t] == id[t];
-          if (!id_ok) {
-            p1 = NW_DAG_INVALID_HEADER_ID;
-          } else if (committee_stake(com, a) == 0) {
-            p1 = NW_DAG_UNKNOWN_AUTHORITY;
-            x1 = ~0ull;
-          } else {
-            const uint32_t np = J.pc[m];
-            const uint64_t wb = J.com.worker_offsets[a], we = J.com.worker_offsets[a + 1];
-            for (uint32_t e = 0; e < np && p1 == 0; ++e) {
-              const uint32_t wid = ld_le32(h + 40 + 36 * (uint64_t)e + 32);
-              bool found = false;
-              for (uint64_t w = wb; w < we; ++w) found |= J.com.worker_ids[w] == wid;
-              if (!found) { p1 = NW_DAG_MALFORMED_HEADER; x1 = e; }
-            }
-          }
-        }
-      }
-    }
+    int32_t p2 = 0;
+    uint64_t x2 = 0;
     if (certs) {
-      // Certificate::verify's quorum (messages.rs:196-211), per owned certificate whose
-      // header passed, lanes over its votes: reuse, then stake, first failure in vote
-      // order; else the u32 weight against 2 total / 3 + 1 (config/src/lib.rs:167-173).
+      // Certificate::verify's quorum (messages.rs:196-211), per owned certificate (its
+      // verdict counts only when the header passed: the combine reads p1 first), lanes
+      // over its votes: reuse, then stake, first failure in vote order; else the u32
+      // weight against 2 total / 3 + 1 (config/src/lib.rs:167-173).
       uint32_t total = 0;
       for (uint32_t a = lane; a < na; a += 64) total += s_stakes[a];
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) total += (uint32_t)__shfl_xor((int)total, off);
       const uint32_t quorum = 2u * total / 3u + 1u;
-      uint64_t todo = __ballot(own && p1 == 0);
+      uint64_t todo = __ballot(own);
       while (todo) {
         const int o = __ffsll((unsigned long long)todo) - 1;
         todo &= todo - 1;
@@ -335,12 +289,66 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
         }
       }
     }
+    s_p2[lane] = p2;
+    s_x2[lane] = x2;
+  } else if (wave == 1) {
+    // ---- wave 1: Header::verify's checks of the messages whose first slot is here (the
+    // header digest is the longest serial chain of a certificate job: ~9 SHA-512 blocks at
+    // N = 50; the quorum runs on wave 0 beside it)
+    const bool own = lane < ns && s_slot[lane].j == 0;
+    int32_t p1 = 0;
+    uint64_t x1 = 0;
+    uint32_t mown = own ? s_slot[lane].m : 0u;
     if (own) {
-      const small_msg_info_t info{p1, p2, x1, x2};
-      s_minfo[lane] = info;
-      const small_slot_t sl = s_slot[lane];
-      if ((first + lane) / S != (first + lane + sl.cnt - 1) / S) J.minfo[sl.m] = info;   // spans
+      const uint64_t m = mown;
+      if (J.kind == kSmallVotes) {
+        uint32_t au[8];
+        load8w(au, J.authors + 8 * m);
+        if (committee_stake(com, committee_find(com, au)) == 0) p1 = NW_DAG_UNKNOWN_AUTHORITY;
+      } else {
+        const uint8_t* h = J.hb + J.ho[m];
+        const uint64_t len = J.ho[m + 1] - J.ho[m];
+        uint32_t author[8], id[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          author[t] = ld_le32(h + 4 * t);
+          id[t] = J.ids[8 * m + t];
+        }
+        const uint64_t round = (uint64_t)ld_le32(h + 32) | ((uint64_t)ld_le32(h + 36) << 32);
+        const int a = committee_find(com, author);
+        uint32_t idor = 0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) idor |= id[t];
+        // Certificate::verify: genesis(committee).contains(self) (messages.rs:190-193)
+        if (certs && idor == 0 && round == 0 && a >= 0) {
+          p1 = -1;
+        } else {
+          // Header::verify (messages.rs:48-67), in order: id, stake, worker ids
+          uint32_t dg[8];
+          sha512_digest32_lane(h, len, dg);
+          bool id_ok = true;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) id_ok &= dg[t] == id[t];
+          if (!id_ok) {
+            p1 = NW_DAG_INVALID_HEADER_ID;
+          } else if (committee_stake(com, a) == 0) {
+            p1 = NW_DAG_UNKNOWN_AUTHORITY;
+            x1 = ~0ull;
+          } else {
+            const uint32_t np = J.pc[m];
+            const uint64_t wb = J.com.worker_offsets[a], we = J.com.worker_offsets[a + 1];
+            for (uint32_t e = 0; e < np && p1 == 0; ++e) {
+              const uint32_t wid = ld_le32(h + 40 + 36 * (uint64_t)e + 32);
+              bool found = false;
+              for (uint64_t w = wb; w < we; ++w) found |= J.com.worker_ids[w] == wid;
+              if (!found) { p1 = NW_DAG_MALFORMED_HEADER; x1 = e; }
+            }
+          }
+        }
+      }
     }
+    s_p1[lane] = p1;
+    s_x1[lane] = x1;
     stamp(J, ST_MSG);
     release_vm();
   } else {
@@ -457,6 +465,14 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
   }
   __syncthreads();
   if (tid == 0) stamp(J, ST_SYNC);
+  // the message info (read by the combine below, and by other workgroups through J.minfo
+  // when the message's slots span several)
+  if (wave == 1 && lane < ns && s_slot[lane].j == 0) {
+    const small_msg_info_t info{s_p1[lane], s_p2[lane], s_x1[lane], s_x2[lane]};
+    s_minfo[lane] = info;
+    const small_slot_t sl = s_slot[lane];
+    if ((first + lane) / S != (first + lane + sl.cnt - 1) / S) J.minfo[sl.m] = info;   // spans
+  }
 
   // ---- per slot: R == R', the strict status or the certificate vote's batch record
   if (wave == 2 && lane < ns) {
