@@ -20,8 +20,9 @@
 //            one lock and fall behind their arrivals, in runs that stayed slow once behind.
 //            The mutex is taken only by a batch's first request (to wake the flusher, or to
 //            submit the batch itself when a job slot is free), when the arrays are full (the
-//            batch is sealed for submission and the next one gets twice the room), and when
-//            a batch reaches max_items units (sealed too: a job holds about max_items).
+//            batch is sealed for submission and a spare of the same room opened: no
+//            allocation on the producers' path unless one request alone needs more room), and
+//            when a batch reaches max_items units (sealed too: a job holds about max_items).
 //   flusher  submits a batch as ONE device job (the committee-aware pipeline, or the
 //            one-launch small-job kernel) when it is sealed, max_delay has passed since its
 //            first request, or fewer than eager_jobs (2) jobs are open (a device with a free
@@ -87,8 +88,8 @@ inline uint64_t c_pack(uint64_t r, uint64_t v1, uint64_t v2) {
   return r | (v1 << kReqBits) | (v2 << (kReqBits + kVar1Bits));
 }
 
-// A fixed-capacity array whose pages are touched when it is (re)allocated: a page fault on a
-// producer's copy costs more than the copy.
+// A fixed-capacity array (not zeroed: allocating one must not stall the producers waiting
+// for a fresh batch; its pages fault in on the first copies instead).
 struct Arr {
   uint8_t* p = nullptr;
   size_t cap = 0;
@@ -101,7 +102,6 @@ struct Arr {
     free(p);
     p = static_cast<uint8_t*>(malloc(c));
     cap = p ? c : 0;
-    if (p) memset(p, 0, c);
     return p != nullptr;
   }
   template <class T>
@@ -383,19 +383,16 @@ struct nw_service {
   }
 
   // b (kind k) has no room for a request of v1 / v2: if it is still the open batch, seal it
-  // as full (the flusher submits it next), grow the kind's room to fit, install a new batch.
+  // as full (the flusher submits it next) and install the next batch — of the same room
+  // (a spare, no allocation) unless the request alone would not fit an empty batch, in
+  // which case the kind's room grows to hold it.
   int make_room(Kind k, Batch* b, uint64_t v1, uint64_t v2) {
     std::unique_lock<std::mutex> lk(m);
     if (open[k].get() != b) return 0;   // someone else did (retry on the new batch)
     Caps& c = caps[k];
-    const uint64_t cur_c = b->cursor.load(std::memory_order_acquire);
-    const uint64_t r = c_req(cur_c);
-    // double what overflowed (twice this request at least), up to the cursor's fields
-    if (r + 1 > c.req) c.req = std::min<uint64_t>(kMaxReq, std::max<uint64_t>(2 * c.req, 64));
-    if (c_v1(cur_c) + v1 > c.v1)
-      c.v1 = std::min<uint64_t>(kMaxVar1, std::max<uint64_t>(2 * c.v1, 2 * v1 + 4096));
-    if (c_v2(cur_c) + v2 > c.v2)
-      c.v2 = std::min<uint64_t>(kMaxVar2, std::max<uint64_t>(2 * c.v2, 2 * v2 + 64));
+    if (1 > c.req) c.req = 64;
+    if (v1 > c.v1) c.v1 = std::min<uint64_t>(kMaxVar1, std::max<uint64_t>(2 * c.v1, 2 * v1 + 4096));
+    if (v2 > c.v2) c.v2 = std::min<uint64_t>(kMaxVar2, std::max<uint64_t>(2 * c.v2, 2 * v2 + 64));
     std::unique_ptr<Batch> old = take_open(k);
     if (!old) return set_err(NW_E_OUT_OF_MEMORY, "service batch");
     if (old->n == 0) {   // empty and too small for this request: recycle it
@@ -668,8 +665,19 @@ int nw_service_create(const nw_committee* committee, size_t max_items, uint32_t 
     s->com.worker_offsets = s->com_wo.data();
     s->com.worker_ids = nz(s->com_wi);
   }
+  // Initial room per kind (~11 MB for certificates, ~7 MB for verify_batch, ~4 MB for
+  // headers, < 1 MB for the others): a 10^6-per-second N = 50 certificate load makes
+  // batches of ~250 certificates (~9k votes, ~280 KB of header bytes), so batches grow only
+  // under a backlog
+  const uint64_t mi = s->max_items;
+  const Caps init[K_COUNT] = {
+      {std::min<uint64_t>(mi + 1, 4096), 1 << 22, std::min<uint64_t>(mi, 1 << 16)},   // cert
+      {std::min<uint64_t>(mi + 1, 4096), 1 << 22, 0},                                 // header
+      {std::min<uint64_t>(mi + 1, 4096), 0, 0},                                       // vote
+      {std::min<uint64_t>(mi + 1, 4096), 0, 0},                                       // strict
+      {std::min<uint64_t>(mi + 1, 1024), 0, std::min<uint64_t>(mi, 1 << 16)}};        // batch
   for (int k = 0; k < K_COUNT; ++k) {
-    s->caps[k] = Caps{1024, 1 << 16, 1 << 14};
+    s->caps[k] = init[k];
     std::unique_ptr<Batch> b = s->take_spare(static_cast<Kind>(k));
     if (!b) {
       delete s;
