@@ -134,6 +134,92 @@ __device__ __forceinline__ void stamp(const small_job_t& J, int which) {
 
 }  // namespace
 
+// Header digests of wave 1 (Header::verify's id check, primary/src/messages.rs:48-55).
+// SHA-512 is a chain per message, and one lane of a lone wave issues each instruction at the
+// wave's full cost (~6.5 us per 128-B block), so a certificate's header (9 blocks at N = 50,
+// 18 at N = 100) is a job's longest chain. When the wave owns ONE header of at most
+// kSchedBlocks blocks, its message schedules are computed by one lane per block side by side
+// into LDS, and the owner runs only the 80 rounds per block, reading W[t] from LDS (the
+// schedule is ~35 % of a block's instructions). Otherwise each owner lane hashes its own
+// header. dg: the digest's 8 LE words in the owner lane(s).
+constexpr uint32_t kSchedBlocks = 32;
+__device__ __forceinline__ void header_digest(bool need, const uint8_t* h, uint64_t len,
+                                              uint32_t dg[8], uint32_t lane,
+                                              uint64_t (*s_w)[80]) {
+  const uint64_t mask = __ballot(need);
+  if (mask == 0) return;
+  if (__popcll(mask) == 1) {
+    const int o = __ffsll((unsigned long long)mask) - 1;
+    const uint64_t hp = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uintptr_t)h >> 32), o) << 32) |
+                        (uint32_t)__shfl((int)(uint32_t)(uintptr_t)h, o);
+    const uint64_t L = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(len >> 32), o) << 32) |
+                       (uint32_t)__shfl((int)(uint32_t)len, o);
+    const uint64_t nb = (L + 17 + 127) / 128;
+    if (nb <= kSchedBlocks) {
+      const uint8_t* msg = reinterpret_cast<const uint8_t*>(hp);
+      if (lane < nb) {
+        uint64_t w[16];
+        const uint64_t base = 128 * (uint64_t)lane;
+        if (base + 128 <= L) {
+          uint32_t d[33];
+          load_block_raw(d, msg + base);
+          block_from_raw(w, d, (uint32_t)((uintptr_t)msg & 3) * 8);
+        } else {
+          load_block_tail(w, msg, base, L, lane + 1 == nb);
+        }
+        uint64_t* W = s_w[lane];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) W[t] = w[t];
+#pragma unroll 1
+        for (int r = 16; r < 80; r += 16) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+            const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), shr64(w15, 7));
+            const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), shr64(w2, 6));
+            w[j] = w[j] + s0 + w[(j + 9) & 15] + s1;
+            W[r + j] = w[j];
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      if ((int)lane == o) {
+        uint64_t st[8];
+        sha512_init(st);
+#pragma unroll 1
+        for (uint64_t b = 0; b < nb; ++b) {
+          const uint64_t* W = s_w[b];
+          uint64_t a = st[0], bb = st[1], c = st[2], d = st[3], e = st[4], f = st[5],
+                   g = st[6], hh = st[7];
+#pragma unroll 1
+          for (int r = 0; r < 80; r += 16) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+              const uint64_t S1 = xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41));
+              const uint64_t t1 = hh + S1 + ch64(e, f, g) + SHA512_K[r + j] + W[r + j];
+              const uint64_t S0 = xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39));
+              const uint64_t t2 = S0 + maj64(a, bb, c);
+              hh = g; g = f; f = e; e = d + t1; d = c; c = bb; bb = a; a = t1 + t2;
+            }
+          }
+          st[0] += a; st[1] += bb; st[2] += c; st[3] += d; st[4] += e; st[5] += f;
+          st[6] += g; st[7] += hh;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          dg[2 * j] = __builtin_bswap32((uint32_t)(st[j] >> 32));
+          dg[2 * j + 1] = __builtin_bswap32((uint32_t)st[j]);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      return;
+    }
+  }
+  if (need) sha512_digest32_lane(h, len, dg);
+}
+
 __global__ __launch_bounds__(256) void k_small(small_job_t J) {
   __shared__ uint32_t s_pks[8 * kLdsAuth], s_stakes[kLdsAuth], s_first[kLdsAuth];
   __shared__ small_slot_t s_slot[kSlotsMax];
@@ -150,6 +236,7 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
   __shared__ uint64_t s_x1[kSlotsMax], s_x2[kSlotsMax];
   __shared__ uint32_t s_ready;
   __shared__ uint32_t s_lp[64];   // wave 0: the limb-parallel power's rows, gathered
+  __shared__ uint64_t s_w[kSchedBlocks][80];   // wave 1: header message schedules
 
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
@@ -299,33 +386,43 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
     int32_t p1 = 0;
     uint64_t x1 = 0;
     uint32_t mown = own ? s_slot[lane].m : 0u;
-    if (own) {
-      const uint64_t m = mown;
-      if (J.kind == kSmallVotes) {
+    if (J.kind == kSmallVotes) {
+      if (own) {
         uint32_t au[8];
-        load8w(au, J.authors + 8 * m);
+        load8w(au, J.authors + 8 * mown);
         if (committee_stake(com, committee_find(com, au)) == 0) p1 = NW_DAG_UNKNOWN_AUTHORITY;
-      } else {
-        const uint8_t* h = J.hb + J.ho[m];
-        const uint64_t len = J.ho[m + 1] - J.ho[m];
-        uint32_t author[8], id[8];
+      }
+    } else {
+      const uint64_t m = mown;
+      const uint8_t* h = nullptr;
+      uint64_t len = 0;
+      uint32_t id[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      int a = -1;
+      bool genesis = false;
+      if (own) {
+        h = J.hb + J.ho[m];
+        len = J.ho[m + 1] - J.ho[m];
+        uint32_t author[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
           author[t] = ld_le32(h + 4 * t);
           id[t] = J.ids[8 * m + t];
         }
         const uint64_t round = (uint64_t)ld_le32(h + 32) | ((uint64_t)ld_le32(h + 36) << 32);
-        const int a = committee_find(com, author);
+        a = committee_find(com, author);
         uint32_t idor = 0;
 #pragma unroll
         for (int t = 0; t < 8; ++t) idor |= id[t];
         // Certificate::verify: genesis(committee).contains(self) (messages.rs:190-193)
-        if (certs && idor == 0 && round == 0 && a >= 0) {
+        genesis = certs && idor == 0 && round == 0 && a >= 0;
+      }
+      uint32_t dg[8];
+      header_digest(own && !genesis, h, len, dg, lane, s_w);
+      if (own) {
+        if (genesis) {
           p1 = -1;
         } else {
           // Header::verify (messages.rs:48-67), in order: id, stake, worker ids
-          uint32_t dg[8];
-          sha512_digest32_lane(h, len, dg);
           bool id_ok = true;
 #pragma unroll
           for (int t = 0; t < 8; ++t) id_ok &= dg[t] == id[t];
