@@ -20,7 +20,7 @@ from narwhal_amd import workloads as W
 from narwhal_amd.crypto import PublicKey, Signature
 from oracle import oracle as O
 
-from cert_cases import mutated_stream, oracle_digest_many, votes_case
+from cert_cases import mutated_stream, oracle_digest_many, oracle_sign_many, votes_case
 from test_gpu_messages import _Com, mixed_order_committee_certs
 
 pytestmark = pytest.mark.gpu
@@ -208,3 +208,30 @@ def test_small_mixed_validity_random_z(monkeypatch, N, n):
     stp, ixp = M.verify_certificates_many(com, m, None)
     assert _lib.path_stats()[0] == s0
     assert stp.tolist() == exp_st.tolist() and ixp.tolist() == exp_ix.tolist()
+
+
+@pytest.mark.parametrize("N,payload,S", [(100, 32, 4), (100, 64, 4), (50, 80, 4), (10, 0, 64)])
+def test_small_header_digest_sizes(monkeypatch, N, payload, S):
+    """The header digest of the small-job kernel (nw_small.hip header_digest): one owned
+    header per wave hashes with its block schedules spread over lanes up to 32 blocks (N =
+    100 with 32 payload entries: 27 blocks; N = 50 with 80: exactly 32), a larger header
+    (N = 100, 64 entries: 36 blocks) and several owned headers per wave (N = 10, S = 64) on
+    one lane each. Honest
+    certificates (the construction: Ok) and the same with every header id flipped in one
+    byte (InvalidHeaderId) - statuses and indices == the oracle's."""
+    _small(monkeypatch, S)
+    keys = O.keys(N)
+    s = W.certificate_stream(6, keys, oracle_sign_many, oracle_digest_many, payload=payload,
+                             seed=N + payload)
+    com = _Com(s["committee"])
+    st, ix = _twice(lambda: M.verify_certificates_many(com, s, None))
+    assert st.tolist() == [0] * 6
+    bad = dict(s)
+    bad["ids"] = s["ids"].copy()
+    bad["ids"][:, 5] ^= 0x10
+    z16 = np.random.Generator(np.random.PCG64(N)).integers(0, 256, size=(len(s["vote_pks"]), 16),
+                                                           dtype=np.uint8)
+    st, ix = _twice(lambda: M.verify_certificates_many(com, bad, z16))
+    ost, oix = O.certificates_verify_many(s["committee"], bad, z16)
+    assert st.tolist() == ost.tolist() and ix.tolist() == oix.tolist()
+    assert set(st.tolist()) == {16}    # NW_DAG_INVALID_HEADER_ID
