@@ -205,6 +205,28 @@ void ensure_fork(nw_job* j) {
   }
 }
 
+}  // namespace
+
+// Puts `count` jobs with their streams, fork streams and `hbytes` / `dbytes` of staging into
+// device dev's pool (nw_service_create: a service's first burst then finds its jobs made,
+// instead of creating streams and pinning memory on the flusher's path).
+int nw::rt::jobs_prewarm(int dev, int count, size_t hbytes, size_t dbytes) {
+  std::vector<nw_job*> got;
+  int rc = 0;
+  for (int i = 0; i < count && !rc; ++i) {
+    nw_job* j = nullptr;
+    rc = job_acquire(dev, &j);
+    if (rc) break;
+    got.push_back(j);
+    rc = job_reserve(j, hbytes, dbytes);
+    if (!rc) ensure_fork(j);
+  }
+  for (nw_job* j : got) job_recycle(j);
+  return rc;
+}
+
+namespace {
+
 int fill_key(nw::z_key_t& k) {
   int rc = nw::rt::os_random(k.key, 32);
   k.nonce = 0;

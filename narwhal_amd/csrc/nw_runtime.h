@@ -30,6 +30,9 @@ std::vector<int> fanout_devices();
 int set_err(int code, const char* what, hipError_t e = hipSuccess);
 // Fill buf from the OS CSPRNG (getrandom).
 int os_random(void* buf, size_t n);
+// count pooled jobs on library device dev, made now with hbytes / dbytes of staging
+// (nw_jobs.cpp; the aggregation service's start-up).
+int jobs_prewarm(int dev, int count, size_t hbytes, size_t dbytes);
 
 // ---- primary messages (nw_api.cpp), shared by the blocking, job and device entry points ----
 // Host-side argument checks of a host-memory committee / certificate stream (0 or

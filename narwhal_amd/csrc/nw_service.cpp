@@ -676,6 +676,14 @@ int nw_service_create(const nw_committee* committee, size_t max_items, uint32_t 
       {std::min<uint64_t>(mi + 1, 4096), 0, 0},                                       // vote
       {std::min<uint64_t>(mi + 1, 4096), 0, 0},                                       // strict
       {std::min<uint64_t>(mi + 1, 1024), 0, std::min<uint64_t>(mi, 1 << 16)}};        // batch
+  // the jobs its first burst needs (max_inflight queued + one being submitted + one
+  // submitting from a caller's thread), made now rather than on the flusher's path
+  if (s->device >= 0) {
+    int dev = 0;
+    if (nw::rt::select_device(&dev) == 0)
+      (void)nw::rt::jobs_prewarm(dev, (int)std::min<size_t>(s->max_inflight + 2, 16), 4 << 20,
+                                 4 << 20);
+  }
   for (int k = 0; k < K_COUNT; ++k) {
     s->caps[k] = init[k];
     std::unique_ptr<Batch> b = s->take_spare(static_cast<Kind>(k));

@@ -165,7 +165,10 @@ int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_s
       for (uint64_t i = p; i < total; i += producers) {
         const Clock::time_point due = recs[i].due;
         Clock::time_point now = Clock::now();
-        if (due - now > std::chrono::microseconds(100)) std::this_thread::sleep_until(due);
+        // sleep to just before the due time, then spin: a sleep wakes up tens of
+        // microseconds late, which would count as the service's latency
+        const auto early = std::chrono::microseconds(200);
+        if (due - now > early) std::this_thread::sleep_until(due - early);
         while ((now = Clock::now()) < due) {
         }
         const double lag = std::chrono::duration<double>(now - due).count();

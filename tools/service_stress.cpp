@@ -65,6 +65,11 @@ namespace rt {
 int ensure_init() { return 0; }
 int set_err(int code, const char*, hipError_t) { return code; }
 int check_committee(const nw_committee*) { return 0; }
+int select_device(int* dev) {
+  *dev = 0;
+  return 0;
+}
+int jobs_prewarm(int, int, size_t, size_t) { return 0; }
 }  // namespace rt
 }  // namespace nw
 
