@@ -1292,7 +1292,7 @@ __device__ __forceinline__ uint32_t pip_lp_load(const lp_ctx& L, const ge* S, ui
   return b == ~0u ? lp_identity(L) : L.k < 10 ? x : 0u;
 }
 
-__global__ __launch_bounds__(64) void k_pip_windows_lp(const uint32_t* __restrict__ pip_list,
+__global__ __launch_bounds__(128) void k_pip_windows_lp(const uint32_t* __restrict__ pip_list,
                                                        const uint64_t* __restrict__ offsets,
                                                        uint64_t b0, uint64_t i0, uint32_t extra,
                                                        uint32_t pmin,
@@ -1301,12 +1301,13 @@ __global__ __launch_bounds__(64) void k_pip_windows_lp(const uint32_t* __restric
   const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
   if (n < pmin) return;
   const pip_region reg = pip_at(tabs, bs - i0, n + extra);
-  const int w = blockIdx.x, q = blockIdx.y, lane = (int)threadIdx.x;
+  const int w = blockIdx.x, q = blockIdx.y, lane = (int)(threadIdx.x & 63);
+  const int half2 = (int)(threadIdx.x >> 6);   // which 16 of the part's 32 entries
   const lp_ctx L = lp_init((uint32_t)lane);
   const fe& d2 = g_bc.k.d2;
   const uint32_t d2l = L.k < 10 ? d2.v[L.k] : 0u;
   if (w == kPipWin) {
-    if (q != 0) return;
+    if (q != 0 || half2 != 0) return;
     uint32_t bb[8];
 #pragma unroll
     for (int m = 0; m < 8; ++m) bb[m] = reg.bb[m];
@@ -1320,10 +1321,15 @@ __global__ __launch_bounds__(64) void k_pip_windows_lp(const uint32_t* __restric
     if (L.k < 10) reinterpret_cast<uint32_t*>(reg.Bc)[10 * (L.row ^ 1u) + L.k] = c;
     return;
   }
-  // this part's bucket list, lane i < 32 holding entry i (additions in whole groups of 8,
-  // identities past the end)
+  // this part's bucket list: wave h of the block sums entries 32 (q & 1) + 16 h .. + 15,
+  // lane i < 16 holding entry i (additions in whole groups of 8, identities past the end);
+  // wave 1's sum is added by wave 0 through LDS. Two chains of <= 16 additions side by side
+  // instead of one of <= 32 (config 1's one call: the window pass 29 -> ~15 us).
+  __shared__ uint32_t s_other[64];
   const int j = q >> 1;
-  const uint32_t mine = lane < 32 ? pip_lp_bucket(w, j, 32u * (uint32_t)(q & 1) + lane) : ~0u;
+  const uint32_t mine =
+      lane < 16 ? pip_lp_bucket(w, j, 32u * (uint32_t)(q & 1) + 16u * (uint32_t)half2 + lane)
+                : ~0u;
   const uint32_t cnt = (uint32_t)__builtin_popcountll(__ballot(mine != ~0u));
   uint32_t v = lp_identity(L);
   if (cnt) {
@@ -1338,11 +1344,15 @@ __global__ __launch_bounds__(64) void k_pip_windows_lp(const uint32_t* __restric
         const uint32_t x = buf[u];
         const uint32_t nx = i + 8 + u;
         buf[u] = pip_lp_load(
-            L, reg.S, nx < 32 ? (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)nx) : ~0u);
+            L, reg.S, nx < 16 ? (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)nx) : ~0u);
         v = lp_add(L, v, lp_to_cached(L, x, d2l));
       }
     }
   }
+  if (half2 == 1) s_other[lane] = lp_to_cached(L, v, d2l);
+  __syncthreads();
+  if (half2 == 1) return;
+  v = lp_add(L, v, s_other[lane]);
   reinterpret_cast<uint32_t*>(reg.pts)[(w * kPipWinLpParts + q) * 64 + lane] =
       lp_to_cached(L, v, d2l);
 }
@@ -1706,7 +1716,7 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
                      (uint32_t)npip, bpb, xcd, extra, pmin, w.tabs);
   if (npip <= pip_win_lp_max()) {
     hipLaunchKernelGGL(k_pip_windows_lp, dim3(kPipWin + 1, kPipWinLpParts, (unsigned)npip),
-                       dim3(64), 0, stream, w.pip_list, offsets, b, i0, extra, pmin, w.tabs);
+                       dim3(128), 0, stream, w.pip_list, offsets, b, i0, extra, pmin, w.tabs);
     hipLaunchKernelGGL(k_pip_wsum, dim3(kPipWin, (unsigned)npip), dim3(64), 0, stream,
                        w.pip_list, offsets, b, i0, extra, pmin, w.tabs);
   } else
