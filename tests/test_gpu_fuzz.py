@@ -1,0 +1,160 @@
+"""Seeded differential fuzz of Certificate::verify / Header::verify: honest certificates with
+random byte-level damage — single-byte xors anywhere in the header bytes, id, header
+signature, vote keys and vote signatures; R or A replaced by encodings the construction
+never makes (small-order points, y >= p, the sign bit on x = 0, off-curve y); s pushed to
+s + l or given high bits; votes duplicated, dropped or reordered — so that the checks meet
+inputs no hand-written class reaches. Every status and index from the GPU (the one-launch
+small-job kernel, the bulk pipeline, and the native aggregation service) must equal the
+oracle's, with injected batch coefficients where the verdict depends on them.
+
+Parity here is against the oracle (oracle/nw_oracle.c, pinned by tests/test_oracle.py);
+for the encodings no reference fixture holds (y >= p with a large-order point, x = 0 with
+the sign bit), the oracle's restatement of curve25519-dalek's decompression is the anchor
+(DESIGN.md section 2)."""
+import numpy as np
+import pytest
+
+from narwhal_amd import _lib
+from narwhal_amd import messages as M
+from narwhal_amd import workloads as W
+from oracle import oracle as O
+
+from cert_cases import oracle_digest_many, oracle_sign_many
+from test_gpu_messages import _Com
+
+pytestmark = pytest.mark.gpu
+
+P_FIELD = 2**255 - 19
+L_ORDER = 2**252 + 27742317777372353535851937790883648493
+T8 = bytes.fromhex("26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05")
+
+
+def _odd_encodings():
+    """32-byte point encodings outside what honest signing produces."""
+    out = [bytes.fromhex("01" + "00" * 31),                    # identity
+           (P_FIELD + 1).to_bytes(32, "little"),                # identity, y = p + 1
+           bytes(31) + b"\x80",                                 # y = 0, sign bit (x^2 = -1/..)
+           (1).to_bytes(32, "little")[:31] + b"\x80",           # identity with the sign bit
+           (2).to_bytes(32, "little"),                          # off the curve
+           (P_FIELD - 1).to_bytes(32, "little"),                # y = -1: order 2
+           T8]
+    for k in range(2, 8):                                       # the 8-torsion points
+        out.append(O.scalarmult(k.to_bytes(32, "little"), T8))
+    return [e for e in out if e is not None]
+
+
+def _damage(s: dict, rng: np.random.Generator, frac: float):
+    """Copy of the packed stream with about `frac` of the certificates damaged."""
+    recs = []
+    hb = s["header_bytes"].tobytes()
+    ho, vo = s["header_offsets"], s["vote_offsets"]
+    odd = _odd_encodings()
+    for i in range(len(ho) - 1):
+        r = {"hb": bytearray(hb[int(ho[i]):int(ho[i + 1])]), "pc": int(s["payload_counts"][i]),
+             "id": bytearray(s["ids"][i].tobytes()), "sig": bytearray(s["header_sigs"][i].tobytes()),
+             "vpk": [bytearray(x.tobytes()) for x in s["vote_pks"][int(vo[i]):int(vo[i + 1])]],
+             "vsig": [bytearray(x.tobytes()) for x in s["vote_sigs"][int(vo[i]):int(vo[i + 1])]]}
+        if rng.random() < frac:
+            kind = int(rng.integers(0, 11))
+            q = len(r["vpk"])
+            v = int(rng.integers(0, q)) if q else 0
+            if kind == 0:   # a byte of the header bytes (author, round, payload, parents)
+                r["hb"][int(rng.integers(0, len(r["hb"])))] ^= 1 << int(rng.integers(0, 8))
+            elif kind == 1:
+                r["id"][int(rng.integers(0, 32))] ^= 1 << int(rng.integers(0, 8))
+            elif kind == 2:
+                r["sig"][int(rng.integers(0, 64))] ^= 1 << int(rng.integers(0, 8))
+            elif kind == 3 and q:
+                r["vsig"][v][int(rng.integers(0, 64))] ^= 1 << int(rng.integers(0, 8))
+            elif kind == 4 and q:
+                r["vpk"][v][int(rng.integers(0, 32))] ^= 1 << int(rng.integers(0, 8))
+            elif kind == 5 and q:   # R of a vote: an odd encoding
+                r["vsig"][v][:32] = odd[int(rng.integers(0, len(odd)))]
+            elif kind == 6:         # R of the header signature: an odd encoding
+                r["sig"][:32] = odd[int(rng.integers(0, len(odd)))]
+            elif kind == 7 and q:   # s + l, or high bits
+                sv = int.from_bytes(bytes(r["vsig"][v][32:]), "little")
+                sv = sv + L_ORDER if rng.random() < 0.5 else sv | (1 << 254)
+                r["vsig"][v][32:] = (sv % 2**256).to_bytes(32, "little")
+            elif kind == 8 and q > 1:   # a vote duplicated over another
+                r["vpk"][v], r["vsig"][v] = bytearray(r["vpk"][v - 1]), bytearray(r["vsig"][v - 1])
+            elif kind == 9 and q > 1:   # a vote dropped
+                del r["vpk"][v], r["vsig"][v]
+            elif kind == 10 and q > 1:  # two votes swapped (order matters for the index)
+                w = int(rng.integers(0, q))
+                r["vpk"][v], r["vpk"][w] = r["vpk"][w], r["vpk"][v]
+                r["vsig"][v], r["vsig"][w] = r["vsig"][w], r["vsig"][v]
+        recs.append(r)
+    n = len(recs)
+    out = {"header_bytes": np.frombuffer(b"".join(bytes(r["hb"]) for r in recs), np.uint8).copy(),
+           "header_offsets": np.concatenate([[0], np.cumsum([len(r["hb"]) for r in recs])]).astype(np.uint64),
+           "payload_counts": np.array([r["pc"] for r in recs], np.uint32),
+           "ids": np.frombuffer(b"".join(bytes(r["id"]) for r in recs), np.uint8).reshape(n, 32).copy(),
+           "header_sigs": np.frombuffer(b"".join(bytes(r["sig"]) for r in recs), np.uint8).reshape(n, 64).copy(),
+           "vote_offsets": np.concatenate([[0], np.cumsum([len(r["vpk"]) for r in recs])]).astype(np.uint64)}
+    out["vote_pks"] = np.frombuffer(b"".join(bytes(x) for r in recs for x in r["vpk"]) or bytes(32),
+                                    np.uint8).reshape(-1, 32).copy()[:int(out["vote_offsets"][-1])]
+    out["vote_sigs"] = np.frombuffer(b"".join(bytes(x) for r in recs for x in r["vsig"]) or bytes(64),
+                                     np.uint8).reshape(-1, 64).copy()[:int(out["vote_offsets"][-1])]
+    return out
+
+
+@pytest.mark.parametrize("N,n,seed", [(4, 600, 1), (10, 300, 2), (50, 60, 3), (4, 2000, 4),
+                                      (7, 700, 5), (10, 1000, 6), (20, 200, 7), (50, 120, 8)])
+def test_fuzz_certificates_small_and_bulk_vs_oracle(monkeypatch, N, n, seed):
+    keys = O.keys(N)
+    s = W.certificate_stream(n, keys, oracle_sign_many, oracle_digest_many, payload=seed % 3,
+                             seed=700 + seed)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    d = _damage(s, rng, 0.5)
+    com = _Com(s["committee"])
+    z16 = rng.integers(0, 256, size=(len(d["vote_pks"]), 16), dtype=np.uint8)
+    ost, oix = O.certificates_verify_many(s["committee"], d, z16)
+    assert len(set(ost.tolist())) >= 5, sorted(set(ost.tolist()))   # the damage reaches many checks
+    for small in ("1", "0"):
+        monkeypatch.setenv("NW_SMALL", small)
+        M.verify_certificates_many(com, d, z16)          # a committee's first job builds tables
+        s0, p0 = _lib.path_stats()
+        st, ix = M.verify_certificates_many(com, d, z16)
+        s1, p1 = _lib.path_stats()
+        assert (s1 > s0) if small == "1" else (s1 == s0 and p1 > p0)
+        bad = [(i, int(a), int(b), int(x), int(y)) for i, (a, b, x, y)
+               in enumerate(zip(st, ost, ix, oix)) if a != b or x != y]
+        assert not bad, (small, bad[:10])
+    # headers only, the same damage
+    monkeypatch.setenv("NW_SMALL", "1")
+    hst, hix = M.verify_headers_many(com, d)
+    ohst, ohix = O.certificates_verify_many(s["committee"], d, headers_only=True)
+    assert hst.tolist() == ohst.tolist() and hix.tolist() == ohix.tolist()
+
+
+def test_fuzz_certificates_through_service_vs_oracle():
+    """The same damaged certificates one by one through the native service (random CSPRNG
+    coefficients there): statuses and indices == the oracle's wherever the verdict does not
+    depend on the coefficients, i.e. for every certificate the oracle gives the same answer
+    under two different coefficient sets."""
+    import asyncio
+    from narwhal_amd import service as S
+    from test_service import _rows
+    keys = O.keys(10)
+    s = W.certificate_stream(300, keys, oracle_sign_many, oracle_digest_many, seed=777)
+    rng = np.random.Generator(np.random.PCG64(9))
+    d = _damage(s, rng, 0.5)
+    z_a = rng.integers(0, 256, size=(len(d["vote_pks"]), 16), dtype=np.uint8)
+    z_b = rng.integers(0, 256, size=(len(d["vote_pks"]), 16), dtype=np.uint8)
+    oa, oia = O.certificates_verify_many(s["committee"], d, z_a)
+    ob, oib = O.certificates_verify_many(s["committee"], d, z_b)
+    stable = (oa == ob) & (oia == oib)
+    rows = _rows(d)
+
+    async def main():
+        svc = S.NativeService(s["committee"], max_delay=0.0002)
+        got = await asyncio.gather(*[svc.certificate_status(r) for r in rows])
+        svc.close()
+        return got
+
+    got = asyncio.run(main())
+    bad = [(i, got[i], (int(oa[i]), int(oia[i]))) for i in range(len(rows))
+           if stable[i] and got[i] != (int(oa[i]), int(oia[i]))]
+    assert not bad, bad[:10]
+    assert stable.mean() > 0.9
