@@ -21,6 +21,7 @@
 //
 // Work per vote: 2 decompressions, ~97 table additions and the tables (SURVEY 8(d):
 // 64,000 MAC/vote at n >= 10k); the 252 doublings and the B term are shared per chunk.
+#include "narwhal_amd.h"
 #include "nw_kernels.h"
 #include "nw_point.hpp"
 #include "nw_scalar.hpp"
@@ -63,6 +64,12 @@ uint64_t env_u64(const char* name, uint64_t dflt) {
   if (!v || !*v) return dflt;
   const unsigned long long x = strtoull(v, nullptr, 10);
   return x ? (uint64_t)x : dflt;
+}
+// as env_u64, but a set value of 0 counts (switches whose "off" is 0)
+uint64_t env_u64_zero(const char* name, uint64_t dflt) {
+  const char* v = getenv(name);
+  if (!v || !*v) return dflt;
+  return (uint64_t)strtoull(v, nullptr, 10);
 }
 // (never above kSliceUnits: k_bv_plan_top scans at most 4096 plan blocks)
 uint64_t slice_units() { return std::min(env_u64("NW_BATCH_SLICE_UNITS", kSliceUnits), kSliceUnits); }
@@ -1108,29 +1115,14 @@ __global__ __launch_bounds__(1024) void k_pip_sort(const uint32_t* __restrict__ 
     });
 }
 
-// grid (bpb = kPipBins * G / 256 blocks per batch, npip): lanes [G bin, G bin + G) share
-// bucket bin. xcd: 1-D grid of 8 * bpb * ceil(npip / 8) blocks, remapped so that every
-// block of a batch runs on one XCD (workgroups are dealt round-robin over the 8 XCDs) and
-// each XCD walks its batches one after another: the batch's points (2n x 120 B, gathered
-// at random by its buckets) then stay in that XCD's L2 instead of in all eight.
-__global__ __launch_bounds__(256) void k_pip_buckets(const uint32_t* __restrict__ pip_list,
-                                                     const uint64_t* __restrict__ offsets,
-                                                     uint64_t b0, uint64_t i0, uint32_t lg,
-                                                     uint32_t npip, uint32_t bpb, int xcd,
-                                                     uint32_t extra, uint32_t pmin,
-                                                     ge_cached* __restrict__ tabs) {
-  uint32_t jb = blockIdx.y, xb = blockIdx.x;
-  if (xcd) {
-    const uint32_t k = blockIdx.x >> 3;
-    jb = (blockIdx.x & 7) + 8 * (k / bpb);
-    xb = k % bpb;
-    if (jb >= npip) return;
-  }
-  const uint64_t bidx = b0 + pip_list[jb];
-  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
-  if (n < pmin) return;
-  const pip_region reg = pip_at(tabs, bs - i0, n + extra);
-  const uint32_t gl = xb * blockDim.x + threadIdx.x;
+// Lanes [G bin, G bin + G) of the batch's bucket pass share bucket bin (gl: the lane's index
+// in the pass, G = 2^lg): partial sums of the bin's entries, combined by a lane-shuffle tree.
+// Entry k + 2's index and entry k + 1's point (whose index is already here) are fetched while
+// entry k is added, so the dependent index -> point loads never stall the chain (a deeper
+// ring of 2 or 3 points in flight measured slower: 0.375 vs 0.364 ms for config 1's call,
+// profiles/r04g/pip_prefetch_ab.txt).
+__device__ __forceinline__ void pip_bucket_lanes(const pip_region& reg, uint32_t gl,
+                                                 uint32_t lg) {
   const uint32_t bin = gl >> lg, G = 1u << lg, g = gl & (G - 1);
   if (bin >= (uint32_t)kPipBins) return;   // whole G-groups (kPipBins is a multiple of 64)
   const uint32_t e0 = reg.off[bin], ne = reg.cnt[bin];
@@ -1138,9 +1130,6 @@ __global__ __launch_bounds__(256) void k_pip_buckets(const uint32_t* __restrict_
                  e = e0 + (uint32_t)((uint64_t)ne * (g + 1) >> lg);
   ge acc;
   ge_identity(acc);
-  // two-stage prefetch: entry k + 2's index and entry k + 1's point (whose index is already
-  // here) are fetched while entry k is added, so the dependent index -> point loads never
-  // stall the chain
   uint32_t x = a < e ? reg.ent[a] : 0u;
   uint32_t x2 = a + 1 < e ? reg.ent[a + 1] : 0u;
   ge_niels nx;
@@ -1165,6 +1154,31 @@ __global__ __launch_bounds__(256) void k_pip_buckets(const uint32_t* __restrict_
     ge_add_ge(acc, acc, other, g_bc.k.d2);
   }
   if (g == 0) reg.S[bin] = acc;
+}
+
+// grid (bpb = kPipBins * G / 256 blocks per batch, npip). xcd: 1-D grid of
+// 8 * bpb * ceil(npip / 8) blocks, remapped so that every block of a batch runs on one XCD
+// (workgroups are dealt round-robin over the 8 XCDs) and each XCD walks its batches one after
+// another: the batch's points (2n x 120 B, gathered at random by its buckets) then stay in
+// that XCD's L2 instead of in all eight.
+__global__ __launch_bounds__(256) void k_pip_buckets(const uint32_t* __restrict__ pip_list,
+                                                     const uint64_t* __restrict__ offsets,
+                                                     uint64_t b0, uint64_t i0, uint32_t lg,
+                                                     uint32_t npip, uint32_t bpb, int xcd,
+                                                     uint32_t extra, uint32_t pmin,
+                                                     ge_cached* __restrict__ tabs) {
+  uint32_t jb = blockIdx.y, xb = blockIdx.x;
+  if (xcd) {
+    const uint32_t k = blockIdx.x >> 3;
+    jb = (blockIdx.x & 7) + 8 * (k / bpb);
+    xb = k % bpb;
+    if (jb >= npip) return;
+  }
+  const uint64_t bidx = b0 + pip_list[jb];
+  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
+  if (n < pmin) return;
+  const pip_region reg = pip_at(tabs, bs - i0, n + extra);
+  pip_bucket_lanes(reg, xb * blockDim.x + threadIdx.x, lg);
 }
 
 // grid (kPipWin, npip), one wave per window: sum_b b S_b as a suffix scan over lanes.
@@ -1257,7 +1271,7 @@ __global__ __launch_bounds__(64) void k_pip_windows(const uint32_t* __restrict__
 constexpr uint32_t kPipWinLpMax = 8;
 constexpr int kPipWinLpParts = 18;
 uint32_t pip_win_lp_max() {   // NW_PIP_WIN_LP_MAX=0: always the one-wave form
-  static const uint32_t v = (uint32_t)env_u64("NW_PIP_WIN_LP_MAX", kPipWinLpMax);
+  static const uint32_t v = (uint32_t)env_u64_zero("NW_PIP_WIN_LP_MAX", kPipWinLpMax);
   return v;
 }
 // the parts live in the dead point + entry arrays (contiguous in pip_at)
@@ -1292,40 +1306,30 @@ __device__ __forceinline__ uint32_t pip_lp_load(const lp_ctx& L, const ge* S, ui
   return b == ~0u ? lp_identity(L) : L.k < 10 ? x : 0u;
 }
 
-__global__ __launch_bounds__(128) void k_pip_windows_lp(const uint32_t* __restrict__ pip_list,
-                                                       const uint64_t* __restrict__ offsets,
-                                                       uint64_t b0, uint64_t i0, uint32_t extra,
-                                                       uint32_t pmin,
-                                                       ge_cached* __restrict__ tabs) {
-  const uint64_t bidx = b0 + pip_list[blockIdx.z];
-  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
-  if (n < pmin) return;
-  const pip_region reg = pip_at(tabs, bs - i0, n + extra);
-  const int w = blockIdx.x, q = blockIdx.y, lane = (int)(threadIdx.x & 63);
-  const int half2 = (int)(threadIdx.x >> 6);   // which 16 of the part's 32 entries
-  const lp_ctx L = lp_init((uint32_t)lane);
-  const fe& d2 = g_bc.k.d2;
-  const uint32_t d2l = L.k < 10 ? d2.v[L.k] : 0u;
-  if (w == kPipWin) {
-    if (q != 0 || half2 != 0) return;
-    uint32_t bb[8];
+// [-sum b_i]B = sum_w comb[w][digit w] (32 additions, no doublings), limb-parallel, stored
+// in cached form for the last addition of the Horner (one wave).
+__device__ __forceinline__ void pip_lp_bsum_point(const pip_region& reg, const lp_ctx& L,
+                                                  uint32_t d2l) {
+  uint32_t bb[8];
 #pragma unroll
-    for (int m = 0; m < 8; ++m) bb[m] = reg.bb[m];
-    uint32_t v = lp_identity(L);
+  for (int m = 0; m < 8; ++m) bb[m] = reg.bb[m];
+  uint32_t v = lp_identity(L);
 #pragma unroll 1
-    for (int m = 0; m < kPipWin; ++m) {
-      const int e = digit8(bb, m);
-      v = lp_add(L, v, lp_niels_component(L, g_comb[129 * m + (e < 0 ? -e : e)], e < 0));
-    }
-    const uint32_t c = lp_to_cached(L, v, d2l);
-    if (L.k < 10) reinterpret_cast<uint32_t*>(reg.Bc)[10 * (L.row ^ 1u) + L.k] = c;
-    return;
+  for (int m = 0; m < kPipWin; ++m) {
+    const int e = digit8(bb, m);
+    v = lp_add(L, v, lp_niels_component(L, g_comb[129 * m + (e < 0 ? -e : e)], e < 0));
   }
-  // this part's bucket list: wave h of the block sums entries 32 (q & 1) + 16 h .. + 15,
-  // lane i < 16 holding entry i (additions in whole groups of 8, identities past the end);
-  // wave 1's sum is added by wave 0 through LDS. Two chains of <= 16 additions side by side
-  // instead of one of <= 32 (config 1's one call: the window pass 29 -> ~15 us).
-  __shared__ uint32_t s_other[64];
+  const uint32_t c = lp_to_cached(L, v, d2l);
+  if (L.k < 10) reinterpret_cast<uint32_t*>(reg.Bc)[10 * (L.row ^ 1u) + L.k] = c;
+}
+
+// Part q of window w (see above), half `half2` of its 32 entries on this wave: wave 1's sum
+// is added by wave 0 through LDS (s_other, 64 words; both waves reach the barrier). Two chains
+// of <= 16 additions side by side instead of one of <= 32 (config 1's one call: the window
+// pass 29 -> 25 us). The part goes to parts[(w * kPipWinLpParts + q) * 64 + lane].
+__device__ __forceinline__ void pip_lp_part(const pip_region& reg, const lp_ctx& L,
+                                            uint32_t d2l, int w, int q, int half2, int lane,
+                                            uint32_t* s_other, uint32_t* parts) {
   const int j = q >> 1;
   const uint32_t mine =
       lane < 16 ? pip_lp_bucket(w, j, 32u * (uint32_t)(q & 1) + 16u * (uint32_t)half2 + lane)
@@ -1353,22 +1357,13 @@ __global__ __launch_bounds__(128) void k_pip_windows_lp(const uint32_t* __restri
   __syncthreads();
   if (half2 == 1) return;
   v = lp_add(L, v, s_other[lane]);
-  reinterpret_cast<uint32_t*>(reg.pts)[(w * kPipWinLpParts + q) * 64 + lane] =
-      lp_to_cached(L, v, d2l);
+  parts[(w * kPipWinLpParts + q) * 64 + lane] = lp_to_cached(L, v, d2l);
 }
 
-__global__ __launch_bounds__(64) void k_pip_wsum(const uint32_t* __restrict__ pip_list,
-                                                 const uint64_t* __restrict__ offsets,
-                                                 uint64_t b0, uint64_t i0, uint32_t extra,
-                                                 uint32_t pmin, ge_cached* __restrict__ tabs) {
-  const uint64_t bidx = b0 + pip_list[blockIdx.y];
-  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
-  if (n < pmin) return;
-  const pip_region reg = pip_at(tabs, bs - i0, n + extra);
-  const int w = blockIdx.x, lane = (int)threadIdx.x;
-  const lp_ctx L = lp_init((uint32_t)lane);
-  const uint32_t* part = reinterpret_cast<const uint32_t*>(reg.pts) +
-                         (size_t)w * kPipWinLpParts * 64 + lane;
+// W_w = sum_j 2^j T_j: the 7-doubling Horner over window w's parts (one wave).
+__device__ __forceinline__ void pip_lp_wsum(const pip_region& reg, const lp_ctx& L, int w,
+                                            int lane, const uint32_t* parts) {
+  const uint32_t* part = parts + (size_t)w * kPipWinLpParts * 64 + lane;
   uint32_t t[kPipWinLpParts];
 #pragma unroll
   for (int q = 0; q < kPipWinLpParts; ++q) t[q] = part[64 * q];
@@ -1392,6 +1387,59 @@ __global__ __launch_bounds__(64) void k_pip_wsum(const uint32_t* __restrict__ pi
   const fe& d2 = g_bc.k.d2;
   const uint32_t c = lp_to_cached(L, r, L.k < 10 ? d2.v[L.k] : 0u);
   if (L.k < 10) reinterpret_cast<uint32_t*>(reg.W + w)[10 * (L.row ^ 1u) + L.k] = c;
+}
+
+// The batch's verdict from the Horner's result (lane 0 writes).
+__device__ __forceinline__ void pip_verdict(const pip_region& reg, const lp_ctx& L, uint32_t v,
+                                            uint32_t* s_tmp, uint64_t bidx, uint64_t n,
+                                            int32_t* status, uint64_t* fail_index,
+                                            uint32_t* group_ok) {
+  const bool ident = lp_is_identity(L, v, s_tmp);
+  if (threadIdx.x != 0) return;
+  const uint32_t ff[3] = {reg.hdr[0], reg.hdr[1], reg.hdr[2]};
+  if (group_ok) {   // group mode: any flag or a nonzero sum sends the group to the fallback
+    group_ok[bidx] = (ff[0] == kNone && ff[1] == kNone && ff[2] == kNone && ident) ? 1u : 0u;
+    return;
+  }
+  uint64_t idx;
+  const int st = batch_status(ff, reg.hdr[3], ident, n, &idx);
+  status[bidx] = st;
+  if (fail_index) fail_index[bidx] = idx;
+}
+
+__global__ __launch_bounds__(128) void k_pip_windows_lp(const uint32_t* __restrict__ pip_list,
+                                                       const uint64_t* __restrict__ offsets,
+                                                       uint64_t b0, uint64_t i0, uint32_t extra,
+                                                       uint32_t pmin,
+                                                       ge_cached* __restrict__ tabs) {
+  const uint64_t bidx = b0 + pip_list[blockIdx.z];
+  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
+  if (n < pmin) return;
+  const pip_region reg = pip_at(tabs, bs - i0, n + extra);
+  const int w = blockIdx.x, q = blockIdx.y, lane = (int)(threadIdx.x & 63);
+  const int half2 = (int)(threadIdx.x >> 6);   // which 16 of the part's 32 entries
+  const lp_ctx L = lp_init((uint32_t)lane);
+  const fe& d2 = g_bc.k.d2;
+  const uint32_t d2l = L.k < 10 ? d2.v[L.k] : 0u;
+  if (w == kPipWin) {
+    if (q == 0 && half2 == 0) pip_lp_bsum_point(reg, L, d2l);
+    return;
+  }
+  __shared__ uint32_t s_other[64];
+  pip_lp_part(reg, L, d2l, w, q, half2, lane, s_other, reinterpret_cast<uint32_t*>(reg.pts));
+}
+
+__global__ __launch_bounds__(64) void k_pip_wsum(const uint32_t* __restrict__ pip_list,
+                                                 const uint64_t* __restrict__ offsets,
+                                                 uint64_t b0, uint64_t i0, uint32_t extra,
+                                                 uint32_t pmin, ge_cached* __restrict__ tabs) {
+  const uint64_t bidx = b0 + pip_list[blockIdx.y];
+  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
+  if (n < pmin) return;
+  const pip_region reg = pip_at(tabs, bs - i0, n + extra);
+  const int lane = (int)threadIdx.x;
+  pip_lp_wsum(reg, lp_init((uint32_t)lane), blockIdx.x, lane,
+              reinterpret_cast<const uint32_t*>(reg.pts));
 }
 
 __global__ __launch_bounds__(64) void k_pip_final(const uint32_t* __restrict__ pip_list,
@@ -1420,17 +1468,178 @@ __global__ __launch_bounds__(64) void k_pip_final(const uint32_t* __restrict__ p
     v = lp_add(L, v, lp_cached_component(L, reg.W[w]));
   }
   v = lp_add(L, v, lp_cached_component(L, *reg.Bc));   // + [-sum b_i]B
-  const bool ident = lp_is_identity(L, v, s_tmp);
-  if (tid != 0) return;
-  const uint32_t ff[3] = {reg.hdr[0], reg.hdr[1], reg.hdr[2]};
-  if (group_ok) {   // group mode: any flag or a nonzero sum sends the group to the fallback
-    group_ok[bidx] = (ff[0] == kNone && ff[1] == kNone && ff[2] == kNone && ident) ? 1u : 0u;
+  pip_verdict(reg, L, v, s_tmp, bidx, n, status, fail_index, group_ok);
+}
+
+// ---- config 1's one-call tail: buckets, window parts, window sums and the Horner in ONE
+// launch, ordered by completion counters instead of kernel boundaries ----------------------
+// The bucket pass is chain-bound and uneven: windows 16..31 hold only the c_i digits (half
+// the entries per bucket of windows 0..15, which also hold z_i's), so their buckets are done
+// at about half the pass. Here their window parts and sums start as soon as their own buckets
+// are summed, and the Horner (the 248-doubling chain) starts on W_31 while windows 0..15 are
+// still in their buckets; it needs W_w only 3.4 us x (31 - w) later, by which time the
+// lower windows are summed.
+//
+// Roles by ticket (a per-launch counter taken by each workgroup as it starts, so a workgroup
+// only ever waits for workgroups with smaller tickets, which are already running: no
+// deadlock, whatever the residency):
+//   [0, nbk)                 bucket workgroups (the bucket pass's blocks), each adding one to
+//                            the completion count of every window its bins touch
+//   nbk                      [-sum b_i]B
+//   nbk + 1 + i              window 31's parts 2 i and 2 i + 1 (waves 0-1, 2-3), i < 9,
+//                            after its buckets; the ninth workgroup of a window to finish
+//                            sums the window (wave 0)
+//   nbk + 10                 the Horner (wave 0): W_31 .. W_0 as their sums land, then the
+//                            verdict
+//   nbk + 11 + 9 (30 - w) + i  window w's parts as window 31's (window 16 also after the
+//                            z-carry bins)
+// Every workgroup but the Horner waits only for smaller tickets; the Horner holds one
+// workgroup slot, so the others always progress. The launch reserves kFuseLds of LDS per
+// workgroup: one workgroup per CU, one wave per SIMD, so the Horner's chain issues alone on
+// its SIMD as in k_pip_final (at 3 waves per SIMD it shared one with bucket and part waves:
+// the tail took 224 vs 209 us as four launches).
+// Waits spin on relaxed loads with s_sleep, bounded by kFuseSpinTicks of the 100 MHz
+// real-time counter: on expiry the workgroup stops and the batch reports NW_E_DEVICE (never
+// expected; a guard against a wedged launch).
+constexpr int kFuseParts = kPipWinLpParts / 2;   // part workgroups per window
+constexpr uint32_t kFuseCtr = 4 * 33 + 4;        // counter words (zeroed by k_iota)
+constexpr uint64_t kFuseSpinTicks = 200000000;   // 2 s
+constexpr uint32_t kFuseLds = 96 * 1024;         // > 160 KiB / 2: one workgroup per CU
+enum : uint32_t { kFzTicket = 0, kFzError = 1, kFzBuckets = 4, kFzParts = 4 + 33,
+                  kFzWsum = 4 + 66 };
+constexpr size_t kFusePartBytes = 4ull * (kPipWin + 1) * kPipWinLpParts * 64;
+// the parts live in the batch's digit arrays (cd, zd: dead after k_pip_sort)
+constexpr uint64_t kFuseMinN = (kFusePartBytes + 51) / 52;
+
+// Polls are relaxed (an acquire per poll would invalidate the XCD's L2 under the bucket
+// lanes' gathers every few hundred cycles); the waiter takes ONE agent-scope acquire fence
+// once the count is reached (fz_acquire), and a producer workgroup ONE release (fz_add after
+// its barrier: the release is cumulative over the workgroup's stores ordered before it).
+__device__ __forceinline__ uint32_t fz_poll(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void fz_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); }
+__device__ __forceinline__ void fz_add(uint32_t* p, uint32_t v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Lane 0 spins until *p >= want (or the budget is spent: false, error flagged).
+__device__ __forceinline__ bool fz_wait(uint32_t* ctr, uint32_t idx, uint32_t want) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (fz_poll(ctr + idx) < want) {
+    __builtin_amdgcn_s_sleep(2);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > kFuseSpinTicks) {
+      __hip_atomic_store(ctr + kFzError, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+  return true;
+}
+// Bucket workgroups whose bins touch window w (w = kPipWin: the z-carry bins).
+__device__ __forceinline__ uint32_t fz_bucket_blocks(int w, uint32_t lg) {
+  const uint32_t b0 = (uint32_t)w * 128, b1 = w == kPipWin ? b0 + kPipCarryBins : b0 + 128;
+  return (((b1 - 1) << lg) >> 8) - ((b0 << lg) >> 8) + 1;
+}
+
+__global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restrict__ offsets,
+                                                        uint64_t bidx, uint64_t i0,
+                                                        uint32_t lg, uint32_t nbk,
+                                                        ge_cached* __restrict__ tabs,
+                                                        uint32_t* __restrict__ ctr,
+                                                        int32_t* __restrict__ status,
+                                                        uint64_t* __restrict__ fail_index) {
+  __shared__ uint32_t s_ticket, s_ok;
+  __shared__ uint32_t s_other[2][64];
+  __shared__ uint32_t s_tmp[40];
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) {
+    s_ticket = __hip_atomic_fetch_add(ctr + kFzTicket, 1u, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+    s_ok = 1u;
+  }
+  __syncthreads();
+  const uint32_t t = s_ticket;
+  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
+  const pip_region reg = pip_at(tabs, bs - i0, n);
+  uint32_t* parts = reinterpret_cast<uint32_t*>(reg.cd);
+  const lp_ctx L = lp_init((uint32_t)lane);
+  const uint32_t d2l = L.k < 10 ? g_bc.k.d2.v[L.k] : 0u;
+  if (t < nbk) {   // ---- buckets
+    pip_bucket_lanes(reg, t * 256 + (uint32_t)tid, lg);
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t bin0 = (t * 256) >> lg, bin1 = ((t + 1) * 256 - 1) >> lg;
+      for (uint32_t wv = bin0 >> 7; wv <= ((bin1 < (uint32_t)kPipBins ? bin1 : kPipBins - 1) >> 7);
+           ++wv)
+        if (bin0 < (uint32_t)kPipBins) fz_add(ctr + kFzBuckets + wv, 1u);
+    }
     return;
   }
-  uint64_t idx;
-  const int st = batch_status(ff, reg.hdr[3], ident, n, &idx);
-  status[bidx] = st;
-  if (fail_index) fail_index[bidx] = idx;
+  if (t == nbk) {   // ---- [-sum b_i]B
+    if (wave == 0) {
+      pip_lp_bsum_point(reg, L, d2l);
+      if (lane == 0) fz_add(ctr + kFzWsum + kPipWin, 1u);
+    }
+    return;
+  }
+  uint32_t pt = t - nbk - 1;
+  const bool horner = pt == (uint32_t)kFuseParts;
+  if (pt > (uint32_t)kFuseParts) --pt;
+  if (!horner) {   // ---- window parts (+ the window's sum)
+    const int w = kPipWin - 1 - (int)(pt / kFuseParts), i = (int)(pt % kFuseParts);
+    if (tid == 0) {
+      bool ok = fz_wait(ctr, kFzBuckets + w, fz_bucket_blocks(w, lg));
+      if (ok && w == kPipZWin - 1) ok = fz_wait(ctr, kFzBuckets + kPipWin, fz_bucket_blocks(kPipWin, lg));
+      s_ok = ok ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    fz_acquire();
+    const int q = 2 * i + (wave >> 1), half2 = wave & 1;
+    pip_lp_part(reg, L, d2l, w, q, half2, lane, s_other[wave >> 1], parts);
+    __syncthreads();   // wave 2's part before wave 0 counts the workgroup (waves 1 and 3
+                       // returned from pip_lp_part after its barrier)
+    if (wave != 0) return;
+    uint32_t last = 0;
+    if (lane == 0)
+      last = __hip_atomic_fetch_add(ctr + kFzParts + w, 1u, __ATOMIC_ACQ_REL,
+                                    __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)kFuseParts - 1;
+    if (!__builtin_amdgcn_readfirstlane(last)) return;
+    fz_acquire();
+    pip_lp_wsum(reg, L, w, lane, parts);
+    if (lane == 0) fz_add(ctr + kFzWsum + w, 1u);
+    return;
+  }
+  // ---- the Horner (wave 0)
+  if (wave != 0) return;
+  uint32_t v = lp_identity(L);
+  bool ok = true;
+#pragma unroll 1
+  for (int w = kPipWin - 1; w >= 0 && ok; --w) {
+    if (w != kPipWin - 1) {
+#pragma unroll 1
+      for (int k = 0; k < 8; ++k) v = lp_dbl(L, v);
+    }
+    uint32_t got = 1;
+    if (lane == 0) got = fz_wait(ctr, kFzWsum + w, 1u) ? 1u : 0u;
+    ok = __builtin_amdgcn_readfirstlane(got) != 0;
+    fz_acquire();
+    v = lp_add(L, v, lp_cached_component(L, reg.W[w]));
+  }
+  uint32_t got = ok ? 1u : 0u;
+  if (ok && lane == 0) got = fz_wait(ctr, kFzWsum + kPipWin, 1u) ? 1u : 0u;
+  ok = __builtin_amdgcn_readfirstlane(got) != 0;
+  fz_acquire();
+  if (lane == 0 && fz_poll(ctr + kFzError)) ok = false;
+  ok = __builtin_amdgcn_readfirstlane(ok ? 1u : 0u) != 0;
+  if (!ok) {
+    if (lane == 0) {
+      status[bidx] = NW_E_DEVICE;
+      if (fail_index) fail_index[bidx] = 0;
+    }
+    return;
+  }
+  v = lp_add(L, v, lp_cached_component(L, *reg.Bc));   // + [-sum b_i]B
+  pip_verdict(reg, L, v, s_tmp, bidx, n, status, fail_index, nullptr);
 }
 
 inline size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1709,7 +1918,21 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
   while (lg < 6 && (49 * (pmax + extra)) / kPipBins > 8ull << lg) ++lg;
   // ... but no more lanes than the chip runs at once (the shuffle tree is overhead)
   while (lg > 0 && ((npip * kPipBins) << lg) > (1ull << 21)) --lg;
+  static const uint64_t lg_env = env_u64("NW_PIP_LG", 99);   // A/B hook
+  if (lg_env <= 6) lg = (uint32_t)lg_env;
   const uint32_t bpb = ((kPipBins << lg) + 255) / 256;
+  // One large batch alone in its slice (config 1's call): the fused tail (NW_PIP_FUSE=0: the
+  // four kernels below; k_iota zeroed the counters in w.chunk_start)
+  static const bool fuse_on = env_u64_zero("NW_PIP_FUSE", 1) != 0;
+  if (fuse_on && !group && npip == 1 && e - b == 1 && pmax >= kFuseMinN &&
+      npip <= pip_win_lp_max()) {
+    const uint32_t nbk = bpb;
+    static const uint32_t lds = (uint32_t)env_u64_zero("NW_PIP_FUSE_LDS", kFuseLds);   // A/B
+    hipLaunchKernelGGL(k_pip_tail_fused, dim3(nbk + 2 + kPipWin * kFuseParts), dim3(256), lds,
+                       stream, offsets, b, i0, lg, nbk, w.tabs, w.chunk_start, status,
+                       fail_index);
+    return hipGetLastError();
+  }
   const int xcd = npip >= 8;
   const dim3 gb = xcd ? dim3((unsigned)(8 * bpb * ((npip + 7) / 8))) : dim3(bpb, (unsigned)npip);
   hipLaunchKernelGGL(k_pip_buckets, gb, dim3(256), 0, stream, w.pip_list, offsets, b, i0, lg,
@@ -1732,9 +1955,11 @@ uint32_t pip_min() {
       kPipFloor, std::min<uint64_t>(0xffffffffu, env_u64("NW_BATCH_PIPPENGER_MIN", kPipMin)));
 }
 
-__global__ __launch_bounds__(256) void k_iota(uint32_t* __restrict__ list, uint32_t n) {
+__global__ __launch_bounds__(256) void k_iota(uint32_t* __restrict__ list, uint32_t n,
+                                              uint32_t* __restrict__ zero, uint32_t nz) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) list[i] = i;
+  if (i < nz) zero[i] = 0;   // k_pip_tail_fused's counters
 }
 
 // Group g = certificates [g K, min(g K + K, ncert)): gofs[g] = its first vote; identity list.
@@ -1814,7 +2039,7 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
       // every batch of the slice takes the Pippenger path (config 1's one 10k batch): no
       // chunk plan, the Pippenger list is the slice's batches in order
       hipLaunchKernelGGL(k_iota, dim3((unsigned)((npip + 255) / 256)), dim3(256), 0, stream,
-                         w.pip_list, (uint32_t)npip);
+                         w.pip_list, (uint32_t)npip, w.chunk_start, kFuseCtr);
     } else {
       hipLaunchKernelGGL(k_bv_plan_local, dim3(nblk), dim3(1024), 0, stream, offsets, b, e, C,
                          pmin, sk, w.plan_tot);

@@ -173,3 +173,31 @@ def test_pippenger_config1_shape():
     ost, oidx = O.verify_batch(dig[0].tobytes(), pk, np.concatenate(
         [sigs[:9999], np.zeros((1, 64), np.uint8)]), rng.integers(0, 256, (10000, 16), dtype=np.uint8))
     assert (e.value.code, e.value.index) == (ost, oidx)
+
+
+@pytest.mark.parametrize("n,cls,skew", [(2925, None, False), (3000, 0, False), (4096, 3, True),
+                                        (10000, 0, False), (10000, None, True), (10000, 5, False),
+                                        (16384, 2, False), (20000, 4, False)])
+def test_pippenger_one_call_fused_tail(n, cls, skew):
+    """One batch alone in a call (config 1's shape, n >= 2925): the fused tail kernel
+    (k_pip_tail_fused: buckets, window parts and sums, Horner in one launch ordered by
+    completion counters). Status and first failing index == the oracle's, with injected z,
+    every failure class, and skewed z (all equal: every vote in the same buckets)."""
+    rng = np.random.Generator(np.random.PCG64(n + 7 * (cls or 0) + skew))
+    dig, pk, sigs, off, z16 = _corpus_sizes(np.array([n]), rng, every=0)
+    if skew:
+        z16 = np.tile(z16[:1], (n, 1))
+    if cls is not None:
+        _mutate(sigs, pk, int(rng.integers(0, n)), cls)
+    ost, oidx = O.verify_batch(dig[0].tobytes(), pk, sigs, z16)
+    votes = [(C.PublicKey(pk[i].tobytes()), C.Signature.from_bytes(sigs[i].tobytes()))
+             for i in range(n)]
+    try:
+        C.Signature.verify_batch(C.Digest(dig[0].tobytes()), votes, z16=z16.tobytes())
+        got = (0, None)
+    except C.CryptoError as err:
+        got = (err.code, err.index)
+    assert got[0] == ost
+    if ost:
+        assert got[1] == oidx
+    assert (ost == 0) == (cls is None)
