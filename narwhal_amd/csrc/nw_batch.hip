@@ -33,6 +33,8 @@
 #include "nw_chacha.hpp"
 
 #include <stdlib.h>
+#include <stdio.h>
+#include <string.h>
 
 #include <algorithm>
 #include <cmath>
@@ -1360,6 +1362,34 @@ __device__ __forceinline__ void pip_lp_part(const pip_region& reg, const lp_ctx&
   parts[(w * kPipWinLpParts + q) * 64 + lane] = lp_to_cached(L, v, d2l);
 }
 
+// Part q of the top window on all four waves of the workgroup (8 entries each; waves 1-3's
+// sums added by wave 0 through LDS, s_other4: 3 x 64 words): chains of <= 8 additions, the
+// top window's parts being on the critical path of the fused tail.
+__device__ __forceinline__ void pip_lp_part4(const pip_region& reg, const lp_ctx& L,
+                                             uint32_t d2l, int q, int wave, int lane,
+                                             uint32_t* s_other4, uint32_t* parts) {
+  const int w = kPipWin - 1, j = q >> 1;
+  const uint32_t mine =
+      lane < 8 ? pip_lp_bucket(w, j, 32u * (uint32_t)(q & 1) + 8u * (uint32_t)wave + lane) : ~0u;
+  const uint32_t cnt = (uint32_t)__builtin_popcountll(__ballot(mine != ~0u));
+  uint32_t v = lp_identity(L);
+  if (cnt) {
+    uint32_t buf[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      buf[u] = pip_lp_load(L, reg.S, (uint32_t)__builtin_amdgcn_readlane((int)mine, u));
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if ((uint32_t)u < cnt) v = lp_add(L, v, lp_to_cached(L, buf[u], d2l));
+  }
+  if (wave != 0) s_other4[64 * (wave - 1) + lane] = lp_to_cached(L, v, d2l);
+  __syncthreads();
+  if (wave != 0) return;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) v = lp_add(L, v, s_other4[64 * k + lane]);
+  parts[(w * kPipWinLpParts + q) * 64 + lane] = lp_to_cached(L, v, d2l);
+}
+
 // W_w = sum_j 2^j T_j: the 7-doubling Horner over window w's parts (one wave).
 __device__ __forceinline__ void pip_lp_wsum(const pip_region& reg, const lp_ctx& L, int w,
                                             int lane, const uint32_t* parts) {
@@ -1486,13 +1516,13 @@ __global__ __launch_bounds__(64) void k_pip_final(const uint32_t* __restrict__ p
 //   [0, nbk)                 bucket workgroups (the bucket pass's blocks), each adding one to
 //                            the completion count of every window its bins touch
 //   nbk                      [-sum b_i]B
-//   nbk + 1 + i              window 31's parts 2 i and 2 i + 1 (waves 0-1, 2-3), i < 9,
-//                            after its buckets; the ninth workgroup of a window to finish
-//                            sums the window (wave 0)
-//   nbk + 10                 the Horner (wave 0): W_31 .. W_0 as their sums land, then the
-//                            verdict
-//   nbk + 11 + 9 (30 - w) + i  window w's parts as window 31's (window 16 also after the
-//                            z-carry bins)
+//   nbk + 1 + q              window 31's part q < 10 (its digits are <= 17: lists j <= 4
+//                            only) on all four waves, after its buckets
+//   nbk + 11                 the Horner (wave 0): W_31 from window 31's ten parts itself
+//                            (4 doublings), then W_30 .. W_0 as their sums land, the verdict
+//   nbk + 12 + 9 (30 - w) + i  window w's parts 2 i and 2 i + 1 (waves 0-1, 2-3), i < 9,
+//                            after its buckets (window 16 also after the z-carry bins); the
+//                            ninth workgroup of the window to finish sums it (wave 0)
 // Every workgroup but the Horner waits only for smaller tickets; the Horner holds one
 // workgroup slot, so the others always progress. The launch reserves kFuseLds of LDS per
 // workgroup: one workgroup per CU, one wave per SIMD, so the Horner's chain issues alone on
@@ -1501,7 +1531,8 @@ __global__ __launch_bounds__(64) void k_pip_final(const uint32_t* __restrict__ p
 // Waits spin on relaxed loads with s_sleep, bounded by kFuseSpinTicks of the 100 MHz
 // real-time counter: on expiry the workgroup stops and the batch reports NW_E_DEVICE (never
 // expected; a guard against a wedged launch).
-constexpr int kFuseParts = kPipWinLpParts / 2;   // part workgroups per window
+constexpr int kFuseParts = kPipWinLpParts / 2;   // part workgroups per window (w < 31)
+constexpr int kFuseTopParts = 10;                 // window 31: lists j <= 4, one part each
 constexpr uint32_t kFuseCtr = 4 * 33 + 4;        // counter words (zeroed by k_iota)
 constexpr uint64_t kFuseSpinTicks = 200000000;   // 2 s
 constexpr uint32_t kFuseLds = 96 * 1024;         // > 160 KiB / 2: one workgroup per CU
@@ -1515,6 +1546,58 @@ constexpr uint64_t kFuseMinN = (kFusePartBytes + 51) / 52;
 // lanes' gathers every few hundred cycles); the waiter takes ONE agent-scope acquire fence
 // once the count is reached (fz_acquire), and a producer workgroup ONE release (fz_add after
 // its barrier: the release is cumulative over the workgroup's stores ordered before it).
+bool pip_fuse_on() {   // NW_PIP_FUSE=0: the tail as four launches (A/B hook)
+  static const bool v = env_u64_zero("NW_PIP_FUSE", 1) != 0;
+  return v;
+}
+
+// NW_PIP_FUSE_STAMPS=1 (diagnostic, one caller at a time): a host-mapped stamp buffer for
+// k_pip_tail_fused; each launch first prints the previous launch's timeline (that call has
+// returned): per role the first start and last end, W_31's arrival at the Horner, the
+// Horner's W_15 and end, in us from the launch's first workgroup start.
+uint64_t* fuse_stamps(uint32_t nblk) {
+  static const bool on = env_u64_zero("NW_PIP_FUSE_STAMPS", 0) != 0;
+  static uint64_t* buf = nullptr;
+  static uint32_t prev = 0;
+  if (!on) return nullptr;
+  if (buf && prev) {
+    uint64_t t0 = ~0ull;
+    for (uint32_t i = 0; i < prev; ++i) t0 = std::min(t0, buf[4 * i]);
+    double rs[8][2];
+    for (auto& r : rs) r[0] = 1e30, r[1] = 0;
+    double w31 = 0, w15 = 0, hend = 0, wsum_end[33] = {0};
+    for (uint32_t i = 0; i < prev; ++i) {
+      const uint64_t* s = buf + 4 * i;
+      const uint32_t role = (uint32_t)(s[2] >> 8);
+      const double a = (s[0] - t0) / 100.0, e = (s[1] - t0) / 100.0;
+      if (role < 8) rs[role][0] = std::min(rs[role][0], a), rs[role][1] = std::max(rs[role][1], e);
+      if (role == 4) wsum_end[s[2] & 63] = e;
+      if (role == 5) w31 = (s[3] - t0) / 100.0, hend = e;
+    }
+    for (uint32_t i = 0; i < prev; ++i)
+      if ((buf[4 * i + 2] >> 8) == 5) w15 = (buf[4 * i + 1] - t0) / 100.0;
+    fprintf(stderr,
+            "[fuse] buckets %.1f-%.1f bsum %.1f-%.1f parts %.1f-%.1f wsum -%.1f horner %.1f-%.1f "
+            "(W_31 at %.1f) | W ready: w31 %.1f w24 %.1f w16 %.1f w15 %.1f w8 %.1f w0 %.1f\n",
+            rs[1][0], rs[1][1], rs[2][0], rs[2][1], rs[3][0], rs[3][1], rs[4][1], rs[5][0],
+            hend, w31, wsum_end[31], wsum_end[24], wsum_end[16], wsum_end[15], wsum_end[8],
+            wsum_end[0]);
+    (void)w15;
+  }
+  if (!buf || nblk > prev) {
+    if (buf) (void)hipHostFree(buf);
+    buf = nullptr;
+    if (hipHostMalloc(reinterpret_cast<void**>(&buf), 32ull * nblk,
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return nullptr;
+  }
+  memset(buf, 0, 32ull * nblk);
+  prev = nblk;
+  void* dp = nullptr;
+  return hipHostGetDevicePointer(&dp, buf, 0) == hipSuccess ? static_cast<uint64_t*>(dp)
+                                                            : nullptr;
+}
+
 __device__ __forceinline__ uint32_t fz_poll(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1546,9 +1629,10 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
                                                         ge_cached* __restrict__ tabs,
                                                         uint32_t* __restrict__ ctr,
                                                         int32_t* __restrict__ status,
-                                                        uint64_t* __restrict__ fail_index) {
+                                                        uint64_t* __restrict__ fail_index,
+                                                        uint64_t* __restrict__ stamps) {
   __shared__ uint32_t s_ticket, s_ok;
-  __shared__ uint32_t s_other[2][64];
+  __shared__ uint32_t s_other[3][64];
   __shared__ uint32_t s_tmp[40];
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid == 0) {
@@ -1558,6 +1642,11 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
   }
   __syncthreads();
   const uint32_t t = s_ticket;
+  // NW_PIP_FUSE_STAMPS: per workgroup (by ticket) start, end, role / window (diagnostic)
+  const auto stamp = [&](int slot, uint64_t v) {
+    if (stamps && tid == 0) stamps[4 * t + slot] = v;
+  };
+  stamp(0, __builtin_amdgcn_s_memrealtime());
   const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
   const pip_region reg = pip_at(tabs, bs - i0, n);
   uint32_t* parts = reinterpret_cast<uint32_t*>(reg.cd);
@@ -1571,6 +1660,8 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
       for (uint32_t wv = bin0 >> 7; wv <= ((bin1 < (uint32_t)kPipBins ? bin1 : kPipBins - 1) >> 7);
            ++wv)
         if (bin0 < (uint32_t)kPipBins) fz_add(ctr + kFzBuckets + wv, 1u);
+      stamp(1, __builtin_amdgcn_s_memrealtime());
+      stamp(2, 0x100u | ((t * 256) >> lg >> 7));
     }
     return;
   }
@@ -1578,14 +1669,28 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
     if (wave == 0) {
       pip_lp_bsum_point(reg, L, d2l);
       if (lane == 0) fz_add(ctr + kFzWsum + kPipWin, 1u);
+      stamp(1, __builtin_amdgcn_s_memrealtime());
+      stamp(2, 0x200u);
     }
     return;
   }
-  uint32_t pt = t - nbk - 1;
-  const bool horner = pt == (uint32_t)kFuseParts;
-  if (pt > (uint32_t)kFuseParts) --pt;
-  if (!horner) {   // ---- window parts (+ the window's sum)
-    const int w = kPipWin - 1 - (int)(pt / kFuseParts), i = (int)(pt % kFuseParts);
+  const uint32_t pt = t - nbk - 1;
+  if (pt < (uint32_t)kFuseTopParts) {   // ---- window 31's parts
+    if (tid == 0) s_ok = fz_wait(ctr, kFzBuckets + kPipWin - 1, fz_bucket_blocks(kPipWin - 1, lg))
+                             ? 1u : 0u;
+    __syncthreads();
+    if (!s_ok) return;
+    fz_acquire();
+    stamp(3, __builtin_amdgcn_s_memrealtime());
+    pip_lp_part4(reg, L, d2l, (int)pt, wave, lane, &s_other[0][0] + 0, parts);
+    if (wave == 0 && lane == 0) fz_add(ctr + kFzParts + kPipWin - 1, 1u);
+    stamp(1, __builtin_amdgcn_s_memrealtime());
+    stamp(2, 0x300u | (uint32_t)(kPipWin - 1));
+    return;
+  }
+  if (pt > (uint32_t)kFuseTopParts) {   // ---- window parts (+ the window's sum)
+    const uint32_t pg = pt - kFuseTopParts - 1;
+    const int w = kPipWin - 2 - (int)(pg / kFuseParts), i = (int)(pg % kFuseParts);
     if (tid == 0) {
       bool ok = fz_wait(ctr, kFzBuckets + w, fz_bucket_blocks(w, lg));
       if (ok && w == kPipZWin - 1) ok = fz_wait(ctr, kFzBuckets + kPipWin, fz_bucket_blocks(kPipWin, lg));
@@ -1594,6 +1699,7 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
     __syncthreads();
     if (!s_ok) return;
     fz_acquire();
+    stamp(3, __builtin_amdgcn_s_memrealtime());   // its buckets were ready
     const int q = 2 * i + (wave >> 1), half2 = wave & 1;
     pip_lp_part(reg, L, d2l, w, q, half2, lane, s_other[wave >> 1], parts);
     __syncthreads();   // wave 2's part before wave 0 counts the workgroup (waves 1 and 3
@@ -1603,26 +1709,46 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
     if (lane == 0)
       last = __hip_atomic_fetch_add(ctr + kFzParts + w, 1u, __ATOMIC_ACQ_REL,
                                     __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)kFuseParts - 1;
+    stamp(1, __builtin_amdgcn_s_memrealtime());
+    stamp(2, 0x300u | (uint32_t)w);
     if (!__builtin_amdgcn_readfirstlane(last)) return;
     fz_acquire();
     pip_lp_wsum(reg, L, w, lane, parts);
     if (lane == 0) fz_add(ctr + kFzWsum + w, 1u);
+    stamp(1, __builtin_amdgcn_s_memrealtime());
+    stamp(2, 0x400u | (uint32_t)w);   // this workgroup also summed the window
     return;
   }
   // ---- the Horner (wave 0)
   if (wave != 0) return;
-  uint32_t v = lp_identity(L);
-  bool ok = true;
+  // W_31 = sum_{j <= 4} 2^j T_j straight from window 31's parts (2 j, 2 j + 1 = T_j)
+  uint32_t got0 = 1;
+  if (lane == 0)
+    got0 = fz_wait(ctr, kFzParts + kPipWin - 1, (uint32_t)kFuseTopParts) ? 1u : 0u;
+  bool ok = __builtin_amdgcn_readfirstlane(got0) != 0;
+  fz_acquire();
+  stamp(3, __builtin_amdgcn_s_memrealtime());
+  const uint32_t* top = parts + (size_t)(kPipWin - 1) * kPipWinLpParts * 64 + lane;
+  uint32_t tp[kFuseTopParts];
+#pragma unroll
+  for (int q = 0; q < kFuseTopParts; ++q) tp[q] = top[64 * q];
+  uint32_t v = lp_add(L, lp_identity(L), tp[8]);
+  v = lp_add(L, v, tp[9]);
+#pragma unroll
+  for (int j = 3; j >= 0; --j) {
+    v = lp_dbl(L, v);
+    v = lp_add(L, v, tp[2 * j]);
+    v = lp_add(L, v, tp[2 * j + 1]);
+  }
 #pragma unroll 1
-  for (int w = kPipWin - 1; w >= 0 && ok; --w) {
-    if (w != kPipWin - 1) {
+  for (int w = kPipWin - 2; w >= 0 && ok; --w) {
 #pragma unroll 1
-      for (int k = 0; k < 8; ++k) v = lp_dbl(L, v);
-    }
+    for (int k = 0; k < 8; ++k) v = lp_dbl(L, v);
     uint32_t got = 1;
     if (lane == 0) got = fz_wait(ctr, kFzWsum + w, 1u) ? 1u : 0u;
     ok = __builtin_amdgcn_readfirstlane(got) != 0;
     fz_acquire();
+    if (w == kPipZWin - 2) stamp(1, __builtin_amdgcn_s_memrealtime());   // reached W_15
     v = lp_add(L, v, lp_cached_component(L, reg.W[w]));
   }
   uint32_t got = ok ? 1u : 0u;
@@ -1635,11 +1761,15 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
     if (lane == 0) {
       status[bidx] = NW_E_DEVICE;
       if (fail_index) fail_index[bidx] = 0;
+      __threadfence_system();
     }
     return;
   }
   v = lp_add(L, v, lp_cached_component(L, *reg.Bc));   // + [-sum b_i]B
   pip_verdict(reg, L, v, s_tmp, bidx, n, status, fail_index, nullptr);
+  stamp(1, __builtin_amdgcn_s_memrealtime());
+  stamp(2, 0x500u);
+  if (lane == 0) __threadfence_system();   // outputs may be host-mapped (direct outputs)
 }
 
 inline size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1923,14 +2053,13 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
   const uint32_t bpb = ((kPipBins << lg) + 255) / 256;
   // One large batch alone in its slice (config 1's call): the fused tail (NW_PIP_FUSE=0: the
   // four kernels below; k_iota zeroed the counters in w.chunk_start)
-  static const bool fuse_on = env_u64_zero("NW_PIP_FUSE", 1) != 0;
-  if (fuse_on && !group && npip == 1 && e - b == 1 && pmax >= kFuseMinN &&
+  if (pip_fuse_on() && !group && npip == 1 && e - b == 1 && pmax >= kFuseMinN &&
       npip <= pip_win_lp_max()) {
     const uint32_t nbk = bpb;
     static const uint32_t lds = (uint32_t)env_u64_zero("NW_PIP_FUSE_LDS", kFuseLds);   // A/B
-    hipLaunchKernelGGL(k_pip_tail_fused, dim3(nbk + 2 + kPipWin * kFuseParts), dim3(256), lds,
-                       stream, offsets, b, i0, lg, nbk, w.tabs, w.chunk_start, status,
-                       fail_index);
+    const uint32_t nblk = nbk + 2 + kFuseTopParts + (kPipWin - 1) * kFuseParts;
+    hipLaunchKernelGGL(k_pip_tail_fused, dim3(nblk), dim3(256), lds, stream, offsets, b, i0, lg,
+                       nbk, w.tabs, w.chunk_start, status, fail_index, fuse_stamps(nblk));
     return hipGetLastError();
   }
   const int xcd = npip >= 8;
@@ -2079,6 +2208,11 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
     b = e;
   }
   return hipSuccess;
+}
+
+bool verify_batch_outputs_direct(uint64_t nbatches, uint64_t nitems) {
+  return nbatches == 1 && pip_fuse_on() && pip_win_lp_max() >= 1 &&
+         nitems >= std::max<uint64_t>(kFuseMinN, pip_min()) && nitems + 1 <= slice_units();
 }
 
 const ge* key_tables_base(const ge_niels_pad* tabs, uint64_t nkeys) {

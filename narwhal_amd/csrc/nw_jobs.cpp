@@ -318,7 +318,11 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
     return e && *e == '1';
   }();
   const bool fork = fork_on && j->fork.s2;
-  rc = job_run(j, o_st, o_st, o_ws - o_st, [&]() -> int {
+  // a lone large batch (config 1's call): the verdict is written straight into the pinned
+  // buffer by the one kernel that computes it, no copy back
+  const bool direct = !fork && nw::verify_batch_outputs_direct(nbatches, nitems);
+  char* const obuf = direct ? j->hdev : j->dbuf;
+  rc = job_run(j, o_st, o_st, direct ? 0 : o_ws - o_st, [&]() -> int {
     JOB_HIP(nw::launch_verify_batch(reinterpret_cast<const uint32_t*>(j->dbuf + o_d),
                                     reinterpret_cast<const uint64_t*>(j->dbuf + o_off), h_off,
                                     nbatches, reinterpret_cast<const uint32_t*>(j->dbuf + o_pk),
@@ -326,8 +330,8 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
                                     z16 ? reinterpret_cast<const uint32_t*>(j->dbuf + o_z)
                                         : nullptr,
                                     key, j->dbuf + o_ws,
-                                    reinterpret_cast<int32_t*>(j->dbuf + o_st),
-                                    reinterpret_cast<uint64_t*>(j->dbuf + o_fi), j->stream,
+                                    reinterpret_cast<int32_t*>(obuf + o_st),
+                                    reinterpret_cast<uint64_t*>(obuf + o_fi), j->stream,
                                     nullptr, nullptr, 0, 1.0, fork ? &fk : nullptr),
             "verify_batch launch");
     return 0;

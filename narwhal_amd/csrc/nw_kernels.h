@@ -82,6 +82,10 @@ hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, struct ge_niel
                              uint32_t* ok, hipStream_t stream, uint32_t* saved = nullptr,
                              uint32_t* flag = nullptr, bool force = true);
 size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems);
+// True when launch_verify_batch over these batches (no skip list, no fork) writes its outputs
+// from ONE kernel, the fused tail of a lone large batch: status / fail_index may then be
+// host-mapped (fine-grained) memory, written in place, with no copy back.
+bool verify_batch_outputs_direct(uint64_t nbatches, uint64_t nitems);
 // Optional second stream for launch_verify_batch's Pippenger batches (decompressions beside
 // the digit lanes and sorts) and two events it records (reused per call).
 struct batch_fork_t {
