@@ -798,13 +798,12 @@ __device__ __forceinline__ void ge_shfl(ge& r, const ge& p, int src) {
 // batches only: in group mode A is a committee key) = decompress A. Three short chains
 // instead of one lane doing the scalars and A's decompression in series (the one-call
 // latency of config 1 is this kernel's longest lane).
-__global__ __launch_bounds__(256, 3) void k_pip_points(
-    const uint32_t* __restrict__ digests, const uint64_t* __restrict__ offsets, uint64_t b0,
-    uint64_t b1, uint64_t i0, uint64_t i1, uint32_t pmin, const uint32_t* __restrict__ pks,
-    const uint32_t* __restrict__ sigs, const uint32_t* __restrict__ z16, z_key_t zkey,
-    bv_item* __restrict__ items, ge_cached* __restrict__ tabs, pip_group_t grp,
-    uint32_t roles, uint32_t role0) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void pip_point_lane(
+    uint64_t g, const uint32_t* __restrict__ digests, const uint64_t* __restrict__ offsets,
+    uint64_t b0, uint64_t b1, uint64_t i0, uint64_t i1, uint32_t pmin,
+    const uint32_t* __restrict__ pks, const uint32_t* __restrict__ sigs,
+    const uint32_t* __restrict__ z16, const z_key_t& zkey, bv_item* __restrict__ items,
+    ge_cached* __restrict__ tabs, const pip_group_t& grp, uint32_t roles, uint32_t role0) {
   const uint64_t wave = g >> 6;
   const int which = (int)(role0 + wave % roles);
   const uint64_t li = (wave / roles) * 64 + (g & 63);
@@ -923,6 +922,16 @@ __global__ __launch_bounds__(256, 3) void k_pip_points(
   it->key = key;
 }
 
+__global__ __launch_bounds__(256, 3) void k_pip_points(
+    const uint32_t* __restrict__ digests, const uint64_t* __restrict__ offsets, uint64_t b0,
+    uint64_t b1, uint64_t i0, uint64_t i1, uint32_t pmin, const uint32_t* __restrict__ pks,
+    const uint32_t* __restrict__ sigs, const uint32_t* __restrict__ z16, z_key_t zkey,
+    bv_item* __restrict__ items, ge_cached* __restrict__ tabs, pip_group_t grp,
+    uint32_t roles, uint32_t role0) {
+  pip_point_lane((uint64_t)blockIdx.x * blockDim.x + threadIdx.x, digests, offsets, b0, b1, i0,
+                 i1, pmin, pks, sigs, z16, zkey, items, tabs, grp, roles, role0);
+}
+
 // Group mode: per group, sum_i c_i per committee key (LDS, 64-bit limb sums), reduced mod l,
 // as the digits of the key "votes" t = n + j, whose A point is the decompressed key.
 __global__ __launch_bounds__(1024) void k_grp_keys(const uint64_t* __restrict__ offsets,
@@ -976,29 +985,6 @@ __global__ __launch_bounds__(1024) void k_grp_keys(const uint64_t* __restrict__ 
   }
 }
 
-// The nonzero digits of vote t in window w (c_i and, for w <= 16, z_i) as
-// f(local bin, point index, negative); local bins 0..127 are buckets w * 128 + j, and in
-// window 16 local bins 128..191 are the z-carry sub-bins.
-template <typename F>
-__device__ __forceinline__ void pip_window_digits(const pip_region& reg, uint64_t n, uint64_t t,
-                                                  int w, F&& f) {
-  const int dc = (int)reg.cd[w * n + t] - 128;
-  if (dc != 0) {
-    const uint32_t ad = (uint32_t)(dc < 0 ? -dc : dc);
-    const uint32_t lb = w == kPipWin - 1 ? (uint32_t)(kPipTopStride * (t % kPipTopSub)) + ad - 1
-                                         : ad - 1;
-    f(lb, (uint32_t)(2 * t), dc < 0);
-  }
-  if (w < kPipZWin) {
-    const int dz = (int)reg.zd[w * n + t] - 128;
-    if (dz != 0) {
-      const uint32_t ad = (uint32_t)(dz < 0 ? -dz : dz);
-      const uint32_t lb = w == kPipZWin - 1 ? (uint32_t)(128 + (t % kPipCarryBins)) : ad - 1;
-      f(lb, (uint32_t)(2 * t + 1), dz < 0);
-    }
-  }
-}
-
 // The extra block of k_pip_sort (1024 threads): sum_i b_i and the first failures (in the
 // reference's order) over the batch's votes; -sum b_i recoded into reg.bb for the comb in
 // k_pip_windows' extra block (off the Horner's critical path).
@@ -1015,15 +1001,17 @@ __device__ __forceinline__ void bsum_merge(sc& a, uint32_t f[4], int o) {
   f[2] = min(f[2], g2);
 }
 
+template <int NT>
 __device__ __forceinline__ void pip_bsum_block(const pip_region& reg, uint64_t n,
                                                const bv_item* __restrict__ its,
                                                uint32_t (*s_b)[8], uint32_t (*s_f)[4]) {
+  constexpr int NW = NT / 64;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   sc bsum;
 #pragma unroll
   for (int j = 0; j < 8; ++j) bsum.w[j] = 0;
   uint32_t f[4] = {kNone, kNone, kNone, 0};
-  for (uint64_t t = tid; t < n; t += 1024) {
+  for (uint64_t t = tid; t < n; t += NT) {
     const uint32_t fl = its[t].flags | its[t].pad | its[t].z[0];   // scalar, R and A lanes
     if ((fl & (BF_S_HIGH | BF_A_DECODE)) && f[0] == kNone) { f[0] = (uint32_t)t; f[3] = fl; }
     if ((fl & BF_S_NONCANON) && f[1] == kNone) f[1] = (uint32_t)t;
@@ -1044,11 +1032,11 @@ __device__ __forceinline__ void pip_bsum_block(const pip_region& reg, uint64_t n
   __syncthreads();
   if (wv != 0) return;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) bsum.w[j] = lane < 16 ? s_b[lane][j] : 0u;
+  for (int j = 0; j < 8; ++j) bsum.w[j] = lane < NW ? s_b[lane][j] : 0u;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) f[j] = lane < 16 ? s_f[lane][j] : (j < 3 ? kNone : 0u);
+  for (int j = 0; j < 4; ++j) f[j] = lane < NW ? s_f[lane][j] : (j < 3 ? kNone : 0u);
 #pragma unroll 1
-  for (int o = 8; o > 0; o >>= 1) bsum_merge(bsum, f, o);
+  for (int o = NW / 2; o > 0; o >>= 1) bsum_merge(bsum, f, o);
   if (lane != 0) return;
 #pragma unroll
   for (int j = 0; j < 4; ++j) reg.hdr[j] = f[j];
@@ -1060,32 +1048,52 @@ __device__ __forceinline__ void pip_bsum_block(const pip_region& reg, uint64_t n
   for (int j = 0; j < 8; ++j) reg.bb[j] = bb[j];
 }
 
-// grid (kPipWin, npip), 1024 threads: histogram of the window's digits in LDS, scan, then
-// scatter with LDS cursors into the window's entry range (capacity 2n).
-__global__ __launch_bounds__(1024) void k_pip_sort(const uint32_t* __restrict__ pip_list,
-                                                   const uint64_t* __restrict__ offsets,
-                                                   uint64_t b0, uint64_t i0, uint32_t extra,
-                                                   uint32_t pmin, ge_cached* __restrict__ tabs,
-                                                   const bv_item* __restrict__ items,
-                                                   uint32_t wbase) {
-  constexpr int NL = 128 + kPipCarryBins;
-  __shared__ uint32_t s_h[NL], s_c[NL];
-  __shared__ uint32_t s_b[16][8];
-  __shared__ uint32_t s_f[16][4];
-  const uint64_t bidx = b0 + pip_list[blockIdx.y];
-  const uint64_t bs = offsets[bidx], n0 = offsets[bidx + 1] - bs;
-  if (n0 < pmin) return;
-  const uint64_t n = n0 + extra;   // votes + (group mode) key sums
-  const pip_region reg = pip_at(tabs, bs - i0, n);
-  const int w = (int)(blockIdx.x + wbase), tid = threadIdx.x;
-  if (w == kPipWin) {     // the batch's b sum and first failures
-    pip_bsum_block(reg, n0, items + (bs - i0), s_b, s_f);
-    return;
+// The nonzero digits of every vote t < n in window w (c_i and, for w <= 16, z_i) as
+// f(local bin, point index, negative), on a workgroup of NT threads; local bins 0..127 are
+// buckets w * 128 + j, and in window 16 local bins 128..191 are the z-carry sub-bins. The
+// digit bytes of 8 votes are loaded before their callbacks (the LDS atomics would otherwise
+// wait out each load's latency in turn).
+template <int NT, typename F>
+__device__ __forceinline__ void pip_digits_pass(const pip_region& reg, uint64_t n, int w, F&& f) {
+  constexpr int U = 8;
+  for (uint64_t t0 = threadIdx.x; t0 < n; t0 += (uint64_t)NT * U) {
+    int dc[U], dz[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t t = t0 + (uint64_t)u * NT;
+      dc[u] = t < n ? (int)reg.cd[w * n + t] - 128 : 0;
+      dz[u] = (w < kPipZWin && t < n) ? (int)reg.zd[w * n + t] - 128 : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t t = t0 + (uint64_t)u * NT;
+      if (dc[u] != 0) {
+        const uint32_t ad = (uint32_t)(dc[u] < 0 ? -dc[u] : dc[u]);
+        const uint32_t lb = w == kPipWin - 1 ? (uint32_t)(kPipTopStride * (t % kPipTopSub)) + ad - 1
+                                             : ad - 1;
+        f(lb, (uint32_t)(2 * t), dc[u] < 0);
+      }
+      if (dz[u] != 0) {
+        const uint32_t ad = (uint32_t)(dz[u] < 0 ? -dz[u] : dz[u]);
+        const uint32_t lb = w == kPipZWin - 1 ? (uint32_t)(128 + (t % kPipCarryBins)) : ad - 1;
+        f(lb, (uint32_t)(2 * t + 1), dz[u] < 0);
+      }
+    }
   }
+}
+
+// Window w's counting sort on one workgroup of NT threads: histogram of the window's digits
+// in LDS, scan, then scatter with LDS cursors into the window's entry range (capacity 2n).
+constexpr int kPipSortBins = 128 + kPipCarryBins;
+template <int NT>
+__device__ __forceinline__ void pip_sort_window(const pip_region& reg, uint64_t n, int w,
+                                                uint32_t* s_h, uint32_t* s_c) {
+  constexpr int NL = kPipSortBins;
+  static_assert(NT >= NL, "one thread per local bin");
+  const int tid = threadIdx.x;
   if (tid < NL) s_h[tid] = 0;
   __syncthreads();
-  for (uint64_t t = tid; t < n; t += 1024)
-    pip_window_digits(reg, n, t, w, [&](uint32_t lb, uint32_t, bool) { atomicAdd(&s_h[lb], 1u); });
+  pip_digits_pass<NT>(reg, n, w, [&](uint32_t lb, uint32_t, bool) { atomicAdd(&s_h[lb], 1u); });
   __syncthreads();
   // inclusive Hillis-Steele scan over the NL local bins (threads < NL)
   uint32_t v = tid < NL ? s_h[tid] : 0u;
@@ -1110,11 +1118,34 @@ __global__ __launch_bounds__(1024) void k_pip_sort(const uint32_t* __restrict__ 
   __syncthreads();
   if (tid < NL) s_c[tid] -= v;   // exclusive: cursors
   __syncthreads();
-  for (uint64_t t = tid; t < n; t += 1024)
-    pip_window_digits(reg, n, t, w, [&](uint32_t lb, uint32_t pt, bool neg) {
-      const uint32_t pos = atomicAdd(&s_c[lb], 1u);
-      reg.ent[base + pos] = pt | (neg ? 0x80000000u : 0u);
-    });
+  pip_digits_pass<NT>(reg, n, w, [&](uint32_t lb, uint32_t pt, bool neg) {
+    const uint32_t pos = atomicAdd(&s_c[lb], 1u);
+    reg.ent[base + pos] = pt | (neg ? 0x80000000u : 0u);
+  });
+}
+
+// grid (kPipWin, npip), 1024 threads: window blockIdx.x + wbase's sort; window kPipWin is the
+// batch's b sum and first failures.
+__global__ __launch_bounds__(1024) void k_pip_sort(const uint32_t* __restrict__ pip_list,
+                                                   const uint64_t* __restrict__ offsets,
+                                                   uint64_t b0, uint64_t i0, uint32_t extra,
+                                                   uint32_t pmin, ge_cached* __restrict__ tabs,
+                                                   const bv_item* __restrict__ items,
+                                                   uint32_t wbase) {
+  __shared__ uint32_t s_h[kPipSortBins], s_c[kPipSortBins];
+  __shared__ uint32_t s_b[16][8];
+  __shared__ uint32_t s_f[16][4];
+  const uint64_t bidx = b0 + pip_list[blockIdx.y];
+  const uint64_t bs = offsets[bidx], n0 = offsets[bidx + 1] - bs;
+  if (n0 < pmin) return;
+  const uint64_t n = n0 + extra;   // votes + (group mode) key sums
+  const pip_region reg = pip_at(tabs, bs - i0, n);
+  const int w = (int)(blockIdx.x + wbase);
+  if (w == kPipWin) {     // the batch's b sum and first failures
+    pip_bsum_block<1024>(reg, n0, items + (bs - i0), s_b, s_f);
+    return;
+  }
+  pip_sort_window<1024>(reg, n, w, s_h, s_c);
 }
 
 // Lanes [G bin, G bin + G) of the batch's bucket pass share bucket bin (gl: the lane's index
@@ -1536,8 +1567,9 @@ constexpr int kFuseTopParts = 10;                 // window 31: lists j <= 4, on
 constexpr uint32_t kFuseCtr = 4 * 33 + 4;        // counter words (zeroed by k_iota)
 constexpr uint64_t kFuseSpinTicks = 200000000;   // 2 s
 constexpr uint32_t kFuseLds = 96 * 1024;         // > 160 KiB / 2: one workgroup per CU
-enum : uint32_t { kFzTicket = 0, kFzError = 1, kFzBuckets = 4, kFzParts = 4 + 33,
-                  kFzWsum = 4 + 66 };
+enum : uint32_t { kFzTicket = 0, kFzError = 1, kFzTicket2 = 2, kFzBuckets = 4, kFzParts = 4 + 33,
+                  kFzWsum = 4 + 66, kFzRole0 = 4 + 99, kFzPoints = 4 + 100 };
+static_assert(kFzPoints < kFuseCtr, "counters zeroed by k_iota");
 constexpr size_t kFusePartBytes = 4ull * (kPipWin + 1) * kPipWinLpParts * 64;
 // the parts live in the batch's digit arrays (cd, zd: dead after k_pip_sort)
 constexpr uint64_t kFuseMinN = (kFusePartBytes + 51) / 52;
@@ -1555,6 +1587,45 @@ bool pip_fuse_on() {   // NW_PIP_FUSE=0: the tail as four launches (A/B hook)
 // k_pip_tail_fused; each launch first prints the previous launch's timeline (that call has
 // returned): per role the first start and last end, W_31's arrival at the Horner, the
 // Horner's W_15 and end, in us from the launch's first workgroup start.
+// The same for k_pip_points_sorted: decompression and digit waves' last ends, the sorts'
+// start (digits ready) and last end, in us from the launch's first workgroup start.
+uint64_t* head_stamps(uint32_t nblk) {
+  static const bool on = env_u64_zero("NW_PIP_FUSE_STAMPS", 0) != 0;
+  static uint64_t* buf = nullptr;
+  static uint32_t prev = 0;
+  if (!on) return nullptr;
+  if (buf && prev) {
+    uint64_t t0 = ~0ull;
+    for (uint32_t i = 0; i < prev; ++i) t0 = std::min(t0, buf[4 * i]);
+    double dec = 0, dig = 0, s0 = 1e30, s1 = 0;
+    for (uint32_t i = 0; i < prev; ++i) {
+      const uint64_t* s = buf + 4 * i;
+      const uint32_t role = (uint32_t)(s[2] >> 8);
+      if (role == 6) {
+        if (s[1]) dec = std::max(dec, (s[1] - t0) / 100.0);
+        if (s[3]) dig = std::max(dig, (s[3] - t0) / 100.0);
+      } else if (role == 7) {
+        s0 = std::min(s0, (s[3] - t0) / 100.0);
+        s1 = std::max(s1, (s[1] - t0) / 100.0);
+      }
+    }
+    fprintf(stderr, "[head] digits done %.1f decompressions done %.1f sorts %.1f-%.1f\n", dig,
+            dec, s0, s1);
+  }
+  if (!buf || nblk > prev) {
+    if (buf) (void)hipHostFree(buf);
+    buf = nullptr;
+    if (hipHostMalloc(reinterpret_cast<void**>(&buf), 32ull * nblk,
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return nullptr;
+  }
+  memset(buf, 0, 32ull * nblk);
+  prev = nblk;
+  void* dp = nullptr;
+  return hipHostGetDevicePointer(&dp, buf, 0) == hipSuccess ? static_cast<uint64_t*>(dp)
+                                                            : nullptr;
+}
+
 uint64_t* fuse_stamps(uint32_t nblk) {
   static const bool on = env_u64_zero("NW_PIP_FUSE_STAMPS", 0) != 0;
   static uint64_t* buf = nullptr;
@@ -1630,7 +1701,9 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
                                                         uint32_t* __restrict__ ctr,
                                                         int32_t* __restrict__ status,
                                                         uint64_t* __restrict__ fail_index,
-                                                        uint64_t* __restrict__ stamps) {
+                                                        uint64_t* __restrict__ stamps,
+                                                        const bv_item* __restrict__ items,
+                                                        int bsum_here) {
   __shared__ uint32_t s_ticket, s_ok;
   __shared__ uint32_t s_other[3][64];
   __shared__ uint32_t s_tmp[40];
@@ -1665,7 +1738,14 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
     }
     return;
   }
-  if (t == nbk) {   // ---- [-sum b_i]B
+  if (t == nbk) {   // ---- (fused head: sum b_i and the first failures, then) [-sum b_i]B
+    if (bsum_here) {
+      __shared__ uint32_t s_b[4][8];
+      __shared__ uint32_t s_f[4][4];
+      pip_bsum_block<256>(reg, n, items + (bs - i0), s_b, s_f);
+      __syncthreads();
+      fz_acquire();   // lane 0 of wave 0 wrote hdr / bb
+    }
     if (wave == 0) {
       pip_lp_bsum_point(reg, L, d2l);
       if (lane == 0) fz_add(ctr + kFzWsum + kPipWin, 1u);
@@ -1993,6 +2073,63 @@ hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, ge_niels_pad* 
 
 namespace {
 
+// ---- config 1's one-call head: the points and the window sorts in ONE launch ------------
+// The sorts read only the digits (role-0 lanes: hash, scalars, recoding), which are done
+// long before the R / A decompressions (the 252-squaring chains); here each window's sort
+// starts when every role-0 wave has counted itself, beside the decompressions, instead of
+// after the whole points kernel (one 10k batch: ~24 us off the chain). Roles by ticket:
+// [0, npb) the points kernel's workgroups (lanes as k_pip_points, three roles; each wave
+// counts itself, role-0 waves also on kFzRole0), then windows 0..31's sorts. The b sum and
+// first failures (k_pip_sort's extra block) move to k_pip_tail_fused's [-sum b_i]B
+// workgroup: they are needed only at the Horner's end. 256 threads, kFuseLds of LDS: one
+// workgroup per CU (waits are only on smaller tickets).
+__global__ __launch_bounds__(256) void k_pip_points_sorted(
+    const uint32_t* __restrict__ digests, const uint64_t* __restrict__ offsets, uint64_t bidx,
+    uint64_t i0, uint64_t i1, const uint32_t* __restrict__ pks,
+    const uint32_t* __restrict__ sigs, const uint32_t* __restrict__ z16, z_key_t zkey,
+    bv_item* __restrict__ items, ge_cached* __restrict__ tabs, uint32_t npb, uint32_t wv,
+    uint32_t* __restrict__ ctr, uint64_t* __restrict__ stamps) {
+  __shared__ uint32_t s_ticket, s_ok;
+  __shared__ uint32_t s_h[kPipSortBins], s_c[kPipSortBins];
+  const int tid = (int)threadIdx.x;
+  if (tid == 0)
+    s_ticket = __hip_atomic_fetch_add(ctr + kFzTicket2, 1u, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const uint32_t t = s_ticket;
+  const auto stamp = [&](int slot, uint64_t v) {   // NW_PIP_FUSE_STAMPS (diagnostic)
+    if (stamps && (tid & 63) == 0) stamps[4 * t + slot] = v;
+  };
+  stamp(0, __builtin_amdgcn_s_memrealtime());
+  if (t < npb) {
+    const uint64_t g = (uint64_t)t * 256 + (uint64_t)tid;
+    const pip_group_t nogrp{};
+    pip_point_lane(g, digests, offsets, bidx, bidx + 1, i0, i1, 0, pks, sigs, z16, zkey, items,
+                   tabs, nogrp, 3u, 0u);
+    const uint64_t wave = g >> 6;
+    if ((tid & 63) == 0 && wave < 3ull * wv) {   // the wave's stores, then its count
+      if (wave % 3 == 0) fz_add(ctr + kFzRole0, 1u);
+      fz_add(ctr + kFzPoints, 1u);
+      // per wave role: slot 1 = end of a decompression wave, slot 3 = end of a role-0 wave
+      stamp(wave % 3 == 0 ? 3 : 1, __builtin_amdgcn_s_memrealtime());
+      stamp(2, 0x600u);
+    }
+    return;
+  }
+  const int w = (int)(t - npb);   // window
+  if (tid == 0) s_ok = fz_wait(ctr, kFzRole0, wv) ? 1u : 0u;
+  __syncthreads();
+  if (!s_ok) return;   // kFzError is set: the tail reports NW_E_DEVICE
+  fz_acquire();
+  stamp(3, __builtin_amdgcn_s_memrealtime());
+  const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
+  pip_sort_window<256>(pip_at(tabs, bs - i0, n), n, w, s_h, s_c);
+  if (tid == 0) {
+    stamp(1, __builtin_amdgcn_s_memrealtime());
+    stamp(2, 0x700u | (uint32_t)w);
+  }
+}
+
 // The Pippenger kernels over the pip_list batches of one slice (plain batches or, with
 // grp.cert_vote_offsets set, certificate groups).
 hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t b, uint64_t e,
@@ -2004,6 +2141,11 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
   const uint32_t extra = group ? grp.nkeys : 0;   // key sums
   const uint32_t roles = group ? 2 : 3;
   const uint64_t wv = (i1 - i0 + 63) / 64;   // waves per role
+  // one large batch alone in its slice (config 1's call): the fused head and tail
+  const bool fused = pip_fuse_on() && !group && npip == 1 && e - b == 1 && pmax >= kFuseMinN &&
+                     npip <= pip_win_lp_max();
+  static const bool head_on = env_u64_zero("NW_PIP_FUSE_HEAD", 1) != 0;   // A/B hook
+  const bool fuse_head = fused && head_on && !(fk && fk->s2);
   if (fk && fk->s2 && !group) {
     // Forked (config 1's one call): the digit lanes (role 0: hash, scalars, digits) and the
     // window sorts, which read only digits, run on `stream` while the R / A decompressions
@@ -2030,6 +2172,13 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
     fe = hipEventRecord(fk->b, fk->s2);
     if (fe == hipSuccess) fe = hipStreamWaitEvent(stream, fk->b, 0);
     if (fe != hipSuccess) return fe;
+  } else if (fuse_head) {
+    // one large batch alone (config 1's call): points and sorts in one launch
+    const uint32_t npb = (uint32_t)((wv * 3 * 64 + 255) / 256);
+    static const uint32_t lds = (uint32_t)env_u64_zero("NW_PIP_FUSE_LDS", kFuseLds);
+    hipLaunchKernelGGL(k_pip_points_sorted, dim3(npb + kPipWin), dim3(256), lds, stream,
+                       digests, offsets, b, i0, i1, pks, sigs, z16, zkey, w.items, w.tabs, npb,
+                       (uint32_t)wv, w.chunk_start, head_stamps(npb + kPipWin));
   } else {
     hipLaunchKernelGGL(k_pip_points, dim3((unsigned)((wv * roles * 64 + 255) / 256)), dim3(256),
                        0, stream, digests, offsets, b, e, i0, i1, pmin, pks, sigs, z16, zkey,
@@ -2053,13 +2202,13 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
   const uint32_t bpb = ((kPipBins << lg) + 255) / 256;
   // One large batch alone in its slice (config 1's call): the fused tail (NW_PIP_FUSE=0: the
   // four kernels below; k_iota zeroed the counters in w.chunk_start)
-  if (pip_fuse_on() && !group && npip == 1 && e - b == 1 && pmax >= kFuseMinN &&
-      npip <= pip_win_lp_max()) {
+  if (fused) {
     const uint32_t nbk = bpb;
     static const uint32_t lds = (uint32_t)env_u64_zero("NW_PIP_FUSE_LDS", kFuseLds);   // A/B
     const uint32_t nblk = nbk + 2 + kFuseTopParts + (kPipWin - 1) * kFuseParts;
     hipLaunchKernelGGL(k_pip_tail_fused, dim3(nblk), dim3(256), lds, stream, offsets, b, i0, lg,
-                       nbk, w.tabs, w.chunk_start, status, fail_index, fuse_stamps(nblk));
+                       nbk, w.tabs, w.chunk_start, status, fail_index, fuse_stamps(nblk), w.items,
+                       fuse_head ? 1 : 0);
     return hipGetLastError();
   }
   const int xcd = npip >= 8;
