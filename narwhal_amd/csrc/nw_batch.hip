@@ -798,15 +798,12 @@ __device__ __forceinline__ void ge_shfl(ge& r, const ge& p, int src) {
 // batches only: in group mode A is a committee key) = decompress A. Three short chains
 // instead of one lane doing the scalars and A's decompression in series (the one-call
 // latency of config 1 is this kernel's longest lane).
-__device__ __forceinline__ void pip_point_lane(
-    uint64_t g, const uint32_t* __restrict__ digests, const uint64_t* __restrict__ offsets,
-    uint64_t b0, uint64_t b1, uint64_t i0, uint64_t i1, uint32_t pmin,
-    const uint32_t* __restrict__ pks, const uint32_t* __restrict__ sigs,
+__device__ __forceinline__ void pip_point_do(
+    int which, uint64_t li, const uint32_t* __restrict__ digests,
+    const uint64_t* __restrict__ offsets, uint64_t b0, uint64_t b1, uint64_t i0, uint64_t i1,
+    uint32_t pmin, const uint32_t* __restrict__ pks, const uint32_t* __restrict__ sigs,
     const uint32_t* __restrict__ z16, const z_key_t& zkey, bv_item* __restrict__ items,
-    ge_cached* __restrict__ tabs, const pip_group_t& grp, uint32_t roles, uint32_t role0) {
-  const uint64_t wave = g >> 6;
-  const int which = (int)(role0 + wave % roles);
-  const uint64_t li = (wave / roles) * 64 + (g & 63);
+    ge_cached* __restrict__ tabs, const pip_group_t& grp) {
   const uint64_t gi = i0 + li;
   if (gi >= i1) return;
   const uint64_t lo = batch_of(offsets, b0, b1, gi);
@@ -928,8 +925,9 @@ __global__ __launch_bounds__(256, 3) void k_pip_points(
     const uint32_t* __restrict__ sigs, const uint32_t* __restrict__ z16, z_key_t zkey,
     bv_item* __restrict__ items, ge_cached* __restrict__ tabs, pip_group_t grp,
     uint32_t roles, uint32_t role0) {
-  pip_point_lane((uint64_t)blockIdx.x * blockDim.x + threadIdx.x, digests, offsets, b0, b1, i0,
-                 i1, pmin, pks, sigs, z16, zkey, items, tabs, grp, roles, role0);
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, wave = g >> 6;
+  pip_point_do((int)(role0 + wave % roles), (wave / roles) * 64 + (g & 63), digests, offsets, b0,
+               b1, i0, i1, pmin, pks, sigs, z16, zkey, items, tabs, grp);
 }
 
 // Group mode: per group, sum_i c_i per committee key (LDS, 64-bit limb sums), reduced mod l,
@@ -1121,6 +1119,61 @@ __device__ __forceinline__ void pip_sort_window(const pip_region& reg, uint64_t 
   pip_digits_pass<NT>(reg, n, w, [&](uint32_t lb, uint32_t pt, bool neg) {
     const uint32_t pos = atomicAdd(&s_c[lb], 1u);
     reg.ent[base + pos] = pt | (neg ? 0x80000000u : 0u);
+  });
+}
+
+// Part k of K of window w's sort on one workgroup of NT threads: the workgroup owns local
+// bins [lo, hi) (a 1/K slice of the window's 128 bins, or 192 with window 16's z-carry
+// sub-bins), reads every digit of the window, histograms and scatters only its own bins, and
+// places them after the window's entries in lower bins, which it counts itself (no workgroup
+// waits for another). The K parts of a window write disjoint bins and entry ranges.
+template <int NT>
+__device__ __forceinline__ void pip_sort_window_part(const pip_region& reg, uint64_t n, int w,
+                                                     int k, int K, uint32_t* s_h,
+                                                     uint32_t* s_c, uint32_t* s_red) {
+  const int tid = threadIdx.x;
+  const int nl = w == kPipZWin - 1 ? kPipSortBins : 128;
+  const uint32_t lo = (uint32_t)(k * nl / K), hi = (uint32_t)((k + 1) * nl / K), m = hi - lo;
+  if (tid < (int)m) s_h[tid] = 0;
+  __syncthreads();
+  uint32_t below = 0;
+  pip_digits_pass<NT>(reg, n, w, [&](uint32_t lb, uint32_t, bool) {
+    if (lb >= lo && lb < hi) atomicAdd(&s_h[lb - lo], 1u);
+    else if (lb < lo) ++below;
+  });
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) below += (uint32_t)__shfl_xor((int)below, o);
+  if ((tid & 63) == 0) s_red[tid >> 6] = below;
+  __syncthreads();
+  uint32_t base_below = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) base_below += s_red[i];
+  // inclusive Hillis-Steele scan over the m bins (threads < m)
+  uint32_t v = tid < (int)m ? s_h[tid] : 0u;
+  if (tid < (int)m) s_c[tid] = v;
+  __syncthreads();
+  for (uint32_t d = 1; d < m; d <<= 1) {
+    const uint32_t x = (tid < (int)m && (uint32_t)tid >= d) ? s_c[tid - d] : 0u;
+    __syncthreads();
+    if (tid < (int)m) s_c[tid] += x;
+    __syncthreads();
+  }
+  const uint32_t base = (uint32_t)(2 * n * (uint64_t)w) + base_below;
+  if (tid < (int)m) {
+    const uint32_t lb = lo + (uint32_t)tid;
+    const uint32_t ex = s_c[tid] - v;
+    const uint32_t bin = lb >= 128 ? (uint32_t)(kPipWin * 128 + lb - 128) : (uint32_t)(w * 128) + lb;
+    reg.off[bin] = base + ex;
+    reg.cnt[bin] = v;
+  }
+  __syncthreads();
+  if (tid < (int)m) s_c[tid] -= v;   // exclusive: cursors
+  __syncthreads();
+  pip_digits_pass<NT>(reg, n, w, [&](uint32_t lb, uint32_t pt, bool neg) {
+    if (lb >= lo && lb < hi) {
+      const uint32_t pos = atomicAdd(&s_c[lb - lo], 1u);
+      reg.ent[base + pos] = pt | (neg ? 0x80000000u : 0u);
+    }
   });
 }
 
@@ -2078,8 +2131,12 @@ namespace {
 // long before the R / A decompressions (the 252-squaring chains); here each window's sort
 // starts when every role-0 wave has counted itself, beside the decompressions, instead of
 // after the whole points kernel (one 10k batch: ~24 us off the chain). Roles by ticket:
-// [0, npb) the points kernel's workgroups (lanes as k_pip_points, three roles; each wave
-// counts itself, role-0 waves also on kFzRole0), then windows 0..31's sorts. The b sum and
+// [0, nb0) digit workgroups (role 0: hash, scalars, recoding; 4 waves of 64 votes each,
+// counted once per workgroup on kFzRole0), [nb0, npb) decompression workgroups (waves
+// alternate R, A), then K workgroups per window's sort (each its own slice of the window's
+// bins, NW_PIP_SORT_SPLIT, 2: with one release per wave K = 1 / 2 / 4 / 8 measured
+// 0.330-0.336 / 0.334-0.335 / 0.336-0.339 / 0.365-0.369 ms, profiles/r04g/sort_split_ab.txt;
+// with grouped digit workgroups 0.318-0.320 for K = 1, 2 and 4, head_ab.txt). The b sum and
 // first failures (k_pip_sort's extra block) move to k_pip_tail_fused's [-sum b_i]B
 // workgroup: they are needed only at the Horner's end. 256 threads, kFuseLds of LDS: one
 // workgroup per CU (waits are only on smaller tickets).
@@ -2088,7 +2145,7 @@ __global__ __launch_bounds__(256) void k_pip_points_sorted(
     uint64_t i0, uint64_t i1, const uint32_t* __restrict__ pks,
     const uint32_t* __restrict__ sigs, const uint32_t* __restrict__ z16, z_key_t zkey,
     bv_item* __restrict__ items, ge_cached* __restrict__ tabs, uint32_t npb, uint32_t wv,
-    uint32_t* __restrict__ ctr, uint64_t* __restrict__ stamps) {
+    uint32_t ksort, uint32_t* __restrict__ ctr, uint64_t* __restrict__ stamps) {
   __shared__ uint32_t s_ticket, s_ok;
   __shared__ uint32_t s_h[kPipSortBins], s_c[kPipSortBins];
   const int tid = (int)threadIdx.x;
@@ -2101,29 +2158,37 @@ __global__ __launch_bounds__(256) void k_pip_points_sorted(
     if (stamps && (tid & 63) == 0) stamps[4 * t + slot] = v;
   };
   stamp(0, __builtin_amdgcn_s_memrealtime());
+  const uint32_t nb0 = (wv + 3) / 4;   // role-0 workgroups (4 digit waves each)
   if (t < npb) {
-    const uint64_t g = (uint64_t)t * 256 + (uint64_t)tid;
     const pip_group_t nogrp{};
-    pip_point_lane(g, digests, offsets, bidx, bidx + 1, i0, i1, 0, pks, sigs, z16, zkey, items,
-                   tabs, nogrp, 3u, 0u);
-    const uint64_t wave = g >> 6;
-    if ((tid & 63) == 0 && wave < 3ull * wv) {   // the wave's stores, then its count
-      if (wave % 3 == 0) fz_add(ctr + kFzRole0, 1u);
-      fz_add(ctr + kFzPoints, 1u);
-      // per wave role: slot 1 = end of a decompression wave, slot 3 = end of a role-0 wave
-      stamp(wave % 3 == 0 ? 3 : 1, __builtin_amdgcn_s_memrealtime());
-      stamp(2, 0x600u);
+    const uint64_t wi = (uint64_t)(t < nb0 ? t : t - nb0) * 4 + (uint64_t)(tid >> 6);
+    const int which = t < nb0 ? 0 : 1 + (int)(wi & 1);
+    const uint64_t grp64 = t < nb0 ? wi : wi >> 1;   // 64-vote group of the wave
+    if (grp64 < wv)
+      pip_point_do(which, grp64 * 64 + (uint64_t)(tid & 63), digests, offsets, bidx, bidx + 1,
+                   i0, i1, 0, pks, sigs, z16, zkey, items, tabs, nogrp);
+    if (t < nb0) {
+      // the workgroup's digits, then ONE count (a release per wave is an L2 write-back
+      // each: 628 of them slowed the decompressions 73 -> 114 us); the decompressions signal
+      // nothing, the launch boundary publishes their points
+      __syncthreads();
+      if (tid == 0) fz_add(ctr + kFzRole0, 1u);
+      stamp(3, __builtin_amdgcn_s_memrealtime());
+    } else {
+      stamp(1, __builtin_amdgcn_s_memrealtime());
     }
+    stamp(2, 0x600u);
     return;
   }
-  const int w = (int)(t - npb);   // window
-  if (tid == 0) s_ok = fz_wait(ctr, kFzRole0, wv) ? 1u : 0u;
+  const int w = (int)((t - npb) / ksort), k = (int)((t - npb) % ksort);   // window, part
+  if (tid == 0) s_ok = fz_wait(ctr, kFzRole0, nb0) ? 1u : 0u;
   __syncthreads();
   if (!s_ok) return;   // kFzError is set: the tail reports NW_E_DEVICE
   fz_acquire();
   stamp(3, __builtin_amdgcn_s_memrealtime());
   const uint64_t bs = offsets[bidx], n = offsets[bidx + 1] - bs;
-  pip_sort_window<256>(pip_at(tabs, bs - i0, n), n, w, s_h, s_c);
+  __shared__ uint32_t s_red[4];
+  pip_sort_window_part<256>(pip_at(tabs, bs - i0, n), n, w, k, (int)ksort, s_h, s_c, s_red);
   if (tid == 0) {
     stamp(1, __builtin_amdgcn_s_memrealtime());
     stamp(2, 0x700u | (uint32_t)w);
@@ -2174,11 +2239,14 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
     if (fe != hipSuccess) return fe;
   } else if (fuse_head) {
     // one large batch alone (config 1's call): points and sorts in one launch
-    const uint32_t npb = (uint32_t)((wv * 3 * 64 + 255) / 256);
+    const uint32_t npb = (uint32_t)((wv + 3) / 4 + (2 * wv + 3) / 4);   // digit + point WGs
     static const uint32_t lds = (uint32_t)env_u64_zero("NW_PIP_FUSE_LDS", kFuseLds);
-    hipLaunchKernelGGL(k_pip_points_sorted, dim3(npb + kPipWin), dim3(256), lds, stream,
+    // K workgroups per window's sort (each its own slice of the bins): NW_PIP_SORT_SPLIT
+    static const uint32_t ks =
+        (uint32_t)std::min<uint64_t>(8, std::max<uint64_t>(1, env_u64("NW_PIP_SORT_SPLIT", 2)));
+    hipLaunchKernelGGL(k_pip_points_sorted, dim3(npb + kPipWin * ks), dim3(256), lds, stream,
                        digests, offsets, b, i0, i1, pks, sigs, z16, zkey, w.items, w.tabs, npb,
-                       (uint32_t)wv, w.chunk_start, head_stamps(npb + kPipWin));
+                       (uint32_t)wv, ks, w.chunk_start, head_stamps(npb + kPipWin * ks));
   } else {
     hipLaunchKernelGGL(k_pip_points, dim3((unsigned)((wv * roles * 64 + 255) / 256)), dim3(256),
                        0, stream, digests, offsets, b, e, i0, i1, pmin, pks, sigs, z16, zkey,

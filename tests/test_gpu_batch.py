@@ -201,3 +201,43 @@ def test_pippenger_one_call_fused_tail(n, cls, skew):
     if ost:
         assert got[1] == oidx
     assert (ost == 0) == (cls is None)
+
+
+def test_pippenger_one_call_fused_concurrent():
+    """Four threads, each verifying its own lone large batch at once (four fused launches
+    side by side on their jobs' streams, each ordered by its own counters): every verdict and
+    first failing index == the oracle's."""
+    import threading
+    rng = np.random.Generator(np.random.PCG64(77))
+    cases = []
+    for k in range(4):
+        n = 4000 + 1500 * k
+        dig, pk, sigs, off, z16 = _corpus_sizes(np.array([n]), rng, every=0)
+        if k % 2:
+            _mutate(sigs, pk, int(rng.integers(0, n)), int(rng.integers(0, 6)))
+        cases.append((dig, pk, sigs, z16, O.verify_batch(dig[0].tobytes(), pk, sigs, z16)))
+    got = [None] * len(cases)
+
+    def run(k):
+        dig, pk, sigs, z16, _ = cases[k]
+        votes = [(C.PublicKey(pk[i].tobytes()), C.Signature.from_bytes(sigs[i].tobytes()))
+                 for i in range(len(pk))]
+        out = []
+        for _ in range(5):
+            try:
+                C.Signature.verify_batch(C.Digest(dig[0].tobytes()), votes, z16=z16.tobytes())
+                out.append((0, None))
+            except C.CryptoError as err:
+                out.append((err.code, err.index))
+        got[k] = out
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(len(cases))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    for k, (_, _, _, _, (ost, oidx)) in enumerate(cases):
+        for code, idx in got[k]:
+            assert code == ost, (k, code, ost)
+            if ost:
+                assert idx == oidx, (k, idx, oidx)
