@@ -1698,8 +1698,21 @@ uint64_t* fuse_stamps(uint32_t nblk) {
       if (role == 4) wsum_end[s[2] & 63] = e;
       if (role == 5) w31 = (s[3] - t0) / 100.0, hend = e;
     }
-    for (uint32_t i = 0; i < prev; ++i)
-      if ((buf[4 * i + 2] >> 8) == 5) w15 = (buf[4 * i + 1] - t0) / 100.0;
+    double b31 = 0, b30 = 0, r31a = 1e30, r31b = 0, p31 = 0;
+    for (uint32_t i = 0; i < prev; ++i) {
+      const uint64_t* s = buf + 4 * i;
+      const uint32_t role = (uint32_t)(s[2] >> 8), wv = (uint32_t)(s[2] & 0xff);
+      if ((buf[4 * i + 2] >> 8) == 5) w15 = (s[1] - t0) / 100.0;
+      if (role == 1 && wv == 31) b31 = std::max(b31, (s[1] - t0) / 100.0);
+      if (role == 1 && wv == 30) b30 = std::max(b30, (s[1] - t0) / 100.0);
+      if (role == 3 && wv == 31) {
+        r31a = std::min(r31a, (s[3] - t0) / 100.0);
+        r31b = std::max(r31b, (s[3] - t0) / 100.0);
+        p31 = std::max(p31, (s[1] - t0) / 100.0);
+      }
+    }
+    fprintf(stderr, "[fuse31] w31 buckets done %.1f (w30 %.1f); w31 parts saw them %.1f-%.1f, "
+            "done %.1f\n", b31, b30, r31a, r31b, p31);
     fprintf(stderr,
             "[fuse] buckets %.1f-%.1f bsum %.1f-%.1f parts %.1f-%.1f wsum -%.1f horner %.1f-%.1f "
             "(W_31 at %.1f) | W ready: w31 %.1f w24 %.1f w16 %.1f w15 %.1f w8 %.1f w0 %.1f\n",

@@ -1,0 +1,7 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_batch.py > gpurun_out/r04al_tests.log 2>&1 || { tail -40 gpurun_out/r04al_tests.log; exit 1; }
+tail -1 gpurun_out/r04al_tests.log
+NW_PIP_FUSE_STAMPS=1 timeout -k 10 60 python -u tools/ab_batch_latency.py 30 > gpurun_out/r04al_stamps.txt 2>&1 || { tail -5 gpurun_out/r04al_stamps.txt; exit 1; }
+tail -7 gpurun_out/r04al_stamps.txt
+for i in 1 2 3; do timeout -k 10 60 python -u tools/ab_batch_latency.py 400 || exit 1; done
