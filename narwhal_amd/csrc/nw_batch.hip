@@ -1626,6 +1626,11 @@ static_assert(kFzPoints < kFuseCtr, "counters zeroed by k_iota");
 constexpr size_t kFusePartBytes = 4ull * (kPipWin + 1) * kPipWinLpParts * 64;
 // the parts live in the batch's digit arrays (cd, zd: dead after k_pip_sort)
 constexpr uint64_t kFuseMinN = (kFusePartBytes + 51) / 52;
+// ... and the fused launches are for latency: one round of one workgroup per CU. Above
+// 16,384 votes the head's digit + point + sort workgroups exceed 256 and the separate
+// kernels (3 waves per SIMD) take the batch.
+constexpr uint64_t kFuseMaxN = 16384;
+constexpr uint32_t kFuseMaxLg = 4;   // bucket lanes per bin in the fused tail (260 workgroups)
 
 // Polls are relaxed (an acquire per poll would invalidate the XCD's L2 under the bucket
 // lanes' gathers every few hundred cycles); the waiter takes ONE agent-scope acquire fence
@@ -2221,7 +2226,7 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
   const uint64_t wv = (i1 - i0 + 63) / 64;   // waves per role
   // one large batch alone in its slice (config 1's call): the fused head and tail
   const bool fused = pip_fuse_on() && !group && npip == 1 && e - b == 1 && pmax >= kFuseMinN &&
-                     npip <= pip_win_lp_max();
+                     pmax <= kFuseMaxN && npip <= pip_win_lp_max();
   static const bool head_on = env_u64_zero("NW_PIP_FUSE_HEAD", 1) != 0;   // A/B hook
   const bool fuse_head = fused && head_on && !(fk && fk->s2);
   if (fk && fk->s2 && !group) {
@@ -2280,6 +2285,7 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
   while (lg > 0 && ((npip * kPipBins) << lg) > (1ull << 21)) --lg;
   static const uint64_t lg_env = env_u64("NW_PIP_LG", 99);   // A/B hook
   if (lg_env <= 6) lg = (uint32_t)lg_env;
+  if (fused && lg > kFuseMaxLg) lg = kFuseMaxLg;
   const uint32_t bpb = ((kPipBins << lg) + 255) / 256;
   // One large batch alone in its slice (config 1's call): the fused tail (NW_PIP_FUSE=0: the
   // four kernels below; k_iota zeroed the counters in w.chunk_start)
@@ -2442,7 +2448,8 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
 
 bool verify_batch_outputs_direct(uint64_t nbatches, uint64_t nitems) {
   return nbatches == 1 && pip_fuse_on() && pip_win_lp_max() >= 1 &&
-         nitems >= std::max<uint64_t>(kFuseMinN, pip_min()) && nitems + 1 <= slice_units();
+         nitems >= std::max<uint64_t>(kFuseMinN, pip_min()) && nitems <= kFuseMaxN &&
+         nitems + 1 <= slice_units();
 }
 
 const ge* key_tables_base(const ge_niels_pad* tabs, uint64_t nkeys) {

@@ -177,12 +177,14 @@ def test_pippenger_config1_shape():
 
 @pytest.mark.parametrize("n,cls,skew", [(2925, None, False), (3000, 0, False), (4096, 3, True),
                                         (10000, 0, False), (10000, None, True), (10000, 5, False),
-                                        (16384, 2, False), (20000, 4, False)])
+                                        (12288, 4, False), (16384, 2, False), (16385, 1, False),
+                                        (20000, 4, False)])
 def test_pippenger_one_call_fused_tail(n, cls, skew):
-    """One batch alone in a call (config 1's shape, n >= 2925): the fused tail kernel
-    (k_pip_tail_fused: buckets, window parts and sums, Horner in one launch ordered by
-    completion counters). Status and first failing index == the oracle's, with injected z,
-    every failure class, and skewed z (all equal: every vote in the same buckets)."""
+    """One batch alone in a call (config 1's shape): 2,925 <= n <= 16,384 takes the fused
+    head and tail (k_pip_points_sorted, k_pip_tail_fused: launches ordered inside by
+    completion counters), larger n the separate kernels. Status and first failing index ==
+    the oracle's, with injected z, every failure class, and skewed z (all equal: every vote
+    in the same buckets)."""
     rng = np.random.Generator(np.random.PCG64(n + 7 * (cls or 0) + skew))
     dig, pk, sigs, off, z16 = _corpus_sizes(np.array([n]), rng, every=0)
     if skew:
