@@ -1640,6 +1640,10 @@ bool pip_fuse_on() {   // NW_PIP_FUSE=0: the tail as four launches (A/B hook)
   static const bool v = env_u64_zero("NW_PIP_FUSE", 1) != 0;
   return v;
 }
+bool pip_fuse_head_on() {   // NW_PIP_FUSE_HEAD=0: the points and sort kernels (A/B hook)
+  static const bool v = env_u64_zero("NW_PIP_FUSE_HEAD", 1) != 0;
+  return v;
+}
 
 // NW_PIP_FUSE_STAMPS=1 (diagnostic, one caller at a time): a host-mapped stamp buffer for
 // k_pip_tail_fused; each launch first prints the previous launch's timeline (that call has
@@ -2219,7 +2223,8 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
                 uint64_t i0, uint64_t i1, uint32_t pmin, uint64_t npip, uint64_t pmax,
                 const uint32_t* pks, const uint32_t* sigs, const uint32_t* z16,
                 const z_key_t& zkey, const bv_ws& w, int32_t* status, uint64_t* fail_index,
-                const pip_group_t& grp, hipStream_t stream, const batch_fork_t* fk) {
+                const pip_group_t& grp, hipStream_t stream, const batch_fork_t* fk,
+                uint32_t* fctr) {
   const bool group = grp.cert_vote_offsets != nullptr;
   const uint32_t extra = group ? grp.nkeys : 0;   // key sums
   const uint32_t roles = group ? 2 : 3;
@@ -2227,8 +2232,7 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
   // one large batch alone in its slice (config 1's call): the fused head and tail
   const bool fused = pip_fuse_on() && !group && npip == 1 && e - b == 1 && pmax >= kFuseMinN &&
                      pmax <= kFuseMaxN && npip <= pip_win_lp_max();
-  static const bool head_on = env_u64_zero("NW_PIP_FUSE_HEAD", 1) != 0;   // A/B hook
-  const bool fuse_head = fused && head_on && !(fk && fk->s2);
+  const bool fuse_head = fused && pip_fuse_head_on() && !(fk && fk->s2);
   if (fk && fk->s2 && !group) {
     // Forked (config 1's one call): the digit lanes (role 0: hash, scalars, digits) and the
     // window sorts, which read only digits, run on `stream` while the R / A decompressions
@@ -2264,7 +2268,7 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
         (uint32_t)std::min<uint64_t>(8, std::max<uint64_t>(1, env_u64("NW_PIP_SORT_SPLIT", 2)));
     hipLaunchKernelGGL(k_pip_points_sorted, dim3(npb + kPipWin * ks), dim3(256), lds, stream,
                        digests, offsets, b, i0, i1, pks, sigs, z16, zkey, w.items, w.tabs, npb,
-                       (uint32_t)wv, ks, w.chunk_start, head_stamps(npb + kPipWin * ks));
+                       (uint32_t)wv, ks, fctr, head_stamps(npb + kPipWin * ks));
   } else {
     hipLaunchKernelGGL(k_pip_points, dim3((unsigned)((wv * roles * 64 + 255) / 256)), dim3(256),
                        0, stream, digests, offsets, b, e, i0, i1, pmin, pks, sigs, z16, zkey,
@@ -2294,7 +2298,7 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
     static const uint32_t lds = (uint32_t)env_u64_zero("NW_PIP_FUSE_LDS", kFuseLds);   // A/B
     const uint32_t nblk = nbk + 2 + kFuseTopParts + (kPipWin - 1) * kFuseParts;
     hipLaunchKernelGGL(k_pip_tail_fused, dim3(nblk), dim3(256), lds, stream, offsets, b, i0, lg,
-                       nbk, w.tabs, w.chunk_start, status, fail_index, fuse_stamps(nblk), w.items,
+                       nbk, w.tabs, fctr, status, fail_index, fuse_stamps(nblk), w.items,
                        fuse_head ? 1 : 0);
     return hipGetLastError();
   }
@@ -2352,7 +2356,7 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                int32_t* status, uint64_t* fail_index, hipStream_t stream,
                                const key_tables_t* keys, const uint32_t* skip_group_ok,
                                uint64_t skip_per_group, double active_frac,
-                               const batch_fork_t* fork) {
+                               const batch_fork_t* fork, uint32_t* fuse_ctr) {
   const key_tables_t kt = keys ? *keys : key_tables_t{nullptr, nullptr, nullptr};
   const batch_skip_t sk{skip_group_ok, skip_per_group ? skip_per_group : 1};
   if (nbatches == 0) return hipSuccess;
@@ -2400,7 +2404,12 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
     }
     const uint64_t i0 = host_offsets[b], i1 = host_offsets[e];
     const unsigned nblk = (unsigned)((e - b + 1023) / 1024);
-    if (npip == e - b) {
+    // the caller's zeroed counters (fused path only, verify_batch_outputs_direct)
+    const bool own_ctr = fuse_ctr && !fork && nbatches == 1 && pip_fuse_head_on() &&
+                         verify_batch_outputs_direct(nbatches, nitems);
+    if (npip == e - b && own_ctr) {
+      // the fused head and tail read neither the Pippenger list nor zeroed workspace
+    } else if (npip == e - b) {
       // every batch of the slice takes the Pippenger path (config 1's one 10k batch): no
       // chunk plan, the Pippenger list is the slice's batches in order
       hipLaunchKernelGGL(k_iota, dim3((unsigned)((npip + 255) / 256)), dim3(256), 0, stream,
@@ -2428,7 +2437,8 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                          w.items, w.tabs, kt, sk);
     if (npip) {
       const hipError_t pe = launch_pip(digests, offsets, b, e, i0, i1, pmin, npip, pmax, pks,
-                                       sigs, z16, zkey, w, status, fail_index, nogrp, stream, fork);
+                                       sigs, z16, zkey, w, status, fail_index, nogrp, stream, fork,
+                                       own_ctr ? fuse_ctr : w.chunk_start);
       if (pe != hipSuccess) return pe;
     }
     if (chunks)
@@ -2445,6 +2455,8 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
   }
   return hipSuccess;
 }
+
+size_t verify_batch_fuse_ctr_bytes() { return 4ull * kFuseCtr; }
 
 bool verify_batch_outputs_direct(uint64_t nbatches, uint64_t nitems) {
   return nbatches == 1 && pip_fuse_on() && pip_win_lp_max() >= 1 &&
@@ -2586,7 +2598,7 @@ hipError_t launch_cert_groups(const uint32_t* cert_digest, const uint64_t* cvo,
     if (i1 > i0) {
       const hipError_t pe = launch_pip(cert_digest, gofs, g, e, i0, i1, pmin, e - g, pmax, pks,
                                        sigs, nullptr, zkey, w, nullptr, nullptr, grp, stream,
-                                       nullptr);
+                                       nullptr, w.chunk_start);
       if (pe != hipSuccess) return pe;
     }
     hipError_t err = hipGetLastError();

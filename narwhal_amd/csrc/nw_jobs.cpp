@@ -290,9 +290,13 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
     return 0;
   }
   const size_t m = nitems ? nitems : 1;
+  // a lone batch on the fused path: its launches' counters ship zeroed with the inputs
+  const bool direct = nw::verify_batch_outputs_direct(nbatches, nitems);
   const size_t o_d = 0, o_off = o_d + a256(32 * nbatches), o_pk = o_off + a256(8 * (nbatches + 1)),
                o_sig = o_pk + a256(32 * m), o_z = o_sig + a256(64 * m),
-               o_st = o_z + (z16 ? a256(16 * m) : 0), o_fi = o_st + a256(4 * nbatches),
+               o_ctr = o_z + (z16 ? a256(16 * m) : 0),
+               o_st = o_ctr + (direct ? a256(nw::verify_batch_fuse_ctr_bytes()) : 0),
+               o_fi = o_st + a256(4 * nbatches),
                o_ws = o_fi + a256(8 * nbatches),
                end = o_ws + a256(nw::batch_workspace_bytes(nbatches, nitems));
   rc = job_reserve(j, o_ws, end);
@@ -304,6 +308,7 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
     memcpy(j->hbuf + o_sig, sigs, 64 * nitems);
     if (z16) memcpy(j->hbuf + o_z, z16, 16 * nitems);
   }
+  if (direct) memset(j->hbuf + o_ctr, 0, nw::verify_batch_fuse_ctr_bytes());
   nw::z_key_t key;
   rc = fill_key(key);
   if (rc) return job_abort(j, rc);
@@ -320,9 +325,9 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
   const bool fork = fork_on && j->fork.s2;
   // a lone large batch (config 1's call): the verdict is written straight into the pinned
   // buffer by the one kernel that computes it, no copy back
-  const bool direct = !fork && nw::verify_batch_outputs_direct(nbatches, nitems);
-  char* const obuf = direct ? j->hdev : j->dbuf;
-  rc = job_run(j, o_st, o_st, direct ? 0 : o_ws - o_st, [&]() -> int {
+  const bool out_direct = direct && !fork;
+  char* const obuf = out_direct ? j->hdev : j->dbuf;
+  rc = job_run(j, o_st, o_st, out_direct ? 0 : o_ws - o_st, [&]() -> int {
     JOB_HIP(nw::launch_verify_batch(reinterpret_cast<const uint32_t*>(j->dbuf + o_d),
                                     reinterpret_cast<const uint64_t*>(j->dbuf + o_off), h_off,
                                     nbatches, reinterpret_cast<const uint32_t*>(j->dbuf + o_pk),
@@ -332,7 +337,9 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
                                     key, j->dbuf + o_ws,
                                     reinterpret_cast<int32_t*>(obuf + o_st),
                                     reinterpret_cast<uint64_t*>(obuf + o_fi), j->stream,
-                                    nullptr, nullptr, 0, 1.0, fork ? &fk : nullptr),
+                                    nullptr, nullptr, 0, 1.0, fork ? &fk : nullptr,
+                                    out_direct ? reinterpret_cast<uint32_t*>(j->dbuf + o_ctr)
+                                               : nullptr),
             "verify_batch launch");
     return 0;
   });
