@@ -1617,12 +1617,13 @@ __global__ __launch_bounds__(64) void k_pip_final(const uint32_t* __restrict__ p
 // expected; a guard against a wedged launch).
 constexpr int kFuseParts = kPipWinLpParts / 2;   // part workgroups per window (w < 31)
 constexpr int kFuseTopParts = 10;                 // window 31: lists j <= 4, one part each
-constexpr uint32_t kFuseCtr = 4 * 33 + 4;        // counter words (zeroed by k_iota)
+constexpr uint32_t kFuseCtr = 4 * 33 + 4;        // counter words (zeroed: the caller's
+                                                 // H2D, or k_iota in w.chunk_start)
 constexpr uint64_t kFuseSpinTicks = 200000000;   // 2 s
 constexpr uint32_t kFuseLds = 96 * 1024;         // > 160 KiB / 2: one workgroup per CU
 enum : uint32_t { kFzTicket = 0, kFzError = 1, kFzTicket2 = 2, kFzBuckets = 4, kFzParts = 4 + 33,
                   kFzWsum = 4 + 66, kFzRole0 = 4 + 99, kFzPoints = 4 + 100 };
-static_assert(kFzPoints < kFuseCtr, "counters zeroed by k_iota");
+static_assert(kFzPoints < kFuseCtr, "counters within the zeroed words");
 constexpr size_t kFusePartBytes = 4ull * (kPipWin + 1) * kPipWinLpParts * 64;
 // the parts live in the batch's digit arrays (cd, zd: dead after k_pip_sort)
 constexpr uint64_t kFuseMinN = (kFusePartBytes + 51) / 52;
@@ -2292,7 +2293,7 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
   if (fused && lg > kFuseMaxLg) lg = kFuseMaxLg;
   const uint32_t bpb = ((kPipBins << lg) + 255) / 256;
   // One large batch alone in its slice (config 1's call): the fused tail (NW_PIP_FUSE=0: the
-  // four kernels below; k_iota zeroed the counters in w.chunk_start)
+  // four kernels below; fctr: zeroed counters, the caller's or w.chunk_start by k_iota)
   if (fused) {
     const uint32_t nbk = bpb;
     static const uint32_t lds = (uint32_t)env_u64_zero("NW_PIP_FUSE_LDS", kFuseLds);   // A/B
