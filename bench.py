@@ -940,10 +940,11 @@ def run_worker_latency(args, rank, world):
     ub = [W.worker_batch(i, seed=11 + rank).tobytes() for i in range(uniq)]
     expect = [hashlib.sha512(b).digest()[:32] for b in ub]
 
-    async def load(rate: float, total: int, lookahead: int):
+    async def load(rate: float, total: int, lookahead: int, hash_on: str = "device"):
         svc = SV.VerificationService(max_delay=args.worker_delay)
         store, rx, tx = WK.Store(), asyncio.Queue(), asyncio.Queue()
-        task = WK.Processor.spawn(0, store, rx, tx, True, svc, max_in_flight=lookahead)
+        task = WK.Processor.spawn(0, store, rx, tx, True, svc, max_in_flight=lookahead,
+                                  hash_on=hash_on)
         loop = asyncio.get_running_loop()
         for i in range(4):                                   # warm: pool, first job
             await rx.put(ub[i])
@@ -971,8 +972,8 @@ def run_worker_latency(args, rank, world):
         await asyncio.gather(produce(), consume(), task)
         el = loop.time() - t_start
         a = np.array(lat) * 1e3
-        return {"offered_batches_per_s": rate, "batches": total, "lookahead": lookahead,
-                "achieved_batches_per_s": total / el,
+        return {"hash_on": hash_on, "offered_batches_per_s": rate, "batches": total,
+                "lookahead": lookahead, "achieved_batches_per_s": total / el,
                 "p50_ms": float(np.percentile(a, 50)), "p99_ms": float(np.percentile(a, 99)),
                 "max_ms": float(a.max()), "jobs": svc.jobs_submitted - jobs0,
                 "batches_per_job": total / max(1, svc.jobs_submitted - jobs0),
@@ -986,13 +987,19 @@ def run_worker_latency(args, rank, world):
         if x:
             r, la = x.split(":")
             plan.append((float(r), int(la)))
-    loads = [asyncio.run(load(r, max(20, int(min(args.worker_seconds,
-                                                   args.worker_max_batches / r) * r)), la))
-             for r, la in plan]
+    def count(r):
+        return max(20, int(min(args.worker_seconds, args.worker_max_batches / r) * r))
+    loads = [asyncio.run(load(r, count(r), la)) for r, la in plan]
+    # the shipped default (Processor hash_on="host", as processor.rs:38): one batch at a time
+    # on the event loop's thread
+    host = [asyncio.run(load(float(x), count(float(x)), 1, "host"))
+            for x in args.worker_host_rates.split(",") if x]
     res = {"batch_bytes": W.BATCH_BYTES, "max_delay_ms": args.worker_delay * 1e3, "loads": loads,
-           "path": "worker.Processor -> VerificationService.digest -> "
-                   "nw_submit_sha512_digest32_many (one lane per batch)",
-           "parity": "ok" if all(x["parity"] == "ok" for x in loads) else "FAIL"}
+           "host_loads": host,
+           "path": "worker.Processor(hash_on='device') -> VerificationService.digest -> "
+                   "nw_submit_sha512_digest32_many (one lane per batch); host_loads: the "
+                   "default hash_on='host' (hashlib on the loop thread)",
+           "parity": "ok" if all(x["parity"] == "ok" for x in loads + host) else "FAIL"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         one = []
         for i in range(100):
@@ -1121,17 +1128,85 @@ def summary(r: dict) -> dict:
         out["worker"] = {"offered_achieved_p50ms_p99ms": [
                              [int(x["offered_batches_per_s"]), int(x["achieved_batches_per_s"]),
                               rnd(x["p50_ms"], 2), rnd(x["p99_ms"], 2)] for x in wl["loads"]],
+                         "host_default": [
+                             [int(x["offered_batches_per_s"]), int(x["achieved_batches_per_s"]),
+                              rnd(x["p50_ms"], 3), rnd(x["p99_ms"], 3)]
+                             for x in wl.get("host_loads", [])],
                          "cpu_1thread_ms": rnd(g(wl, "cpu_sha2_equivalent", "one_thread_p50_ms"), 3),
                          "cpu16_batches_s": rnd(g(wl, "cpu_sha2_equivalent",
                                                   "threads16_batches_per_s"), 0)}
     if r.get("service_latency"):
-        out["service"] = {k: {"offered_achieved_p50ms_p99ms": [
+        out["service"] = {k: {"offered_achieved_p50_p90_p99_max_ms": [
                                   [int(x["offered_certs_per_s"]),
                                    int(x["achieved_certs_per_s"] or 0), rnd(x["p50_ms"], 2),
-                                   rnd(x["p99_ms"], 2)] for x in v["loads"]],
+                                   rnd(x.get("p90_ms"), 2), rnd(x["p99_ms"], 2),
+                                   rnd(x["max_ms"], 2)] for x in v["loads"]],
                               "cpu_1cert_ms": rnd(g(v, "cpu_oracle_one_thread", "p50_ms"), 2)}
                           for k, v in r["service_latency"].items()}
     return out
+
+
+# The driver parses bench.py's last stdout line; round 4's ~30 KB line was not parsed, so the
+# line is kept well below this and the per-leg detail goes to a side file.
+LINE_LIMIT = 16384
+LINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+             "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "parity")
+ROOFLINE_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_unit",
+                 "traffic_source", "algorithmic_bytes", "kernel", "kernel_ms", "work_per_unit",
+                 "peak_measured", "frac_measured", "issue_peak", "issue_frac")
+CPU_KEYS = ("value", "unit", "cores", "kind", "sample")
+
+
+def compact_line(result: dict, detail_path: str | None = None) -> dict:
+    """The one JSON object printed on stdout: the contract's keys, a trimmed roofline and
+    cpu_baseline, and the summary of every other leg; everything else lives in the detail
+    file. Optional parts are dropped (least important first) if the line would not fit."""
+    line = {k: result[k] for k in LINE_KEYS if k in result}
+    if isinstance(result.get("roofline"), dict):
+        line["roofline"] = {k: result["roofline"][k] for k in ROOFLINE_KEYS
+                            if k in result["roofline"]}
+    if isinstance(result.get("cpu_baseline"), dict):
+        line["cpu_baseline"] = {k: result["cpu_baseline"][k] for k in CPU_KEYS
+                                if k in result["cpu_baseline"]}
+    if "summary" in result:
+        line["summary"] = dict(result["summary"])
+    if detail_path:
+        line["detail"] = os.path.relpath(detail_path, ROOT)
+    for drop in ("worker", "service", "cert_alternating_worst_vs_all_valid",
+                 "cert_cpu_certs_s", "cert_stream_p32_Mcerts_s"):
+        if len(json.dumps(line, separators=(",", ":"))) < LINE_LIMIT // 2:
+            break
+        line.get("summary", {}).pop(drop, None)
+    return line
+
+
+def write_detail(result: dict) -> str | None:
+    """Every leg's full record (NW_BENCH_DETAIL, default gpurun_out/bench_detail.json)."""
+    path = os.environ.get("NW_BENCH_DETAIL", os.path.join(ROOT, "gpurun_out", "bench_detail.json"))
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(result, f)
+        return path
+    except OSError as e:
+        log(f"could not write {path}: {e}")
+        return None
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: start N ranks (one per GPU) as the driver's
+    torch.distributed.run command would, as a child process of this one (this process never
+    touches a GPU), and return its exit code. Rank 0's JSON line reaches stdout unchanged."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"launching {n} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd)
 
 
 def main():
@@ -1183,6 +1258,8 @@ def main():
     ap.add_argument("--worker-rates", default="50,500,5000")
     ap.add_argument("--worker-seconds", type=float, default=2.0)
     ap.add_argument("--worker-max-batches", type=float, default=2000)
+    ap.add_argument("--worker-host-rates", default="50,500,2000",
+                    help="offered rates of the default host-hashing Processor (empty = skip)")
     ap.add_argument("--worker-deep", default="10000:1024",
                     help="extra worker loads rate:lookahead (Processor max_in_flight)")
     ap.add_argument("--worker-delay", type=float, default=0.0005,
@@ -1190,6 +1267,14 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        log(f"--gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE')}: one rank per "
+            "GPU is the contract; refusing to report a mismatched n_gpus")
+        sys.exit(2)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -1436,7 +1521,9 @@ def main():
             result["cpu_baseline"] = cpu_baseline_sha(s["sample"], min(3.0, args.cpu_seconds))
     result["summary"] = summary(result)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        detail = write_detail(result)
+        log(f"full per-leg record: {detail}")
+        print(json.dumps(compact_line(result, detail), separators=(",", ":")), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -1,0 +1,91 @@
+"""bench.py's output contract (the driver left a ~30 KB line unparsed).
+
+CPU: the line assembly over a canned full result (round 4's round-end record) stays under
+the driver's size limit, parses, and carries the contract keys, a roofline and a
+cpu_baseline; `--gpus N` disagreeing with the launcher's WORLD_SIZE exits non-zero before
+any GPU work. GPU: `bench.py --gpus 2` with no launcher starts two ranks itself (gloo,
+sharing the box's one GPU) and reports n_gpus 2 with parity ok."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CANNED = os.path.join(ROOT, "profiles", "r04j", "bench_full.json")
+CONTRACT = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "parity")
+
+
+def _bench():
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench
+
+
+def _check_line(line):
+    text = json.dumps(line, separators=(",", ":"))
+    assert len(text) < 16384, len(text)
+    back = json.loads(text)
+    for k in CONTRACT:
+        assert k in back, k
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in back["roofline"], k
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in back["cpu_baseline"], k
+    return back
+
+
+def test_compact_line_from_round4_record():
+    B = _bench()
+    full = json.load(open(CANNED))
+    assert len(json.dumps(full)) > 16384          # the record the driver could not parse
+    full["summary"] = B.summary(full)
+    back = _check_line(B.compact_line(full, os.path.join(ROOT, "gpurun_out", "d.json")))
+    assert back["value"] == full["value"] and back["parity"] == "ok"
+    assert back["detail"] == os.path.join("gpurun_out", "d.json")
+    s = back["summary"]
+    assert s["batch10k"]["latency_ms"] == round(full["verify_batch_10k"]["latency_ms"], 3)
+    assert set(s["cert_stream_Mcerts_s"]) == {"N4", "N10", "N50", "N100"}
+    # the service tail is reported with p90 and max, not only the good percentiles
+    assert len(s["service"]["N50"]["offered_achieved_p50_p90_p99_max_ms"][0]) == 6
+
+
+def test_compact_line_bounded_when_legs_grow():
+    B = _bench()
+    full = json.load(open(CANNED))
+    full["summary"] = B.summary(full)
+    # many more committees and rates than the default bench runs
+    full["summary"]["service"] = {f"N{n}": full["summary"]["service"]["N50"] for n in range(200)}
+    full["summary"]["worker"]["offered_achieved_p50ms_p99ms"] *= 100
+    back = _check_line(B.compact_line(full))
+    assert "service" not in back["summary"] and back["summary"]["batch10k"]
+
+
+def test_gpus_mismatch_exits_nonzero():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 2, p.stderr[-2000:]
+    assert "WORLD_SIZE=2" in p.stderr
+    assert p.stdout.strip() == ""
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_spawns_ranks():
+    env = dict(os.environ, NW_BENCH_BACKEND="gloo",
+               NW_BENCH_DETAIL=os.path.join(ROOT, "gpurun_out", "bench_n2_detail.json"))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--steps", "2", "--warmup", "1", "--items-per-gpu", "65536",
+                        "--unique", "8192", "--no-sha", "--no-cert", "--no-batch", "--no-wire",
+                        "--no-worker", "--no-service", "--no-cpu-baseline"],
+                       env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["parity"] == "ok", r
+    assert r["config"]["items_total"] == 2 * 65536

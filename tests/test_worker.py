@@ -17,12 +17,12 @@ from narwhal_amd.worker import Processor, Store, our_batch_message
 from test_service import _OracleBackend
 
 
-def _run(backend, batches, own=True, worker_id=0):
+def _run(backend, batches, own=True, worker_id=0, hash_on="device"):
     async def main():
         svc = VerificationService(backend=backend, max_delay=0.001)
         store = Store()
         rx, tx = asyncio.Queue(), asyncio.Queue()
-        task = Processor.spawn(worker_id, store, rx, tx, own, svc)
+        task = Processor.spawn(worker_id, store, rx, tx, own, svc, hash_on=hash_on)
         for b in batches:
             await rx.put(b)
         await rx.put(None)
@@ -65,9 +65,43 @@ def test_order_preserved_and_batches_share_jobs():
 def test_processor_on_gpu():
     batches = [W.worker_batch(i, seed=4).tobytes() for i in range(6)] + \
               [W.reference_serialized_batch()]
-    out, stored, _ = _run(None, batches)
+    out, stored, jobs = _run(None, batches, hash_on="device")
     assert out == _expect(batches)
     assert stored == batches
+    assert jobs >= 1
+
+
+def test_host_default_matches_reference_and_submits_no_jobs():
+    """The default hashes on the host, one batch at a time, as processor.rs:38 does: same
+    messages, same store contents, and the service is never asked for a digest."""
+    batches = [W.serialize_batch([bytes([i]) * (50 + 13 * j) for j in range(i % 5 + 1)])
+               for i in range(12)] + [W.reference_serialized_batch()]
+
+    async def main():
+        svc = VerificationService(backend=_OracleBackend(), max_delay=0.001)
+        store, rx, tx = Store(), asyncio.Queue(), asyncio.Queue()
+        task = Processor.spawn(7, store, rx, tx, False, svc)          # default: host
+        task2 = Processor.spawn(7, Store(), asyncio.Queue(), asyncio.Queue(), False)  # no svc
+        for b in batches:
+            await rx.put(b)
+        await rx.put(None)
+        await task
+        task2.cancel()
+        out = [tx.get_nowait() for _ in range(tx.qsize())]
+        stored = [await store.read(hashlib.sha512(b).digest()[:32]) for b in batches]
+        return out, stored, svc.jobs_submitted
+    out, stored, jobs = asyncio.run(main())
+    assert out == _expect(batches, own=False, worker_id=7)
+    assert stored == batches
+    assert jobs == 0
+
+
+def test_hash_on_rejects_bad_modes():
+    q = asyncio.Queue
+    with pytest.raises(ValueError):
+        Processor.spawn(0, Store(), q(), q(), True, None, hash_on="device")
+    with pytest.raises(ValueError):
+        Processor.spawn(0, Store(), q(), q(), True, None, hash_on="gpu")
 
 
 def test_backpressure_bounded_in_flight():
@@ -81,7 +115,8 @@ def test_backpressure_bounded_in_flight():
     async def main():
         svc = VerificationService(backend=_OracleBackend(), max_delay=0.001)
         rx, tx = asyncio.Queue(maxsize=1), asyncio.Queue()
-        task = Processor.spawn(0, StuckStore(), rx, tx, True, svc, max_in_flight=3)
+        task = Processor.spawn(0, StuckStore(), rx, tx, True, svc, max_in_flight=3,
+                               hash_on="device")
         sent = 0
         batches = [W.serialize_batch([bytes([i]) * 64]) for i in range(20)]
         for b in batches:
