@@ -805,7 +805,7 @@ def run_service_latency(args, rank, world, N: int, cache=None):
     def native_load(rate: float, seconds: float):
         total = max(1, int(rate * seconds))
         lat = np.zeros(total)
-        out3 = np.zeros(11)
+        out3 = np.zeros(13)
         rc = LG.nw_loadgen_certificates(ctypes.byref(cc), ctypes.byref(cs), ptr_np(exp_st),
                                         ptr_np(exp_ix), rate, total, args.service_max_items,
                                         delay_us, args.service_inflight, args.service_producers,
@@ -816,7 +816,8 @@ def run_service_latency(args, rank, world, N: int, cache=None):
                "producer_lag_mean_ms": float(out3[4] * 1e3),
                "producer_cpu_per_wall": float(out3[5]), "producer_vcsw": int(out3[6]),
                "producer_ivcsw": int(out3[7]), "call_mean_us": float(out3[8] * 1e6),
-               "call_max_us": float(out3[9] * 1e6), "calls_over_20us": int(out3[10])}
+               "call_max_us": float(out3[9] * 1e6), "calls_over_20us": int(out3[10]),
+               "small_jobs": int(out3[11]), "pipeline_jobs": int(out3[12])}
         inval = exp_st[np.arange(total) % uniq] != 0
         slow = np.argsort(lat)[-max(1, total // 100):]   # the slowest 1 %: where in the run
         diag = {"p99_valid_ms": float(np.percentile(lat[~inval], 99) * 1e3),

@@ -50,6 +50,7 @@
 #include <memory>
 #include <mutex>
 #include <new>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -124,6 +125,7 @@ struct Batch {
   Caps caps{0, 0, 0};
   uint64_t n = 0, nv1 = 0, nv2 = 0;        // final counts (from the cursor when taken)
   int64_t t_taken = 0, t_sub0 = 0, t_sub1 = 0;   // NW_SERVICE_DEBUG: taken, submit start / end
+  int how = 0;                                     // NW_SERVICE_DEBUG: see JobRec
   Arr reqs;
   // Header / Certificate (nw_certificates)
   Arr header_bytes, header_offsets, payload_counts, ids, header_sigs, vote_offsets, vote_pks,
@@ -262,6 +264,16 @@ struct nw_service {
   // submitted, done seen by the completer, callbacks delivered (medians printed at destroy)
   bool debug = false;
   std::vector<float> d_taken, d_sub0, d_sub1, d_done, d_cb;
+  // NW_SERVICE_DEBUG=<path containing '/'>: one CSV row per job written there at destroy
+  // (kind, requests, votes, how it was submitted, ns timestamps), the per-job timeline the
+  // medians above summarise
+  std::string debug_path;
+  struct JobRec {
+    int kind, how;   // how: 0 flusher (timer / eager), 1 caller's thread, 2 sealed full
+    uint64_t n, nv2;
+    int64_t first, taken, sub0, sub1, done, cb;
+  };
+  std::vector<JobRec> d_jobs;
   size_t open_jobs = 0;   // submitted (or being submitted), callbacks not yet delivered
   size_t submitting = 0;  // submits in progress outside the lock
   bool inline_submit = true;   // NW_SERVICE_INLINE=0: only the flusher submits
@@ -334,6 +346,7 @@ struct nw_service {
       std::unique_ptr<Batch> old = take_open(k);
       if (old) {
         ++n_full;
+        old->how = 2;
         sealed[k].push_back(std::move(old));
         ++nsealed;
       }
@@ -371,6 +384,7 @@ struct nw_service {
           std::unique_ptr<Batch> own = take_open(static_cast<Kind>(pick));
           if (own) {
             ++n_inline;
+            own->how = 1;
             launch(lk, std::move(own));
             return 0;
           }
@@ -400,6 +414,7 @@ struct nw_service {
       return 0;
     }
     ++n_full;
+    old->how = 2;
     sealed[k].push_back(std::move(old));
     ++nsealed;
     lk.unlock();
@@ -614,6 +629,9 @@ struct nw_service {
         d_sub1.push_back(us(b->t_sub1));
         d_done.push_back(us(tdone));
         d_cb.push_back(us(tcb));
+        if (!debug_path.empty())
+          d_jobs.push_back({b->kind, b->how, b->n, b->nv2, f, b->t_taken, b->t_sub0, b->t_sub1,
+                            tdone, tcb});
       }
       lk.lock();
       std::unique_ptr<Batch> own = std::move(inflight.front());
@@ -624,6 +642,7 @@ struct nw_service {
       completed += n;
       // a job slot freed below eager_jobs: flush what has queued
       if (--open_jobs < eager_jobs) cv_flush.notify_one();
+      own->how = 0;
       spare[own->kind].push_back(std::move(own));    // cursor stays sealed while spare
       cv_idle.notify_all();
     }
@@ -650,6 +669,7 @@ int nw_service_create(const nw_committee* committee, size_t max_items, uint32_t 
   s->max_inflight = max_inflight ? max_inflight : 1;
   if (const char* e = getenv("NW_SERVICE_INLINE")) s->inline_submit = atoi(e) != 0;
   s->debug = getenv("NW_SERVICE_DEBUG") != nullptr;
+  if (s->debug && strchr(getenv("NW_SERVICE_DEBUG"), '/')) s->debug_path = getenv("NW_SERVICE_DEBUG");
   if (const char* e = getenv("NW_SERVICE_EAGER")) s->eager_jobs = std::max(1, atoi(e));
   if (committee) {
     const size_t na = committee->nauth, nwk = na ? committee->worker_offsets[na] : 0;
@@ -863,6 +883,21 @@ void nw_service_destroy(nw_service* s) {
             "(%zu jobs)\n",
             med(s->d_taken), med(s->d_sub0), med(s->d_sub1), med(s->d_done), med(s->d_cb),
             s->d_done.size());
+  }
+  if (!s->debug_path.empty() && !s->d_jobs.empty()) {
+    // one file per service: <path>.<first job's first-request ns>
+    char name[4096];
+    snprintf(name, sizeof name, "%s.%lld.csv", s->debug_path.c_str(),
+             (long long)s->d_jobs.front().first);
+    if (FILE* f = fopen(name, "w")) {
+      fprintf(f, "kind,how,n,votes,first_ns,taken_ns,sub0_ns,sub1_ns,done_ns,cb_ns\n");
+      for (const auto& j : s->d_jobs)
+        fprintf(f, "%d,%d,%llu,%llu,%lld,%lld,%lld,%lld,%lld,%lld\n", j.kind, j.how,
+                (unsigned long long)j.n, (unsigned long long)j.nv2, (long long)j.first,
+                (long long)j.taken, (long long)j.sub0, (long long)j.sub1, (long long)j.done,
+                (long long)j.cb);
+      fclose(f);
+    }
   }
   delete s;
 }

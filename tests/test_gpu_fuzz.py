@@ -158,3 +158,134 @@ def test_fuzz_certificates_through_service_vs_oracle():
            if stable[i] and got[i] != (int(oa[i]), int(oia[i]))]
     assert not bad, bad[:10]
     assert stable.mean() > 0.9
+
+
+# ---- irregular committee members ----------------------------------
+# Committees holding mixed-order (aB + T), small-order (every decodable encoding),
+# non-canonical large-order and undecodable keys, as header authors and as voters at every
+# index (tests/irregular.py), plus the byte damage above on a quarter of the certificates.
+# Injected coefficients: every (status, index) == the oracle on the small-job kernel, the
+# bulk keyed pipeline and the per-certificate path. Random coefficients (the service, the
+# merged-group and small-group policies): every verdict is one the oracle gives for some
+# coefficient set (irregular.possible_verdicts over 64 sets).
+IRREGULAR_SHAPES = [(4, 160, 21), (7, 160, 22), (10, 120, 23), (20, 60, 24), (50, 24, 25),
+                    (100, 12, 26)]
+INJECTED_PATHS = ({"NW_SMALL": "1"}, {"NW_SMALL": "0"}, {"NW_SMALL": "0", "NW_CERT_MERGE": "0"})
+RANDOM_PATHS = ({"NW_SMALL": "1"}, {"NW_SMALL": "0"}, {"NW_SMALL": "0", "NW_CERT_KEYED": "0"},
+                {"NW_SMALL": "0", "NW_CERT_KEYED": "0", "NW_CERT_SMALL_K": "4"},
+                {"NW_SMALL": "0", "NW_CERT_KEYED": "0", "NW_CERT_GROUP_VOTES": "256"})
+ENV_KEYS = ("NW_SMALL", "NW_CERT_MERGE", "NW_CERT_KEYED", "NW_CERT_SMALL_K",
+            "NW_CERT_GROUP_VOTES")
+
+
+def _irregular_case(N, n, seed):
+    import irregular as I
+    com, s, kinds = I.irregular_stream(N, n, seed)
+    rng = np.random.Generator(np.random.PCG64([seed, 5]))
+    d = _damage(s, rng, 0.25)
+    z16 = rng.integers(0, 256, size=(len(d["vote_pks"]), 16), dtype=np.uint8)
+    return com, d, z16, kinds
+
+
+def _set_env(monkeypatch, env):
+    for k in ENV_KEYS:
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+
+
+@pytest.mark.parametrize("N,n,seed", IRREGULAR_SHAPES)
+def test_fuzz_irregular_committees_injected_vs_oracle(monkeypatch, N, n, seed):
+    com, d, z16, kinds = _irregular_case(N, n, seed)
+    assert any(k != "honest" for k in kinds)
+    ost, oix = O.certificates_verify_many(com, d, z16)
+    for env in INJECTED_PATHS:
+        _set_env(monkeypatch, env)
+        for rep in range(2):                              # the first call builds the tables
+            st, ix = M.verify_certificates_many(_Com(com), d, z16)
+            bad = [(i, int(a), int(b), int(x), int(y)) for i, (a, b, x, y)
+                   in enumerate(zip(st, ost, ix, oix)) if a != b or x != y]
+            assert not bad, (env, rep, kinds, bad[:10])
+    ohst, ohix = O.certificates_verify_many(com, d, headers_only=True)
+    for small in ("1", "0"):
+        _set_env(monkeypatch, {"NW_SMALL": small})
+        hst, hix = M.verify_headers_many(_Com(com), d)
+        assert hst.tolist() == ohst.tolist() and hix.tolist() == ohix.tolist(), small
+
+
+@pytest.mark.parametrize("N,n,seed", IRREGULAR_SHAPES[:4])
+def test_fuzz_irregular_committees_random_z(monkeypatch, N, n, seed):
+    import irregular as I
+    com, d, _, kinds = _irregular_case(N, n, seed)
+    poss = I.possible_verdicts(com, d, 64, seed)
+    assert any(len(v) > 1 for v in poss)                  # z decides some certificates
+    for env in RANDOM_PATHS:
+        _set_env(monkeypatch, env)
+        for rep in range(2):
+            st, ix = M.verify_certificates_many(_Com(com), d, None)
+            bad = [(i, int(a), int(x), sorted(poss[i])) for i, (a, x) in enumerate(zip(st, ix))
+                   if (int(a), int(x)) not in poss[i]]
+            assert not bad, (env, rep, kinds, bad[:10])
+
+
+def test_fuzz_irregular_committees_through_service():
+    import asyncio
+    import irregular as I
+    from narwhal_amd import service as S
+    from test_service import _rows
+    com, d, _, kinds = _irregular_case(10, 120, 31)
+    poss = I.possible_verdicts(com, d, 64, 31)
+    rows = _rows(d)
+
+    async def main():
+        svc = S.NativeService(com, max_delay=0.0002)
+        got = await asyncio.gather(*[svc.certificate_status(r) for r in rows])
+        got += await asyncio.gather(*[svc.certificate_status(r) for r in rows[::-1]])
+        svc.close()
+        return got
+
+    got = asyncio.run(main())
+    n = len(rows)
+    pairs = [(i, got[i]) for i in range(n)] + [(n - 1 - j, got[n + j]) for j in range(n)]
+    bad = [(i, g, sorted(poss[i])) for i, g in pairs if tuple(g) not in poss[i]]
+    assert not bad, (kinds, bad[:10])
+
+
+_FALLBACK_CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, ROOT)
+sys.path.insert(0, ROOT + "/tests")
+from narwhal_amd import _lib
+from narwhal_amd import messages as M
+from oracle import oracle as O
+from test_gpu_fuzz import _irregular_case
+from test_gpu_messages import _Com
+L = _lib.lib()
+assert L.nw_prepare() == -4, L.nw_last_error()      # no room for the keyed tables
+for N, n, seed in ((4, 80, 41), (10, 60, 42), (20, 30, 43)):
+    com, d, z16, kinds = _irregular_case(N, n, seed)
+    ost, oix = O.certificates_verify_many(com, d, z16)
+    for _ in range(2):
+        st, ix = M.verify_certificates_many(_Com(com), d, z16)
+        assert st.tolist() == ost.tolist() and ix.tolist() == oix.tolist(), (N, kinds)
+    hst, hix = M.verify_headers_many(_Com(com), d)
+    ohst, ohix = O.certificates_verify_many(com, d, headers_only=True)
+    assert hst.tolist() == ohst.tolist() and hix.tolist() == ohix.tolist(), N
+small, pipe = _lib.path_stats()
+assert small == 0 and pipe > 0, (small, pipe)
+print("IRREGULAR_FALLBACK_OK")
+"""
+
+
+def test_fuzz_irregular_committees_unkeyed_fallback():
+    """The same construction with no room for the keyed tables (NW_DEVICE_MEM_LIMIT, as
+    tests/test_gpu_memory.py): the unkeyed strict ladder and per-certificate verify_batch."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, NW_DEVICE_MEM_LIMIT=str(3 * 10**9))
+    r = subprocess.run([sys.executable, "-c", f"ROOT = {root!r}\n" + _FALLBACK_CHILD], env=env,
+                       capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and "IRREGULAR_FALLBACK_OK" in r.stdout, r.stderr[-3000:]

@@ -58,11 +58,13 @@ int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_s
 extern "C" {
 
 // Returns 0 or the first negative NW_E_* from the service. lat_out: total seconds;
-// out (11 doubles): elapsed seconds (t0 .. last verdict), jobs, mismatches, and the
+// out (13 doubles): elapsed seconds (t0 .. last verdict), jobs, mismatches, and the
 // producers' lateness: the largest and the mean (call time - due time) of a submit, seconds
 // (a producer that cannot keep its schedule shows here before it shows as latency), then
 // the producers' CPU / wall time and their voluntary / involuntary context switches, and
-// the nw_service_certificate calls' mean and longest duration and the count above 20 us.
+// the nw_service_certificate calls' mean and longest duration and the count above 20 us;
+// out[11..12]: jobs that took the small-job launch and
+// the bulk pipeline during the timed run (nw_path_stats).
 int nw_loadgen_certificates(const nw_committee* com, const nw_certificates* corpus,
                             const int32_t* exp_status, const uint64_t* exp_index, double rate,
                             uint64_t total, size_t max_items, uint32_t max_delay_us,
@@ -145,8 +147,9 @@ int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_s
       first_err.compare_exchange_strong(z, e);
     }
   };
-  uint64_t jobs0 = 0;
+  uint64_t jobs0 = 0, sm0 = 0, pp0 = 0;
   nw_service_stats(s, nullptr, &jobs0);
+  nw_path_stats(&sm0, &pp0);
   run.t0 = Clock::now() + std::chrono::milliseconds(2);
   const double period = 1.0 / rate;
   for (uint64_t i = 0; i < total; ++i)
@@ -189,8 +192,9 @@ int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_s
     });
   for (auto& t : th) t.join();
   nw_service_drain(s);
-  uint64_t jobs1 = 0;
+  uint64_t jobs1 = 0, sm1 = 0, pp1 = 0;
   nw_service_stats(s, nullptr, &jobs1);
+  nw_path_stats(&sm1, &pp1);
   out[0] = (double)run.last_ns.load() * 1e-9;
   out[1] = (double)(jobs1 - jobs0);
   out[2] = (double)run.mismatches.load();
@@ -220,6 +224,8 @@ int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_s
   out[8] = cs2 / (double)(total ? total : 1);   // mean nw_service_certificate call, seconds
   out[9] = cm;                                  // longest call
   out[10] = sl;                                 // calls longer than 20 us
+  out[11] = (double)(sm1 - sm0);                // small-job launches
+  out[12] = (double)(pp1 - pp0);                // bulk-pipeline jobs
   return first_err.load();
 }
 }  // namespace
