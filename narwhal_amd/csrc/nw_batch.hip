@@ -1617,13 +1617,15 @@ __global__ __launch_bounds__(64) void k_pip_final(const uint32_t* __restrict__ p
 // expected; a guard against a wedged launch).
 constexpr int kFuseParts = kPipWinLpParts / 2;   // part workgroups per window (w < 31)
 constexpr int kFuseTopParts = 10;                 // window 31: lists j <= 4, one part each
-constexpr uint32_t kFuseCtr = 4 * 33 + 4;        // counter words (zeroed: the caller's
-                                                 // H2D, or k_iota in w.chunk_start)
+constexpr uint32_t kFuseCtr = 4 * 33 + 4;        // counter words: zero before the head
+                                                 // (k_iota in w.chunk_start, or a job's own
+                                                 // counters), and zero again after the tail:
+                                                 // its last workgroup clears them (fz_exit)
 constexpr uint64_t kFuseSpinTicks = 200000000;   // 2 s
 constexpr uint32_t kFuseLds = 96 * 1024;         // > 160 KiB / 2: one workgroup per CU
 enum : uint32_t { kFzTicket = 0, kFzError = 1, kFzTicket2 = 2, kFzBuckets = 4, kFzParts = 4 + 33,
-                  kFzWsum = 4 + 66, kFzRole0 = 4 + 99, kFzPoints = 4 + 100 };
-static_assert(kFzPoints < kFuseCtr, "counters within the zeroed words");
+                  kFzWsum = 4 + 66, kFzRole0 = 4 + 99, kFzPoints = 4 + 100, kFzExit = 4 + 101 };
+static_assert(kFzExit < kFuseCtr, "counters within the zeroed words");
 constexpr size_t kFusePartBytes = 4ull * (kPipWin + 1) * kPipWinLpParts * 64;
 // the parts live in the batch's digit arrays (cd, zd: dead after k_pip_sort)
 constexpr uint64_t kFuseMinN = (kFusePartBytes + 51) / 52;
@@ -1764,6 +1766,18 @@ __device__ __forceinline__ bool fz_wait(uint32_t* ctr, uint32_t idx, uint32_t wa
   }
   return true;
 }
+// A workgroup of k_pip_tail_fused is done with the counters: its one thread that made the
+// workgroup's last counter access counts it out, and the last of the launch's workgroups
+// clears every counter word (the head's too: it has finished), so the next call on the same
+// counters starts from zero with no zeroing kernel or copy. Every role calls this exactly
+// once per workgroup, on every return path, after its last wait / add.
+__device__ __forceinline__ void fz_exit(uint32_t* ctr) {
+  const uint32_t prev = __hip_atomic_fetch_add(ctr + kFzExit, 1u, __ATOMIC_ACQ_REL,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+  if (prev + 1 == gridDim.x)
+    for (uint32_t i = 0; i < kFuseCtr; ++i)
+      __hip_atomic_store(ctr + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // Bucket workgroups whose bins touch window w (w = kPipWin: the z-carry bins).
 __device__ __forceinline__ uint32_t fz_bucket_blocks(int w, uint32_t lg) {
   const uint32_t b0 = (uint32_t)w * 128, b1 = w == kPipWin ? b0 + kPipCarryBins : b0 + 128;
@@ -1811,6 +1825,7 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
         if (bin0 < (uint32_t)kPipBins) fz_add(ctr + kFzBuckets + wv, 1u);
       stamp(1, __builtin_amdgcn_s_memrealtime());
       stamp(2, 0x100u | ((t * 256) >> lg >> 7));
+      fz_exit(ctr);
     }
     return;
   }
@@ -1827,6 +1842,7 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
       if (lane == 0) fz_add(ctr + kFzWsum + kPipWin, 1u);
       stamp(1, __builtin_amdgcn_s_memrealtime());
       stamp(2, 0x200u);
+      if (lane == 0) fz_exit(ctr);
     }
     return;
   }
@@ -1835,13 +1851,17 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
     if (tid == 0) s_ok = fz_wait(ctr, kFzBuckets + kPipWin - 1, fz_bucket_blocks(kPipWin - 1, lg))
                              ? 1u : 0u;
     __syncthreads();
-    if (!s_ok) return;
+    if (!s_ok) {
+      if (tid == 0) fz_exit(ctr);
+      return;
+    }
     fz_acquire();
     stamp(3, __builtin_amdgcn_s_memrealtime());
     pip_lp_part4(reg, L, d2l, (int)pt, wave, lane, &s_other[0][0] + 0, parts);
     if (wave == 0 && lane == 0) fz_add(ctr + kFzParts + kPipWin - 1, 1u);
     stamp(1, __builtin_amdgcn_s_memrealtime());
     stamp(2, 0x300u | (uint32_t)(kPipWin - 1));
+    if (wave == 0 && lane == 0) fz_exit(ctr);
     return;
   }
   if (pt > (uint32_t)kFuseTopParts) {   // ---- window parts (+ the window's sum)
@@ -1853,7 +1873,10 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
       s_ok = ok ? 1u : 0u;
     }
     __syncthreads();
-    if (!s_ok) return;
+    if (!s_ok) {
+      if (tid == 0) fz_exit(ctr);
+      return;
+    }
     fz_acquire();
     stamp(3, __builtin_amdgcn_s_memrealtime());   // its buckets were ready
     const int q = 2 * i + (wave >> 1), half2 = wave & 1;
@@ -1867,12 +1890,16 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
                                     __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)kFuseParts - 1;
     stamp(1, __builtin_amdgcn_s_memrealtime());
     stamp(2, 0x300u | (uint32_t)w);
-    if (!__builtin_amdgcn_readfirstlane(last)) return;
+    if (!__builtin_amdgcn_readfirstlane(last)) {
+      if (lane == 0) fz_exit(ctr);
+      return;
+    }
     fz_acquire();
     pip_lp_wsum(reg, L, w, lane, parts);
     if (lane == 0) fz_add(ctr + kFzWsum + w, 1u);
     stamp(1, __builtin_amdgcn_s_memrealtime());
     stamp(2, 0x400u | (uint32_t)w);   // this workgroup also summed the window
+    if (lane == 0) fz_exit(ctr);
     return;
   }
   // ---- the Horner (wave 0)
@@ -1918,9 +1945,11 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
       status[bidx] = NW_E_DEVICE;
       if (fail_index) fail_index[bidx] = 0;
       __threadfence_system();
+      fz_exit(ctr);
     }
     return;
   }
+  if (lane == 0) fz_exit(ctr);   // the Horner's counter accesses are over
   v = lp_add(L, v, lp_cached_component(L, *reg.Bc));   // + [-sum b_i]B
   pip_verdict(reg, L, v, s_tmp, bidx, n, status, fail_index, nullptr);
   stamp(1, __builtin_amdgcn_s_memrealtime());

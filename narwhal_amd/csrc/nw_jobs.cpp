@@ -50,6 +50,8 @@ struct nw_job {
   char* hdev = nullptr;   // the device's address of hbuf (small jobs read it directly)
   uint32_t* dcnt = nullptr;   // small jobs' per-message arrival counters (kept zero)
   size_t ccap = 0;
+  uint32_t* dfz = nullptr;    // config-1 fused launches' counters (the tail leaves them zero)
+  bool dfz_dirty = false;     // a launch failed after the head ran: clear before reuse
   struct Out {
     void* dst;
     size_t off;
@@ -133,8 +135,29 @@ int job_abort(nw_job* j, int rc) {
   return rc;
 }
 
+int job_counters(nw_job* j, size_t n);
+
+// Growth log (nw::rt::job_growth_log): a staging buffer that grows inside a burst pins or
+// allocates memory on the submitting thread, which the service's debug timeline must show.
+struct GrowEv {
+  uint64_t t_ns, cap, us, kind;
+};
+constexpr size_t kGrowLog = 4096;
+GrowEv g_grow[kGrowLog];
+std::atomic<size_t> g_ngrow{0};
+void log_growth(uint64_t kind, size_t cap, std::chrono::steady_clock::time_point t0) {
+  const auto t1 = std::chrono::steady_clock::now();
+  const size_t i = g_ngrow.fetch_add(1, std::memory_order_relaxed);
+  if (i < kGrowLog)
+    g_grow[i] = {(uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                     t0.time_since_epoch()).count(),
+                 cap, (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0)
+                          .count(), kind};
+}
+
 int job_reserve(nw_job* j, size_t hbytes, size_t dbytes) {
   if (hbytes > j->hcap) {
+    const auto t0 = std::chrono::steady_clock::now();
     if (j->hbuf) (void)hipHostFree(j->hbuf);
     j->hbuf = nullptr;
     j->hcap = 0;
@@ -149,8 +172,10 @@ int job_reserve(nw_job* j, size_t hbytes, size_t dbytes) {
     e = hipHostGetDevicePointer(&dp, j->hbuf, 0);
     if (e != hipSuccess) return set_err(NW_E_DEVICE, "hipHostGetDevicePointer (job staging)", e);
     j->hdev = static_cast<char*>(dp);
+    log_growth(0, cap, t0);
   }
   if (dbytes > j->dcap) {
+    const auto t0 = std::chrono::steady_clock::now();
     if (j->dbuf) (void)hipFree(j->dbuf);
     j->dbuf = nullptr;
     j->dcap = 0;
@@ -158,6 +183,7 @@ int job_reserve(nw_job* j, size_t hbytes, size_t dbytes) {
     hipError_t e = hipMalloc(reinterpret_cast<void**>(&j->dbuf), cap);
     if (e != hipSuccess) return set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (job buffer)", e);
     j->dcap = cap;
+    log_growth(1, cap, t0);
   }
   return 0;
 }
@@ -207,6 +233,17 @@ void ensure_fork(nw_job* j) {
 
 }  // namespace
 
+size_t nw::rt::job_growth_log(uint64_t* out, size_t max) {
+  const size_t n = std::min(g_ngrow.load(std::memory_order_acquire), kGrowLog);
+  for (size_t i = 0; i < n && i < max; ++i) {
+    out[4 * i] = g_grow[i].t_ns;
+    out[4 * i + 1] = g_grow[i].cap;
+    out[4 * i + 2] = g_grow[i].us;
+    out[4 * i + 3] = g_grow[i].kind;
+  }
+  return n;
+}
+
 // Puts `count` jobs with their streams, fork streams and `hbytes` / `dbytes` of staging into
 // device dev's pool (nw_service_create: a service's first burst then finds its jobs made,
 // instead of creating streams and pinning memory on the flusher's path).
@@ -219,6 +256,9 @@ int nw::rt::jobs_prewarm(int dev, int count, size_t hbytes, size_t dbytes) {
     if (rc) break;
     got.push_back(j);
     rc = job_reserve(j, hbytes, dbytes);
+    // small jobs' arrival counters too: a first small job on a job without them would
+    // allocate (hipMalloc + hipMemsetAsync) on the submitting thread in the middle of a burst
+    if (!rc) rc = job_counters(j, 4096);
     if (!rc) ensure_fork(j);
   }
   for (nw_job* j : got) job_recycle(j);
@@ -290,12 +330,12 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
     return 0;
   }
   const size_t m = nitems ? nitems : 1;
-  // a lone batch on the fused path: its launches' counters ship zeroed with the inputs
+  // a lone batch on the fused path: the launches read the inputs from the pinned buffer and
+  // write the verdict into it (no copies), with the job's own counters
   const bool direct = nw::verify_batch_outputs_direct(nbatches, nitems);
   const size_t o_d = 0, o_off = o_d + a256(32 * nbatches), o_pk = o_off + a256(8 * (nbatches + 1)),
                o_sig = o_pk + a256(32 * m), o_z = o_sig + a256(64 * m),
-               o_ctr = o_z + (z16 ? a256(16 * m) : 0),
-               o_st = o_ctr + (direct ? a256(nw::verify_batch_fuse_ctr_bytes()) : 0),
+               o_st = o_z + (z16 ? a256(16 * m) : 0),
                o_fi = o_st + a256(4 * nbatches),
                o_ws = o_fi + a256(8 * nbatches),
                end = o_ws + a256(nw::batch_workspace_bytes(nbatches, nitems));
@@ -308,7 +348,6 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
     memcpy(j->hbuf + o_sig, sigs, 64 * nitems);
     if (z16) memcpy(j->hbuf + o_z, z16, 16 * nitems);
   }
-  if (direct) memset(j->hbuf + o_ctr, 0, nw::verify_batch_fuse_ctr_bytes());
   nw::z_key_t key;
   rc = fill_key(key);
   if (rc) return job_abort(j, rc);
@@ -324,23 +363,38 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
   }();
   const bool fork = fork_on && j->fork.s2;
   // a lone large batch (config 1's call): the verdict is written straight into the pinned
-  // buffer by the one kernel that computes it, no copy back
+  // buffer by the one kernel that computes it, no copy back; the inputs are read from it
+  // too unless NW_BATCH_PINNED=0 (A/B hook: then one H2D of them first)
+  static const bool pinned_in = [] {
+    const char* e = getenv("NW_BATCH_PINNED");
+    return !(e && *e == '0');
+  }();
   const bool out_direct = direct && !fork;
+  const bool in_direct = out_direct && pinned_in;
+  if (out_direct && (!j->dfz || j->dfz_dirty)) {
+    if (!j->dfz &&
+        hipMalloc(reinterpret_cast<void**>(&j->dfz), nw::verify_batch_fuse_ctr_bytes()) != hipSuccess) {
+      j->dfz = nullptr;
+      return job_abort(j, set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (fused counters)"));
+    }
+    if (hipMemsetAsync(j->dfz, 0, nw::verify_batch_fuse_ctr_bytes(), j->stream) != hipSuccess)
+      return job_abort(j, set_err(NW_E_DEVICE, "hipMemsetAsync (fused counters)"));
+    j->dfz_dirty = false;
+  }
   char* const obuf = out_direct ? j->hdev : j->dbuf;
-  rc = job_run(j, o_st, o_st, out_direct ? 0 : o_ws - o_st, [&]() -> int {
-    JOB_HIP(nw::launch_verify_batch(reinterpret_cast<const uint32_t*>(j->dbuf + o_d),
-                                    reinterpret_cast<const uint64_t*>(j->dbuf + o_off), h_off,
-                                    nbatches, reinterpret_cast<const uint32_t*>(j->dbuf + o_pk),
-                                    reinterpret_cast<const uint32_t*>(j->dbuf + o_sig), nitems,
-                                    z16 ? reinterpret_cast<const uint32_t*>(j->dbuf + o_z)
-                                        : nullptr,
-                                    key, j->dbuf + o_ws,
-                                    reinterpret_cast<int32_t*>(obuf + o_st),
-                                    reinterpret_cast<uint64_t*>(obuf + o_fi), j->stream,
-                                    nullptr, nullptr, 0, 1.0, fork ? &fk : nullptr,
-                                    out_direct ? reinterpret_cast<uint32_t*>(j->dbuf + o_ctr)
-                                               : nullptr),
-            "verify_batch launch");
+  char* const ibuf = in_direct ? j->hdev : j->dbuf;
+  rc = job_run(j, in_direct ? 0 : o_st, o_st, out_direct ? 0 : o_ws - o_st, [&]() -> int {
+    const hipError_t e = nw::launch_verify_batch(
+        reinterpret_cast<const uint32_t*>(ibuf + o_d),
+        reinterpret_cast<const uint64_t*>(ibuf + o_off), h_off, nbatches,
+        reinterpret_cast<const uint32_t*>(ibuf + o_pk),
+        reinterpret_cast<const uint32_t*>(ibuf + o_sig), nitems,
+        z16 ? reinterpret_cast<const uint32_t*>(ibuf + o_z) : nullptr, key, j->dbuf + o_ws,
+        reinterpret_cast<int32_t*>(obuf + o_st), reinterpret_cast<uint64_t*>(obuf + o_fi),
+        j->stream, nullptr, nullptr, 0, 1.0, fork ? &fk : nullptr,
+        out_direct ? j->dfz : nullptr);
+    if (e != hipSuccess && out_direct) j->dfz_dirty = true;   // the head may have run
+    JOB_HIP(e, "verify_batch launch");
     return 0;
   });
   if (rc) return job_abort(j, rc);
@@ -470,6 +524,7 @@ std::atomic<uint64_t> g_small_jobs{0}, g_pipeline_jobs{0};
 // The per-message arrival counters of a job (device, zero; kernels leave them zero).
 int job_counters(nw_job* j, size_t n) {
   if (n <= j->ccap) return 0;
+  const auto t0 = std::chrono::steady_clock::now();
   if (j->dcnt) (void)hipFree(j->dcnt);
   j->dcnt = nullptr;
   j->ccap = 0;
@@ -478,6 +533,7 @@ int job_counters(nw_job* j, size_t n) {
   if (e == hipSuccess) e = hipMemsetAsync(j->dcnt, 0, 4 * cap, j->stream);
   if (e != hipSuccess) return set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (job counters)", e);
   j->ccap = cap;
+  log_growth(2, 4 * cap, t0);
   return 0;
 }
 

@@ -124,6 +124,38 @@ __device__ __forceinline__ uint64_t lp_mac2(uint64_t acc, uint32_t f, uint32_t g
   return acc + (uint64_t)lp_dpp<0x150 + J>(f) * gj;
 }
 
+#ifndef NW_LP_ROR
+#define NW_LP_ROR 1
+#endif
+#if NW_LP_ROR
+// Term j of column k from ONE rotate: the row's dead lanes 10..15 carry the wrapped operand
+// (lane L holds 19 g_{L-6}), so row_ror:j hands lane k < j exactly 19 g_{k+10-j} and lane
+// k >= j g_{k-j}. For j >= 7 the wrap also reaches lanes 7..9, so those terms rotate a second
+// vector whose lanes 7..15 hold 19 g_{L-6} (lanes 0..2 keep g; 3..6 are never read by them).
+// Three instructions per term instead of five (broadcast, rotate, multiply-accumulate); the
+// dead lanes accumulate garbage that lp_carry64 drops (mask 0, incoming-carry factor 0, and
+// no live lane reads a dead lane's carry: lane 0 takes lane 9's).
+template <int J>
+__device__ __forceinline__ uint64_t lp_mac_ror(uint64_t acc, uint32_t f, uint32_t gsrc) {
+  const uint32_t gj = J == 0 ? gsrc : lp_dpp<0x120 + J>(gsrc);   // row_ror:J
+  return acc + (uint64_t)lp_dpp<0x150 + J>(f) * gj;
+}
+
+__device__ __forceinline__ uint32_t lp_mul(const lp_ctx& c, uint32_t f, uint32_t g) {
+  const uint32_t go = g << c.odd;                                // odd source limbs x 2
+  const uint32_t we = lp_dpp<0x126>(g * 19u), wo = lp_dpp<0x126>(go * 19u);   // row_ror:6
+  const bool lo10 = c.k < 10, lo7 = c.k < 7;
+  const uint32_t ge = lo10 ? g : we, gov = lo10 ? go : wo;       // terms 0..6
+  const uint32_t he = lo7 ? g : we, ho = lo7 ? go : wo;          // terms 7..9
+  uint64_t a = 0, b = 0;   // two chains
+  a = lp_mac_ror<0>(a, f, g);    b = lp_mac_ror<1>(b, f, gov);
+  a = lp_mac_ror<2>(a, f, ge);   b = lp_mac_ror<3>(b, f, gov);
+  a = lp_mac_ror<4>(a, f, ge);   b = lp_mac_ror<5>(b, f, gov);
+  a = lp_mac_ror<6>(a, f, ge);   b = lp_mac_ror<7>(b, f, ho);
+  a = lp_mac_ror<8>(a, f, he);   b = lp_mac_ror<9>(b, f, ho);
+  return lp_carry64(c, a + b);
+}
+#else
 // h = f g (fe_mul's operand roles: f first, g second; g's limbs x 38 / x 19 stay in 32 bits,
 // tests/test_field_bounds.py).
 __device__ __forceinline__ uint32_t lp_mul(const lp_ctx& c, uint32_t f, uint32_t g) {
@@ -136,6 +168,7 @@ __device__ __forceinline__ uint32_t lp_mul(const lp_ctx& c, uint32_t f, uint32_t
   a = lp_mac2<8>(a, f, g, ge19);  b = lp_mac2<9>(b, f, go, go19);
   return lp_carry64(c, a + b);
 }
+#endif
 #else
 // h = f g (fe_mul's operand roles: f first, g second).
 __device__ __forceinline__ uint32_t lp_mul(const lp_ctx& c, uint32_t f, uint32_t g) {

@@ -33,6 +33,10 @@ int os_random(void* buf, size_t n);
 // count pooled jobs on library device dev, made now with hbytes / dbytes of staging
 // (nw_jobs.cpp; the aggregation service's start-up).
 int jobs_prewarm(int dev, int count, size_t hbytes, size_t dbytes);
+// Diagnostics (NW_SERVICE_DEBUG): job staging growths so far — pinned (kind 0), device
+// (kind 1), small-job counters (kind 2) — with their time (steady-clock ns), new capacity and
+// duration in us. Copies up to `max` of them into `out` (4 words each) and returns the count.
+size_t job_growth_log(uint64_t* out, size_t max);
 
 // ---- primary messages (nw_api.cpp), shared by the blocking, job and device entry points ----
 // Host-side argument checks of a host-memory committee / certificate stream (0 or

@@ -898,6 +898,19 @@ void nw_service_destroy(nw_service* s) {
                 (long long)j.cb);
       fclose(f);
     }
+    // the job staging growths of the process so far (steady-clock ns, as first_ns above)
+    std::vector<uint64_t> g(4 * 4096);
+    const size_t ng = nw::rt::job_growth_log(g.data(), 4096);
+    snprintf(name, sizeof name, "%s.%lld.grow.csv", s->debug_path.c_str(),
+             (long long)s->d_jobs.front().first);
+    if (FILE* f = fopen(name, "w")) {
+      fprintf(f, "t_ns,capacity,us,kind\n");
+      for (size_t i = 0; i < ng && i < 4096; ++i)
+        fprintf(f, "%llu,%llu,%llu,%llu\n", (unsigned long long)g[4 * i],
+                (unsigned long long)g[4 * i + 1], (unsigned long long)g[4 * i + 2],
+                (unsigned long long)g[4 * i + 3]);
+      fclose(f);
+    }
   }
   delete s;
 }
