@@ -330,8 +330,8 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
     return 0;
   }
   const size_t m = nitems ? nitems : 1;
-  // a lone batch on the fused path: the launches read the inputs from the pinned buffer and
-  // write the verdict into it (no copies), with the job's own counters
+  // a lone batch on the fused path: the launches write the verdict into the pinned buffer
+  // (no copy back) and use the job's own counters (zero between calls)
   const bool direct = nw::verify_batch_outputs_direct(nbatches, nitems);
   const size_t o_d = 0, o_off = o_d + a256(32 * nbatches), o_pk = o_off + a256(8 * (nbatches + 1)),
                o_sig = o_pk + a256(32 * m), o_z = o_sig + a256(64 * m),
@@ -363,14 +363,11 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
   }();
   const bool fork = fork_on && j->fork.s2;
   // a lone large batch (config 1's call): the verdict is written straight into the pinned
-  // buffer by the one kernel that computes it, no copy back; the inputs are read from it
-  // too unless NW_BATCH_PINNED=0 (A/B hook: then one H2D of them first)
-  static const bool pinned_in = [] {
-    const char* e = getenv("NW_BATCH_PINNED");
-    return !(e && *e == '0');
-  }();
+  // buffer by the one kernel that computes it, no copy back. (Its inputs still go over in
+  // one H2D: read from the pinned buffer by the head instead, they cost the head's digit
+  // lanes 24 -> 56 us and its decompressions 74 -> 100 us, the ~27 us the copy takes;
+  // profiles/r05e, r05f.)
   const bool out_direct = direct && !fork;
-  const bool in_direct = out_direct && pinned_in;
   if (out_direct && (!j->dfz || j->dfz_dirty)) {
     if (!j->dfz &&
         hipMalloc(reinterpret_cast<void**>(&j->dfz), nw::verify_batch_fuse_ctr_bytes()) != hipSuccess) {
@@ -382,8 +379,8 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
     j->dfz_dirty = false;
   }
   char* const obuf = out_direct ? j->hdev : j->dbuf;
-  char* const ibuf = in_direct ? j->hdev : j->dbuf;
-  rc = job_run(j, in_direct ? 0 : o_st, o_st, out_direct ? 0 : o_ws - o_st, [&]() -> int {
+  char* const ibuf = j->dbuf;
+  rc = job_run(j, o_st, o_st, out_direct ? 0 : o_ws - o_st, [&]() -> int {
     const hipError_t e = nw::launch_verify_batch(
         reinterpret_cast<const uint32_t*>(ibuf + o_d),
         reinterpret_cast<const uint64_t*>(ibuf + o_off), h_off, nbatches,
@@ -1123,6 +1120,25 @@ int nw_job_wait(nw_job* job) {
     return first;
   }
   if (!job->pending) return 0;
+  // Poll before blocking: hipEventSynchronize sleeps in the runtime and wakes tens of
+  // microseconds after the device finished, a tenth of a 0.3 ms verify_batch call. The
+  // caller is blocked either way, so up to NW_WAIT_SPIN_US (default 5 ms) of its CPU time goes
+  // to polling; longer jobs then block.
+  static const int64_t spin_us = [] {
+    const char* e = getenv("NW_WAIT_SPIN_US");
+    return e && *e ? (int64_t)atoll(e) : (int64_t)5000;
+  }();
+  if (spin_us > 0) {
+    const auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
+    do {
+      const hipError_t e = hipEventQuery(job->done);
+      if (e == hipSuccess) {
+        job_deliver(job);
+        return 0;
+      }
+      if (e != hipErrorNotReady) return set_err(NW_E_DEVICE, "hipEventQuery", e);
+    } while (std::chrono::steady_clock::now() < end);
+  }
   JOB_HIP(hipEventSynchronize(job->done), "hipEventSynchronize");
   job_deliver(job);
   return 0;

@@ -8,6 +8,8 @@
 // request i = verdict-callback time - scheduled arrival time, so a producer that falls
 // behind its schedule shows up as latency, not as a lower offered rate. Every verdict is
 // compared with the expected (status, index) of the corpus row it came from.
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/resource.h>
 
@@ -156,6 +158,25 @@ int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_s
     recs[i] = {&run, i,
                run.t0 + std::chrono::duration_cast<Clock::duration>(
                             std::chrono::duration<double>(period * (double)i))};
+  // NW_LOADGEN_GAPS=<file>: a monitor thread that only reads the clock records every gap
+  // above 0.5 ms (the thread was not running: the whole process, or its CPU, stalled), as
+  // steady-clock ns, to set beside the service's per-job timeline (NW_SERVICE_DEBUG)
+  std::atomic<bool> mon_stop{false};
+  std::vector<std::pair<int64_t, int64_t>> gaps;
+  std::thread mon;
+  const char* gap_path = getenv("NW_LOADGEN_GAPS");
+  if (gap_path && *gap_path)
+    mon = std::thread([&] {
+      auto prev = Clock::now();
+      while (!mon_stop.load(std::memory_order_relaxed)) {
+        const auto now = Clock::now();
+        if (now - prev > std::chrono::microseconds(500) && gaps.size() < 100000)
+          gaps.emplace_back(
+              std::chrono::duration_cast<std::chrono::nanoseconds>(prev.time_since_epoch()).count(),
+              std::chrono::duration_cast<std::chrono::nanoseconds>(now - prev).count());
+        prev = now;
+      }
+    });
   std::vector<std::thread> th;
   std::vector<double> lag_max(producers, 0.0), lag_sum(producers, 0.0);
   std::vector<double> cpu_s(producers, 0.0), wall_s(producers, 0.0);
@@ -192,6 +213,14 @@ int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_s
     });
   for (auto& t : th) t.join();
   nw_service_drain(s);
+  if (mon.joinable()) {
+    mon_stop = true;
+    mon.join();
+    if (FILE* f = fopen(gap_path, "a")) {
+      for (const auto& g : gaps) fprintf(f, "%lld,%lld\n", (long long)g.first, (long long)g.second);
+      fclose(f);
+    }
+  }
   uint64_t jobs1 = 0, sm1 = 0, pp1 = 0;
   nw_service_stats(s, nullptr, &jobs1);
   nw_path_stats(&sm1, &pp1);
