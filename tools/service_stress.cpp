@@ -70,6 +70,7 @@ int select_device(int* dev) {
   return 0;
 }
 int jobs_prewarm(int, int, size_t, size_t) { return 0; }
+size_t job_growth_log(uint64_t*, size_t) { return 0; }
 }  // namespace rt
 }  // namespace nw
 
