@@ -1120,25 +1120,6 @@ int nw_job_wait(nw_job* job) {
     return first;
   }
   if (!job->pending) return 0;
-  // Poll before blocking: hipEventSynchronize sleeps in the runtime and wakes tens of
-  // microseconds after the device finished, a tenth of a 0.3 ms verify_batch call. The
-  // caller is blocked either way, so up to NW_WAIT_SPIN_US (default 5 ms) of its CPU time goes
-  // to polling; longer jobs then block.
-  static const int64_t spin_us = [] {
-    const char* e = getenv("NW_WAIT_SPIN_US");
-    return e && *e ? (int64_t)atoll(e) : (int64_t)5000;
-  }();
-  if (spin_us > 0) {
-    const auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
-    do {
-      const hipError_t e = hipEventQuery(job->done);
-      if (e == hipSuccess) {
-        job_deliver(job);
-        return 0;
-      }
-      if (e != hipErrorNotReady) return set_err(NW_E_DEVICE, "hipEventQuery", e);
-    } while (std::chrono::steady_clock::now() < end);
-  }
   JOB_HIP(hipEventSynchronize(job->done), "hipEventSynchronize");
   job_deliver(job);
   return 0;
