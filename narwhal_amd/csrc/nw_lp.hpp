@@ -97,28 +97,10 @@ __device__ __forceinline__ uint32_t lp_carry_in32(const lp_ctx& c, uint32_t carr
 // 2^18.3, limb 1 < 2^25 + 2^17.3, the others < 2^26 / 2^25 + 2^14 -- the "T_LP" bound,
 // checked with every operand pair of the point formulas in tests/test_field_bounds.py.
 // (Lanes 10..15 hold 0 and receive no carry, so they stay 0.)
-#ifndef NW_LP_CARRY
-#define NW_LP_CARRY 2
-#endif
-#if NW_LP_CARRY == 2
-// The first pass does not wrap: limb 9's carry goes to dead lane 10 (row_shr:1 with
-// bound_ctrl hands lane 0 a zero), so it needs no rotate, select or x19 of a 64-bit value;
-// limb 9 then holds < 2^25 + 2^39 until the second pass, whose carry of it (< 2^14.1,
-// x19 < 2^18.3) wraps into limb 0 as before. Output bounds: limb 0 < 2^26 + 2^18.3, limb 1
-// < 2^25 (lane 0 got no first-pass carry), the rest < 2^26 / 2^25 + 2^14 -- inside T_LP
-// (tests/test_field_bounds.py). Dead lanes end at 0 (mask 0, incoming factor 0).
-__device__ __forceinline__ uint32_t lp_carry64(const lp_ctx& c, uint64_t col) {
-  const uint64_t cy = col >> c.sh;
-  const uint32_t lo = lp_dpp<0x111>((uint32_t)cy), hi = lp_dpp<0x111>((uint32_t)(cy >> 32));
-  const uint64_t t = (uint64_t)((uint32_t)col & c.mask) + (((uint64_t)hi << 32) | lo);
-  return ((uint32_t)t & c.mask) + lp_carry_in32(c, (uint32_t)(t >> c.sh));
-}
-#else
 __device__ __forceinline__ uint32_t lp_carry64(const lp_ctx& c, uint64_t col) {
   const uint64_t t = (col & c.mask) + lp_carry_in64(c, col >> c.sh);
   return (uint32_t)(t & c.mask) + lp_carry_in32(c, (uint32_t)(t >> c.sh));
 }
-#endif
 // 32-bit limbs below 2^29 (a difference a + 4p - b) -> one pass: carries < 2^4 (x19 into
 // limb 0), inside T_LP.
 __device__ __forceinline__ uint32_t lp_carry32(const lp_ctx& c, uint32_t x) {
@@ -153,17 +135,12 @@ __device__ __forceinline__ uint64_t lp_mac2(uint64_t acc, uint32_t f, uint32_t g
 // Three instructions per term instead of five (broadcast, rotate, multiply-accumulate); the
 // dead lanes accumulate garbage that lp_carry64 drops (mask 0, incoming-carry factor 0, and
 // no live lane reads a dead lane's carry: lane 0 takes lane 9's).
-#ifndef NW_LP_CHAINS
-#define NW_LP_CHAINS 2
-#endif
+// (The compiler merges the two accumulator chains below into one; keeping them apart with
+// an empty asm measured slower: config 1 0.3240 vs 0.3184 ms, profiles/r05j.)
 template <int J>
 __device__ __forceinline__ uint64_t lp_mac_ror(uint64_t acc, uint32_t f, uint32_t gsrc) {
   const uint32_t gj = J == 0 ? gsrc : lp_dpp<0x120 + J>(gsrc);   // row_ror:J
-  uint64_t r = acc + (uint64_t)lp_dpp<0x150 + J>(f) * gj;
-#if NW_LP_CHAINS == 2
-  asm("" : "+v"(r));   // keep the two accumulator chains apart (else merged into one)
-#endif
-  return r;
+  return acc + (uint64_t)lp_dpp<0x150 + J>(f) * gj;
 }
 
 __device__ __forceinline__ uint32_t lp_mul(const lp_ctx& c, uint32_t f, uint32_t g) {

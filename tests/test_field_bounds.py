@@ -105,12 +105,6 @@ def test_limb_parallel_bounds():
     assert (2**64 >> 25) * 19 < 2**44
     assert 19 * (((2**25 + 2**39) >> 25) + 1) < 2**18.3
     assert ((2**26 + 19 * 2**39) >> 26) < 2**17.3
-    # NW_LP_CARRY=2 (default): no wrap in the first pass; limb 9 < 2^25 + 2^39 carries
-    # < 2^14.1 (x19 < 2^18.3) into limb 0 in the second, limb 1 gets nothing from limb 0
-    assert 19 * (((2**25 + 2**39) >> 25) + 1) < 2**18.3
-    for i in range(2, 10):   # limb i <= mask_i + (t_{i-1} >> 25), t_{i-1} <= mask + 2^39 - 1
-        mask = (2**26 if i % 2 == 0 else 2**25) - 1
-        assert mask + ((2**26 - 1 + 2**39 - 1) >> 25) <= T_LP[i]
     # one-pass lp_sub: a + 4p - b < 2^29, carry < 2^4, x19 into limb 0 < 2^9
     assert max(a + b for a, b in zip(P15_, P4)) < 2**29
     assert 19 * (2**29 >> 25) < 2**18.3

@@ -17,3 +17,8 @@ for r in 1 2; do for v in var/c1 var/c2 narwhal_amd; do
 NW_LIB=$PWD/$v/libnarwhal_amd.so NW_BENCH_DETAIL=$O/b.json timeout -k 10 300 python -u bench.py --workload batch --steps 10 --no-cpu-baseline > /dev/null 2> $O/b.err || { tail -20 $O/b.err; exit 1; }
 python3 -c "import json; d=json.load(open('$O/b.json'))['verify_batch_10k']; print('$v config1 latency ms %.4f mean %.4f resident %.1f M/s %s' % (d['latency_ms'], d['latency_ms_mean'], d['verifies_per_s_resident']/1e6, d['parity']))"
 done; done
+# (3) the Horner wave at issue priority 3 (var/p3) with 1 / 2 / 3 workgroups per CU
+for lds in 98304 65536 49152; do for v in narwhal_amd var/p3; do
+NW_PIP_FUSE_LDS=$lds NW_LIB=$PWD/$v/libnarwhal_amd.so NW_BENCH_DETAIL=$O/b.json timeout -k 10 300 python -u bench.py --workload batch --steps 10 --no-cpu-baseline > /dev/null 2> $O/b.err || { tail -20 $O/b.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/b.json'))['verify_batch_10k']; print('lds=$lds $v config1 latency ms %.4f mean %.4f resident %.1f M/s %s' % (d['latency_ms'], d['latency_ms_mean'], d['verifies_per_s_resident']/1e6, d['parity']))"
+done; done
