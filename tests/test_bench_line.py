@@ -78,9 +78,14 @@ def test_bench_gpus2_spawns_ranks():
                NW_BENCH_DETAIL=os.path.join(ROOT, "gpurun_out", "bench_n2_detail.json"))
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
+    # every leg the driver's N > 1 run times (strict, SHA-512, certificates, verify_batch,
+    # wire ingest) at toy sizes; the latency legs (service, worker) are per-process
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
                         "--steps", "2", "--warmup", "1", "--items-per-gpu", "65536",
-                        "--unique", "8192", "--no-sha", "--no-cert", "--no-batch", "--no-wire",
+                        "--unique", "8192", "--sha-batches", "256", "--sha-unique", "16",
+                        "--certs", "2048", "--cert-unique", "512", "--committees", "4",
+                        "--cert-payload-committees", "", "--batch-many", "2",
+                        "--wire-frames", "512", "--wire-steps", "1",
                         "--no-worker", "--no-service", "--no-cpu-baseline"],
                        env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stderr[-3000:]
@@ -89,3 +94,6 @@ def test_bench_gpus2_spawns_ranks():
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["parity"] == "ok", r
     assert r["config"]["items_total"] == 2 * 65536
+    s = r["summary"]
+    assert s["sha512"]["GB_s"] > 0 and s["cert_stream_Mcerts_s"]["N4"] > 0
+    assert s["batch10k"]["resident_M_s"] > 0 and s["wire_Mcerts_s"] > 0
