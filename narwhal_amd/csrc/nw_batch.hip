@@ -2253,7 +2253,7 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
                 uint64_t i0, uint64_t i1, uint32_t pmin, uint64_t npip, uint64_t pmax,
                 const uint32_t* pks, const uint32_t* sigs, const uint32_t* z16,
                 const z_key_t& zkey, const bv_ws& w, int32_t* status, uint64_t* fail_index,
-                const pip_group_t& grp, hipStream_t stream, const batch_fork_t* fk,
+                const pip_group_t& grp, hipStream_t stream,
                 uint32_t* fctr) {
   const bool group = grp.cert_vote_offsets != nullptr;
   const uint32_t extra = group ? grp.nkeys : 0;   // key sums
@@ -2262,34 +2262,8 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
   // one large batch alone in its slice (config 1's call): the fused head and tail
   const bool fused = pip_fuse_on() && !group && npip == 1 && e - b == 1 && pmax >= kFuseMinN &&
                      pmax <= kFuseMaxN && npip <= pip_win_lp_max();
-  const bool fuse_head = fused && pip_fuse_head_on() && !(fk && fk->s2);
-  if (fk && fk->s2 && !group) {
-    // Forked (config 1's one call): the digit lanes (role 0: hash, scalars, digits) and the
-    // window sorts, which read only digits, run on `stream` while the R / A decompressions
-    // (roles 1, 2: the 255-squaring chains) run on s2; the b-sum / first-failure block of
-    // the sort needs both, so it joins on s2. The bucket pass waits for s2. The sort no
-    // longer sits between the decompressions and the buckets (~25 us of a 10k batch).
-    // (An event's wait takes the record made before it: `a` is recorded twice.)
-    hipError_t fe = hipEventRecord(fk->a, stream);
-    if (fe == hipSuccess) fe = hipStreamWaitEvent(fk->s2, fk->a, 0);
-    if (fe != hipSuccess) return fe;
-    hipLaunchKernelGGL(k_pip_points, dim3((unsigned)((wv * 2 * 64 + 255) / 256)), dim3(256), 0,
-                       fk->s2, digests, offsets, b, e, i0, i1, pmin, pks, sigs, z16, zkey,
-                       w.items, w.tabs, grp, 2u, 1u);
-    hipLaunchKernelGGL(k_pip_points, dim3((unsigned)((wv * 64 + 255) / 256)), dim3(256), 0,
-                       stream, digests, offsets, b, e, i0, i1, pmin, pks, sigs, z16, zkey,
-                       w.items, w.tabs, grp, 1u, 0u);
-    fe = hipEventRecord(fk->a, stream);
-    if (fe == hipSuccess) fe = hipStreamWaitEvent(fk->s2, fk->a, 0);
-    if (fe != hipSuccess) return fe;
-    hipLaunchKernelGGL(k_pip_sort, dim3(1, (unsigned)npip), dim3(1024), 0, fk->s2, w.pip_list,
-                       offsets, b, i0, extra, pmin, w.tabs, w.items, (uint32_t)kPipWin);
-    hipLaunchKernelGGL(k_pip_sort, dim3(kPipWin, (unsigned)npip), dim3(1024), 0, stream,
-                       w.pip_list, offsets, b, i0, extra, pmin, w.tabs, w.items, 0u);
-    fe = hipEventRecord(fk->b, fk->s2);
-    if (fe == hipSuccess) fe = hipStreamWaitEvent(stream, fk->b, 0);
-    if (fe != hipSuccess) return fe;
-  } else if (fuse_head) {
+  const bool fuse_head = fused && pip_fuse_head_on();
+  if (fuse_head) {
     // one large batch alone (config 1's call): points and sorts in one launch
     const uint32_t npb = (uint32_t)((wv + 3) / 4 + (2 * wv + 3) / 4);   // digit + point WGs
     static const uint32_t lds = (uint32_t)env_u64_zero("NW_PIP_FUSE_LDS", kFuseLds);
@@ -2386,7 +2360,7 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                int32_t* status, uint64_t* fail_index, hipStream_t stream,
                                const key_tables_t* keys, const uint32_t* skip_group_ok,
                                uint64_t skip_per_group, double active_frac,
-                               const batch_fork_t* fork, uint32_t* fuse_ctr) {
+                               uint32_t* fuse_ctr) {
   const key_tables_t kt = keys ? *keys : key_tables_t{nullptr, nullptr, nullptr};
   const batch_skip_t sk{skip_group_ok, skip_per_group ? skip_per_group : 1};
   if (nbatches == 0) return hipSuccess;
@@ -2435,7 +2409,7 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
     const uint64_t i0 = host_offsets[b], i1 = host_offsets[e];
     const unsigned nblk = (unsigned)((e - b + 1023) / 1024);
     // the caller's zeroed counters (fused path only, verify_batch_outputs_direct)
-    const bool own_ctr = fuse_ctr && !fork && nbatches == 1 && pip_fuse_head_on() &&
+    const bool own_ctr = fuse_ctr && nbatches == 1 && pip_fuse_head_on() &&
                          verify_batch_outputs_direct(nbatches, nitems);
     if (npip == e - b && own_ctr) {
       // the fused head and tail read neither the Pippenger list nor zeroed workspace
@@ -2467,7 +2441,7 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                          w.items, w.tabs, kt, sk);
     if (npip) {
       const hipError_t pe = launch_pip(digests, offsets, b, e, i0, i1, pmin, npip, pmax, pks,
-                                       sigs, z16, zkey, w, status, fail_index, nogrp, stream, fork,
+                                       sigs, z16, zkey, w, status, fail_index, nogrp, stream,
                                        own_ctr ? fuse_ctr : w.chunk_start);
       if (pe != hipSuccess) return pe;
     }
@@ -2628,7 +2602,7 @@ hipError_t launch_cert_groups(const uint32_t* cert_digest, const uint64_t* cvo,
     if (i1 > i0) {
       const hipError_t pe = launch_pip(cert_digest, gofs, g, e, i0, i1, pmin, e - g, pmax, pks,
                                        sigs, nullptr, zkey, w, nullptr, nullptr, grp, stream,
-                                       nullptr, w.chunk_start);
+                                       w.chunk_start);
       if (pe != hipSuccess) return pe;
     }
     hipError_t err = hipGetLastError();

@@ -134,99 +134,9 @@ NW_HD void fe_join(fe& h, uint64_t a, uint64_t b) {
   h.v[1] += (uint32_t)(t0 >> 26);
 }
 
-#ifndef NW_MAC_CHAINS
-#define NW_MAC_CHAINS 2
-#endif
-
-#if NW_MAC_CHAINS == 5
-// Variant (NW_MAC_CHAINS=5, measured slower): five interleaved carry-folded
-// chains of two columns each (columns 2c and 2c + 1). On gfx950 a v_mad_u64_u32 whose
-// accumulator was written two instructions before needs one wait state (the hazard
-// recognizer inserts s_nop 0); with two chains most MACs pay one. Five chains put four
-// independent MACs between dependent ones: the strict kernel's s_nops drop 1,469 -> 181, yet
-// it ran 4 % slower (92.6 vs 96.7 M/s, same-process A/B): at 3 waves per SIMD the other waves
-// issue during the nops, and the five joins and accumulators cost instructions and spills.
-// Joins: chain c's final carry (column 2c + 1) goes into limb 2c + 2 (times 19 into limb 0
-// for c = 4), re-split once, so limbs 1, 3, 5, 7, 9 receive < 2^17.3 / 2^13
-// (tests/test_field_bounds.py).
-NW_HD constexpr uint32_t limb_bits(int i) { return (i & 1) ? 25u : 26u; }
-
-NW_HD void fe_join5(fe& h, const uint64_t acc[5]) {
-#pragma unroll
-  for (int c = 0; c < 5; ++c) h.v[2 * c + 1] = (uint32_t)acc[c] & ((1u << limb_bits(2 * c + 1)) - 1);
-#pragma unroll
-  for (int c = 0; c < 5; ++c) {
-    const uint64_t carry = acc[c] >> limb_bits(2 * c + 1);
-    const int t = (2 * c + 2) % 10;
-    const uint64_t x = (uint64_t)h.v[t] + (c == 4 ? carry * 19 : carry);
-    h.v[t] = (uint32_t)x & ((1u << limb_bits(t)) - 1);
-    h.v[t + 1] += (uint32_t)(x >> limb_bits(t));
-  }
-}
-
-NW_HD void fe_mul(fe& h, const fe& f, const fe& g) {
-  uint32_t F[10], F2[10], G[10], G19[10];
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    F[i] = f.v[i];
-    F2[i] = 2 * f.v[i];
-    G[i] = g.v[i];
-    G19[i] = 19 * g.v[i];
-  }
-  uint64_t acc[5] = {0, 0, 0, 0, 0};
-#pragma unroll
-  for (int s = 0; s < 20; ++s) {
-#pragma unroll
-    for (int c = 0; c < 5; ++c) {
-      const int k = 2 * c + s / 10, i = s % 10, j = (k - i + 10) % 10;
-      const uint32_t l = ((i & 1) && (j & 1)) ? F2[i] : F[i];
-      const uint32_t r = (i + j >= 10) ? G19[j] : G[j];
-      acc[c] = mac(acc[c], l, r);
-      if (s == 9) {
-        h.v[2 * c] = (uint32_t)acc[c] & ((1u << limb_bits(2 * c)) - 1);
-        acc[c] >>= limb_bits(2 * c);
-      }
-    }
-  }
-  fe_join5(h, acc);
-}
-
-// Column k of f^2: pairs i <= j with i + j = k (mod 10); coefficient 2 (i != j) x 2 (both
-// odd) x 19 (i + j >= 10), split as left {f, 2f} x right {f, 2f, 19f, 38f}.
-NW_HD void fe_sq(fe& h, const fe& f) {
-  uint32_t F[10], F2[10], F19[10], F38[10];
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    F[i] = f.v[i];
-    F2[i] = 2 * f.v[i];
-    F19[i] = 19 * f.v[i];
-    F38[i] = 2 * F19[i];
-  }
-  uint64_t acc[5] = {0, 0, 0, 0, 0};
-  // step s of chain c: its first column has 6 terms (even k), its second 5 (odd k)
-#pragma unroll
-  for (int s = 0; s < 11; ++s) {
-#pragma unroll
-    for (int c = 0; c < 5; ++c) {
-      const int k = 2 * c + (s < 6 ? 0 : 1), n = s < 6 ? s : s - 6;
-      // n-th pair of column k: non-wrapping i = 0.. while i <= k - i, then wrapping
-      // i = k + 1.. while i <= k + 10 - i
-      const int nlo = k / 2 + 1;
-      const int i = n < nlo ? n : k + 1 + (n - nlo);
-      const int j = n < nlo ? k - i : k + 10 - i;
-      const bool odd2 = (i & 1) && (j & 1), wrap = i + j >= 10;
-      const uint32_t l = i != j ? F2[i] : F[i];
-      const uint32_t r = wrap ? (odd2 ? F38[j] : F19[j]) : (odd2 ? F2[j] : F[j]);
-      acc[c] = mac(acc[c], l, r);
-      if (s == 5) {
-        h.v[2 * c] = (uint32_t)acc[c] & ((1u << limb_bits(2 * c)) - 1);
-        acc[c] >>= limb_bits(2 * c);
-      }
-    }
-  }
-  fe_join5(h, acc);
-}
-#else
+// (Five interleaved chains of two columns each measured 4 % slower in the strict kernel: fewer
+// s_nop wait states, but at 3 waves per SIMD the other waves issue during them, and the
+// extra joins and accumulators cost instructions and spills)
 NW_HD void fe_mul(fe& h, const fe& f, const fe& g) {
   const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
   const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
@@ -338,7 +248,6 @@ NW_HD void fe_sq(fe& h, const fe& f) {
   a = mac(a, f7, f7_38);
   fe_join(h, a, b);
 }
-#endif
 
 // h = f^(2^n), rolled loop (keeps code size down inside the exponentiations).
 NW_HD void fe_sqn(fe& h, const fe& f, int n) {

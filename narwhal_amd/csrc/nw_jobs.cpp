@@ -352,22 +352,10 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
   rc = fill_key(key);
   if (rc) return job_abort(j, rc);
   const uint64_t* h_off = reinterpret_cast<const uint64_t*>(j->hbuf + o_off);
-  ensure_fork(j);
-  const nw::batch_fork_t fk{j->fork.s2, j->fork.ev_fork, j->fork.ev_join};
-  // NW_BATCH_FORK=1: the Pippenger digit lanes and sorts beside the decompressions on a
-  // second stream. Measured slower for config 1's one call (0.405 vs 0.371 ms: the
-  // cross-stream event waits cost more than the 25 us sort they hide), so off by default.
-  static const bool fork_on = [] {
-    const char* e = getenv("NW_BATCH_FORK");
-    return e && *e == '1';
-  }();
-  const bool fork = fork_on && j->fork.s2;
-  // a lone large batch (config 1's call): the verdict is written straight into the pinned
-  // buffer by the one kernel that computes it, no copy back. (Its inputs still go over in
-  // one H2D: read from the pinned buffer by the head instead, they cost the head's digit
-  // lanes 24 -> 56 us and its decompressions 74 -> 100 us, the ~27 us the copy takes;
-  // profiles/r05e, r05f.)
-  const bool out_direct = direct && !fork;
+  // (The Pippenger digit lanes and sorts on a second stream beside the decompressions
+  // measured slower for config 1's one call, 0.405 vs 0.371 ms: the cross-stream event waits
+  // cost more than the 25 us sort they hid; the fused head runs them side by side instead.)
+  const bool out_direct = direct;
   if (out_direct && (!j->dfz || j->dfz_dirty)) {
     if (!j->dfz &&
         hipMalloc(reinterpret_cast<void**>(&j->dfz), nw::verify_batch_fuse_ctr_bytes()) != hipSuccess) {
@@ -388,8 +376,7 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
         reinterpret_cast<const uint32_t*>(ibuf + o_sig), nitems,
         z16 ? reinterpret_cast<const uint32_t*>(ibuf + o_z) : nullptr, key, j->dbuf + o_ws,
         reinterpret_cast<int32_t*>(obuf + o_st), reinterpret_cast<uint64_t*>(obuf + o_fi),
-        j->stream, nullptr, nullptr, 0, 1.0, fork ? &fk : nullptr,
-        out_direct ? j->dfz : nullptr);
+        j->stream, nullptr, nullptr, 0, 1.0, out_direct ? j->dfz : nullptr);
     if (e != hipSuccess && out_direct) j->dfz_dirty = true;   // the head may have run
     JOB_HIP(e, "verify_batch launch");
     return 0;

@@ -90,12 +90,6 @@ bool verify_batch_outputs_direct(uint64_t nbatches, uint64_t nitems);
 // a zeroed device array of this size (fuse_ctr, e.g. shipped with its inputs' H2D copy),
 // which saves the kernel that would zero them.
 size_t verify_batch_fuse_ctr_bytes();
-// Optional second stream for launch_verify_batch's Pippenger batches (decompressions beside
-// the digit lanes and sorts) and two events it records (reused per call).
-struct batch_fork_t {
-  hipStream_t s2;
-  hipEvent_t a, b;
-};
 // skip_group_ok (optional, device): batch b is settled (status Ok) when
 // skip_group_ok[b / skip_per_group] != 0 (launch_cert_groups, launch_votes_keyed);
 // active_frac: the caller's estimate of the fraction of votes not skipped (chunk sizing).
@@ -107,7 +101,7 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                const key_tables_t* keys = nullptr,
                                const uint32_t* skip_group_ok = nullptr,
                                uint64_t skip_per_group = 0, double active_frac = 1.0,
-                               const batch_fork_t* fork = nullptr, uint32_t* fuse_ctr = nullptr);
+                               uint32_t* fuse_ctr = nullptr);
 
 // Certificate::verify vote batches merged over groups of certificates (nw_batch.hip):
 // cert_group_size() = certificates per group, 0 when the merge does not apply;

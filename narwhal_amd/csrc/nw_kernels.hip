@@ -24,10 +24,6 @@
 #include <atomic>
 #include <mutex>
 
-#ifndef NW_STRICT_PLAIN_KEYED
-#define NW_STRICT_PLAIN_KEYED 0
-#endif
-
 namespace nw {
 
 struct dev_consts {
@@ -177,10 +173,8 @@ struct vote_planes_t {
 #ifndef NW_STRICT_PF
 #define NW_STRICT_PF 1
 #endif
-#ifndef NW_KEYED_PF
-#define NW_KEYED_PF 0   // 1: the keyed comb checks through the same LDS slots (measured slower)
-#endif
-#if (NW_STRICT_PF && NW_BWIN != 8) || NW_KEYED_PF
+// (The keyed comb checks through the same slots measured slower)
+#if NW_STRICT_PF && NW_BWIN != 8
 __shared__ uint4 s_pf[10][256];
 struct pf_lds {
   static constexpr bool enabled = true;
@@ -312,11 +306,7 @@ __global__ __launch_bounds__(256, NW_KEYED_WAVES) void k_strict_keyed(
                                 msgs + (uint64_t)msg_stride_words * gi};
     fe X, Z;
     st = keyed_vote_check(src, g_consts.sk, bcomb_wide{bcomb},
-                          keytab_wide{keys.tabs + kKeyTab * (uint64_t)kk}, keys.ok[kk], X, Z
-#if NW_KEYED_PF
-                          , pf_lds{(uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)}
-#endif
-    );
+                          keytab_wide{keys.tabs + kKeyTab * (uint64_t)kk}, keys.ok[kk], X, Z);
     if (st >= kVotePending) {
 #pragma unroll
       for (int k = 0; k < 10; ++k) {
@@ -518,11 +508,7 @@ __global__ __launch_bounds__(256, NW_KEYED_WAVES) void k_votes_keyed(
       const strict_src_global src{pks + 8 * v, sigs + 16 * v, cert_digest + 8 * (uint64_t)c};
       fe X, Z;
       st = keyed_vote_check(src, g_consts.sk, bcomb_wide{bcomb},
-                            keytab_wide{keys.tabs + kKeyTab * (uint64_t)kk}, keys.ok[kk], X, Z
-#if NW_KEYED_PF
-                            , pf_lds{(uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)}
-#endif
-      );
+                            keytab_wide{keys.tabs + kKeyTab * (uint64_t)kk}, keys.ok[kk], X, Z);
       if (st >= kVotePending) {
 #pragma unroll
         for (int k = 0; k < 10; ++k) {
@@ -876,9 +862,7 @@ hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
   if (eb != hipSuccess) return eb;
   const char* kf = getenv("NW_STRICT_KEYED_FAST");
   if (!kt.vote_key) {
-    // -DNW_STRICT_PLAIN_KEYED=1: the keyed/list instance here too (the A/B of the
-    // specialisation, tools/strict_variants.py)
-    hipLaunchKernelGGL(k_verify_strict<NW_STRICT_PLAIN_KEYED != 0>, dim3(grid), dim3(256), 0,
+    hipLaunchKernelGGL(k_verify_strict<false>, dim3(grid), dim3(256), 0,
                        stream, msgs,
                        msg_stride_words, pks, sigs, n, status, bitmap,
                        static_cast<ge_cached*>(workspace), kt, btw, bcomb, nullptr, nullptr);

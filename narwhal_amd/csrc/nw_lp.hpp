@@ -11,22 +11,18 @@
 // for odd j with even k), with f_j broadcast by DPP row_newbcast. The four independent
 // products of each formula stage run in the four rows.
 //
-// Cross-lane moves stay in the VALU (NW_LP_XLANE=1, the default): g_{k-j} is DPP row_shr:j
-// of g and the wrapped g_{k+10-j} is row_shl:(10-j) of 19 g (lanes 10..15 hold 0, so each
-// shift contributes exactly its own lanes), the x2 of odd x odd limbs is folded into g's odd
-// source lanes for odd j; a coordinate is broadcast to all four rows by gfx950's
-// v_permlane16_swap + v_permlane32_swap (three instructions for all four rows). NW_LP_XLANE=0
-// is the earlier ds_bpermute form (an LDS-path round trip per move, 0.52 us per doubling).
+// Cross-lane moves stay in the VALU: g_{k-j} (or the wrapped 19 g_{k+10-j}) is one DPP
+// row_ror:j of g with the wrap parked in the dead lanes (lp_mul), the x2 of odd x odd limbs
+// is folded into g's odd source lanes for odd j; a coordinate is broadcast to all four rows
+// by gfx950's v_permlane16_swap + v_permlane32_swap (three instructions for all four rows).
+// (The round-2 ds_bpermute form, an LDS-path round trip per move, took 0.52 us per doubling;
+// the round-4 shift pair per term, row_shr:j + row_shl:(10-j) + an add, 0.43 us.)
 //
 // Operand discipline is nw_point.hpp's (same products, same first/second operand roles:
 // the second operand is the one scaled by 19, the first by 2); lp_carry64 leaves limbs in
 // the T_LP bound, for which tests/test_field_bounds.py checks every operand pair.
 #pragma once
 #include "nw_point.hpp"
-
-#ifndef NW_LP_XLANE
-#define NW_LP_XLANE 1
-#endif
 
 namespace nw {
 
@@ -40,9 +36,6 @@ struct lp_ctx {
   uint32_t p4;         // limb k of 4p (0 above limb 9)
   uint32_t odd;        // 1 in odd limbs (the source side of the x2 of odd x odd limbs)
   uint32_t m1, m2;     // ~0 in rows with bit 0 / bit 1 of the row index set (lp_sel masks)
-  uint32_t rot[10];    // ds_bpermute address of limb (k - j) mod 10 of this row
-  uint32_t c19[10];    // 19 where column k wraps past limb 9 (k < j), else 1
-  uint32_t s2[10];     // 1 for odd j with even k (the x2 of odd x odd limbs), else 0
 };
 
 __device__ __forceinline__ lp_ctx lp_init(uint32_t lane) {
@@ -57,14 +50,6 @@ __device__ __forceinline__ lp_ctx lp_init(uint32_t lane) {
   c.odd = c.k & 1;
   c.m1 = (c.row & 1) ? ~0u : 0u;
   c.m2 = (c.row & 2) ? ~0u : 0u;
-  const uint32_t base = 16 * c.row;
-#pragma unroll
-  for (int j = 0; j < 10; ++j) {
-    const uint32_t src = live ? (c.k + 10 - j) % 10 : 15u;   // lane 15 of a row holds 0
-    c.rot[j] = 4 * (base + src);
-    c.c19[j] = (live && (int)c.k < j) ? 19u : 1u;
-    c.s2[j] = ((j & 1) && !(c.k & 1)) ? 1u : 0u;
-  }
   return c;
 }
 
@@ -72,9 +57,6 @@ __device__ __forceinline__ lp_ctx lp_init(uint32_t lane) {
 template <int CTRL>
 __device__ __forceinline__ uint32_t lp_dpp(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, true);
-}
-__device__ __forceinline__ uint32_t lp_perm(uint32_t addr, uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)addr, (int)x);
 }
 
 // Carry of value x (64-bit) of limb k into limb k+1 (limb 9's times 19 into limb 0):
@@ -107,27 +89,6 @@ __device__ __forceinline__ uint32_t lp_carry32(const lp_ctx& c, uint32_t x) {
   return (x & c.mask) + lp_carry_in32(c, x >> c.sh);
 }
 
-template <int J>
-__device__ __forceinline__ uint64_t lp_mac(const lp_ctx& c, uint64_t acc, uint32_t f,
-                                           uint32_t gj) {
-  const uint32_t fj = lp_dpp<0x150 + J>(f) << c.s2[J];   // row_newbcast:J, x2 odd x odd
-  return acc + (uint64_t)fj * (gj * c.c19[J]);
-}
-
-#if NW_LP_XLANE
-// term j of column k: f_j (row_newbcast:j) x [g_{k-j} (row_shr:j) + 19 g_{k+10-j} (row_shl:
-// (10-j))]; odd j reads the operand whose odd limbs are doubled.
-template <int J>
-__device__ __forceinline__ uint64_t lp_mac2(uint64_t acc, uint32_t f, uint32_t g,
-                                            uint32_t g19) {
-  const uint32_t gj = J == 0 ? g : lp_dpp<0x110 + J>(g) + lp_dpp<0x100 + 10 - J>(g19);
-  return acc + (uint64_t)lp_dpp<0x150 + J>(f) * gj;
-}
-
-#ifndef NW_LP_ROR
-#define NW_LP_ROR 1
-#endif
-#if NW_LP_ROR
 // Term j of column k from ONE rotate: the row's dead lanes 10..15 carry the wrapped operand
 // (lane L holds 19 g_{L-6}), so row_ror:j hands lane k < j exactly 19 g_{k+10-j} and lane
 // k >= j g_{k-j}. For j >= 7 the wrap also reaches lanes 7..9, so those terms rotate a second
@@ -157,46 +118,11 @@ __device__ __forceinline__ uint32_t lp_mul(const lp_ctx& c, uint32_t f, uint32_t
   a = lp_mac_ror<8>(a, f, he);   b = lp_mac_ror<9>(b, f, ho);
   return lp_carry64(c, a + b);
 }
-#else
-// h = f g (fe_mul's operand roles: f first, g second; g's limbs x 38 / x 19 stay in 32 bits,
-// tests/test_field_bounds.py).
-__device__ __forceinline__ uint32_t lp_mul(const lp_ctx& c, uint32_t f, uint32_t g) {
-  const uint32_t go = g << c.odd, ge19 = g * 19u, go19 = go * 19u;
-  uint64_t a = 0, b = 0;   // two chains
-  a = lp_mac2<0>(a, f, g, ge19);  b = lp_mac2<1>(b, f, go, go19);
-  a = lp_mac2<2>(a, f, g, ge19);  b = lp_mac2<3>(b, f, go, go19);
-  a = lp_mac2<4>(a, f, g, ge19);  b = lp_mac2<5>(b, f, go, go19);
-  a = lp_mac2<6>(a, f, g, ge19);  b = lp_mac2<7>(b, f, go, go19);
-  a = lp_mac2<8>(a, f, g, ge19);  b = lp_mac2<9>(b, f, go, go19);
-  return lp_carry64(c, a + b);
-}
-#endif
-#else
-// h = f g (fe_mul's operand roles: f first, g second).
-__device__ __forceinline__ uint32_t lp_mul(const lp_ctx& c, uint32_t f, uint32_t g) {
-  uint32_t gr[10];
-#pragma unroll
-  for (int j = 0; j < 10; ++j) gr[j] = lp_perm(c.rot[j], g);
-  uint64_t a = 0, b = 0;   // two chains
-  a = lp_mac<0>(c, a, f, gr[0]); b = lp_mac<1>(c, b, f, gr[1]);
-  a = lp_mac<2>(c, a, f, gr[2]); b = lp_mac<3>(c, b, f, gr[3]);
-  a = lp_mac<4>(c, a, f, gr[4]); b = lp_mac<5>(c, b, f, gr[5]);
-  a = lp_mac<6>(c, a, f, gr[6]); b = lp_mac<7>(c, b, f, gr[7]);
-  a = lp_mac<8>(c, a, f, gr[8]); b = lp_mac<9>(c, b, f, gr[9]);
-  return lp_carry64(c, a + b);
-}
-#endif
-
-// Limb k of row q, in every row.
-__device__ __forceinline__ uint32_t lp_row(const lp_ctx& c, uint32_t q, uint32_t x) {
-  return lp_perm(4 * (16 * q + c.k), x);
-}
 // Limb k of rows 0..3, each in every row.
 struct lp_rows {
   uint32_t r0, r1, r2, r3;
 };
 __device__ __forceinline__ lp_rows lp_rows_of(const lp_ctx& c, uint32_t x) {
-#if NW_LP_XLANE
   // permlane16_swap(x, x): odd rows of the first copy <-> even rows of the second, giving
   // rows (0, 0, 2, 2) and (1, 1, 3, 3); permlane32_swap of each with itself: upper half of
   // the first copy <-> lower half of the second, giving (0, 0, 0, 0) / (2, 2, 2, 2) etc.
@@ -205,9 +131,6 @@ __device__ __forceinline__ lp_rows lp_rows_of(const lp_ctx& c, uint32_t x) {
   const auto e = __builtin_amdgcn_permlane32_swap(p[0], p[0], false, false);
   const auto o = __builtin_amdgcn_permlane32_swap(p[1], p[1], false, false);
   return {e[0], o[0], e[1], o[1]};
-#else
-  return {lp_row(c, 0, x), lp_row(c, 1, x), lp_row(c, 2, x), lp_row(c, 3, x)};
-#endif
 }
 // Row-wise select as three bitfield inserts (v_bfi_b32): a ternary chain on the row index
 // is compiled into divergent branches with every operand sunk into its own arm.

@@ -22,15 +22,6 @@
 #define NW_BWIN 24
 #endif
 
-#ifndef NW_TAB_RELOAD
-#define NW_TAB_RELOAD 0
-#endif
-#ifndef NW_DBL_UNROLL
-#define NW_DBL_UNROLL 0
-#endif
-#ifndef NW_LAST_T
-#define NW_LAST_T 0   // 1: T3 also for a window's last addition (A/B variant)
-#endif
 #include "nw_ladder.hpp"
 
 namespace nw {
@@ -144,18 +135,8 @@ NW_HD void build_table8(ge_cached tab[8], const ge& P, const fe& d2) {
   tab[1] = cj;
 #pragma unroll 1
   for (int j = 3; j <= 8; ++j) {
-#if NW_TAB_RELOAD
-    // 1*P re-read from the lane's own table slot instead of held in 40 registers
-    const ge_cached* t0 = tab;
-#ifdef __HIP_DEVICE_COMPILE__
-    asm volatile("" : "+v"(t0));   // a fresh load each iteration, not hoisted
-#endif
-    ge_cached c = *t0;
-    ge_add_cached(acc, acc, c, true);
-#else
     // P is affine (Z = 1): 2 Z1 Z2 = 2 Z1, one multiplication fewer than a cached addition
     ge_add_any(acc, acc, c1, true, true);
-#endif
     ge_to_cached(cj, acc, d2);
     tab[j - 1] = cj;
   }
@@ -626,9 +607,6 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
   int W = ((bu > bv ? bu : bv) + 3) / 4;
   if (W < 32) W = 32;
   W = wave_max(W);
-#ifdef NW_EXP_NO_LADDER
-  W = 0;   // timing experiment only (tools/strict_variants.py): the cost without the ladder
-#endif
 
   // One rolled doubling and one addition routine serve every term (code size: the ladder
   // body stays inside the instruction cache). Per 4-bit window j: 4 doublings, then the
@@ -692,7 +670,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
         }
         if (cur) {
           ge_cached_cneg(e, d < 0);
-          ge_add_any(acc, acc, e, niels, NW_LAST_T || slot != nslots - 1);
+          ge_add_any(acc, acc, e, niels, slot != nslots - 1);
         }
       }
     }
@@ -700,11 +678,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
 #pragma unroll 1
   for (int j = W - 1; j >= 0; --j) {
     if (j != W - 1) {
-#if NW_DBL_UNROLL
-#pragma unroll
-#else
 #pragma unroll 1
-#endif
       for (int t = 0; t < 4; ++t) ge_dbl(acc, acc, t == 3);
     }
     const int p0 = 4 * j, p1 = 4 * j + 128;
@@ -733,7 +707,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
           bt((slot == 3 || !has0) ? 1 : 0, ad, e);
         }
         ge_cached_cneg(e, d < 0);
-        ge_add_any(acc, acc, e, slot >= 2, NW_LAST_T || slot != nslots - 1);
+        ge_add_any(acc, acc, e, slot >= 2, slot != nslots - 1);
       }
     }
   }
