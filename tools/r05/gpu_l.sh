@@ -1,0 +1,11 @@
+# Round 5: the -m gpu suite on the cleaned-up sources, then the strict kernel's A/B against
+# the previous build is not needed (the ladder code is unchanged); a default bench line.
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r05l; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > $O/gputests.log 2>&1 || { tail -40 $O/gputests.log; exit 1; }
+tail -2 $O/gputests.log
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+NW_BENCH_DETAIL=$O/bench_detail.json timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['parity'], d['summary']['batch10k'], d['summary']['service']['N50'])"
