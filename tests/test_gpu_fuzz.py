@@ -289,3 +289,87 @@ def test_fuzz_irregular_committees_unkeyed_fallback():
     r = subprocess.run([sys.executable, "-c", f"ROOT = {root!r}\n" + _FALLBACK_CHILD], env=env,
                        capture_output=True, text=True, timeout=100)
     assert r.returncode == 0 and "IRREGULAR_FALLBACK_OK" in r.stdout, r.stderr[-3000:]
+
+
+# ---- Signature::verify_batch / verify over irregular keys (Straus, Pippenger, fused) ------
+# Batches whose votes come from a key pool with mixed-order, small-order, non-canonical and
+# undecodable members (tests/irregular.py) among honest ones, with a sprinkle of byte damage,
+# odd R encodings, s + l and high bits; sizes across the chunked-Straus path, the Pippenger
+# path (n >= 512) and config 1's fused one-call launches (a lone batch of 2,925..16,384).
+# Injected coefficients: every batch status == the oracle's; every item's strict status too.
+def _irregular_vote_corpus(sizes, seed, bad=0.03, irr=0.08, kinds=None):
+    """kinds: the irregular member kinds (default all); the decodable ones alone let large
+    batches reach the random linear combination instead of failing fast on a decode."""
+    import irregular as I
+    from narwhal_amd import crypto as C
+    rng = np.random.Generator(np.random.PCG64([seed, 77]))
+    honest = [I.Member("honest", rng, kp) for kp in O.keys(48)]
+    odd_kinds = [I.Member(k, rng) for k in (kinds or I.KINDS) for _ in range(3)]
+    nb = len(sizes)
+    off = np.zeros(nb + 1, np.uint64)
+    off[1:] = np.cumsum(sizes)
+    n = int(off[-1])
+    dig = rng.integers(0, 256, size=(nb, 32), dtype=np.uint8)
+    bidx = np.repeat(np.arange(nb), sizes)
+    who = rng.integers(0, len(honest), size=n)
+    irregular_item = rng.random(n) < irr
+    pks = np.array([np.frombuffer(honest[w].pk, np.uint8) for w in who]).reshape(-1, 32)
+    sks = np.array([np.frombuffer(honest[w].sk, np.uint8) for w in who]).reshape(-1, 64)
+    sigs = C.sign_many(sks, dig[bidx]) if n else np.zeros((0, 64), np.uint8)
+    odd = _odd_encodings()
+    for i in np.nonzero(irregular_item)[0]:
+        m = odd_kinds[int(rng.integers(0, len(odd_kinds)))]
+        pks[i] = np.frombuffer(m.pk, np.uint8)
+        sigs[i] = np.frombuffer(m.sign(dig[bidx[i]].tobytes()), np.uint8)
+    for i in np.nonzero(rng.random(n) < bad)[0]:
+        kind = int(rng.integers(0, 5 if kinds is None else 4))   # no key damage with kinds
+        if kind == 0:
+            sigs[i, int(rng.integers(0, 64))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+        elif kind == 1:
+            sigs[i, :32] = np.frombuffer(odd[int(rng.integers(0, len(odd)))], np.uint8)
+        elif kind == 2:
+            v = int.from_bytes(sigs[i, 32:].tobytes(), "little") + L_ORDER
+            sigs[i, 32:] = np.frombuffer((v % 2**256).to_bytes(32, "little"), np.uint8)
+        elif kind == 3:
+            sigs[i, 63] |= np.uint8(0x40)
+        else:
+            pks[i, int(rng.integers(0, 32))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    z16 = rng.integers(0, 256, size=(max(n, 1), 16), dtype=np.uint8)
+    return dig, pks, sigs, off, z16, bidx
+
+
+DECODABLE = ("mixed", "small", "noncanon")
+
+
+@pytest.mark.parametrize("sizes,seed,irr,bad,kinds", [
+    ([0, 1, 2, 3, 5, 8, 17, 33, 67, 100, 189, 190, 300], 61, 0.08, 0.03, None),
+    ([1, 2, 3, 5, 8, 17, 33, 67, 100, 189, 190, 300] * 2, 67, 0.01, 0.002, DECODABLE),
+    ([511, 512, 600, 1024, 40, 7], 62, 0.003, 0.0005, DECODABLE),
+    ([2000, 3, 64, 900], 63, 0.002, 0.0005, DECODABLE),
+    ([3000], 64, 0.001, 0.0, DECODABLE), ([5000], 65, 0.0006, 0.0, ("mixed",)),
+    ([700], 66, 0.003, 0.0, ("mixed", "small")), ([3000], 68, 0.08, 0.03, None)])
+def test_fuzz_irregular_keys_verify_batch_and_strict(sizes, seed, irr, bad, kinds):
+    from narwhal_amd import crypto as C
+    dig, pks, sigs, off, z16, bidx = _irregular_vote_corpus(np.array(sizes), seed, bad, irr, kinds)
+    ost = O.verify_batch_many(dig, pks, sigs, off, z16)
+    for rep in range(2):
+        st = C.verify_batch_many(dig, pks, sigs, off, z16)
+        assert st.tolist() == ost.tolist(), (rep, st.tolist(), ost.tolist())
+    if len(pks):
+        sst, _ = C.verify_strict_many(dig[bidx], pks, sigs)
+        osst = O.verify_strict_many(dig[bidx], pks, sigs)
+        bad = np.nonzero(sst != osst)[0]
+        assert not len(bad), [(int(i), int(sst[i]), int(osst[i])) for i in bad[:10]]
+    # one batch alone through the blocking call: status AND failing index (crypto_tests.rs
+    # 96-115 shape), against the oracle's verify_batch
+    b = int(np.argmax(np.diff(off)))
+    a, e = int(off[b]), int(off[b + 1])
+    votes = [(C.PublicKey(pks[i].tobytes()), C.Signature.from_bytes(sigs[i].tobytes()))
+             for i in range(a, e)]
+    ost1, oix1 = O.verify_batch(dig[b].tobytes(), pks[a:e], sigs[a:e], z16[a:e])
+    try:
+        C.Signature.verify_batch(C.Digest(dig[b].tobytes()), votes, z16=z16[a:e].tobytes())
+        got = (0, 0)
+    except C.CryptoError as err:
+        got = (err.code, err.index)
+    assert got == (ost1, oix1 if ost1 else 0), (got, ost1, oix1)
