@@ -1420,12 +1420,15 @@ def main():
             result["wire_ingest"] = rw
             if rw["parity"] != "ok":
                 result["parity"] = "FAIL"
-        if not args.no_worker:
+        # the latency legs are per process (one service / worker loop and its host threads):
+        # at N > 1 rank 0 runs them while the other ranks wait at the final barrier, so that
+        # N load generators do not compete for the node's cores
+        if not args.no_worker and rank == 0:
             rwk = run_worker_latency(args, rank, world)
             result["worker_latency"] = rwk
             if rwk["parity"] != "ok":
                 result["parity"] = "FAIL"
-        if not args.no_service:
+        if not args.no_service and rank == 0:
             result["service_latency"] = {}
             for N in [int(x) for x in args.service_committees.split(",") if x]:
                 rs = run_service_latency(args, rank, world, N)

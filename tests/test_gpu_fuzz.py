@@ -167,7 +167,8 @@ def test_fuzz_certificates_through_service_vs_oracle():
 # Injected coefficients: every (status, index) == the oracle on the small-job kernel, the
 # bulk keyed pipeline and the per-certificate path. Random coefficients (the service, the
 # merged-group and small-group policies): every verdict is one the oracle gives for some
-# coefficient set (irregular.possible_verdicts over 64 sets).
+# coefficient set (irregular.possible_verdicts over 64 sets, widened to 4,096 more sets for a
+# verdict outside them: irregular.verdict_possible).
 IRREGULAR_SHAPES = [(4, 160, 21), (7, 160, 22), (10, 120, 23), (20, 60, 24), (50, 24, 25),
                     (100, 12, 26)]
 INJECTED_PATHS = ({"NW_SMALL": "1"}, {"NW_SMALL": "0"}, {"NW_SMALL": "0", "NW_CERT_MERGE": "0"})
@@ -224,7 +225,8 @@ def test_fuzz_irregular_committees_random_z(monkeypatch, N, n, seed):
         for rep in range(2):
             st, ix = M.verify_certificates_many(_Com(com), d, None)
             bad = [(i, int(a), int(x), sorted(poss[i])) for i, (a, x) in enumerate(zip(st, ix))
-                   if (int(a), int(x)) not in poss[i]]
+                   if (int(a), int(x)) not in poss[i]
+                   and not I.verdict_possible(com, d, i, (a, x), seed)]
             assert not bad, (env, rep, kinds, bad[:10])
 
 
@@ -247,7 +249,8 @@ def test_fuzz_irregular_committees_through_service():
     got = asyncio.run(main())
     n = len(rows)
     pairs = [(i, got[i]) for i in range(n)] + [(n - 1 - j, got[n + j]) for j in range(n)]
-    bad = [(i, g, sorted(poss[i])) for i, g in pairs if tuple(g) not in poss[i]]
+    bad = [(i, g, sorted(poss[i])) for i, g in pairs
+           if tuple(g) not in poss[i] and not I.verdict_possible(com, d, i, g, 31)]
     assert not bad, (kinds, bad[:10])
 
 

@@ -58,3 +58,23 @@ def test_irregular_stream_has_coefficient_dependent_certificates():
     poss = I.possible_verdicts(com, p, 16, seed=2)
     assert any(v == {(0, 0)} for v in poss)        # votes without the mixed key: always Ok
     assert any(v == {(0, 0), (48 + 7, 7)} for v in poss)
+
+
+def test_one_certificate_slice_and_widened_search():
+    com, p, _ = I.irregular_stream(7, 30, seed=8, n_irregular=2, kinds=("mixed",))
+    rng = np.random.Generator(np.random.PCG64(4))
+    z16 = rng.integers(0, 256, size=(len(p["vote_pks"]), 16), dtype=np.uint8)
+    st, ix = O.certificates_verify_many(com, p, z16)
+    vo = p["vote_offsets"]
+    for i in range(len(st)):
+        q = I.one_certificate(p, i)
+        s1, x1 = O.certificates_verify_many(com, q, z16[int(vo[i]):int(vo[i + 1])])
+        assert (int(s1[0]), int(x1[0])) == (int(st[i]), int(ix[i]))
+    poss = I.possible_verdicts(com, p, 16, seed=3)
+    split = [i for i, v in enumerate(poss) if len(v) > 1]
+    assert split
+    for i in split[:3]:
+        for v in poss[i]:
+            assert I.verdict_possible(com, p, i, v, seed=9, sets=512)
+    # a verdict no coefficient set gives
+    assert not I.verdict_possible(com, p, split[0], (48 + 4, 0), seed=9, sets=64)
