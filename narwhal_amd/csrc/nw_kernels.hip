@@ -167,15 +167,16 @@ struct vote_planes_t {
 #define NW_KEYED_WAVES 1
 #endif
 // The strict ladder's LDS prefetcher (nw_strict.hpp pf_none for the contract): one
-// 160-byte slot per lane (10 chunks of 16 B, chunk k of lane l at s_pf[k][l]: the lanes of a
-// wave write and read 16 consecutive bytes each, conflict-free), 40 KB per 256-thread block,
-// 120 KB at 3 blocks per CU.
+// 128-byte slot per lane (8 chunks of 16 B, chunk k of lane l at s_pf[k][l]: the lanes of a
+// wave write and read 16 consecutive bytes each, conflict-free), 32 KB per 256-thread block,
+// 96 KB at 3 blocks per CU. Every entry is one 128-byte line: a B-table entry (affine niels,
+// ge_niels_pad) or a per-lane entry packed to 128 B (ge_cached_pk; unpacked here).
 #ifndef NW_STRICT_PF
 #define NW_STRICT_PF 1
 #endif
 // (The keyed comb checks through the same slots measured slower)
 #if NW_STRICT_PF && NW_BWIN != 8
-__shared__ uint4 s_pf[10][256];
+__shared__ uint4 s_pf[8][256];
 struct pf_lds {
   static constexpr bool enabled = true;
   uint32_t wave;   // wave index in the block (uniform)
@@ -183,41 +184,39 @@ struct pf_lds {
     const uint4* g = static_cast<const uint4*>(src);
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this lane's last slot read is done
 #pragma unroll
-    for (int k = 0; k < 10; ++k)
+    for (int k = 0; k < 8; ++k)
       if (k < chunks) __builtin_amdgcn_global_load_lds(g + k, &s_pf[k][wave * 64], 16, 0, 0);
   }
   __device__ void get(ge_cached& e, bool niels) const {
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the DMA into LDS has landed
     asm volatile("" ::: "memory");
-    uint32_t* w = reinterpret_cast<uint32_t*>(&e);
     const uint32_t l = threadIdx.x;
+    uint32_t p[32];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {   // YpX, YmX
+    for (int k = 0; k < 8; ++k) {
       const uint4 v = s_pf[k][l];
-      w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+      p[4 * k] = v.x; p[4 * k + 1] = v.y; p[4 * k + 2] = v.z; p[4 * k + 3] = v.w;
     }
-    uint32_t t[20];
+    if (niels) {   // y+x, y-x, xy2d (-> YpX, YmX, T2d; Z2 unused)
 #pragma unroll
-    for (int k = 5; k < 10; ++k) {
-      if (k < 8 || !niels) {
-        const uint4 v = s_pf[k][l];
-        t[4 * (k - 5)] = v.x; t[4 * (k - 5) + 1] = v.y; t[4 * (k - 5) + 2] = v.z;
-        t[4 * (k - 5) + 3] = v.w;
+      for (int i = 0; i < 10; ++i) {
+        e.YpX.v[i] = p[i];
+        e.YmX.v[i] = p[10 + i];
+        e.T2d.v[i] = p[20 + i];
       }
+      return;
     }
-    // cached: words 20..39 = Z2, T2d; niels: words 20..29 = xy2d (-> T2d), Z2 unused
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      e.T2d.v[i] = niels ? t[i] : t[10 + i];
-      e.Z2.v[i] = t[i];
-    }
+    fe_unpack(e.YpX, p);
+    fe_unpack(e.YmX, p + 8);
+    fe_unpack(e.Z2, p + 16);
+    fe_unpack(e.T2d, p + 24);
   }
 };
 #endif
 
 // Persistent: the grid covers the resident waves once and strides over the items, so the
-// per-lane tables j*A, j*R live in a fixed workspace (16 entries x 160 B per lane slot, lane-
-// contiguous: a lookup reads 160 consecutive bytes per lane instead of 40 scattered dwords).
+// per-lane tables j*A, j*R live in a fixed workspace (16 packed entries x 128 B per lane slot,
+// lane-contiguous: a lookup reads one 128-byte line per lane instead of 40 scattered dwords).
 #ifndef NW_STRICT_WAVES
 #define NW_STRICT_WAVES 3
 #endif
@@ -232,7 +231,7 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
                                                        const uint32_t* __restrict__ sigs,
                                                        uint64_t n, int32_t* __restrict__ status,
                                                        uint64_t* __restrict__ bitmap,
-                                                       ge_cached* __restrict__ tabs,
+                                                       ge_cached_pk* __restrict__ tabs,
                                                        key_tables_t keys,
                                                        const ge_niels_pad* __restrict__ btw,
                                                        const ge_niels_pad* __restrict__ bcomb,
@@ -252,8 +251,8 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
 #else
   const btab_wide bt{btw, bdigits<NW_BWIN>::ENTRIES};
 #endif
-  ge_cached* tabA = tabs + 16 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
-  ge_cached* tabR = tabA + 8;
+  ge_cached_pk* tabA = tabs + 16 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  ge_cached_pk* tabR = tabA + 8;
 #pragma unroll 1
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n;
        base += (uint64_t)gridDim.x * blockDim.x) {
@@ -845,6 +844,7 @@ static unsigned strict_grid() {
 // The keyed fast path reuses the per-lane table region for its limb planes (84 B per item of
 // a slice) and keeps its list (4 B per item) and count in a tail after it.
 constexpr uint64_t kKeyedSliceMax = 1ull << 22;
+// (sized for 160-byte entries; the packed ones use 128 of each 160)
 static size_t strict_tabs_bytes() { return (size_t)strict_grid() * 256 * 16 * sizeof(ge_cached); }
 size_t strict_workspace_bytes() { return strict_tabs_bytes() + 4 * kKeyedSliceMax + 256; }
 
@@ -865,13 +865,13 @@ hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
     hipLaunchKernelGGL(k_verify_strict<false>, dim3(grid), dim3(256), 0,
                        stream, msgs,
                        msg_stride_words, pks, sigs, n, status, bitmap,
-                       static_cast<ge_cached*>(workspace), kt, btw, bcomb, nullptr, nullptr);
+                       static_cast<ge_cached_pk*>(workspace), kt, btw, bcomb, nullptr, nullptr);
     return hipGetLastError();
   }
   if (kf && kf[0] == '0') {
     hipLaunchKernelGGL(k_verify_strict<true>, dim3(grid), dim3(256), 0, stream, msgs,
                        msg_stride_words, pks, sigs, n, status, bitmap,
-                       static_cast<ge_cached*>(workspace), kt, btw, bcomb, nullptr, nullptr);
+                       static_cast<ge_cached_pk*>(workspace), kt, btw, bcomb, nullptr, nullptr);
     return hipGetLastError();
   }
   // keyed fast path (k_strict_keyed above), slice by slice through the workspace
@@ -894,7 +894,7 @@ hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
     // the leftovers: full verification (exact status codes), the tables over the planes
     hipLaunchKernelGGL(k_verify_strict<true>, dim3(std::min<uint64_t>(strict_grid(), grid_for(ns, 256))),
                        dim3(256), 0, stream, msgs, msg_stride_words, pks, sigs, ns, status,
-                       bitmap, static_cast<ge_cached*>(workspace), kt, btw, bcomb, list, count);
+                       bitmap, static_cast<ge_cached_pk*>(workspace), kt, btw, bcomb, list, count);
   }
   if (bitmap)
     hipLaunchKernelGGL(k_status_bitmap, dim3(grid_for(n, 256)), dim3(256), 0, stream, status, n,

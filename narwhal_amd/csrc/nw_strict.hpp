@@ -97,14 +97,72 @@ NW_HD void ge_from_cached_not(ge& r, const ge_cached& c) {
   fe_copy(r.Z, c.Z2);
 }
 
+// A per-lane table entry packed into one 128-byte line (the device kernel's tables; the host
+// self-check runs both forms): the four coordinates
+// of the cached form, each carried to limbs < 2^26 / 2^25 (limb 1 < 2^26) and packed into 8
+// words (limb widths 26, 26, 26, 25, 26, 25, 26, 25, 26, 25 = 256 bits). A 160-byte entry
+// spans two 128-byte lines, so each lookup fetches 256 bytes; a packed one fetches 128
+// (20.2 -> 12 KB of HBM traffic per strict verification; the unpacking, 7 funnel shifts
+// and 10 masks per coordinate, costs less than the second line: DESIGN.md 5).
+struct alignas(16) ge_cached_pk { uint32_t w[32]; };
+
+NW_HD uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __builtin_amdgcn_alignbit(hi, lo, s);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> s);
+#endif
+}
+NW_HD void fe_pack(uint32_t* w, const fe& f) {
+  const uint32_t* v = f.v;
+  w[0] = v[0] | v[1] << 26;
+  w[1] = v[1] >> 6 | v[2] << 20;
+  w[2] = v[2] >> 12 | v[3] << 14;
+  w[3] = v[3] >> 18 | v[4] << 7;
+  w[4] = v[4] >> 25 | v[5] << 1 | v[6] << 26;
+  w[5] = v[6] >> 6 | v[7] << 20;
+  w[6] = v[7] >> 12 | v[8] << 13;
+  w[7] = v[8] >> 19 | v[9] << 7;
+}
+NW_HD void fe_unpack(fe& f, const uint32_t* w) {
+  f.v[0] = w[0] & M26;
+  f.v[1] = funnel(w[1], w[0], 26) & M26;
+  f.v[2] = funnel(w[2], w[1], 20) & M26;
+  f.v[3] = funnel(w[3], w[2], 14) & M25;
+  f.v[4] = funnel(w[4], w[3], 7) & M26;
+  f.v[5] = (w[4] >> 1) & M25;
+  f.v[6] = funnel(w[5], w[4], 26) & M26;
+  f.v[7] = funnel(w[6], w[5], 20) & M25;
+  f.v[8] = funnel(w[7], w[6], 13) & M26;
+  f.v[9] = w[7] >> 7;
+}
+NW_HD void tab_put(ge_cached* t, int j, const ge_cached& c) { t[j] = c; }
+NW_HD void tab_put(ge_cached_pk* t, int j, const ge_cached& c) {
+  fe t2;
+  fe_copy(t2, c.T2d);
+  fe_carry(t2);   // a product's limbs 1 and 6 may sit just above their width
+  fe_pack(t[j].w, c.YpX);
+  fe_pack(t[j].w + 8, c.YmX);
+  fe_pack(t[j].w + 16, c.Z2);
+  fe_pack(t[j].w + 24, t2);
+}
+NW_HD void tab_get(const ge_cached* t, int j, ge_cached& e) { e = t[j]; }
+NW_HD void tab_get(const ge_cached_pk* t, int j, ge_cached& e) {
+  fe_unpack(e.YpX, t[j].w);
+  fe_unpack(e.YmX, t[j].w + 8);
+  fe_unpack(e.Z2, t[j].w + 16);
+  fe_unpack(e.T2d, t[j].w + 24);
+}
+
 #ifndef NW_TAB_DBL
 #define NW_TAB_DBL 0   // 1: four doublings + three mixed additions (measured 0.5 % slower, r02b)
 #endif
 
-NW_HD void build_table8(ge_cached tab[8], const ge& P, const fe& d2) {
+template <class Tab>
+NW_HD void build_table8(Tab* tab, const ge& P, const fe& d2) {
   ge_cached c1;
   ge_to_cached(c1, P, d2);
-  tab[0] = c1;
+  tab_put(tab, 0, c1);
 #if NW_TAB_DBL
   // P is affine (decompressed, Z = 1), so its additions are mixed (2 Z1 instead of Z1 Z2).
   // Four doublings and three mixed additions instead of one doubling and six additions,
@@ -123,7 +181,7 @@ NW_HD void build_table8(ge_cached tab[8], const ge& P, const fe& d2) {
       if (dbl) ge_dbl(cur, cur, true);
       else ge_add_any(cur, cur, c1, true, true);
       ge_to_cached(cj, cur, d2);
-      tab[dst] = cj;
+      tab_put(tab, dst, cj);
     }
     return;
   }
@@ -132,13 +190,13 @@ NW_HD void build_table8(ge_cached tab[8], const ge& P, const fe& d2) {
   ge_dbl(acc, P, true);
   ge_cached cj;
   ge_to_cached(cj, acc, d2);
-  tab[1] = cj;
+  tab_put(tab, 1, cj);
 #pragma unroll 1
   for (int j = 3; j <= 8; ++j) {
     // P is affine (Z = 1): 2 Z1 Z2 = 2 Z1, one multiplication fewer than a cached addition
     ge_add_any(acc, acc, c1, true, true);
     ge_to_cached(cj, acc, d2);
-    tab[j - 1] = cj;
+    tab_put(tab, j - 1, cj);
   }
 }
 
@@ -300,8 +358,9 @@ struct bcomb_lazy {
 // (nw_kernels.hip pf_lds) loads the NEXT addition's entry straight into LDS
 // (global_load_lds_dwordx4, no registers) while the current addition or the window's four
 // doublings run, so the ladder's ~77 dependent table loads per verification stop stalling
-// the wave. issue(src, chunks): 16-byte chunks at src (10 = ge_cached, 8 = ge_niels_pad);
-// get(e, niels): wait for it and read it (niels: Y+x, Y-x, xy2d into YpX, YmX, T2d).
+// the wave. issue(src, chunks): 16-byte chunks at src (8: a packed per-lane entry or a
+// ge_niels_pad; 10: an unpacked ge_cached); get(e, niels): wait for it and read it (niels:
+// Y+x, Y-x, xy2d into YpX, YmX, T2d).
 struct pf_none {
   static constexpr bool enabled = false;
   NW_HD void issue(const void*, int) const {}
@@ -544,9 +603,9 @@ NW_HD int strict_keyed_comb(const Src& src, const strict_consts& K, const BComb&
 // Status of one strict verification. wave_max maps this lane's ladder length (in 4-bit
 // windows) to the wave's maximum (identity on the host). tabA/tabR: 8 entries each of
 // per-lane scratch. bt: j*B and j*2^128 B, j = 0..2^(BW-1) (btab_pair / btab_wide).
-template <int BW, class BTab, class Src, class WaveMax, class PF = pf_none>
+template <int BW, class BTab, class Src, class WaveMax, class PF = pf_none, class Tab = ge_cached>
 NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab& bt,
-                             ge_cached* tabA, ge_cached* tabR,
+                             Tab* tabA, Tab* tabR,
                              WaveMax wave_max, const PF& pf = PF{}) {
   using BD = bdigits<BW>;
   // Decompress A, then R, in one rolled loop (one copy of the sqrt_ratio_i chain in the
@@ -644,7 +703,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
       int d0;
       bool nl0;
       const void* s0 = slot_src(W - 1, 0, d0, nl0);
-      if (s0) pf.issue(s0, nl0 ? 8 : 10);
+      if (s0) pf.issue(s0, nl0 ? 8 : int(sizeof(Tab) / 16));
     }
 #pragma unroll 1
     for (int j = W - 1; j >= 0; --j) {
@@ -666,7 +725,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
           int d2;
           bool n2;
           const void* nx = slot_src(j2, s2, d2, n2);
-          if (nx) pf.issue(nx, n2 ? 8 : 10);
+          if (nx) pf.issue(nx, n2 ? 8 : int(sizeof(Tab) / 16));
         }
         if (cur) {
           ge_cached_cneg(e, d < 0);
@@ -702,7 +761,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
         const int ad = d < 0 ? -d : d;
         ge_cached e;
         if (slot < 2) {
-          e = (slot == 0 ? tabA : tabR)[ad - 1];
+          tab_get(slot == 0 ? tabA : tabR, ad - 1, e);
         } else {
           bt((slot == 3 || !has0) ? 1 : 0, ad, e);
         }

@@ -155,7 +155,7 @@ def test_half_split_lehmer_equals_one_step(hc):
         assert outs[0] == outs[1], k
 
 
-@pytest.mark.parametrize("bw", [16, 8, 20, 24])
+@pytest.mark.parametrize("bw", [16, 8, 20, 24, -16, -24])
 def test_strict_half_edge_corpus(hc, golden, bw):
     for it in golden["edge_corpus"]["items"]:
         m, pk, sig = (bytes.fromhex(it[k]) for k in ("msg", "pk", "sig"))
@@ -303,5 +303,5 @@ def test_strict_half_random_and_tampered(hc):
             sig[int(rng.integers(0, 32))] ^= 1 << int(rng.integers(0, 8))
         k = O.hram(bytes(sig[:32]), pk, m)
         want = O.verify_strict(m, pk, bytes(sig))
-        for bw in (16, 8, 20, 24):
+        for bw in (16, 8, 20, 24, -24):   # -24: packed per-lane table entries
             assert hc.hc_verify_strict_half(_b(pk), _b(bytes(sig)), _b(k), bw) == want

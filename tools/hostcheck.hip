@@ -129,7 +129,8 @@ int hc_half_split_onestep(const uint8_t k32[32], uint8_t u32[32], uint8_t v20[20
 
 // The kernel's strict verification (nw_strict.hpp), k supplied (device-only SHA), with
 // B windows of bw = 16 bits (wide tables; the host-built copy), 8 bits (LDS tables) or
-// 20 / 24 bits (entries computed per lookup).
+// 20 / 24 bits (entries computed per lookup). bw < 0: |bw| with the per-lane tables packed
+// into 128-byte entries (ge_cached_pk, NW_PACK_TAB).
 int hc_verify_strict_half(const uint8_t pk[32], const uint8_t sig[64], const uint8_t k32[32],
                           int bw) {
   init();
@@ -139,6 +140,11 @@ int hc_verify_strict_half(const uint8_t pk[32], const uint8_t sig[64], const uin
   ge_cached ta[8], tr[8];
   const strict_src_arrays src{Aw, Rw, Sw, kw};
   auto id = [](int w) { return w; };
+  if (bw < 0) {
+    ge_cached_pk pa[8], pr[8];
+    if (bw == -24) return strict_verify_core<24>(src, SK, btab_lazy{BT, &SK.k.d2}, pa, pr, id);
+    return strict_verify_core<16>(src, SK, btab_wide{BTW, BTW_N}, pa, pr, id);
+  }
   if (bw == 8) return strict_verify_core<8>(src, SK, btab_pair{BT, B128}, ta, tr, id);
   if (bw == 20) return strict_verify_core<20>(src, SK, btab_lazy{BT, &SK.k.d2}, ta, tr, id);
   if (bw == 24) return strict_verify_core<24>(src, SK, btab_lazy{BT, &SK.k.d2}, ta, tr, id);
