@@ -168,18 +168,26 @@ struct vote_planes_t {
 #endif
 // The strict ladder's LDS prefetcher (nw_strict.hpp pf_none for the contract): one
 // 128-byte slot per lane (8 chunks of 16 B, chunk k of lane l at s_pf[k][l]: the lanes of a
-// wave write and read 16 consecutive bytes each, conflict-free), 32 KB per 256-thread block,
-// 96 KB at 3 blocks per CU. Every entry is one 128-byte line: a B-table entry (affine niels,
-// ge_niels_pad) or a per-lane entry packed to 128 B (ge_cached_pk; unpacked here).
+// wave write and read 16 consecutive bytes each, conflict-free), 32 KB per 256-thread block.
+// Every entry is one 128-byte line: a B-table entry (affine niels, ge_niels_pad) or a
+// per-lane entry packed to 128 B (ge_cached_pk; unpacked here).
 #ifndef NW_STRICT_PF
 #define NW_STRICT_PF 1
 #endif
 // (The keyed comb checks through the same slots measured slower)
 #if NW_STRICT_PF && NW_BWIN != 8
+// The ladder's digit words (u, |v|, w recoded: 21 per lane) live in LDS too, 21 KB per block:
+// read with a wave-uniform index once per addition, they were otherwise a scratch array (a
+// dependent scratch load per addition; scratch 272 -> 180 B per lane, +0.2 % in the same
+// process, profiles/r05w). 53 KB per block: three blocks per CU fit the 160 KB.
 __shared__ uint4 s_pf[8][256];
+__shared__ uint32_t s_dig[21][256];
 struct pf_lds {
   static constexpr bool enabled = true;
+  static constexpr bool lds_digits = true;
   uint32_t wave;   // wave index in the block (uniform)
+  __device__ void dput(int k, uint32_t v) const { s_dig[k][threadIdx.x] = v; }
+  __device__ uint32_t dget(int k) const { return s_dig[k][threadIdx.x]; }
   __device__ void issue(const void* src, int chunks) const {
     const uint4* g = static_cast<const uint4*>(src);
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this lane's last slot read is done

@@ -271,12 +271,16 @@ struct bdigits {
       c >>= 32;
     }
   }
-  // digit m (wave-uniform) of the recoded words
-  NW_HD static int digit(const uint32_t wd[8], int m) {
+  // digit m (wave-uniform) of the recoded words, word i read by get(i)
+  template <class Get>
+  NW_HD static int digit_g(Get get, int m) {
     const int p = BW * m, wi = p >> 5, sh = p & 31;
-    const uint32_t lo = sel8(wd, wi), hi = wi < 7 ? sel8(wd, wi + 1) : 0u;
+    const uint32_t lo = get(wi), hi = wi < 7 ? get(wi + 1) : 0u;
     const uint32_t v = (uint32_t)(((((uint64_t)hi) << 32) | lo) >> sh) & ((1u << BW) - 1);
     return m < NSIGNED ? (int)v - (1 << (BW - 1)) : (int)v;
+  }
+  NW_HD static int digit(const uint32_t wd[8], int m) {
+    return digit_g([&](int i) { return sel8(wd, i); }, m);
   }
 };
 
@@ -361,10 +365,17 @@ struct bcomb_lazy {
 // the wave. issue(src, chunks): 16-byte chunks at src (8: a packed per-lane entry or a
 // ge_niels_pad; 10: an unpacked ge_cached); get(e, niels): wait for it and read it (niels:
 // Y+x, Y-x, xy2d into YpX, YmX, T2d).
+// A prefetcher may also hold the ladder's digit words (lds_digits: dput(k, word) once after
+// the recoding, dget(k) per addition; words 0-7 u, 8-12 |v|, 13-20 w): the words are read
+// with a wave-uniform index, which the compiler otherwise serves from a scratch array (a
+// dependent scratch load per addition).
 struct pf_none {
   static constexpr bool enabled = false;
+  static constexpr bool lds_digits = false;
   NW_HD void issue(const void*, int) const {}
   NW_HD void get(ge_cached&, bool) const {}
+  NW_HD void dput(int, uint32_t) const {}
+  NW_HD uint32_t dget(int) const { return 0; }
 };
 
 // A committee key's comb tables: keytab_wide reads the device copy (keytab[kStrictKeyN t + j]
@@ -676,18 +687,37 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
   if constexpr (PF::enabled) {
     // The same additions in the same order as below; the entry of addition (j, slot) is
     // requested one addition ahead (window j's first one before its doublings).
+    if constexpr (PF::lds_digits) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) { pf.dput(t, ud[t]); pf.dput(13 + t, wd[t]); }
+#pragma unroll
+      for (int t = 0; t < 5; ++t) pf.dput(8 + t, vd[t]);
+    }
+    // digit j of u / |v| (4-bit, biased by 8) and digit m of w
+    auto dig4 = [&](int base, int nw, const uint32_t* arr, int j) -> int {
+      if constexpr (PF::lds_digits) {
+        const uint32_t word = (j >> 3) < nw ? pf.dget(base + (j >> 3)) : 0x88888888u;
+        return (int)((word >> ((j & 7) * 4)) & 15u) - 8;
+      } else {
+        return digit4_of(arr, nw, j);
+      }
+    };
+    auto digw = [&](int m) -> int {
+      if constexpr (PF::lds_digits) return BD::digit_g([&](int i) { return pf.dget(13 + i); }, m);
+      else return BD::digit(wd, m);
+    };
     auto slot_src = [&](int j, int slot, int& d, bool& niels) -> const void* {
       const int p0 = 4 * j, p1 = 4 * j + 128;
       const bool has0 = j < 32 && p0 % BW == 0;
       niels = slot >= 2;
       if (slot == 0) {
-        d = digit4_of(ud, 8, j);
+        d = dig4(0, 8, ud, j);
       } else if (slot == 1) {
-        d = j < 40 ? digit4_of(vd, 5, j) : 0;
+        d = j < 40 ? dig4(8, 5, vd, j) : 0;
         if (h.vneg) d = -d;
       } else {
         const bool t1 = slot == 3 || !has0;
-        d = BD::digit(wd, t1 ? p1 / BW : p0 / BW);
+        d = digw(t1 ? p1 / BW : p0 / BW);
         return d ? static_cast<const void*>(bt.entry(t1 ? 1 : 0, d < 0 ? -d : d)) : nullptr;
       }
       const int ad = d < 0 ? -d : d;
