@@ -491,6 +491,11 @@ __global__ __launch_bounds__(256) void k_bv_chunks(
     uint64_t* __restrict__ fail_index, const uint32_t* __restrict__ ctotal) {
   __shared__ ge_niels s_btab[129];
   __shared__ ge_niels s_b128[129];
+  const uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nch = min(nchunks, *ctotal);   // host bound, device total
+  // a workgroup with no live chunk leaves before filling its 31 KB of LDS tables (the
+  // certificate path launches for every certificate and runs only the failed ones)
+  if (blockIdx.x * blockDim.x >= nch) return;
   {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(&g_bc.btab[0]);
     const uint32_t* src2 = reinterpret_cast<const uint32_t*>(&g_bc.b128[0]);
@@ -502,9 +507,6 @@ __global__ __launch_bounds__(256) void k_bv_chunks(
     }
   }
   __syncthreads();
-  const uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t nch = min(nchunks, *ctotal);   // host bound, device total
-  if (nch == 0) return;
   const bool live = ci < nch;
   const bv_chunk ch = chunks[live ? ci : nch - 1];
   const uint64_t bidx = b0 + ch.batch;
@@ -594,7 +596,11 @@ __global__ __launch_bounds__(256) void k_bv_chunks(
 
 // ------------------------------------------------------------------------------ combine
 // One 256-thread workgroup per listed batch (k_b == 0 or >= 2): threads sum a strided
-// subset of the chunk points, then a tree through LDS.
+// subset of the chunk points, then a tree through LDS. The grid is bounded
+// (kCombineMaxBlocks) and strides over the device's count of listed batches: the host only
+// knows an upper bound (every certificate of a group, 10^6 at N = 4), and a workgroup per
+// bound that exits at once cost 0.24 ms per config-2 call.
+constexpr uint32_t kCombineMaxBlocks = 2048;
 __global__ __launch_bounds__(256) void k_bv_combine(const uint32_t* __restrict__ multi,
                                                     const uint32_t* __restrict__ multi_first,
                                                     uint32_t nmulti, const uint64_t* __restrict__ offsets,
@@ -605,55 +611,57 @@ __global__ __launch_bounds__(256) void k_bv_combine(const uint32_t* __restrict__
                                                     const uint32_t* __restrict__ mtotal) {
   __shared__ ge s_p[256];
   __shared__ uint32_t s_f[256][4];
-  const uint32_t m = blockIdx.x;
-  if (m >= nmulti || m >= *mtotal) return;   // host bound, device total
+  const uint32_t mt = *mtotal, mend = mt < nmulti ? mt : nmulti;   // device total, host bound
   const int tid = threadIdx.x;
-  const uint64_t bidx = b0 + multi[m];
-  const uint64_t bn = offsets[bidx + 1] - offsets[bidx];
-  const uint32_t kb = (uint32_t)((bn + C - 1) / C);
-  const uint32_t c0 = multi_first[m];
-  const curve_consts& K = g_bc.k;
-  ge acc;
-  ge_identity(acc);
-  uint32_t f[3] = {kNone, kNone, kNone};
-  uint32_t flags0 = 0;
-  for (uint32_t k = tid; k < kb; k += 256) {
-    const bv_chunk_out& o = out[c0 + k];
-    ge_cached c;
-    ge_to_cached(c, o.P, K.d2);
-    ge_add_cached(acc, acc, c, true);
-    if (o.first[0] < f[0]) { f[0] = o.first[0]; flags0 = o.pad; }
-    f[1] = min(f[1], o.first[1]);
-    f[2] = min(f[2], o.first[2]);
-  }
-  s_p[tid] = acc;
-  s_f[tid][0] = f[0]; s_f[tid][1] = f[1]; s_f[tid][2] = f[2]; s_f[tid][3] = flags0;
-  __syncthreads();
-  for (int stride = 128; stride > 0; stride >>= 1) {
-    if (tid < stride && (uint32_t)(tid + stride) < kb) {
+  for (uint32_t m = blockIdx.x; m < mend; m += gridDim.x) {
+    const uint64_t bidx = b0 + multi[m];
+    const uint64_t bn = offsets[bidx + 1] - offsets[bidx];
+    const uint32_t kb = (uint32_t)((bn + C - 1) / C);
+    const uint32_t c0 = multi_first[m];
+    const curve_consts& K = g_bc.k;
+    ge acc;
+    ge_identity(acc);
+    uint32_t f[3] = {kNone, kNone, kNone};
+    uint32_t flags0 = 0;
+    for (uint32_t k = tid; k < kb; k += 256) {
+      const bv_chunk_out& o = out[c0 + k];
       ge_cached c;
-      ge_to_cached(c, s_p[tid + stride], K.d2);
-      ge t;
-      ge_add_cached(t, s_p[tid], c, true);
-      s_p[tid] = t;
-      if (s_f[tid + stride][0] < s_f[tid][0]) {
-        s_f[tid][0] = s_f[tid + stride][0];
-        s_f[tid][3] = s_f[tid + stride][3];
-      }
-      s_f[tid][1] = min(s_f[tid][1], s_f[tid + stride][1]);
-      s_f[tid][2] = min(s_f[tid][2], s_f[tid + stride][2]);
+      ge_to_cached(c, o.P, K.d2);
+      ge_add_cached(acc, acc, c, true);
+      if (o.first[0] < f[0]) { f[0] = o.first[0]; flags0 = o.pad; }
+      f[1] = min(f[1], o.first[1]);
+      f[2] = min(f[2], o.first[2]);
     }
+    s_p[tid] = acc;
+    s_f[tid][0] = f[0]; s_f[tid][1] = f[1]; s_f[tid][2] = f[2]; s_f[tid][3] = flags0;
     __syncthreads();
-  }
-  if (tid == 0) {
-    uint64_t idx = 0;
-    int st = NW_OK;
-    if (bn > 0) {
-      const uint32_t ff[3] = {s_f[0][0], s_f[0][1], s_f[0][2]};
-      st = batch_status(ff, s_f[0][3], ge_is_identity(s_p[0]), bn, &idx);
+    for (int stride = 128; stride > 0; stride >>= 1) {
+      if (tid < stride && (uint32_t)(tid + stride) < kb) {
+        ge_cached c;
+        ge_to_cached(c, s_p[tid + stride], K.d2);
+        ge t;
+        ge_add_cached(t, s_p[tid], c, true);
+        s_p[tid] = t;
+        if (s_f[tid + stride][0] < s_f[tid][0]) {
+          s_f[tid][0] = s_f[tid + stride][0];
+          s_f[tid][3] = s_f[tid + stride][3];
+        }
+        s_f[tid][1] = min(s_f[tid][1], s_f[tid + stride][1]);
+        s_f[tid][2] = min(s_f[tid][2], s_f[tid + stride][2]);
+      }
+      __syncthreads();
     }
-    status[bidx] = st;
-    if (fail_index) fail_index[bidx] = idx;
+    if (tid == 0) {
+      uint64_t idx = 0;
+      int st = NW_OK;
+      if (bn > 0) {
+        const uint32_t ff[3] = {s_f[0][0], s_f[0][1], s_f[0][2]};
+        st = batch_status(ff, s_f[0][3], ge_is_identity(s_p[0]), bn, &idx);
+      }
+      status[bidx] = st;
+      if (fail_index) fail_index[bidx] = idx;
+    }
+    __syncthreads();   // slot 0 read before the next batch's sums overwrite it
   }
 }
 
@@ -2450,9 +2458,10 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                          stream, w.chunks, (uint32_t)chunks, offsets, b, i0, w.items, w.tabs,
                          kt.tabs, w.outs, status, fail_index, w.chunk_start + (e - b));
     if (multi)
-      hipLaunchKernelGGL(k_bv_combine, dim3((unsigned)multi), dim3(256), 0, stream, w.multi,
-                         w.multi_first, (uint32_t)multi, offsets, b, C, w.outs, status,
-                         fail_index, w.plan_tot + 3 * nblk + 1);
+      hipLaunchKernelGGL(k_bv_combine,
+                         dim3((unsigned)std::min<uint64_t>(multi, kCombineMaxBlocks)), dim3(256),
+                         0, stream, w.multi, w.multi_first, (uint32_t)multi, offsets, b, C,
+                         w.outs, status, fail_index, w.plan_tot + 3 * nblk + 1);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
     b = e;
@@ -2516,6 +2525,9 @@ __global__ __launch_bounds__(256) void k_grp_count(
     ++v[1];
     v[2] += batch_st[c] != 0;
   }
+  // wave sums, then the workgroup's through LDS: three atomics per workgroup (one per wave
+  // on one address serialised at the L2: 82 us for a 10^6-certificate call)
+  __shared__ uint32_t s_v[4][3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
 #pragma unroll
@@ -2523,7 +2535,13 @@ __global__ __launch_bounds__(256) void k_grp_count(
   }
   if ((threadIdx.x & 63) == 0) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) atomicAdd(&cnt[k], v[k]);
+    for (int k = 0; k < 3; ++k) s_v[threadIdx.x >> 6][k] = v[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    uint32_t t = 0;
+    for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) t += s_v[wv][threadIdx.x];
+    if (t) atomicAdd(&cnt[threadIdx.x], t);
   }
 }
 
@@ -2545,7 +2563,7 @@ hipError_t launch_group_feedback(const uint32_t* group_ok, uint64_t ncert, uint6
                                  uint32_t* fb, hipStream_t stream) {
   const uint64_t ngroups = K && group_ok ? (ncert + K - 1) / K : 0;
   const uint64_t work = std::max(ngroups, ncert);
-  const unsigned blocks = (unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, (work + 2047) / 2048));
+  const unsigned blocks = (unsigned)std::min<uint64_t>(256, std::max<uint64_t>(1, (work + 2047) / 2048));
   hipLaunchKernelGGL(k_grp_count, dim3(blocks), dim3(256), 0, stream, group_ok, ngroups, ncert,
                      batch_st, pre1, pre2, hdr_st, cnt);
   hipLaunchKernelGGL(k_grp_publish, dim3(1), dim3(1), 0, stream, (uint32_t)ngroups, tag, cnt, fb);
@@ -2975,9 +2993,10 @@ hipError_t launch_cert_sgroups(const uint32_t* cert_digest, const uint64_t* cvo,
                          keys.tabs, w.outs, status, fail_index, w.chunk_start + (be - b));
     }
     if (multi)
-      hipLaunchKernelGGL(k_bv_combine, dim3((unsigned)multi), dim3(256), 0, stream, w.multi,
-                         w.multi_first, (uint32_t)multi, cvo, b, C, w.outs, status, fail_index,
-                         w.plan_tot + 3 * nblk + 1);
+      hipLaunchKernelGGL(k_bv_combine,
+                         dim3((unsigned)std::min<uint64_t>(multi, kCombineMaxBlocks)), dim3(256),
+                         0, stream, w.multi, w.multi_first, (uint32_t)multi, cvo, b, C, w.outs,
+                         status, fail_index, w.plan_tot + 3 * nblk + 1);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
     g = e;
