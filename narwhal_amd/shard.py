@@ -30,6 +30,13 @@ def gather_bitmaps(local_words: torch.Tensor, n_total: int, world: int,
     rank, on local_words' device."""
     if world <= 1:
         return local_words.view(torch.uint8)[: (n_total + 7) // 8]
+    return _gather_words(local_words, n_total, world, group)
+
+
+def _gather_words(local_words: torch.Tensor, n_total: int, world: int,
+                  group=None) -> torch.Tensor:
+    """The all_gather of gather_bitmaps (also with world 1: tests/test_gpu_distributed.py
+    runs it on a one-rank RCCL group)."""
     sizes = [shard_range(n_total, r, world) for r in range(world)]
     max_words = max((e - s + 63) // 64 for s, e in sizes)
     comm_dev = local_words.device

@@ -102,3 +102,38 @@ def test_two_ranks_shard_verify_gather_on_gpu():
     assert st0 == st[: len(st0)].tolist()       # rank 0's statuses == oracle
     ref = np.packbits((st == 0).astype(np.uint8), bitorder="little").tobytes()
     assert full == ref
+
+
+_RCCL_CHILD = r"""
+import os, sys
+sys.path.insert(0, os.environ["NW_ROOT"])
+import torch, torch.distributed as dist
+from narwhal_amd.shard import gather_bitmaps, _gather_words
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ["NW_PORT"], RANK="0",
+                  WORLD_SIZE="1")
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1)
+dev = torch.device("cuda", 0)
+words = torch.arange(7, dtype=torch.int64, device=dev) * 0x0101010101010101
+out = _gather_words(words, 7 * 64, 1)            # the all_gather itself, on the device
+assert out.device == dev and out.dtype == torch.uint8
+assert torch.equal(out.view(torch.int64), words), (out, words)
+full = gather_bitmaps(words, 7 * 64 - 5, 1)
+assert full.numel() == (7 * 64 - 5 + 7) // 8
+dist.destroy_process_group()
+print("rccl ok")
+"""
+
+
+@pytest.mark.timeout(180)
+def test_rccl_all_gather_on_device():
+    """The RCCL ("nccl" backend) branch of gather_bitmaps on the box's one GPU: a one-rank
+    process group, the device-tensor all_gather the driver's 8-GPU run performs (gloo
+    stages through host memory; RCCL gathers device memory directly)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, NW_ROOT=root, NW_PORT=str(_free_port()))
+    p = subprocess.run([sys.executable, "-c", _RCCL_CHILD], env=env, capture_output=True,
+                       text=True, timeout=170)
+    assert p.returncode == 0 and "rccl ok" in p.stdout, p.stderr[-3000:]
