@@ -2026,12 +2026,13 @@ size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems) {
 
 // Committee key tables (a committee's keys, tabulated once while the committee is
 // unchanged): per key the comb tables j * 2^(W t) A (W = kKeyW, t < kKeyCombT,
-// j = 0..2^(W-1), affine niels; nw_kernels.h). Keyed strict checks (headers, votes) take
+// j = 0..2^(W-1), affine niels; nw_kernels.h), plus a j * 2^128 A table when W does not
+// divide 128. Keyed strict checks (headers, votes) take
 // [k]A from them with no doublings; keyed vote chunks use the j * A and j * 2^128 A tables.
 //   k_key_cmp   one block: flag = force or (pks != saved); then saved = pks when they differ.
 //   k_key_base  one lane per key: decompress (dalek semantics), the comb bases 2^(W t) A by
 //               W doublings each; base[2 key] = A, base[2 key + 1] = 2^128 A for the group
-//               path, comb[kKeyCombT key + t] for k_key_tabs.
+//               path, comb[kKeyTables key + t] for k_key_tabs.
 //   k_key_tabs  one lane per run of kKeyRun consecutive entries of one (key, t): j0 * P by
 //               double-and-add, then j * P for the run by additions of P, each point parked
 //               in its own output slot (X, Y, Z and the product of the run's earlier Z's,
@@ -2082,15 +2083,22 @@ __global__ __launch_bounds__(256) void k_key_base(const uint32_t* __restrict__ p
   ok[i] = (dec ? kKeyDecoded : 0u) | (dec && ge_is_small_order(P) ? kKeySmall : 0u) |
           (lam << kKeyLambdaShift);
   base[2 * i] = P;
+  ge H;   // 2^(W floor(128 / W)) A, doubled up to 2^128 A when W does not divide 128
 #pragma unroll 1
   for (int t = 0; t < (int)kKeyCombT; ++t) {
     if (t) {
 #pragma unroll 1
       for (int d = 0; d < (int)kKeyW; ++d) ge_dbl(P, P, d == (int)kKeyW - 1);
     }
-    comb[kKeyCombT * i + t] = P;
-    if (t * kKeyW == 128) base[2 * i + 1] = P;
+    comb[kKeyTables * i + t] = P;
+    if (t == (int)(128 / kKeyW)) H = P;
   }
+  if (kKeyHalfExtra) {
+#pragma unroll 1
+    for (int d = 0; d < (int)(128 % kKeyW); ++d) ge_dbl(H, H, true);
+    comb[kKeyTables * i + kKeyCombT] = H;
+  }
+  base[2 * i + 1] = H;
 }
 
 constexpr uint32_t kKeyRun = 64;
@@ -2107,8 +2115,8 @@ __global__ __launch_bounds__(256) void k_key_tabs(uint64_t nkeys, const ge* __re
                                                   ge_niels_pad* __restrict__ tabs,
                                                   const uint32_t* __restrict__ flag) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= nkeys * kKeyCombT * kKeyRuns || (flag && *flag == 0)) return;
-  const uint64_t pt = g / kKeyRuns;   // kKeyCombT * key + t
+  if (g >= nkeys * kKeyTables * kKeyRuns || (flag && *flag == 0)) return;
+  const uint64_t pt = g / kKeyRuns;   // kKeyTables * key + t
   const uint32_t j0 = (uint32_t)(g % kKeyRuns) * kKeyRun;
   const uint32_t cnt = kKeyN - j0 < kKeyRun ? kKeyN - j0 : kKeyRun;
   const ge P = comb[pt];
@@ -2164,7 +2172,7 @@ __global__ __launch_bounds__(256) void k_key_tabs(uint64_t nkeys, const ge* __re
 
 size_t key_tables_bytes(uint64_t nkeys) {
   const uint64_t n = nkeys ? nkeys : 1;
-  return sizeof(ge_niels_pad) * (uint64_t)kKeyTab * n + sizeof(ge) * (2 + kKeyCombT) * n;
+  return sizeof(ge_niels_pad) * (uint64_t)kKeyTab * n + sizeof(ge) * (2 + kKeyTables) * n;
 }
 
 hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, ge_niels_pad* tabs, uint32_t* ok,
@@ -2178,7 +2186,7 @@ hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, ge_niels_pad* 
                        force ? 1u : 0u, flag);
   hipLaunchKernelGGL(k_key_base, dim3((unsigned)((nkeys + 63) / 64)), dim3(64), 0, stream, pks,
                      nkeys, base, comb, ok, fl);
-  hipLaunchKernelGGL(k_key_tabs, dim3((unsigned)((nkeys * kKeyCombT * kKeyRuns + 255) / 256)),
+  hipLaunchKernelGGL(k_key_tabs, dim3((unsigned)((nkeys * kKeyTables * kKeyRuns + 255) / 256)),
                      dim3(256), 0,
                      stream, nkeys, comb, tabs, fl);
   return hipGetLastError();

@@ -50,8 +50,9 @@ hipError_t launch_sign(const uint32_t* sks, uint32_t sk_stride_words, const uint
 hipError_t upload_batch_consts();
 
 // Pre-decompressed public keys (a committee): per key the comb tables j * 2^(W t) A
-// (W = NW_KEYW = 16: t = 0..15, j = 0..32,768, 67 MB per key; W = 8: t = 0..31,
-// j = 0..128; affine niels) and whether it decompressed. vote_key[i] = key index of vote i,
+// (W = NW_KEYW = 16: t = 0..15, j = 0..32,768, 67 MB per key; 20: t = 0..12 and a j * 2^128 A
+// table, j = 0..2^19, 940 MB per key; 8: t = 0..31, j = 0..128; affine niels) and whether it
+// decompressed. vote_key[i] = key index of vote i,
 // or kNoKey to decompress that vote's key in the kernel (the verdict semantics are
 // unchanged: a key's decompression is deterministic). Keyed strict verifications take [k]A
 // from the 256 / W tables with no doublings; chunks whose votes are all keyed run 8-bit A
@@ -67,10 +68,14 @@ struct key_tables_t {
 #endif
 constexpr uint32_t kNoKey = 0xffffffffu;
 constexpr uint32_t kKeyW = NW_KEYW;                       // bits per comb digit of k
-constexpr uint32_t kKeyCombT = 256 / kKeyW;               // comb tables per key
+constexpr uint32_t kKeyCombT = (253 + kKeyW - 1) / kKeyW; // comb tables per key (k < 2^253)
 constexpr uint32_t kKeyN = (1u << (kKeyW - 1)) + 1;       // entries per table, j = 0..2^(W-1)
-constexpr uint32_t kKeyTab = kKeyCombT * kKeyN;           // entries per key
-constexpr uint32_t kKeyHalf = (128 / kKeyW) * kKeyN;      // offset of the j * 2^128 A table
+// the keyed vote chunks' j * 2^128 A table: comb table 128 / W when W divides 128, else one
+// extra table built from 2^128 A
+constexpr uint32_t kKeyHalfExtra = 128 % kKeyW ? 1 : 0;
+constexpr uint32_t kKeyTables = kKeyCombT + kKeyHalfExtra; // tables built per key
+constexpr uint32_t kKeyTab = kKeyTables * kKeyN;          // entries per key
+constexpr uint32_t kKeyHalf = (kKeyHalfExtra ? kKeyCombT : 128 / kKeyW) * kKeyN;
 // ok[key]: bit 0 = decompressed, bit 1 = small order (8A == identity), bits 2..4 = lambda
 // with [l]A == [lambda]T8 (nw_strict.hpp kKeyLambdaShift: the key's torsion image)
 size_t key_tables_bytes(uint64_t nkeys);

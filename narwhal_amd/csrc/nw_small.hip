@@ -64,7 +64,7 @@ __constant__ small_consts g_sc;
 
 constexpr int kSlotsMax = 64;
 constexpr int kDigits = kStrictKeyTables + kBCombT;   // 16 + 11 comb entries per slot
-static_assert(kDigits == 27, "16 key-comb + 11 B-comb digits");
+static_assert(kDigits <= 27, "at most 16 key-comb + 11 B-comb digits (LDS per slot)");
 
 // Per-slot record (slot_rec, s_rec).
 enum : uint32_t {
@@ -504,10 +504,10 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
         sc k;
         sc_reduce512(k, hx);
         uint32_t kd[8], sd[8];
-        sc_recode(kd, k, kStrictKeyMask);
+        keydigits::recode(kd, k);
         bdigits<kBCombW>::recode(sd, s);
 #pragma unroll
-        for (int t = 0; t < kStrictKeyTables; ++t) s_dig[lane][t] = comb_digit<kStrictKeyW>(kd, t);
+        for (int t = 0; t < kStrictKeyTables; ++t) s_dig[lane][t] = keydigits::digit(kd, t);
 #pragma unroll
         for (int t = 0; t < kBCombT; ++t)
           s_dig[lane][kStrictKeyTables + t] = bdigits<kBCombW>::digit(sd, t);

@@ -316,15 +316,16 @@ struct btab_lazy {
 constexpr int kBCombW = NW_BCOMBW;
 constexpr int kBCombT = bdigits<NW_BCOMBW>::NB;
 constexpr uint32_t kBCombN = bdigits<NW_BCOMBW>::ENTRIES;
-// Committee-key comb width (= nw_kernels.h kKeyW): 256 / W tables j * 2^(W t) A, j = 0..2^(W-1)
+// Committee-key comb width (= nw_kernels.h kKeyW): ceil(253 / W) tables j * 2^(W t) A,
+// j = 0..2^(W-1), over k's digits recoded as bdigits<W> (signed; the top one unsigned when
+// the digits overrun 256 bits, W = 20 / 24)
 #ifndef NW_KEYW
 #define NW_KEYW 16
 #endif
 constexpr int kStrictKeyW = NW_KEYW;
-constexpr int kStrictKeyTables = 256 / kStrictKeyW;   // = nw_kernels.h kKeyCombT
-constexpr uint32_t kStrictKeyN = (1u << (kStrictKeyW - 1)) + 1;
-constexpr uint32_t kStrictKeyMask = kStrictKeyW == 16 ? 0x80008000u : 0x80808080u;
-static_assert(kStrictKeyW == 8 || kStrictKeyW == 16, "NW_KEYW must be 8 or 16");
+using keydigits = bdigits<kStrictKeyW>;
+constexpr int kStrictKeyTables = keydigits::NB;   // = nw_kernels.h kKeyCombT
+constexpr uint32_t kStrictKeyN = keydigits::ENTRIES;
 struct bcomb_wide {
   const ge_niels_pad* t;
   NW_HD const ge_niels_pad* entry(int m, int ad) const {
@@ -408,24 +409,17 @@ struct keytab_lazy {
   }
 };
 
-// acc = [s]B - [k]A for k, s < l: -[k]A as k's 256 / W signed W-bit digits against the
+// acc = [s]B - [k]A for k, s < l: -[k]A as k's ceil(253 / W) W-bit digits against the
 // key's comb tables (kt), [s]B as s's 16 signed 16-bit digits against the B comb (bc). No
 // doublings.
 #ifndef NW_KEYED_SPLIT
 #define NW_KEYED_SPLIT 0   // 1: the A and B terms in two interleaved accumulators (ILP)
 #endif
-// Signed W-bit digit t of a recoded scalar (sc_recode with kStrictKeyMask / 0x80008000).
-template <int W>
-NW_HD int comb_digit(const uint32_t rd[8], int t) {
-  constexpr int per = 32 / W;
-  constexpr uint32_t m = (W == 32) ? 0xffffffffu : ((1u << W) - 1u);
-  return (int)((sel8(rd, t / per) >> ((t % per) * W)) & m) - (1 << (W - 1));
-}
 template <class BComb, class KeyTab, class PF = pf_none>
 NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
                           const KeyTab& kt, const fe& d2, const PF& pf = PF{}) {
   uint32_t kd[8], sd[8];
-  sc_recode(kd, k, kStrictKeyMask);   // k < l: 256 / W signed W-bit digits
+  keydigits::recode(kd, k);           // k < l: ceil(253 / W) W-bit digits
   bdigits<kBCombW>::recode(sd, s);    // s < l: kBCombT digits of kBCombW bits
   ge_identity(acc);
   if constexpr (PF::enabled) {
@@ -434,7 +428,7 @@ NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
     constexpr int KT = kStrictKeyTables, NS = kStrictKeyTables + kBCombT;
     auto step_src = [&](int st, int& d) -> const void* {
       if (st < KT) {
-        d = comb_digit<kStrictKeyW>(kd, st);
+        d = keydigits::digit(kd, st);
         return d ? static_cast<const void*>(kt.entry(st, d < 0 ? -d : d)) : nullptr;
       }
       d = bdigits<kBCombW>::digit(sd, st - KT);
@@ -472,7 +466,7 @@ NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
 #pragma unroll 1
   for (int t = 0; t < (kStrictKeyTables > kBCombT ? kStrictKeyTables : kBCombT); ++t) {
     if (t < kStrictKeyTables) {
-      const int d = comb_digit<kStrictKeyW>(kd, t);
+      const int d = keydigits::digit(kd, t);
       if (d != 0) {
         ge_niels nb;
         kt(t, d < 0 ? -d : d, nb);
@@ -500,7 +494,7 @@ NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
   // -[k]A: digit t of k against table t, negated
 #pragma unroll 1
   for (int t = 0; t < kStrictKeyTables; ++t) {
-    const int d = comb_digit<kStrictKeyW>(kd, t);
+    const int d = keydigits::digit(kd, t);
     if (d != 0) {
       ge_niels nb;
       kt(t, d < 0 ? -d : d, nb);
