@@ -46,6 +46,7 @@ struct SharedDev {
   void* ktabs = nullptr;       // committee key tables (grow-only)
   uint32_t* kok = nullptr;
   size_t kcap = 0;             // keys
+  uint32_t kW = 0;             // their comb width (nw::keyspec)
   uint32_t* ksaved = nullptr;  // the keys the tables were last built from (device)
   uint32_t* kflag = nullptr;   // rebuild flag (device, written by k_key_cmp)
   size_t ksaved_n = 0;         // their count; 0 = none
@@ -564,8 +565,8 @@ size_t cert_workspace_bytes(size_t n, size_t nvotes) {
 // Key tables for a keyed pipeline, or (out of device memory for them or for the keyed B
 // comb) *use_keys = false and 0: the caller then runs unkeyed.
 static int keyed_tables_or_fallback(Lease& lease, size_t nauth, void** tabs, uint32_t** ok,
-                                    uint32_t** saved, uint32_t** flag, bool* force,
-                                    bool* use_keys) {
+                                    nw::keyspec* ks, uint32_t** saved, uint32_t** flag,
+                                    bool* force, bool* use_keys) {
   const nw::ge_niels_pad* bc = nullptr;
   const hipError_t eb = nw::bcomb_table(&bc);
   if (eb == hipErrorOutOfMemory) {
@@ -573,7 +574,7 @@ static int keyed_tables_or_fallback(Lease& lease, size_t nauth, void** tabs, uin
     return 0;
   }
   if (eb != hipSuccess) return ::set_err(NW_E_DEVICE, "keyed B comb build", eb);
-  const int rc = lease.key_tables(nauth, tabs, ok, saved, flag, force);
+  const int rc = lease.key_tables(nauth, tabs, ok, ks, saved, flag, force);
   if (rc == NW_E_OUT_OF_MEMORY) {
     *use_keys = false;
     return 0;
@@ -627,14 +628,15 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
   // (67 MB per key) every check still runs, unkeyed: headers through the strict ladder,
   // votes through each certificate's own verify_batch (same statuses).
   bool use_keys = com.nauth > 0;
-  if (!rc && use_keys) rc = keyed_tables_or_fallback(lease, com.nauth, &ktabs_v, &kok, &ksaved,
-                                                     &kflag, &kforce, &use_keys);
+  nw::keyspec ks{};
+  if (!rc && use_keys) rc = keyed_tables_or_fallback(lease, com.nauth, &ktabs_v, &kok, &ks,
+                                                     &ksaved, &kflag, &kforce, &use_keys);
   if (!rc) rc = lease.strict_ws(&sws);
   if (rc) return rc;
   nw::ge_niels_pad* ktabs = static_cast<nw::ge_niels_pad*>(ktabs_v);
   if (use_keys) {
-    NW_HIP(nw::launch_key_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth, ktabs,
-                                 kok, s, ksaved, kflag, kforce),
+    NW_HIP(nw::launch_key_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth, ks,
+                                 ktabs, kok, s, ksaved, kflag, kforce),
            "k_key_tables");
     lease.keys_built(com.nauth, host_pks);
   }
@@ -644,7 +646,7 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
                                  headers_only ? nullptr : w.vote_cert,
                                  headers_only ? 0 : cs.nvotes, s),
          "k_cert_prepare");
-  const nw::key_tables_t hk{ktabs, kok, w.author_key};
+  const nw::key_tables_t hk{ktabs, kok, w.author_key, ks};
   // With a fork stream (host-buffer jobs) and the keyed vote checks, the headers run on the
   // fork stream while the votes run here: the votes then do not skip header-failed
   // certificates (k_cert_ok_headers settles those after the join), and the two latency
@@ -672,7 +674,7 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
     join_guard.e = fork->ev_join;
   }
   if (!headers_only) {
-    const nw::key_tables_t kt{ktabs, kok, w.vote_key};
+    const nw::key_tables_t kt{ktabs, kok, w.vote_key, ks};
     // Default: the keyed vote checks (launch_votes_keyed): every vote of an undecided
     // certificate through its committee key's comb tables, R compared in compressed form,
     // then verify_batch only for the certificates with a failing vote. A vote that passes
@@ -732,7 +734,7 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
                                     reinterpret_cast<const uint32_t*>(cs.vote_pks),
                                     reinterpret_cast<const uint32_t*>(cs.vote_sigs), cs.nvotes,
                                     key, w.batch_ws, w.group_ws, w.pre1, w.pre2, w.hdr_st, kt,
-                                    nw::key_tables_base(ktabs, com.nauth), (uint32_t)com.nauth,
+                                    nw::key_tables_base(ktabs, com.nauth, ks), (uint32_t)com.nauth,
                                     K, &group_ok, s),
              "certificate groups (votes)");
     if (K && small)
@@ -799,19 +801,20 @@ int votes_pipeline(int dev, const nw_committee& com, size_t n, const uint8_t* id
   void* sws = nullptr;
   int rc = lease.acquire(dev, s);
   bool use_keys = com.nauth > 0;
+  nw::keyspec ks{};
   if (!rc && use_keys)
-    rc = keyed_tables_or_fallback(lease, com.nauth, &ktabs, &kok, &ksaved, &kflag, &kforce,
-                                  &use_keys);
+    rc = keyed_tables_or_fallback(lease, com.nauth, &ktabs, &kok, &ks, &ksaved, &kflag,
+                                  &kforce, &use_keys);
   if (!rc) rc = lease.strict_ws(&sws);
   if (rc) return rc;
   if (use_keys) {
-    NW_HIP(nw::launch_key_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth,
+    NW_HIP(nw::launch_key_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth, ks,
                                  static_cast<nw::ge_niels_pad*>(ktabs), kok, s, ksaved, kflag,
                                  kforce),
            "k_key_tables");
     lease.keys_built(com.nauth, host_pks);
   }
-  const nw::key_tables_t kt{static_cast<nw::ge_niels_pad*>(ktabs), kok, d_key};
+  const nw::key_tables_t kt{static_cast<nw::ge_niels_pad*>(ktabs), kok, d_key, ks};
   NW_HIP(nw::launch_verify_strict(d_dig, 8, reinterpret_cast<const uint32_t*>(authors),
                                   reinterpret_cast<const uint32_t*>(sigs), n, d_sst, d_bm, sws, s,
                                   use_keys ? &kt : nullptr),
@@ -980,7 +983,7 @@ int Lease::acquire(int dev_index, hipStream_t stream) {
 }
 
 int ReadLease::acquire(int dev_index, hipStream_t stream, const uint8_t* pks, size_t nkeys,
-                       const void** tabs, const uint32_t** ok) {
+                       const void** tabs, const uint32_t** ok, nw::keyspec* ks) {
   if (held_) return ::set_err(NW_E_INVALID_ARG, "read lease already held");
   if (dev_index < 0 || dev_index >= kMaxDevices) return ::set_err(NW_E_INVALID_ARG, "bad device");
   SharedDev& d = g_shared[dev_index];
@@ -1001,6 +1004,7 @@ int ReadLease::acquire(int dev_index, hipStream_t stream, const uint8_t* pks, si
   held_ = true;
   *tabs = d.ktabs;
   *ok = d.kok;
+  *ks = nw::keyspec_for(d.kW);
   return 0;
 }
 
@@ -1052,10 +1056,27 @@ int Lease::strict_ws(void** out) {
   return 0;
 }
 
-int Lease::key_tables(size_t nkeys, void** tabs, uint32_t** ok, uint32_t** saved,
-                      uint32_t** flag, bool* force) {
+// Comb width of a committee's key tables: 20 bits (13 tables, 940 MB per key: three fewer
+// additions per keyed check) up to kKeyW20Keys keys, whose tables stay gathered locally;
+// 16 bits (16 tables, 67 MB per key) above, where 20-bit tables outgrow the caches and the
+// device (profiles/r05k20: N = 4 / 10 +7 / +9 %, N = 50 -18 % at 20 bits). NW_KEY_WIDTH
+// = 16 / 20 / 24 forces one width.
+constexpr size_t kKeyW20Keys = 16;
+static uint32_t key_width(size_t nkeys) {
+  static const uint32_t forced = [] {
+    const char* e = getenv("NW_KEY_WIDTH");
+    const uint32_t w = e ? (uint32_t)atoi(e) : 0u;
+    return (w == 16 || w == 20 || w == 24) ? w : 0u;
+  }();
+  if (forced) return forced;
+  return nkeys <= kKeyW20Keys ? 20u : 16u;
+}
+
+int Lease::key_tables(size_t nkeys, void** tabs, uint32_t** ok, nw::keyspec* ks,
+                      uint32_t** saved, uint32_t** flag, bool* force) {
   SharedDev& d = g_shared[dev_];
-  if (nkeys > d.kcap || !d.ktabs) {
+  const uint32_t W = key_width(nkeys);
+  if (nkeys > d.kcap || !d.ktabs || W != d.kW) {
     // every earlier user of the old tables is ordered before d.last
     if (d.last_valid) (void)hipEventSynchronize(d.last);
     if (d.ktabs) (void)hipFree(d.ktabs);
@@ -1066,16 +1087,19 @@ int Lease::key_tables(size_t nkeys, void** tabs, uint32_t** ok, uint32_t** saved
     d.kok = d.ksaved = d.kflag = nullptr;
     d.kcap = d.ksaved_n = 0;
     d.khost.clear();
-    const size_t cap = nkeys < 16 ? 16 : nkeys;   // 528 KB of comb tables per key
-    hipError_t e = nw::table_malloc(&d.ktabs, nw::key_tables_bytes(cap));
+    // room for 16 keys at 16 bits (1 GB), for the committee itself at wider combs
+    const size_t cap = W == 16 ? (nkeys < 16 ? 16 : nkeys) : nkeys;
+    hipError_t e = nw::table_malloc(&d.ktabs, nw::key_tables_bytes(cap, nw::keyspec_for(W)));
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.kok), 4 * cap);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.ksaved), 32 * cap);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.kflag), 4);
     if (e != hipSuccess) return ::set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (key tables)", e);
     d.kcap = cap;
+    d.kW = W;
   }
   *tabs = d.ktabs;
   *ok = d.kok;
+  *ks = nw::keyspec_for(d.kW);
   if (saved) *saved = d.ksaved;
   if (flag) *flag = d.kflag;
   if (force) *force = d.ksaved_n != nkeys;

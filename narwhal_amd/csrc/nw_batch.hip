@@ -486,7 +486,7 @@ __device__ __forceinline__ void add_key_entry(ge& acc, const ge_niels_pad* tab12
 __global__ __launch_bounds__(256) void k_bv_chunks(
     const bv_chunk* __restrict__ chunks, uint32_t nchunks, const uint64_t* __restrict__ offsets,
     uint64_t b0, uint64_t i0, const bv_item* __restrict__ items,
-    const ge_cached* __restrict__ tabs, const ge_niels_pad* __restrict__ ktabs,
+    const ge_cached* __restrict__ tabs, const ge_niels_pad* __restrict__ ktabs, keyspec ks,
     bv_chunk_out* __restrict__ out, int32_t* __restrict__ status,
     uint64_t* __restrict__ fail_index, const uint32_t* __restrict__ ctotal) {
   __shared__ ge_niels s_btab[129];
@@ -557,9 +557,9 @@ __global__ __launch_bounds__(256) void k_bv_chunks(
       const ge_cached* tab = tabs + 16 * (l0 + t);
       if (keyed) {
         if ((j & 1) == 0 && j < 32) {
-          const ge_niels_pad* kt = ktabs + kKeyTab * (uint64_t)it->key;
+          const ge_niels_pad* kt = ktabs + ks.tab * (uint64_t)it->key;
           add_key_entry(acc, kt, digit8(it->c, j >> 1));
-          add_key_entry(acc, kt + kKeyHalf, digit8(it->c, 16 + (j >> 1)));
+          add_key_entry(acc, kt + ks.half, digit8(it->c, 16 + (j >> 1)));
         }
       } else {
         add_entry(acc, tab, digit4(it->c[j >> 3], j));
@@ -2053,7 +2053,8 @@ __global__ __launch_bounds__(256) void k_key_cmp(const uint32_t* __restrict__ pk
 }
 
 __global__ __launch_bounds__(256) void k_key_base(const uint32_t* __restrict__ pks,
-                                                  uint64_t nkeys, ge* __restrict__ base,
+                                                  uint64_t nkeys, keyspec ks,
+                                                  ge* __restrict__ base,
                                                   ge* __restrict__ comb,
                                                   uint32_t* __restrict__ ok,
                                                   const uint32_t* __restrict__ flag) {
@@ -2083,26 +2084,26 @@ __global__ __launch_bounds__(256) void k_key_base(const uint32_t* __restrict__ p
   ok[i] = (dec ? kKeyDecoded : 0u) | (dec && ge_is_small_order(P) ? kKeySmall : 0u) |
           (lam << kKeyLambdaShift);
   base[2 * i] = P;
+  const uint32_t W = ks.W, nt = keyspec_tables(ks);
   ge H;   // 2^(W floor(128 / W)) A, doubled up to 2^128 A when W does not divide 128
 #pragma unroll 1
-  for (int t = 0; t < (int)kKeyCombT; ++t) {
+  for (int t = 0; t < (int)ks.ntab; ++t) {
     if (t) {
 #pragma unroll 1
-      for (int d = 0; d < (int)kKeyW; ++d) ge_dbl(P, P, d == (int)kKeyW - 1);
+      for (int d = 0; d < (int)W; ++d) ge_dbl(P, P, d == (int)W - 1);
     }
-    comb[kKeyTables * i + t] = P;
-    if (t == (int)(128 / kKeyW)) H = P;
+    comb[nt * i + t] = P;
+    if (t == (int)(128 / W)) H = P;
   }
-  if (kKeyHalfExtra) {
+  if (128 % W) {
 #pragma unroll 1
-    for (int d = 0; d < (int)(128 % kKeyW); ++d) ge_dbl(H, H, true);
-    comb[kKeyTables * i + kKeyCombT] = H;
+    for (int d = 0; d < (int)(128 % W); ++d) ge_dbl(H, H, true);
+    comb[nt * i + ks.ntab] = H;
   }
   base[2 * i + 1] = H;
 }
 
 constexpr uint32_t kKeyRun = 64;
-constexpr uint32_t kKeyRuns = (kKeyN + kKeyRun - 1) / kKeyRun;   // runs per table
 
 NW_HD void put_fe32(uint32_t* w, const fe& f) {
   uint32_t b[8];
@@ -2111,14 +2112,16 @@ NW_HD void put_fe32(uint32_t* w, const fe& f) {
   for (int i = 0; i < 8; ++i) w[i] = b[i];
 }
 
-__global__ __launch_bounds__(256) void k_key_tabs(uint64_t nkeys, const ge* __restrict__ comb,
+__global__ __launch_bounds__(256) void k_key_tabs(uint64_t nkeys, keyspec ks,
+                                                  const ge* __restrict__ comb,
                                                   ge_niels_pad* __restrict__ tabs,
                                                   const uint32_t* __restrict__ flag) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= nkeys * kKeyTables * kKeyRuns || (flag && *flag == 0)) return;
-  const uint64_t pt = g / kKeyRuns;   // kKeyTables * key + t
-  const uint32_t j0 = (uint32_t)(g % kKeyRuns) * kKeyRun;
-  const uint32_t cnt = kKeyN - j0 < kKeyRun ? kKeyN - j0 : kKeyRun;
+  const uint32_t N = ks.nent, runs = (N + kKeyRun - 1) / kKeyRun;   // runs per table
+  if (g >= nkeys * keyspec_tables(ks) * runs || (flag && *flag == 0)) return;
+  const uint64_t pt = g / runs;   // tables * key + t
+  const uint32_t j0 = (uint32_t)(g % runs) * kKeyRun;
+  const uint32_t cnt = N - j0 < kKeyRun ? N - j0 : kKeyRun;
   const ge P = comb[pt];
   ge_cached Pc;
   ge_to_cached(Pc, P, g_bc.k.d2);
@@ -2131,7 +2134,7 @@ __global__ __launch_bounds__(256) void k_key_tabs(uint64_t nkeys, const ge* __re
       if ((j0 >> bit) & 1) ge_add_cached(acc, acc, Pc, true);
     }
   }
-  uint32_t* slot = reinterpret_cast<uint32_t*>(tabs + pt * kKeyN + j0);
+  uint32_t* slot = reinterpret_cast<uint32_t*>(tabs + pt * N + j0);
   static_assert(sizeof(ge_niels_pad) == 128, "slot = 32 words");
   fe prefix;   // product of the Z's of the run's earlier entries
   fe_1(prefix);
@@ -2166,29 +2169,32 @@ __global__ __launch_bounds__(256) void k_key_tabs(uint64_t nkeys, const ge* __re
     fe_mul(out.n.xy2d, x, y);
     fe_mul(out.n.xy2d, out.n.xy2d, g_bc.k.d2);
     out.pad[0] = out.pad[1] = 0;
-    tabs[pt * kKeyN + j0 + (uint32_t)e] = out;
+    tabs[pt * N + j0 + (uint32_t)e] = out;
   }
 }
 
-size_t key_tables_bytes(uint64_t nkeys) {
+size_t key_tables_bytes(uint64_t nkeys, const keyspec& ks) {
   const uint64_t n = nkeys ? nkeys : 1;
-  return sizeof(ge_niels_pad) * (uint64_t)kKeyTab * n + sizeof(ge) * (2 + kKeyTables) * n;
+  return sizeof(ge_niels_pad) * (uint64_t)ks.tab * n + sizeof(ge) * (2 + keyspec_tables(ks)) * n;
 }
 
-hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, ge_niels_pad* tabs, uint32_t* ok,
-                             hipStream_t stream, uint32_t* saved, uint32_t* flag, bool force) {
+hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, const keyspec& ks,
+                             ge_niels_pad* tabs, uint32_t* ok, hipStream_t stream,
+                             uint32_t* saved, uint32_t* flag, bool force) {
   if (nkeys == 0) return hipSuccess;
-  ge* base = reinterpret_cast<ge*>(tabs + kKeyTab * nkeys);
+  if (ks.W < 16 || ks.W > kKeyWMax || ks.ntab > 16) return hipErrorInvalidValue;
+  ge* base = reinterpret_cast<ge*>(tabs + (uint64_t)ks.tab * nkeys);
   ge* comb = base + 2 * nkeys;
   const uint32_t* fl = saved && flag ? flag : nullptr;
   if (fl)
     hipLaunchKernelGGL(k_key_cmp, dim3(1), dim3(256), 0, stream, pks, saved, nkeys,
                        force ? 1u : 0u, flag);
   hipLaunchKernelGGL(k_key_base, dim3((unsigned)((nkeys + 63) / 64)), dim3(64), 0, stream, pks,
-                     nkeys, base, comb, ok, fl);
-  hipLaunchKernelGGL(k_key_tabs, dim3((unsigned)((nkeys * kKeyTables * kKeyRuns + 255) / 256)),
-                     dim3(256), 0,
-                     stream, nkeys, comb, tabs, fl);
+                     nkeys, ks, base, comb, ok, fl);
+  const uint64_t runs = (ks.nent + kKeyRun - 1) / kKeyRun;
+  hipLaunchKernelGGL(k_key_tabs,
+                     dim3((unsigned)((nkeys * keyspec_tables(ks) * runs + 255) / 256)),
+                     dim3(256), 0, stream, nkeys, ks, comb, tabs, fl);
   return hipGetLastError();
 }
 
@@ -2377,7 +2383,7 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                const key_tables_t* keys, const uint32_t* skip_group_ok,
                                uint64_t skip_per_group, double active_frac,
                                uint32_t* fuse_ctr) {
-  const key_tables_t kt = keys ? *keys : key_tables_t{nullptr, nullptr, nullptr};
+  const key_tables_t kt = keys ? *keys : key_tables_t{nullptr, nullptr, nullptr, {}};
   const batch_skip_t sk{skip_group_ok, skip_per_group ? skip_per_group : 1};
   if (nbatches == 0) return hipSuccess;
   const uint64_t cap = std::min<uint64_t>(nitems + nbatches, slice_units());
@@ -2464,7 +2470,7 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
     if (chunks)
       hipLaunchKernelGGL(k_bv_chunks, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
                          stream, w.chunks, (uint32_t)chunks, offsets, b, i0, w.items, w.tabs,
-                         kt.tabs, w.outs, status, fail_index, w.chunk_start + (e - b));
+                         kt.tabs, kt.ks, w.outs, status, fail_index, w.chunk_start + (e - b));
     if (multi)
       hipLaunchKernelGGL(k_bv_combine,
                          dim3((unsigned)std::min<uint64_t>(multi, kCombineMaxBlocks)), dim3(256),
@@ -2485,8 +2491,8 @@ bool verify_batch_outputs_direct(uint64_t nbatches, uint64_t nitems) {
          nitems + 1 <= slice_units();
 }
 
-const ge* key_tables_base(const ge_niels_pad* tabs, uint64_t nkeys) {
-  return reinterpret_cast<const ge*>(tabs + kKeyTab * nkeys);
+const ge* key_tables_base(const ge_niels_pad* tabs, uint64_t nkeys, const keyspec& ks) {
+  return reinterpret_cast<const ge*>(tabs + (uint64_t)ks.tab * nkeys);
 }
 
 // Certificates per merged group, or 0 to verify every certificate's votes on its own:
@@ -2790,7 +2796,7 @@ __global__ __launch_bounds__(64) void k_sgrp_keys(
 __global__ __launch_bounds__(256) void k_sgrp_ladder(
     const uint64_t* __restrict__ cvo, uint64_t g0, uint64_t g1, uint64_t ncert, uint64_t K,
     uint32_t nch, uint64_t i0, const bv_item* __restrict__ items,
-    const ge_cached* __restrict__ tabs, const ge_niels_pad* __restrict__ ktabs,
+    const ge_cached* __restrict__ tabs, const ge_niels_pad* __restrict__ ktabs, keyspec ks,
     bv_chunk_out* __restrict__ out) {
   __shared__ ge_niels s_btab[129];
   __shared__ ge_niels s_b128[129];
@@ -2839,9 +2845,9 @@ __global__ __launch_bounds__(256) void k_sgrp_ladder(
 #pragma unroll 1
       for (uint32_t m = k; m < h.nkeys; m += nch) {
         const sgrp_key& e = *reinterpret_cast<const sgrp_key*>(slots + 16 * (uint64_t)m);
-        const ge_niels_pad* kt = ktabs + kKeyTab * (uint64_t)e.key;
+        const ge_niels_pad* kt = ktabs + ks.tab * (uint64_t)e.key;
         add_key_entry(acc, kt, digit8(e.c, j >> 1));
-        add_key_entry(acc, kt + kKeyHalf, digit8(e.c, 16 + (j >> 1)));
+        add_key_entry(acc, kt + ks.half, digit8(e.c, 16 + (j >> 1)));
       }
       if (k == 0) {
         add_digit_niels(acc, s_btab, digit8(h.bb, j >> 1), true);
@@ -2981,7 +2987,7 @@ hipError_t launch_cert_sgroups(const uint32_t* cert_digest, const uint64_t* cvo,
                        K, i0, nkeys, pre1, pre2, hdr_st, w.items, w.tabs);
     hipLaunchKernelGGL(k_sgrp_ladder, dim3((unsigned)(((e - g) * nch + 255) / 256)), dim3(256),
                        0, stream, cvo, g, e, ncert, K, nch, i0, w.items, w.tabs, keys.tabs,
-                       w.outs);
+                       keys.ks, w.outs);
     hipLaunchKernelGGL(k_sgrp_combine, dim3((unsigned)((e - g + 255) / 256)), dim3(256), 0,
                        stream, cvo, g, e, ncert, K, nch, i0, w.tabs, w.outs, group_ok);
     // the certificates of failed groups: their own verify_batch from the same items
@@ -2998,7 +3004,7 @@ hipError_t launch_cert_sgroups(const uint32_t* cert_digest, const uint64_t* cvo,
                          stream, cvo, b, be - b, (uint32_t)chunks, w.chunk_start, w.chunks);
       hipLaunchKernelGGL(k_bv_chunks, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
                          stream, w.chunks, (uint32_t)chunks, cvo, b, i0, w.items, w.tabs,
-                         keys.tabs, w.outs, status, fail_index, w.chunk_start + (be - b));
+                         keys.tabs, keys.ks, w.outs, status, fail_index, w.chunk_start + (be - b));
     }
     if (multi)
       hipLaunchKernelGGL(k_bv_combine,

@@ -661,13 +661,15 @@ int submit_small(int dev, uint32_t kind, const nw_committee* com, const nw_certi
   nw::rt::ReadLease rl;
   const void* tabs = nullptr;
   const uint32_t* ok = nullptr;
-  rc = rl.acquire(dev, j->stream, com->pks, na, &tabs, &ok);
+  nw::keyspec ks{};
+  rc = rl.acquire(dev, j->stream, com->pks, na, &tabs, &ok, &ks);
   if (rc) {   // 1: no tables for this committee yet (or an error): not taken here
     job_recycle(j);
     return rc;
   }
   J.ktabs = static_cast<const nw::ge_niels_pad*>(tabs);
   J.kok = ok;
+  J.ks = ks;
   const char* se = getenv("NW_SMALL_STAMPS");   // diagnostics: per-phase times of this launch
   const uint64_t nwg = (nslots + J.slots_per_wg - 1) / J.slots_per_wg;
   if (se && *se && *se != '0') (void)hipMalloc(reinterpret_cast<void**>(&J.stamps), 64 * nwg);

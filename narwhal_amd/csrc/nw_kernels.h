@@ -49,43 +49,59 @@ hipError_t launch_sign(const uint32_t* sks, uint32_t sk_stride_words, const uint
 // the workspace slices).
 hipError_t upload_batch_consts();
 
-// Pre-decompressed public keys (a committee): per key the comb tables j * 2^(W t) A
-// (W = NW_KEYW = 16: t = 0..15, j = 0..32,768, 67 MB per key; 20: t = 0..12 and a j * 2^128 A
-// table, j = 0..2^19, 940 MB per key; 8: t = 0..31, j = 0..128; affine niels) and whether it
-// decompressed. vote_key[i] = key index of vote i,
-// or kNoKey to decompress that vote's key in the kernel (the verdict semantics are
-// unchanged: a key's decompression is deterministic). Keyed strict verifications take [k]A
-// from the 256 / W tables with no doublings; chunks whose votes are all keyed run 8-bit A
-// windows over the tables of j * A and j * 2^128 A (entries 0..128) and a 128-doubling
-// ladder.
+// Layout of a committee's key comb tables at digit width W (chosen per committee when its
+// tables are built: nw_api.cpp key_width): ntab = ceil(253 / W) comb tables j * 2^(W t) A,
+// j = 0..2^(W-1) (affine niels), k's digits signed except the top one when ntab W > 256;
+// the keyed vote chunks' second 8-bit table j * 2^128 A is comb table 128 / W when W divides
+// 128, else one more table built from 2^128 A. W = 16: 16 tables, 67 MB per key; W = 20:
+// 13 + 1 tables, 940 MB per key.
+#define NW_KS __host__ __device__ __forceinline__
+struct keyspec {
+  uint32_t W, ntab, nsigned, nent, tab, half;
+  uint32_t bias[8];   // k + bias: the recoded digit words (2^(W-1) per signed digit)
+};
+NW_KS constexpr keyspec keyspec_for(uint32_t W) {
+  keyspec ks{};
+  ks.W = W;
+  ks.ntab = (253 + W - 1) / W;
+  ks.nsigned = ks.ntab * W > 256 ? ks.ntab - 1 : ks.ntab;
+  ks.nent = (1u << (W - 1)) + 1;
+  const uint32_t extra = 128 % W ? 1u : 0u;
+  ks.tab = (ks.ntab + extra) * ks.nent;
+  ks.half = (extra ? ks.ntab : 128 / W) * ks.nent;
+  for (uint32_t m = 0; m < ks.nsigned; ++m) {
+    const uint32_t b = W * m + W - 1;
+    ks.bias[b >> 5] |= 1u << (b & 31);
+  }
+  return ks;
+}
+NW_KS constexpr uint32_t keyspec_tables(const keyspec& ks) { return ks.tab / ks.nent; }
+
+// Pre-decompressed public keys (a committee): per key its comb tables (layout ks) and
+// whether it decompressed. vote_key[i] = key index of vote i, or kNoKey to decompress that
+// vote's key in the kernel (the verdict semantics are unchanged: a key's decompression is
+// deterministic). Keyed strict verifications take [k]A from the ntab tables with no
+// doublings; chunks whose votes are all keyed run 8-bit A windows over the tables of j * A
+// and j * 2^128 A (entries 0..128) and a 128-doubling ladder.
 struct key_tables_t {
-  const struct ge_niels_pad* tabs;   // nkeys x kKeyTab, affine niels (mixed additions)
+  const struct ge_niels_pad* tabs;   // nkeys x ks.tab, affine niels (mixed additions)
   const uint32_t* ok;             // nkeys
   const uint32_t* vote_key;       // nitems (global item index)
+  keyspec ks;
 };
-#ifndef NW_KEYW
-#define NW_KEYW 16
-#endif
 constexpr uint32_t kNoKey = 0xffffffffu;
-constexpr uint32_t kKeyW = NW_KEYW;                       // bits per comb digit of k
-constexpr uint32_t kKeyCombT = (253 + kKeyW - 1) / kKeyW; // comb tables per key (k < 2^253)
-constexpr uint32_t kKeyN = (1u << (kKeyW - 1)) + 1;       // entries per table, j = 0..2^(W-1)
-// the keyed vote chunks' j * 2^128 A table: comb table 128 / W when W divides 128, else one
-// extra table built from 2^128 A
-constexpr uint32_t kKeyHalfExtra = 128 % kKeyW ? 1 : 0;
-constexpr uint32_t kKeyTables = kKeyCombT + kKeyHalfExtra; // tables built per key
-constexpr uint32_t kKeyTab = kKeyTables * kKeyN;          // entries per key
-constexpr uint32_t kKeyHalf = (kKeyHalfExtra ? kKeyCombT : 128 / kKeyW) * kKeyN;
+constexpr uint32_t kKeyWMax = 24;   // widths 16 / 20 / 24 (at most 16 comb digits)
 // ok[key]: bit 0 = decompressed, bit 1 = small order (8A == identity), bits 2..4 = lambda
 // with [l]A == [lambda]T8 (nw_strict.hpp kKeyLambdaShift: the key's torsion image)
-size_t key_tables_bytes(uint64_t nkeys);
+size_t key_tables_bytes(uint64_t nkeys, const keyspec& ks);
 // tabs: key_tables_bytes(nkeys) of device memory; ok: nkeys words. saved (nkeys x 8 words)
 // and flag (1 word), optional: the keys the tables were last built from; the tables are
 // rebuilt only when force or the keys differ (a device-side compare, so the call stays
 // asynchronous), and saved is updated — the committee of an epoch is tabulated once.
-hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, struct ge_niels_pad* tabs,
-                             uint32_t* ok, hipStream_t stream, uint32_t* saved = nullptr,
-                             uint32_t* flag = nullptr, bool force = true);
+hipError_t launch_key_tables(const uint32_t* pks, uint64_t nkeys, const keyspec& ks,
+                             struct ge_niels_pad* tabs, uint32_t* ok, hipStream_t stream,
+                             uint32_t* saved = nullptr, uint32_t* flag = nullptr,
+                             bool force = true);
 size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems);
 // True when launch_verify_batch over these batches (no skip list, no fork) writes its outputs
 // from ONE kernel, the fused tail of a lone large batch: status / fail_index may then be
@@ -127,7 +143,7 @@ hipError_t launch_group_feedback(const uint32_t* group_ok, uint64_t ncert, uint6
                                  const int32_t* pre2, const int32_t* hdr_st, uint32_t* cnt,
                                  uint32_t* fb, hipStream_t stream);
 size_t cert_groups_bytes(uint64_t ncert);
-const ge* key_tables_base(const ge_niels_pad* tabs, uint64_t nkeys);
+const ge* key_tables_base(const ge_niels_pad* tabs, uint64_t nkeys, const keyspec& ks);
 hipError_t launch_cert_groups(const uint32_t* cert_digest, const uint64_t* cvo,
                               const uint64_t* host_cvo, uint64_t ncert, const uint32_t* pks,
                               const uint32_t* sigs, uint64_t nvotes, const z_key_t& zkey,
@@ -247,6 +263,7 @@ struct small_job_t {
   // device: the committee's key tables (built for exactly these keys) and the B comb
   const struct ge_niels_pad* ktabs;
   const uint32_t* kok;
+  keyspec ks;              // the key tables' layout
   const struct ge_niels_pad* bcomb;
   uint32_t zkey[8];        // ChaCha20 key of the batch coefficients when z16 is null
   // device scratch: message info and slot records of messages spanning workgroups, and

@@ -269,11 +269,12 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
     const uint64_t i = list ? list[active ? gi : n - 1] : active ? gi : n - 1;
     const strict_src_global src{pks + 8 * i, sigs + 16 * i, msgs + (uint64_t)msg_stride_words * i};
     const uint32_t kk = KEYED && keys.vote_key ? keys.vote_key[i] : kNoKey;
-    const ge_niels_pad* keytab = kk != kNoKey ? keys.tabs + kKeyTab * (uint64_t)kk : nullptr;
+    const ge_niels_pad* keytab = kk != kNoKey ? keys.tabs + keys.ks.tab * (uint64_t)kk : nullptr;
     // committee keys: [s]B - [k]A from comb tables, no ladder; others: the half-size ladder
     int st;
     if (KEYED && keytab) {
-      st = strict_keyed_comb(src, g_consts.sk, bcomb_wide{bcomb}, keytab_wide{keytab}, keys.ok[kk]);
+      st = strict_keyed_comb(src, g_consts.sk, bcomb_wide{bcomb}, keytab_wide{keytab, keys.ks},
+                             keys.ok[kk]);
     } else {
 #if NW_STRICT_PF && NW_BWIN != 8
       st = strict_verify_core<NW_BWIN>(src, g_consts.sk, bt, tabA, tabR, WaveMax{},
@@ -313,7 +314,7 @@ __global__ __launch_bounds__(256, NW_KEYED_WAVES) void k_strict_keyed(
                                 msgs + (uint64_t)msg_stride_words * gi};
     fe X, Z;
     st = keyed_vote_check(src, g_consts.sk, bcomb_wide{bcomb},
-                          keytab_wide{keys.tabs + kKeyTab * (uint64_t)kk}, keys.ok[kk], X, Z);
+                          keytab_wide{keys.tabs + keys.ks.tab * (uint64_t)kk, keys.ks}, keys.ok[kk], X, Z);
     if (st >= kVotePending) {
 #pragma unroll
       for (int k = 0; k < 10; ++k) {
@@ -515,7 +516,7 @@ __global__ __launch_bounds__(256, NW_KEYED_WAVES) void k_votes_keyed(
       const strict_src_global src{pks + 8 * v, sigs + 16 * v, cert_digest + 8 * (uint64_t)c};
       fe X, Z;
       st = keyed_vote_check(src, g_consts.sk, bcomb_wide{bcomb},
-                            keytab_wide{keys.tabs + kKeyTab * (uint64_t)kk}, keys.ok[kk], X, Z);
+                            keytab_wide{keys.tabs + keys.ks.tab * (uint64_t)kk, keys.ks}, keys.ok[kk], X, Z);
       if (st >= kVotePending) {
 #pragma unroll
         for (int k = 0; k < 10; ++k) {
@@ -758,7 +759,7 @@ hipError_t table_malloc(void** p, size_t bytes) {
   }
   return hipMalloc(p, bytes);
 }
-static_assert(kStrictKeyTables == (int)kKeyCombT && kStrictKeyN == kKeyN, "keyed comb tables");
+
 
 // Table set `which` of the current device (0: the ladder's 2 x kBtwPerHalf; 1: the keyed
 // comb's kBCombT x kBCombN: 11 x 8,388,609 = 11.8 GB at 24-bit digits), built on first use.
@@ -862,7 +863,7 @@ hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
                                 hipStream_t stream, const key_tables_t* keys) {
   if (n == 0) return hipSuccess;
   const unsigned grid = std::min<uint64_t>(strict_grid(), grid_for(n, 256));
-  const key_tables_t kt = keys ? *keys : key_tables_t{nullptr, nullptr, nullptr};
+  const key_tables_t kt = keys ? *keys : key_tables_t{nullptr, nullptr, nullptr, {}};
   const ge_niels_pad* btw = nullptr;
   const ge_niels_pad* bcomb = nullptr;
   hipError_t eb = btab_for_current_device(0, &btw);

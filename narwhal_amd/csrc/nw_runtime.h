@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "narwhal_amd.h"
+#include "nw_kernels.h"
 
 namespace nw {
 namespace rt {
@@ -89,11 +90,12 @@ class Lease {
   int acquire(int dev_index, hipStream_t stream);
   // The device's strict workspace (nw::strict_workspace_bytes(), allocated once).
   int strict_ws(void** out);
-  // Key tables for nkeys keys (grow-only): tabs (nw::key_tables_bytes) and ok words, plus
-  // the reuse state of nw::launch_key_tables: the device copy of the keys they were last
-  // built from, the rebuild flag word, and whether a rebuild is forced (new size/buffers).
-  int key_tables(size_t nkeys, void** tabs, uint32_t** ok, uint32_t** saved = nullptr,
-                 uint32_t** flag = nullptr, bool* force = nullptr);
+  // Key tables for nkeys keys (grow-only at one comb width, nw_api.cpp key_width): tabs
+  // (nw::key_tables_bytes) and ok words, their layout (ks), plus the reuse state of
+  // nw::launch_key_tables: the device copy of the keys they were last built from, the
+  // rebuild flag word, and whether a rebuild is forced (new size / width / buffers).
+  int key_tables(size_t nkeys, void** tabs, uint32_t** ok, nw::keyspec* ks,
+                 uint32_t** saved = nullptr, uint32_t** flag = nullptr, bool* force = nullptr);
   // After a successful launch_key_tables: the saved keys now describe the tables; host_pks
   // (nkeys x 32 bytes, optional) are those keys in host memory (small jobs compare them).
   void keys_built(size_t nkeys, const uint8_t* host_pks = nullptr);
@@ -120,7 +122,7 @@ class ReadLease {
   ReadLease& operator=(const ReadLease&) = delete;
   ~ReadLease() { (void)release(); }
   int acquire(int dev_index, hipStream_t stream, const uint8_t* pks, size_t nkeys,
-              const void** tabs, const uint32_t** ok);
+              const void** tabs, const uint32_t** ok, nw::keyspec* ks);
   int release();
 
  private:

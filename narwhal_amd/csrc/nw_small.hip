@@ -63,7 +63,8 @@ struct small_consts {
 __constant__ small_consts g_sc;
 
 constexpr int kSlotsMax = 64;
-constexpr int kDigits = kStrictKeyTables + kBCombT;   // 16 + 11 comb entries per slot
+// comb entries per slot: at most 16 key-comb digits (W >= 16) + the B comb's
+constexpr int kDigits = 16 + kBCombT;
 static_assert(kDigits <= 27, "at most 16 key-comb + 11 B-comb digits (LDS per slot)");
 
 // Per-slot record (slot_rec, s_rec).
@@ -504,13 +505,14 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
         sc k;
         sc_reduce512(k, hx);
         uint32_t kd[8], sd[8];
-        keydigits::recode(kd, k);
+        key_recode(kd, k, J.ks);
         bdigits<kBCombW>::recode(sd, s);
 #pragma unroll
-        for (int t = 0; t < kStrictKeyTables; ++t) s_dig[lane][t] = keydigits::digit(kd, t);
+        for (int t = 0; t < 16; ++t)
+          if (t < (int)J.ks.ntab) s_dig[lane][t] = key_digit(kd, t, J.ks);
 #pragma unroll
         for (int t = 0; t < kBCombT; ++t)
-          s_dig[lane][kStrictKeyTables + t] = bdigits<kBCombW>::digit(sd, t);
+          s_dig[lane][J.ks.ntab + t] = bdigits<kBCombW>::digit(sd, t);
 #pragma unroll
         for (int t = 0; t < 8; ++t) s_k[lane][t] = k.w[t];
       }
@@ -534,15 +536,16 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
     ge_identity(acc);
     if (live) {
       const uint32_t kk = s_key[sl];
-      const ge_niels_pad* kt = J.ktabs + (uint64_t)kKeyTab * kk;
+      const ge_niels_pad* kt = J.ktabs + (uint64_t)J.ks.tab * kk;
+      const uint32_t KT = J.ks.ntab, ND = KT + (uint32_t)kBCombT;
 #pragma unroll 1
-      for (uint32_t e = g; e < (uint32_t)kDigits; e += G) {
+      for (uint32_t e = g; e < ND; e += G) {
         const int d = s_dig[sl][e];
         if (d == 0) continue;
         const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
-        const bool isA = e < (uint32_t)kStrictKeyTables;
-        const ge_niels_pad* ent = isA ? kt + e * kStrictKeyN + ad
-                                      : J.bcomb + (e - kStrictKeyTables) * kBCombN + ad;
+        const bool isA = e < KT;
+        const ge_niels_pad* ent = isA ? kt + e * J.ks.nent + ad
+                                      : J.bcomb + (e - KT) * kBCombN + ad;
         ge_niels nb = ent->n;
         ge_niels_cneg(nb, isA ? d > 0 : d < 0);   // -[k]A: key digits negated
         ge_add_niels(acc, acc, nb, true);

@@ -17,6 +17,7 @@
 //      (2 x 8,388,609, 2.1 GB; 11 additions), or 8-bit over 2 x 129 entries in LDS (32).
 #pragma once
 #include "narwhal_amd.h"
+#include "nw_kernels.h"
 
 #ifndef NW_BWIN
 #define NW_BWIN 24
@@ -316,16 +317,24 @@ struct btab_lazy {
 constexpr int kBCombW = NW_BCOMBW;
 constexpr int kBCombT = bdigits<NW_BCOMBW>::NB;
 constexpr uint32_t kBCombN = bdigits<NW_BCOMBW>::ENTRIES;
-// Committee-key comb width (= nw_kernels.h kKeyW): ceil(253 / W) tables j * 2^(W t) A,
-// j = 0..2^(W-1), over k's digits recoded as bdigits<W> (signed; the top one unsigned when
-// the digits overrun 256 bits, W = 20 / 24)
-#ifndef NW_KEYW
-#define NW_KEYW 16
-#endif
-constexpr int kStrictKeyW = NW_KEYW;
-using keydigits = bdigits<kStrictKeyW>;
-constexpr int kStrictKeyTables = keydigits::NB;   // = nw_kernels.h kKeyCombT
-constexpr uint32_t kStrictKeyN = keydigits::ENTRIES;
+// Committee-key comb digits at the tables' runtime width (nw_kernels.h keyspec): k + bias
+// recoded once, digit t = bits W t .. W t + W - 1, signed (minus 2^(W-1)) except the top one
+// when the digits overrun 256 bits — bdigits<W>'s recoding with W a value.
+NW_HD void key_recode(uint32_t kd[8], const sc& k, const keyspec& ks) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    c += (uint64_t)k.w[i] + ks.bias[i];
+    kd[i] = (uint32_t)c;
+    c >>= 32;
+  }
+}
+NW_HD int key_digit(const uint32_t kd[8], int t, const keyspec& ks) {
+  const uint32_t p = ks.W * (uint32_t)t, wi = p >> 5, sh = p & 31;
+  const uint32_t lo = sel8(kd, (int)wi), hi = wi < 7 ? sel8(kd, (int)wi + 1) : 0u;
+  const uint32_t v = (uint32_t)(((((uint64_t)hi) << 32) | lo) >> sh) & ((1u << ks.W) - 1u);
+  return (uint32_t)t < ks.nsigned ? (int)v - (1 << (ks.W - 1)) : (int)v;
+}
 struct bcomb_wide {
   const ge_niels_pad* t;
   NW_HD const ge_niels_pad* entry(int m, int ad) const {
@@ -379,29 +388,31 @@ struct pf_none {
   NW_HD uint32_t dget(int) const { return 0; }
 };
 
-// A committee key's comb tables: keytab_wide reads the device copy (keytab[kStrictKeyN t + j]
+// A committee key's comb tables: keytab_wide reads the device copy (keytab[ks.nent t + j]
 // = j * 2^(W t) A, affine niels, built by k_key_tabs); keytab_lazy computes an entry per
 // lookup from A (host self-check: the full 16-bit tables are 67 MB per key).
 struct keytab_wide {
   const ge_niels_pad* t;
+  keyspec ks;
   NW_HD const ge_niels_pad* entry(int tab, int j) const {
-    return t + (uint32_t)tab * kStrictKeyN + (uint32_t)j;
+    return t + (uint32_t)tab * ks.nent + (uint32_t)j;
   }
   NW_HD void operator()(int tab, int j, ge_niels& e) const {
-    e = t[(uint32_t)tab * kStrictKeyN + (uint32_t)j].n;
+    e = t[(uint32_t)tab * ks.nent + (uint32_t)j].n;
   }
 };
 struct keytab_lazy {
   const ge* A;
   const fe* d2;
+  keyspec ks;
   NW_HD void operator()(int tab, int j, ge_niels& e) const {
     ge P = *A;
-    for (int d = 0; d < kStrictKeyW * tab; ++d) ge_dbl(P, P, true);
+    for (int d = 0; d < (int)ks.W * tab; ++d) ge_dbl(P, P, true);
     ge_cached c;
     ge_to_cached(c, P, *d2);
     ge acc;
     ge_identity(acc);
-    for (int bit = kStrictKeyW - 1; bit >= 0; --bit) {
+    for (int bit = (int)ks.W - 1; bit >= 0; --bit) {
       ge_dbl(acc, acc, true);
       if ((j >> bit) & 1) ge_add_cached(acc, acc, c, true);
     }
@@ -419,16 +430,17 @@ template <class BComb, class KeyTab, class PF = pf_none>
 NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
                           const KeyTab& kt, const fe& d2, const PF& pf = PF{}) {
   uint32_t kd[8], sd[8];
-  keydigits::recode(kd, k);           // k < l: ceil(253 / W) W-bit digits
+  const keyspec& ks = kt.ks;
+  key_recode(kd, k, ks);              // k < l: ceil(253 / W) W-bit digits
   bdigits<kBCombW>::recode(sd, s);    // s < l: kBCombT digits of kBCombW bits
   ge_identity(acc);
   if constexpr (PF::enabled) {
     // the same additions in the same order, each entry requested one addition ahead
     // (pf_lds: global_load_lds into a per-lane LDS slot while the current addition runs)
-    constexpr int KT = kStrictKeyTables, NS = kStrictKeyTables + kBCombT;
+    const int KT = (int)ks.ntab, NS = KT + kBCombT;
     auto step_src = [&](int st, int& d) -> const void* {
       if (st < KT) {
-        d = keydigits::digit(kd, st);
+        d = key_digit(kd, st, ks);
         return d ? static_cast<const void*>(kt.entry(st, d < 0 ? -d : d)) : nullptr;
       }
       d = bdigits<kBCombW>::digit(sd, st - KT);
@@ -464,9 +476,9 @@ NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
   ge accB;
   ge_identity(accB);
 #pragma unroll 1
-  for (int t = 0; t < (kStrictKeyTables > kBCombT ? kStrictKeyTables : kBCombT); ++t) {
-    if (t < kStrictKeyTables) {
-      const int d = keydigits::digit(kd, t);
+  for (int t = 0; t < ((int)ks.ntab > kBCombT ? (int)ks.ntab : kBCombT); ++t) {
+    if (t < (int)ks.ntab) {
+      const int d = key_digit(kd, t, ks);
       if (d != 0) {
         ge_niels nb;
         kt(t, d < 0 ? -d : d, nb);
@@ -493,8 +505,8 @@ NW_HD void keyed_comb_sum(ge& acc, const sc& k, const sc& s, const BComb& bc,
 #endif
   // -[k]A: digit t of k against table t, negated
 #pragma unroll 1
-  for (int t = 0; t < kStrictKeyTables; ++t) {
-    const int d = keydigits::digit(kd, t);
+  for (int t = 0; t < (int)ks.ntab; ++t) {
+    const int d = key_digit(kd, t, ks);
     if (d != 0) {
       ge_niels nb;
       kt(t, d < 0 ? -d : d, nb);

@@ -190,7 +190,16 @@ def test_wide_btab_entries(hc):
             assert enc == O.scalarmult_base(s.to_bytes(32, "little")), (h, j)
 
 
-def test_strict_keyed_comb(hc, golden):
+@pytest.fixture(params=[16, 20])
+def keyw(request, hc):
+    """The key-comb widths the device builds (nw_api.cpp key_width: 20 bits up to 16 keys)."""
+    hc.hc_set_key_width.restype = ctypes.c_int
+    assert hc.hc_set_key_width(request.param) == 0
+    yield request.param
+    hc.hc_set_key_width(16)
+
+
+def test_strict_keyed_comb(hc, golden, keyw):
     """Committee-key strict path (no ladder: [s]B - [k]A from comb tables) against the
     oracle on the edge corpus and on random honest / tampered signatures."""
     for it in golden["edge_corpus"]["items"]:
@@ -219,7 +228,7 @@ def _scalar_a(seed: bytes) -> int:
     return int.from_bytes(h, "little")
 
 
-def test_keyed_vote_check_compressed_r(hc, golden):
+def test_keyed_vote_check_compressed_r(hc, golden, keyw):
     """Certificate votes' keyed check with R compared in compressed form (Y' == y_R Z' and
     the parity of X'/Z', no decompression of R): pass iff the oracle's strict verify is Ok,
     on the edge corpus (every Appendix A class), random honest / tampered signatures, and

@@ -187,6 +187,15 @@ int hc_key_lambda(const uint8_t pk[32]) {
   return (f & kKeyDecoded) ? (int)((f & kKeyLambdaMask) >> kKeyLambdaShift) : -1;
 }
 
+// Comb width of the keyed checks' (lazily computed) key tables: 16 or 20 (the widths the
+// device builds, nw_api.cpp key_width).
+static uint32_t g_key_w = 16;
+int hc_set_key_width(int w) {
+  if (w != 16 && w != 20 && w != 24) return -1;
+  g_key_w = (uint32_t)w;
+  return 0;
+}
+
 int hc_verify_strict_keyed(const uint8_t pk[32], const uint8_t sig[64], const uint8_t k32[32]) {
   init();
   uint32_t Aw[8], Rw[8], Sw[8], kw[8];
@@ -194,7 +203,7 @@ int hc_verify_strict_keyed(const uint8_t pk[32], const uint8_t sig[64], const ui
   ge A;
   const uint32_t flags = keyed_key(A, Aw);
   const strict_src_arrays src{Aw, Rw, Sw, kw};
-  return strict_keyed_comb(src, SK, bcomb_lazy{BT, &SK.k.d2}, keytab_lazy{&A, &SK.k.d2}, flags);
+  return strict_keyed_comb(src, SK, bcomb_lazy{BT, &SK.k.d2}, keytab_lazy{&A, &SK.k.d2, keyspec_for(g_key_w)}, flags);
 }
 
 // The certificate-vote keyed check without R decompression (nw_strict.hpp
@@ -209,7 +218,7 @@ int hc_keyed_vote_check(const uint8_t pk[32], const uint8_t sig[64], const uint8
   const strict_src_arrays src{Aw, Rw, Sw, kw};
   fe X, Z;
   const uint32_t st = keyed_vote_check(src, SK, bcomb_lazy{BT, &SK.k.d2},
-                                       keytab_lazy{&A, &SK.k.d2}, flags, X, Z);
+                                       keytab_lazy{&A, &SK.k.d2, keyspec_for(g_key_w)}, flags, X, Z);
   if (st < kVotePending) return (int)st;
   fe zi, x;
   fe_invert(zi, Z);
