@@ -428,7 +428,7 @@ __global__ __launch_bounds__(256) void k_votes_keyed_init(const uint64_t* __rest
 // N = 100: HBM and TLB bound); sorted, the chip works on one or two keys' tables at a time,
 // which stay in the last-level caches.
 constexpr uint32_t kVkMaxBins = 1024;
-constexpr uint32_t kVkSortMinKeys = 64;
+constexpr uint32_t kVkSortMinKeys = 32;
 __device__ __forceinline__ uint32_t vk_bin(const uint32_t* __restrict__ vote_cert,
                                            const uint32_t* __restrict__ vote_key, uint64_t v,
                                            const int32_t* __restrict__ pre1,
@@ -936,10 +936,11 @@ hipError_t launch_votes_keyed(const uint32_t* cert_digest, const uint64_t* cvo, 
   if (nvotes && S == 0) return hipErrorInvalidValue;
   uint32_t* gh = static_cast<uint32_t*>(scratch);
   uint32_t* base = gh + kVkMaxBins;
-  // key-major order for committees whose tables overflow the caches (>= 64 keys: 4.3 GB of
-  // 16-bit tables; config 2 N = 100: 7.58 -> 9.11 M certs/s) — below that the cert-major
-  // order's coalesced signature reads win (N = 4 / 10 / 50: 143 / 74 / 19.2 unsorted vs
-  // 137 / 72 / 17.7 sorted). NW_VOTES_KEY_MAJOR=1 / 0 forces it on / off.
+  // key-major order for committees whose tables overflow the caches (>= 32 keys: 2.1 GB of
+  // 16-bit tables; config 2 N = 100: 7.58 -> 9.11 M certs/s in round 3; N = 50 22.4 -> 23.3
+  // in round 5, profiles/r05kw2, though round 3 measured it slower there) — below that the
+  // cert-major order's coalesced signature reads win (round 3: N = 4 / 10: 143 / 74
+  // unsorted vs 137 / 72 sorted). NW_VOTES_KEY_MAJOR=1 / 0 forces it on / off.
   const char* km = getenv("NW_VOTES_KEY_MAJOR");
   const bool sort = nkeys + 1 <= kVkMaxBins &&
                     (km ? km[0] == '1' : nkeys >= kVkSortMinKeys);
