@@ -708,7 +708,8 @@ constexpr int kPipTopSub = 7, kPipTopStride = 17, kPipCarryBins = 64;
 constexpr int kPipBins = kPipWin * 128 + kPipCarryBins;
 
 struct pip_region {
-  ge_niels* pts;     // 2n: A_t at 2t, R_t at 2t + 1
+  ge_niels_pad* pts; // 2n: A_t at 2t, R_t at 2t + 1 (one 128-byte line each: a bucket
+                     // lane's gather of a 120-byte entry at a 120-byte stride fetched two)
   uint32_t* ent;     // window w: entries [2n w, 2n w + 2n), point index | sign << 31
   uint8_t* cd;       // 32 x n, window-major: byte w of recoded c_t at cd[w n + t]
   uint8_t* zd;       // 17 x n (+ pad): byte w of recoded z_t at zd[w n + t]
@@ -722,7 +723,7 @@ struct pip_region {
 };
 
 constexpr size_t pip_region_bytes(uint64_t n) {
-  return 2 * n * sizeof(ge_niels) + 4 * kPipWinCap * n + 52 * n + 8 * kPipBins +
+  return 2 * n * sizeof(ge_niels_pad) + 4 * kPipWinCap * n + 52 * n + 8 * kPipBins +
          sizeof(ge) * kPipBins + sizeof(ge_cached) * kPipWin + 16 + 32 + sizeof(ge_cached);
 }
 // per-vote bytes grow slower than the item slots (2560 B), so the floor is the binding n
@@ -753,7 +754,7 @@ struct pip_group_t {
 __device__ __forceinline__ pip_region pip_at(ge_cached* tabs, uint64_t li0, uint64_t n) {
   char* p = reinterpret_cast<char*>(tabs + 16 * li0);
   pip_region r;
-  r.pts = reinterpret_cast<ge_niels*>(p); p += 2 * n * sizeof(ge_niels);
+  r.pts = reinterpret_cast<ge_niels_pad*>(p); p += 2 * n * sizeof(ge_niels_pad);
   r.ent = reinterpret_cast<uint32_t*>(p); p += 4 * kPipWinCap * n;
   r.cd = reinterpret_cast<uint8_t*>(p); p += 32 * n;
   r.zd = reinterpret_cast<uint8_t*>(p); p += 20 * n;
@@ -857,10 +858,10 @@ __device__ __forceinline__ void pip_point_do(
     ge_to_niels_z1(q, P, K.d2);
     if (which == 1) {
       it->pad = ok ? 0u : (uint32_t)BF_R_DECODE;
-      reg.pts[2 * t + 1] = q;
+      reg.pts[2 * t + 1].n = q;
     } else {
       it->z[0] = ok ? 0u : (uint32_t)BF_A_DECODE;   // Pippenger batches: z[] is unused
-      reg.pts[2 * t] = q;
+      reg.pts[2 * t].n = q;
     }
     return;
   }
@@ -987,7 +988,7 @@ __global__ __launch_bounds__(1024) void k_grp_keys(const uint64_t* __restrict__ 
     for (int w = 0; w < kPipZWin; ++w) reg.zd[w * nreg + t] = 0x80;
     ge_niels q;
     ge_to_niels_z1(q, grp.key_base[2 * j], g_bc.k.d2);
-    reg.pts[2 * t] = q;
+    reg.pts[2 * t].n = q;
   }
 }
 
@@ -1227,14 +1228,14 @@ __device__ __forceinline__ void pip_bucket_lanes(const pip_region& reg, uint32_t
   uint32_t x = a < e ? reg.ent[a] : 0u;
   uint32_t x2 = a + 1 < e ? reg.ent[a + 1] : 0u;
   ge_niels nx;
-  if (a < e) nx = reg.pts[x & 0x7fffffffu];
+  if (a < e) nx = reg.pts[x & 0x7fffffffu].n;
 #pragma unroll 1
   for (uint32_t k = a; k < e; ++k) {
     ge_niels q = nx;
     const bool neg = (x >> 31) != 0;
     if (k + 1 < e) {
       x = x2;
-      nx = reg.pts[x & 0x7fffffffu];
+      nx = reg.pts[x & 0x7fffffffu].n;
     }
     if (k + 2 < e) x2 = reg.ent[k + 2];
     ge_niels_cneg(q, neg);
@@ -1369,7 +1370,7 @@ uint32_t pip_win_lp_max() {   // NW_PIP_WIN_LP_MAX=0: always the one-wave form
   return v;
 }
 // the parts live in the dead point + entry arrays (contiguous in pip_at)
-static_assert(2 * kPipFloor * sizeof(ge_niels) + 4 * kPipWinCap * kPipFloor >=
+static_assert(2 * kPipFloor * sizeof(ge_niels_pad) + 4 * kPipWinCap * kPipFloor >=
                   4 * kPipWin * kPipWinLpParts * 64,
               "window parts do not fit the point array");
 
