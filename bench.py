@@ -1225,7 +1225,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--certs", type=int, default=1_000_000)
     ap.add_argument("--cert-unique", type=int, default=65536)
-    ap.add_argument("--cert-steps", type=int, default=2)
+    ap.add_argument("--cert-steps", type=int, default=4)
     ap.add_argument("--cert-invalid", type=float, default=0.01,
                     help="extra config-2 leg with this fraction of certificates carrying a bad "
                          "vote (0 = skip)")

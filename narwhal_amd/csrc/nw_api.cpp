@@ -1090,6 +1090,14 @@ int Lease::key_tables(size_t nkeys, void** tabs, uint32_t** ok, nw::keyspec* ks,
     // room for 16 keys at 16 bits (1 GB), for the committee itself at wider combs
     const size_t cap = W == 16 ? (nkeys < 16 ? 16 : nkeys) : nkeys;
     hipError_t e = nw::table_malloc(&d.ktabs, nw::key_tables_bytes(cap, nw::keyspec_for(W)));
+    static const bool klog = getenv("NW_KEYTAB_LOG") != nullptr;   // diagnostics
+    if (klog) {
+      size_t fr = 0, tot = 0;
+      (void)hipMemGetInfo(&fr, &tot);
+      fprintf(stderr, "[keytab] keys %zu width %u bytes %zu -> %s (free %zu of %zu)\n", nkeys, W,
+              nw::key_tables_bytes(cap, nw::keyspec_for(W)), e == hipSuccess ? "ok" : "FAILED",
+              fr, tot);
+    }
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.kok), 4 * cap);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.ksaved), 32 * cap);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.kflag), 4);
