@@ -88,8 +88,8 @@ int nw_synchronize(void);
  * calling thread's device, or on every device under NW_ALL_DEVICES: the strict kernel's B
  * tables (2 x 8,388,609 entries of 128 B = 2.15 GB, ~0.2 s) and the keyed comb's B tables
  * (11 x 8,388,609 entries = 11.8 GB, ~0.7 s). Besides these a device holds, per committee
- * in use, its key tables (committees of up to 16 keys: 20-bit combs, 14 x 524,289 entries
- * = 940 MB per key, 15 GB at 16 authorities; larger ones: 16-bit combs, 16 x 32,769 entries
+ * in use, its key tables (committees of up to 64 keys: 20-bit combs, 14 x 524,289 entries
+ * = 940 MB per key, 47 GB at 50 authorities; larger ones: 16-bit combs, 16 x 32,769 entries
  * = 67 MB per key, 6.7 GB at 100 authorities; NW_KEY_WIDTH=16 forces the small ones; built
  * by the first Header / Vote / Certificate call with that committee, ~0.4 s at N = 100) and
  * the strict workspace (~0.5 GB): ~21 GB in all at N = 100. Returns 0, or

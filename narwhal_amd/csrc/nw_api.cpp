@@ -1057,11 +1057,13 @@ int Lease::strict_ws(void** out) {
 }
 
 // Comb width of a committee's key tables: 20 bits (13 tables, 940 MB per key: three fewer
-// additions per keyed check) up to kKeyW20Keys keys, whose tables stay gathered locally;
-// 16 bits (16 tables, 67 MB per key) above, where 20-bit tables outgrow the caches and the
-// device (profiles/r05k20: N = 4 / 10 +7 / +9 %, N = 50 -18 % at 20 bits). NW_KEY_WIDTH
-// = 16 / 20 / 24 forces one width.
-constexpr size_t kKeyW20Keys = 16;
+// additions per keyed check) up to kKeyW20Keys keys, 16 bits (16 tables, 67 MB per key)
+// above. Measured (config 2, alternating runs): N = 4 / 10 +7 / +9 % (profiles/r05kw),
+// N = 50 +6 % over 16-bit once its votes are sorted by key (r05kw2; unsorted it lost 18 %,
+// r05k20), the service at N = 50 unchanged (r05svc20); N = 100 (94 GB of tables, ~1 s to
+// rebuild when the committee changes) stays at 16 bits. NW_KEY_WIDTH = 16 / 20 / 24 forces
+// one width.
+constexpr size_t kKeyW20Keys = 64;
 static uint32_t key_width(size_t nkeys) {
   static const uint32_t forced = [] {
     const char* e = getenv("NW_KEY_WIDTH");
