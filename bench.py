@@ -757,6 +757,23 @@ def run_wire(args, dev, stream, rank, world, N: int = 4):
             "parity_check": "status and index of every frame's certificate == construction"}
 
 
+def cgroup_cpu_stat():
+    """usage_usec / nr_throttled / throttled_usec of this process's cgroup (v2), or None."""
+    try:
+        rel = [ln[3:] for ln in open("/proc/self/cgroup").read().split("\n") if ln.startswith("0::")]
+    except OSError:
+        rel = []
+    for path in [os.path.join("/sys/fs/cgroup", r.lstrip("/"), "cpu.stat") for r in rel] + \
+            ["/sys/fs/cgroup/cpu.stat"]:
+        try:
+            with open(path) as f:
+                st = dict(line.split()[:2] for line in f if line.strip())
+            return {k: int(st[k]) for k in ("usage_usec", "nr_throttled", "throttled_usec")}
+        except (OSError, KeyError, ValueError):
+            continue
+    return None
+
+
 def loadgen_lib():
     """tools/libnw_loadgen.so (bench tooling over the public C ABI, tools/nw_loadgen.cpp)."""
     path = os.path.join(ROOT, "tools", "libnw_loadgen.so")
@@ -806,12 +823,19 @@ def run_service_latency(args, rank, world, N: int, cache=None):
         total = max(1, int(rate * seconds))
         lat = np.zeros(total)
         out3 = np.zeros(13)
+        cg0, t_cg0 = cgroup_cpu_stat(), time.perf_counter()
         rc = LG.nw_loadgen_certificates(ctypes.byref(cc), ctypes.byref(cs), ptr_np(exp_st),
                                         ptr_np(exp_ix), rate, total, args.service_max_items,
                                         delay_us, args.service_inflight, args.service_producers,
                                         ptr_np(lat), ptr_np(out3))
+        cg1, t_cg1 = cgroup_cpu_stat(), time.perf_counter()
         check(rc, "nw_loadgen_certificates")
         el, jobs, bad = float(out3[0]), int(out3[1]), int(out3[2])
+        # the process's cgroup over the load: CFS quota throttling stalls every thread of it
+        cg = ({"cgroup_cpus_used": (cg1["usage_usec"] - cg0["usage_usec"]) / 1e6 / (t_cg1 - t_cg0),
+               "cgroup_throttled_periods": cg1["nr_throttled"] - cg0["nr_throttled"],
+               "cgroup_throttled_ms": (cg1["throttled_usec"] - cg0["throttled_usec"]) / 1e3}
+              if cg0 and cg1 else {})
         lag = {"producer_lag_max_ms": float(out3[3] * 1e3),
                "producer_lag_mean_ms": float(out3[4] * 1e3),
                "producer_cpu_per_wall": float(out3[5]), "producer_vcsw": int(out3[6]),
@@ -824,7 +848,7 @@ def run_service_latency(args, rank, world, N: int, cache=None):
                 "p99_invalid_ms": float(np.percentile(lat[inval], 99) * 1e3) if inval.any() else None,
                 "slowest1pct_in_first_tenth": float(np.mean(slow < total // 10)),
                 "slowest1pct_invalid_frac": float(np.mean(inval[slow]))}
-        return {**diag, **lag, "offered_certs_per_s": rate, "certs": total,
+        return {**diag, **lag, **cg, "offered_certs_per_s": rate, "certs": total,
                 "achieved_certs_per_s": total / el if el > 0 else None,
                 "p50_ms": float(np.percentile(lat, 50) * 1e3),
                 "p90_ms": float(np.percentile(lat, 90) * 1e3),
