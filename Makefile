@@ -4,7 +4,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -Inarwhal_amd/csrc -Wall -Wno-unused-function
 CSRC := narwhal_amd/csrc
-HDRS := $(wildcard $(CSRC)/*.hpp) $(CSRC)/nw_kernels.h $(CSRC)/nw_runtime.h include/narwhal_amd.h
+HDRS := $(wildcard $(CSRC)/*.hpp) $(CSRC)/nw_kernels.h $(CSRC)/nw_runtime.h $(CSRC)/nw_host.h include/narwhal_amd.h
 LIB := narwhal_amd/libnarwhal_amd.so
 BUILD := build
 
@@ -38,11 +38,15 @@ $(BUILD)/nw_service.o: $(CSRC)/nw_service.cpp $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
+$(BUILD)/nw_host.o: $(CSRC)/nw_host.cpp $(CSRC)/nw_host.h $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
 $(BUILD)/nw_api.o: $(CSRC)/nw_api.cpp $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-$(LIB): $(BUILD)/nw_kernels.o $(BUILD)/nw_batch.o $(BUILD)/nw_cert.o $(BUILD)/nw_small.o $(BUILD)/nw_api.o $(BUILD)/nw_jobs.o $(BUILD)/nw_wire.o $(BUILD)/nw_service.o
+$(LIB): $(BUILD)/nw_kernels.o $(BUILD)/nw_batch.o $(BUILD)/nw_cert.o $(BUILD)/nw_small.o $(BUILD)/nw_api.o $(BUILD)/nw_jobs.o $(BUILD)/nw_wire.o $(BUILD)/nw_service.o $(BUILD)/nw_host.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 oracle:

@@ -599,11 +599,12 @@ def run_cert_alternating(args, dev, stream, rank, world, N: int, invalid: float,
 
 
 def cpu_baseline_cert(sample, N: int, seconds: float):
-    """Config 2 on the host cores (BASELINE.md row 2): the oracle's Certificate::verify
-    restatement (Header::verify strict + Signature::verify_batch per certificate, the
-    reference's per-certificate algorithm, primary/src/messages.rs:189-215) over a bounded
-    prefix of the same unique stream, all threads, pinned, median of 5 runs; statuses and
-    indices compared with the construction (= the GPU's)."""
+    """Config 2 on the host cores (BASELINE.md row 2): Certificate::verify with the
+    dalek-equivalent signature checks (oracle/nw_dalek.c: Header::verify strict +
+    Signature::verify_batch per certificate, the reference's per-certificate algorithm,
+    primary/src/messages.rs:189-215) over a bounded prefix of the same unique stream, all
+    threads, pinned, median of 5 runs; statuses and indices compared with the construction
+    (= the GPU's)."""
     O = oracle_module()
     s, exp_st, exp_ix = sample
     cores = host_cores()
@@ -618,17 +619,20 @@ def cpu_baseline_cert(sample, N: int, seconds: float):
 
     m = min(len(exp_st), 256)
     t0 = time.perf_counter()
-    O.certificates_verify_many(s["committee"], prefix(m), nthreads=T)
+    O.certificates_verify_many(s["committee"], prefix(m), nthreads=T, engine="dalek")
     per = (time.perf_counter() - t0) / m
     m = int(min(len(exp_st), max(m, seconds / 6 / max(per, 1e-9))))
     p = prefix(m)
-    st, ix = O.certificates_verify_many(s["committee"], p, nthreads=T)
+    st, ix = O.certificates_verify_many(s["committee"], p, nthreads=T, engine="dalek")
     agree = bool(np.array_equal(st, exp_st[:m]) and np.array_equal(ix, exp_ix[:m]))
-    rate, secs = median_rate(lambda: O.certificates_verify_many(s["committee"], p, nthreads=T), m)
-    return {"value": rate, "unit": "certs/s", "cores": T, "kind": "port",
+    rate, secs = median_rate(lambda: O.certificates_verify_many(s["committee"], p, nthreads=T,
+                                                                engine="dalek"), m)
+    return {"value": rate, "unit": "certs/s", "cores": T, "kind": "port", "engine": "dalek",
             "host": cores, "pinned": os.environ.get("OMP_PROC_BIND"),
-            "sample": f"median of {len(secs)} runs over the first {m} unique N={N} certificates, "
-                      f"oracle certificates_verify_many (per-certificate verify_batch), {T} threads",
+            "sample": f"dalek-equivalent restatement; median of {len(secs)} runs over the first "
+                      f"{m} unique N={N} certificates, certificates_verify_many "
+                      f"(per-certificate verify_batch), {T} threads",
+            "algorithm": O.DALEK_ALGORITHM,
             "run_s": secs, "statuses_match": agree}
 
 
@@ -932,18 +936,20 @@ def run_service_latency(args, rank, world, N: int, cache=None):
                     "vote_sigs": s["vote_sigs"][int(vo[a]):int(vo[m])]}
         singles = [prefix(i, i + 1) for i in range(200)]
         for p1 in singles[:5]:
-            O.certificates_verify_many(s["committee"], p1, nthreads=1)
+            O.certificates_verify_many(s["committee"], p1, nthreads=1, engine="dalek")
         secs = []
         for p1 in singles:
             t = time.perf_counter()
-            O.certificates_verify_many(s["committee"], p1, nthreads=1)
+            O.certificates_verify_many(s["committee"], p1, nthreads=1, engine="dalek")
             secs.append(time.perf_counter() - t)
         res["cpu_oracle_one_thread"] = {
             "p50_ms": float(np.percentile(secs, 50) * 1e3),
             "p99_ms": float(np.percentile(secs, 99) * 1e3),
             "certs_per_s": 1.0 / float(np.mean(secs)), "cores": 1, "kind": "port",
-            "sample": "200 single Certificate::verify calls (oracle certificates_verify_many, "
-                      "1 thread, per-certificate verify_batch as the reference)"}
+            "engine": "dalek",
+            "sample": "dalek-equivalent restatement; 200 single Certificate::verify calls "
+                      "(certificates_verify_many, 1 thread, per-certificate verify_batch as the "
+                      "reference)"}
     return res
 
 
@@ -1054,37 +1060,42 @@ def run_worker_latency(args, rank, world):
 
 
 def cpu_baseline_batch(sample, seconds: float):
-    """Config 1 on the host: the oracle's verify_batch (the
-    dalek-equivalent restatement, crypto/src/lib.rs:206-219) on the same 10k batch --
+    """Config 1 on the host: the dalek-equivalent verify_batch
+    (oracle/nw_dalek.c: Pippenger w = 8 over 20,001 points, crypto/src/lib.rs:206-219) on
+    the same 10k batch --
     1 thread (dalek's verify_batch is single-threaded; one call = one batch) and all threads
     with one 10k batch per thread concurrently; pinned; median of 5 runs each."""
     O = oracle_module()
     digest, pks, sigs = sample
     cores = host_cores()
     T = cores["threads"]
-    st, _ = O.verify_batch(digest.tobytes(), pks, sigs)
+    st, _ = O.verify_batch(digest.tobytes(), pks, sigs, engine="dalek")
     assert st == 0
     n = len(pks)
-    r1, s1 = median_rate(lambda: O.verify_batch(digest.tobytes(), pks, sigs), n)
+    r1, s1 = median_rate(lambda: O.verify_batch(digest.tobytes(), pks, sigs, engine="dalek"), n)
     dg = np.tile(digest, (T, 1))
     pk_t, sg_t = np.tile(pks, (T, 1)), np.tile(sigs, (T, 1))
     off = (np.arange(T + 1) * n).astype(np.uint64)
-    stT = O.verify_batch_many(dg, pk_t, sg_t, off, nthreads=T)
+    stT = O.verify_batch_many(dg, pk_t, sg_t, off, nthreads=T, engine="dalek")
     assert (stT == 0).all()
-    rT, sT = median_rate(lambda: O.verify_batch_many(dg, pk_t, sg_t, off, nthreads=T), T * n)
-    return {"value": rT, "unit": "verifies/s", "cores": T, "kind": "port", "host": cores,
-            "pinned": os.environ.get("OMP_PROC_BIND"),
-            "sample": f"median of 5 runs: {T} concurrent verify_batch calls over the 10k config-1 "
-                      f"batch (one per thread), oracle verify_batch_many",
+    rT, sT = median_rate(lambda: O.verify_batch_many(dg, pk_t, sg_t, off, nthreads=T,
+                                                     engine="dalek"), T * n)
+    return {"value": rT, "unit": "verifies/s", "cores": T, "kind": "port", "engine": "dalek",
+            "host": cores, "pinned": os.environ.get("OMP_PROC_BIND"),
+            "sample": f"dalek-equivalent restatement; median of 5 runs: {T} concurrent "
+                      f"verify_batch calls over the 10k config-1 batch (one per thread), "
+                      f"verify_batch_many", "algorithm": O.DALEK_ALGORITHM,
             "run_s": sT, "one_thread": {"value": r1, "unit": "verifies/s", "cores": 1,
                                         "sample": "median of 5 single verify_batch calls "
                                                   "(one 10k batch, 1 thread)", "run_s": s1}}
 
 
 def cpu_baseline_strict(sample, seconds: float):
-    """Oracle ('port', the dalek-equivalent restatement) on the host cores, pinned, bounded:
-    a prefix of the unique corpus sized to ~seconds/6 per run, median of 5 runs; the
-    prefix's statuses are compared with the GPU's."""
+    """The dalek-equivalent restatement ('port', oracle/nw_dalek.c: ed25519-dalek 1.0.1
+    verify_strict's NAF-5 / affine NAF-8 double-base chain over curve25519-dalek's u64
+    field) on the host cores, pinned, bounded: a prefix of the unique corpus sized to
+    ~seconds/6 per run, median of 5 runs; the prefix's statuses are compared with the
+    GPU's."""
     O = oracle_module()
     msgs_u, pks_u, sigs_u, gpu_st = sample
     cores = host_cores()
@@ -1092,17 +1103,23 @@ def cpu_baseline_strict(sample, seconds: float):
     m, p, s = (t.cpu().numpy() for t in (msgs_u, pks_u, sigs_u))
     k = min(len(m), 4096)
     t0 = time.perf_counter()
-    O.verify_strict_many(m[:k], p[:k], s[:k], nthreads=T)
+    O.verify_strict_many(m[:k], p[:k], s[:k], nthreads=T, engine="dalek")
     per = (time.perf_counter() - t0) / k
     k = int(min(len(m), max(k, seconds / 6 / max(per, 1e-9))))
     m, p, s = m[:k], p[:k], s[:k]
-    st = O.verify_strict_many(m, p, s, nthreads=T)
+    st = O.verify_strict_many(m, p, s, nthreads=T, engine="dalek")
     agree = bool(np.array_equal(st, gpu_st[:k]))
-    rate, secs = median_rate(lambda: O.verify_strict_many(m, p, s, nthreads=T), k)
-    return dict(value=rate, unit="verifies/s", cores=T, kind="port", host=cores,
+    rate, secs = median_rate(lambda: O.verify_strict_many(m, p, s, nthreads=T, engine="dalek"), k)
+    # the checker (nw_oracle.c, fixed 4-bit windows) on the same prefix, for the record
+    kc = min(k, 16384)
+    rc, _ = median_rate(lambda: O.verify_strict_many(m[:kc], p[:kc], s[:kc], nthreads=T), kc, runs=3)
+    return dict(value=rate, unit="verifies/s", cores=T, kind="port", engine="dalek", host=cores,
                 pinned=os.environ.get("OMP_PROC_BIND"),
-                sample=f"median of {len(secs)} runs over the first {k} items of the unique mixed "
-                       f"corpus, oracle verify_strict_many, {T} threads", run_s=secs), agree
+                sample=f"dalek-equivalent restatement (NAF-5 A / affine NAF-8 B double-base); "
+                       f"median of {len(secs)} runs over the first {k} items of the unique mixed "
+                       f"corpus, verify_strict_many, {T} threads, statuses == GPU's",
+                algorithm=O.DALEK_ALGORITHM, statuses_match=agree, checker_value=rc,
+                run_s=secs), agree
 
 
 def summary(r: dict) -> dict:
@@ -1179,7 +1196,7 @@ LINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_ste
 ROOFLINE_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_unit",
                  "traffic_source", "algorithmic_bytes", "kernel", "kernel_ms", "work_per_unit",
                  "peak_measured", "frac_measured", "issue_peak", "issue_frac")
-CPU_KEYS = ("value", "unit", "cores", "kind", "sample")
+CPU_KEYS = ("value", "unit", "cores", "kind", "engine", "sample")
 
 
 def compact_line(result: dict, detail_path: str | None = None) -> dict:

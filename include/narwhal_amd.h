@@ -225,7 +225,8 @@ int nw_path_stats(uint64_t* small_jobs, uint64_t* pipeline_jobs);
  * max_inflight jobs are on the device at once (the next batch keeps filling meanwhile).
  * Small jobs (up to ~64k signatures) are single launches that do not wait for one another
  * (nw_path_stats). A second service thread waits for the jobs in
- * order and calls fn(arg, status, index) once per accepted request: status / index as the
+ * order and calls fn(arg, status, index) once per accepted request (or a hedge thread does,
+ * nw_service_set_hedge): status / index as the
  * corresponding bulk call returns them (NW_DAG_* for messages, NW_ERR_* for verify /
  * verify_batch, index = the batch's fail index), or a negative NW_E_* if the job failed.
  * fn runs on that thread; it may submit new requests but must not call nw_service_drain or
@@ -261,6 +262,25 @@ int nw_service_flush(nw_service* s);
 int nw_service_drain(nw_service* s);
 /* Requests accepted and jobs submitted so far (either pointer may be NULL). */
 int nw_service_stats(nw_service* s, uint64_t* requests, uint64_t* jobs);
+/* Hedge (on by default: 1000 us, 4 threads, 512 units; NW_SERVICE_HEDGE_US / _THREADS /
+ * _QUEUED change the defaults). A request whose verdict has not arrived deadline_us after
+ * its batch's first request (its device job is late, or its batch still waits for a job
+ * slot) is verified on the host as well (the nw_host_* path below: the kernels' arithmetic
+ * compiled for the CPU, same statuses and indices, fresh CSPRNG coefficients), and the
+ * first verdict is delivered: fn is still called exactly once per request, but then from
+ * one of the `threads` hedge threads, possibly before requests accepted earlier. At most
+ * max_queued units (certificate = 1 + votes, batch = its votes, else 1) wait for the hedge
+ * threads; later late requests wait for the device, so a stall under load costs at most
+ * `threads` cores. deadline_us = 0 or threads = 0 turns hedging off. Why: the primary's Core
+ * verifies inline on one task (primary/src/core.rs:338-346), so a late device job would
+ * stall the primary. Header / vote / certificate requests are hedged once the committee's
+ * host tables exist (built in the background at create, ~2-5 ms of a core per key). */
+int nw_service_set_hedge(nw_service* s, uint32_t deadline_us, uint32_t threads,
+                         uint64_t max_queued);
+/* Requests queued for the hedge, requests the host answered first, batches the host took
+ * whole before submission (any pointer may be NULL). */
+int nw_service_hedge_stats(nw_service* s, uint64_t* hedged, uint64_t* host_first,
+                           uint64_t* host_only_batches);
 /* Drain, stop the service threads and free the service. */
 void nw_service_destroy(nw_service* s);
 
@@ -382,6 +402,26 @@ int nw_dev_certificates_verify_many(const nw_committee* committee, const nw_cert
                                     int headers_only, const void* z16, const uint8_t* zkey32,
                                     void* workspace, int32_t* status_out, uint64_t* index_out,
                                     void* stream);
+
+/* ---- host verification path: the aggregation service's hedge --------------------------
+ * The kernels' own arithmetic headers compiled for the CPU (narwhal_amd/csrc/nw_host.cpp),
+ * with the same statuses and indices as the device entry points above. The service uses it
+ * to answer a request whose device job is late (nw_service_set_hedge); these entries expose
+ * it for the parity tests and need no device. No device entry point ever falls back to it.
+ * Random coefficients (z16 NULL) come from ChaCha20 keyed by the OS CSPRNG, as on the
+ * device. Return 0, or a negative NW_E_* (the verdicts go to status_out / index_out). */
+int nw_host_verify_strict_many(const uint8_t* msgs, size_t msg_stride, const uint8_t* pks,
+                               const uint8_t* sigs, size_t n, int32_t* status_out);
+int nw_host_verify_batch_many(const uint8_t* digests, const uint8_t* pks, const uint8_t* sigs,
+                              const uint64_t* offsets, size_t nbatches, const uint8_t* z16,
+                              int32_t* status_out, uint64_t* fail_index_out);
+int nw_host_certificates_verify_many(const nw_committee* committee, const nw_certificates* certs,
+                                     const uint8_t* z16, int headers_only, int32_t* status_out,
+                                     uint64_t* index_out);
+int nw_host_votes_verify_many(const nw_committee* committee, const uint8_t* ids,
+                              const uint64_t* rounds, const uint8_t* origins,
+                              const uint8_t* authors, const uint8_t* sigs, size_t n,
+                              int32_t* status_out);
 
 #ifdef __cplusplus
 }

@@ -1074,38 +1074,68 @@ static uint32_t key_width(size_t nkeys) {
   return nkeys <= kKeyW20Keys ? 20u : 16u;
 }
 
+// Frees the device's key tables (every earlier user is ordered before d.last).
+static void free_key_tables(SharedDev& d) {
+  if (d.last_valid) (void)hipEventSynchronize(d.last);
+  if (d.ktabs) (void)hipFree(d.ktabs);
+  if (d.kok) (void)hipFree(d.kok);
+  if (d.ksaved) (void)hipFree(d.ksaved);
+  if (d.kflag) (void)hipFree(d.kflag);
+  d.ktabs = nullptr;
+  d.kok = d.ksaved = d.kflag = nullptr;
+  d.kcap = d.ksaved_n = 0;
+  d.kW = 0;
+  d.khost.clear();
+}
+
+// Key tables of width W for nkeys keys (room for 16 keys at 16 bits, 1 GB; for the committee
+// itself at wider combs). NW_KEYTAB_LIMIT=bytes (test hook) fails a key-table allocation above
+// it, as a device shared with other ranks or tenants would.
+static hipError_t alloc_key_tables(SharedDev& d, size_t nkeys, uint32_t W) {
+  const size_t cap = W == 16 ? (nkeys < 16 ? 16 : nkeys) : nkeys;
+  const size_t bytes = nw::key_tables_bytes(cap, nw::keyspec_for(W));
+  static const unsigned long long limit = [] {
+    const char* e = getenv("NW_KEYTAB_LIMIT");
+    return e ? strtoull(e, nullptr, 10) : 0ull;
+  }();
+  hipError_t e = limit && bytes > limit ? hipErrorOutOfMemory
+                                        : nw::table_malloc(&d.ktabs, bytes);
+  static const bool klog = getenv("NW_KEYTAB_LOG") != nullptr;   // diagnostics
+  if (klog) {
+    size_t fr = 0, tot = 0;
+    (void)hipMemGetInfo(&fr, &tot);
+    fprintf(stderr, "[keytab] keys %zu width %u bytes %zu -> %s (free %zu of %zu)\n", nkeys, W,
+            bytes, e == hipSuccess ? "ok" : "FAILED", fr, tot);
+  }
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.kok), 4 * cap);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.ksaved), 32 * cap);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.kflag), 4);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    free_key_tables(d);
+    return e;
+  }
+  d.kcap = cap;
+  d.kW = W;
+  return hipSuccess;
+}
+
 int Lease::key_tables(size_t nkeys, void** tabs, uint32_t** ok, nw::keyspec* ks,
                       uint32_t** saved, uint32_t** flag, bool* force) {
   SharedDev& d = g_shared[dev_];
   const uint32_t W = key_width(nkeys);
-  if (nkeys > d.kcap || !d.ktabs || W != d.kW) {
-    // every earlier user of the old tables is ordered before d.last
-    if (d.last_valid) (void)hipEventSynchronize(d.last);
-    if (d.ktabs) (void)hipFree(d.ktabs);
-    if (d.kok) (void)hipFree(d.kok);
-    if (d.ksaved) (void)hipFree(d.ksaved);
-    if (d.kflag) (void)hipFree(d.kflag);
-    d.ktabs = nullptr;
-    d.kok = d.ksaved = d.kflag = nullptr;
-    d.kcap = d.ksaved_n = 0;
-    d.khost.clear();
-    // room for 16 keys at 16 bits (1 GB), for the committee itself at wider combs
-    const size_t cap = W == 16 ? (nkeys < 16 ? 16 : nkeys) : nkeys;
-    hipError_t e = nw::table_malloc(&d.ktabs, nw::key_tables_bytes(cap, nw::keyspec_for(W)));
-    static const bool klog = getenv("NW_KEYTAB_LOG") != nullptr;   // diagnostics
-    if (klog) {
-      size_t fr = 0, tot = 0;
-      (void)hipMemGetInfo(&fr, &tot);
-      fprintf(stderr, "[keytab] keys %zu width %u bytes %zu -> %s (free %zu of %zu)\n", nkeys, W,
-              nw::key_tables_bytes(cap, nw::keyspec_for(W)), e == hipSuccess ? "ok" : "FAILED",
-              fr, tot);
-    }
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.kok), 4 * cap);
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.ksaved), 32 * cap);
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.kflag), 4);
+  // Tables that hold nkeys keys are kept when they have the preferred width, or when they are
+  // 16-bit tables and the preferred width is wider (a device alternating between committees of
+  // 50 and 100 keys keeps its 16-bit tables instead of reallocating 47-94 GB per switch; the
+  // keys themselves are rebuilt in place, k_key_cmp).
+  const bool usable = d.ktabs && nkeys <= d.kcap && (d.kW == W || (d.kW == 16 && W > 16));
+  if (!usable) {
+    free_key_tables(d);
+    hipError_t e = alloc_key_tables(d, nkeys, W);
+    // no room at the wider comb: 16 bits (67 MB per key) still run the keyed checks, several
+    // times faster than the unkeyed fallback the caller takes on NW_E_OUT_OF_MEMORY
+    if (e == hipErrorOutOfMemory && W != 16) e = alloc_key_tables(d, nkeys, 16);
     if (e != hipSuccess) return ::set_err(NW_E_OUT_OF_MEMORY, "hipMalloc (key tables)", e);
-    d.kcap = cap;
-    d.kW = W;
   }
   *tabs = d.ktabs;
   *ok = d.kok;

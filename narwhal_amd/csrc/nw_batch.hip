@@ -2026,9 +2026,9 @@ size_t batch_workspace_bytes(uint64_t nbatches, uint64_t nitems) {
 }
 
 // Committee key tables (a committee's keys, tabulated once while the committee is
-// unchanged): per key the comb tables j * 2^(W t) A (W = kKeyW, t < kKeyCombT,
-// j = 0..2^(W-1), affine niels; nw_kernels.h), plus a j * 2^128 A table when W does not
-// divide 128. Keyed strict checks (headers, votes) take
+// unchanged): per key the comb tables j * 2^(W t) A with the runtime keyspec (nw_kernels.h
+// keyspec_for: W = 20 up to 64 keys, else 16; t < ntab = ceil(253 / W), j = 0..2^(W-1),
+// affine niels), plus a j * 2^128 A table when W does not divide 128. Keyed strict checks (headers, votes) take
 // [k]A from them with no doublings; keyed vote chunks use the j * A and j * 2^128 A tables.
 //   k_key_cmp   one block: flag = force or (pks != saved); then saved = pks when they differ.
 //   k_key_base  one lane per key: decompress (dalek semantics), the comb bases 2^(W t) A by

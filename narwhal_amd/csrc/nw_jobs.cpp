@@ -131,6 +131,8 @@ void job_recycle(nw_job* j) {
 int job_abort(nw_job* j, int rc) {
   (void)hipStreamSynchronize(j->stream);
   j->pending = false;
+  // a fused config-1 launch may have queued: its counters are no longer known to be zero
+  if (j->dfz) j->dfz_dirty = true;
   job_recycle(j);
   return rc;
 }
@@ -1093,7 +1095,10 @@ int nw_job_poll(nw_job* job) {
   if (!job->pending) return 1;
   hipError_t e = hipEventQuery(job->done);
   if (e == hipErrorNotReady) return 0;
-  if (e != hipSuccess) return set_err(NW_E_DEVICE, "hipEventQuery", e);
+  if (e != hipSuccess) {
+    if (job->dfz) job->dfz_dirty = true;   // counters of a failed fused launch: clear on reuse
+    return set_err(NW_E_DEVICE, "hipEventQuery", e);
+  }
   job_deliver(job);
   return 1;
 }
@@ -1109,7 +1114,11 @@ int nw_job_wait(nw_job* job) {
     return first;
   }
   if (!job->pending) return 0;
-  JOB_HIP(hipEventSynchronize(job->done), "hipEventSynchronize");
+  const hipError_t e = hipEventSynchronize(job->done);
+  if (e != hipSuccess) {
+    if (job->dfz) job->dfz_dirty = true;   // counters of a failed fused launch: clear on reuse
+    return set_err(NW_E_DEVICE, "hipEventSynchronize", e);
+  }
   job_deliver(job);
   return 0;
 }

@@ -54,7 +54,10 @@ hipError_t upload_batch_consts();
 // j = 0..2^(W-1) (affine niels), k's digits signed except the top one when ntab W > 256;
 // the keyed vote chunks' second 8-bit table j * 2^128 A is comb table 128 / W when W divides
 // 128, else one more table built from 2^128 A. W = 16: 16 tables, 67 MB per key; W = 20:
-// 13 + 1 tables, 940 MB per key.
+// 13 + 1 tables, 940 MB per key; W = 24 (NW_KEY_WIDTH=24 only): 11 tables.
+// Only these three widths are built (nw_api.cpp key_width / alloc_key_tables); any other W
+// (e.g. the 0 of a device without tables) is mapped to 16, so that no caller can divide by
+// zero or shift by W - 1 < 0 here, on the host or the device.
 #define NW_KS __host__ __device__ __forceinline__
 struct keyspec {
   uint32_t W, ntab, nsigned, nent, tab, half;
@@ -62,6 +65,7 @@ struct keyspec {
 };
 NW_KS constexpr keyspec keyspec_for(uint32_t W) {
   keyspec ks{};
+  if (W != 16 && W != 20 && W != 24) W = 16;
   ks.W = W;
   ks.ntab = (253 + W - 1) / W;
   ks.nsigned = ks.ntab * W > 256 ? ks.ntab - 1 : ks.ntab;

@@ -757,7 +757,13 @@ hipError_t table_malloc(void** p, size_t bytes) {
     const unsigned long long lim = strtoull(e, nullptr, 10);
     if (lim && bytes > lim) return hipErrorOutOfMemory;
   }
-  return hipMalloc(p, bytes);
+  const hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) {
+    // reported by the return value; leave no last error behind for the next launch check
+    *p = nullptr;
+    (void)hipGetLastError();
+  }
+  return e;
 }
 
 

@@ -36,6 +36,19 @@
 //            callback. At most max_inflight jobs are on the device at once (backpressure on
 //            the flusher; requests keep accumulating into the next, larger batch meanwhile,
 //            which is what keeps the device efficient under load).
+//   hedge    (nw_service_set_hedge; on by default) a request whose verdict has not arrived
+//            `deadline` after its batch's first request is verified on the host as well
+//            (nw_host.cpp: the kernels' own arithmetic compiled for the CPU, same statuses
+//            and indices), and whichever verdict comes first is delivered, exactly once (one
+//            atomic flag per request). A hedger thread looks every deadline / 4 at the batches
+//            on the device or being submitted, and at batches still waiting for a job slot
+//            (those are then taken for the host alone and never submitted); `threads` host
+//            threads answer them, oldest first. At most `max_queued` units wait for those
+//            threads, so a device stall under heavy load costs at most `threads` cores and
+//            the rest waits for the device as before. Why: the primary verifies on its one
+//            Core task (primary/src/core.rs:338-346), so a device job that stalls for 10-40 ms
+//            (the box's host-memory access episodes) stalls the primary, while
+//            one certificate costs a host core well under a millisecond.
 // Batches are recycled; a batch is never freed before the service (a request that loaded a
 // batch just before it was taken only touches its cursor and writer count, and fails).
 #include <stdio.h>
@@ -55,6 +68,7 @@
 #include <vector>
 
 #include "narwhal_amd.h"
+#include "nw_host.h"
 #include "nw_runtime.h"
 
 namespace {
@@ -139,8 +153,27 @@ struct Batch {
   std::vector<uint64_t> index;
   nw_job* job = nullptr;
   int rc = 0;
+  // hedge: answered[i] = 1 once request i's callback has been claimed (device or host)
+  std::vector<uint8_t> answered;
+  bool hedged = false;             // queued for the hedge threads (guarded by the hedge mutex)
+  bool host_only = false;          // taken for the host alone, never submitted
+  std::atomic<size_t> hnext{0};    // next request a hedge thread claims
+  std::atomic<size_t> hdone{0};    // requests the hedge threads have finished with
+  std::atomic<int> hrefs{0};       // hedge threads inside the batch
 
   explicit Batch(Kind k) : kind(k) {}
+
+  // the callback of request i is ours to call (exactly one caller wins)
+  bool claim(size_t i) { return __atomic_exchange_n(&answered[i], (uint8_t)1, __ATOMIC_ACQ_REL) == 0; }
+  bool is_answered(size_t i) const { return __atomic_load_n(&answered[i], __ATOMIC_ACQUIRE) != 0; }
+  // fresh per-request flags once the final count n is known (before anyone can claim)
+  void reset_answers() {
+    answered.assign(n, 0);
+    hedged = host_only = false;
+    hnext.store(0, std::memory_order_relaxed);
+    hdone.store(0, std::memory_order_relaxed);
+    hrefs.store(0, std::memory_order_relaxed);
+  }
 
   // arrays for caps c (only the ones this kind uses)
   bool reserve(const Caps& c) {
@@ -254,7 +287,8 @@ struct nw_service {
   std::atomic<bool> stop{false};
   bool force = false, flusher_done = false;
   std::atomic<uint64_t> accepted{0};
-  uint64_t completed = 0, jobs = 0;
+  std::atomic<uint64_t> completed{0};   // callbacks delivered (completer and hedge threads)
+  uint64_t jobs = 0;
   // NW_SERVICE_DEBUG: seconds the flusher spent submitting / blocked on max_inflight, the
   // completer waiting for jobs / running callbacks, caller-thread submits and full batches
   // (printed at destroy)
@@ -285,6 +319,30 @@ struct nw_service {
   // 0.18 ms (smaller jobs, each paying the header digest's serial chain)
   size_t eager_jobs = 2;
   std::thread flusher, completer;
+
+  // ---- hedge (nw_service_set_hedge) ----
+  int64_t hedge_ns = 1000000;          // deadline after a batch's first request; 0 = off
+  uint32_t hedge_threads = 4;
+  uint64_t hedge_max_queued = 512;     // units (certificate = 1 + votes) waiting at most
+  // NW_SERVICE_TEST_DELAY_US (test hook): the completer holds every device verdict until this
+  // long after its batch's first request, so the hedge answers first
+  int64_t test_delay_ns = 0;
+  nw::host::Committee* hc = nullptr;   // the committee's host tables (built in the background)
+  std::atomic<bool> hc_ready{false};
+  std::thread hc_builder;
+  std::mutex hm;                       // hedge queue (lock order: m before hm)
+  std::condition_variable cv_hw;       // hedge threads: work queued / stop
+  std::condition_variable cv_hedger;   // hedger: stop
+  std::deque<Batch*> hq;               // batches the hedge threads answer, oldest first
+  uint64_t hq_units = 0;
+  std::vector<std::unique_ptr<Batch>> hostonly;   // taken for the host alone (owned here)
+  std::vector<std::unique_ptr<Batch>> retired;    // device-done hedged batches still entered
+  std::vector<Batch*> submitting_b;    // batches inside launch() (under m)
+  bool hworkers_stop = false;          // under hm
+  std::atomic<bool> hedger_stop{false};
+  std::thread hedger;
+  std::vector<std::thread> hworkers;
+  std::atomic<uint64_t> n_hedged{0}, n_host_first{0}, n_host_only{0};
 
   // One request of kind k with v1 header bytes and v2 votes / items: reserve its ranges in
   // the open batch (write(b, i, v1_off, v2_off) fills them), then wake the flusher or submit.
@@ -460,6 +518,9 @@ struct nw_service {
   void launch(std::unique_lock<std::mutex>& lk, std::unique_ptr<Batch> b) {
     ++open_jobs;
     ++submitting;
+    b->reset_answers();
+    Batch* const raw = b.get();
+    submitting_b.push_back(raw);   // the hedger may hedge it while the submit is slow
     lk.unlock();
     if (debug) b->t_taken = now_ns();
     b->wait_writers();
@@ -473,6 +534,7 @@ struct nw_service {
     const double ds = std::chrono::duration<double>(Clock::now() - s0).count();
     if (debug) b->t_sub1 = now_ns();
     lk.lock();
+    submitting_b.erase(std::find(submitting_b.begin(), submitting_b.end(), raw));
     --submitting;
     t_submit += ds;
     ++jobs;
@@ -600,6 +662,10 @@ struct nw_service {
       lk.unlock();
       int rc = b->rc;
       const Clock::time_point w0 = Clock::now();
+      if (test_delay_ns) {   // test hook: a late device verdict
+        const int64_t until = b->first_ns.load(std::memory_order_relaxed) + test_delay_ns;
+        while (now_ns() < until) std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
       if (b->job) {
         // poll first (a small job finishes in ~0.1 ms; a blocking event wait adds the
         // runtime's wake-up latency to every verdict), then block
@@ -617,8 +683,13 @@ struct nw_service {
       const int64_t tdone = debug ? now_ns() : 0;
       const size_t n = b->n;
       const Req* reqs = b->reqs.as<Req>();
+      uint64_t mine = 0;
       for (size_t i = 0; i < n; ++i)
-        reqs[i].fn(reqs[i].arg, rc ? rc : b->status[i], rc ? 0 : b->index[i]);
+        if (b->claim(i)) {   // not already answered by the hedge
+          reqs[i].fn(reqs[i].arg, rc ? rc : b->status[i], rc ? 0 : b->index[i]);
+          ++mine;
+        }
+      completed.fetch_add(mine, std::memory_order_acq_rel);
       const Clock::time_point c1 = Clock::now();
       if (debug && b->n && d_done.size() < (1u << 22)) {
         const int64_t f = b->first_ns.load(std::memory_order_relaxed);
@@ -639,13 +710,238 @@ struct nw_service {
       cv_space.notify_one();
       t_wait += std::chrono::duration<double>(c0 - w0).count();
       t_callbacks += std::chrono::duration<double>(c1 - c0).count();
-      completed += n;
       // a job slot freed below eager_jobs: flush what has queued
       if (--open_jobs < eager_jobs) cv_flush.notify_one();
       own->how = 0;
-      spare[own->kind].push_back(std::move(own));    // cursor stays sealed while spare
+      recycle(std::move(own));
       cv_idle.notify_all();
     }
+  }
+
+  // ---- hedge --------------------------------------------------------------------------
+  // A finished device batch back to the spares (under m), unless hedge threads are still
+  // inside it: then the hedger recycles it once they have left.
+  void recycle(std::unique_ptr<Batch> b) {
+    if (b->hedged) {
+      std::lock_guard<std::mutex> g(hm);
+      auto it = std::find(hq.begin(), hq.end(), b.get());
+      if (it != hq.end()) {
+        hq_units -= b->units();
+        hq.erase(it);
+      }
+      if (b->hrefs.load(std::memory_order_acquire) > 0) {
+        retired.push_back(std::move(b));
+        return;
+      }
+    }
+    spare[b->kind].push_back(std::move(b));
+  }
+
+  // Queue b for the hedge threads (under m); host_only: b was taken before submission and is
+  // owned by the hedge from now on. False when the budget has no room for it.
+  bool queue_hedge(std::unique_ptr<Batch>* own, Batch* b) {
+    std::lock_guard<std::mutex> g(hm);
+    if (hq_units + b->units() > hedge_max_queued || hworkers.empty()) return false;
+    b->hedged = true;
+    hq.push_back(b);
+    hq_units += b->units();
+    if (own) {
+      b->host_only = true;
+      hostonly.push_back(std::move(*own));
+      n_host_only.fetch_add(1, std::memory_order_relaxed);
+    }
+    n_hedged.fetch_add(b->n, std::memory_order_relaxed);
+    cv_hw.notify_all();
+    return true;
+  }
+
+  bool hedgeable(const Batch& b, int64_t now) const {
+    if (b.hedged || b.n == 0) return false;
+    const int64_t f = b.first_ns.load(std::memory_order_relaxed);
+    if (f == 0 || now - f < hedge_ns) return false;
+    // messages need the committee's host tables (built at create, in the background)
+    return b.kind == K_STRICT || b.kind == K_BATCH || hc_ready.load(std::memory_order_acquire);
+  }
+
+  void hedger_main() {
+    std::unique_lock<std::mutex> lk(m);
+    while (!hedger_stop.load(std::memory_order_acquire)) {
+      const int64_t tick = std::max<int64_t>(50000, std::min<int64_t>(250000, hedge_ns / 4));
+      wait_ns(cv_hedger, lk, hedge_ns ? tick : 2000000);
+      if (hedger_stop.load(std::memory_order_acquire)) break;
+      // hedged batches the hedge threads have left: back to the spares
+      {
+        std::lock_guard<std::mutex> g(hm);
+        for (size_t i = 0; i < retired.size();) {
+          if (retired[i]->hrefs.load(std::memory_order_acquire) == 0) {
+            spare[retired[i]->kind].push_back(std::move(retired[i]));
+            retired[i] = std::move(retired.back());
+            retired.pop_back();
+          } else {
+            ++i;
+          }
+        }
+        for (size_t i = 0; i < hostonly.size();) {
+          Batch& b = *hostonly[i];
+          if (b.hdone.load(std::memory_order_acquire) == b.n &&
+              b.hrefs.load(std::memory_order_acquire) == 0) {
+            std::unique_ptr<Batch> own = std::move(hostonly[i]);
+            hostonly[i] = std::move(hostonly.back());
+            hostonly.pop_back();
+            spare[own->kind].push_back(std::move(own));
+          } else {
+            ++i;
+          }
+        }
+      }
+      if (!hedge_ns) continue;
+      const int64_t now = now_ns();
+      // batches on the device, or inside a submit, whose verdicts are late
+      for (auto& u : inflight)
+        if (u->rc == 0 && hedgeable(*u, now)) (void)queue_hedge(nullptr, u.get());
+      for (Batch* b : submitting_b)
+        if (hedgeable(*b, now)) (void)queue_hedge(nullptr, b);
+      // batches still waiting for a job slot (backpressure): the host takes them whole
+      for (int k = 0; k < K_COUNT; ++k) {
+        while (!sealed[k].empty() && hedgeable(*sealed[k].front(), now)) {
+          std::unique_ptr<Batch> own = std::move(sealed[k].front());
+          Batch* b = own.get();
+          b->reset_answers();
+          if (!queue_hedge(&own, b)) {
+            sealed[k].front() = std::move(own);
+            break;
+          }
+          sealed[k].pop_front();
+          --nsealed;
+        }
+        Batch& ob = *open[k];
+        const uint64_t c = ob.cursor.load(std::memory_order_acquire);
+        if (c_req(c) == 0 || (c & kSealed)) continue;
+        const int64_t f = ob.first_ns.load(std::memory_order_relaxed);
+        {
+          std::lock_guard<std::mutex> g(hm);
+          if (f == 0 || now - f < hedge_ns || hworkers.empty() ||
+              hq_units + Batch::units_of(static_cast<Kind>(k), c_req(c), c_v2(c)) > hedge_max_queued)
+            continue;
+        }
+        if (k != K_STRICT && k != K_BATCH && !hc_ready.load(std::memory_order_acquire)) continue;
+        std::unique_ptr<Batch> own = take_open(static_cast<Kind>(k));
+        if (!own) continue;
+        Batch* b = own.get();
+        b->reset_answers();
+        if (!queue_hedge(&own, b)) {   // grew past the budget meanwhile: the flusher's again
+          sealed[k].push_front(std::move(own));
+          ++nsealed;
+          cv_flush.notify_one();
+        }
+      }
+    }
+  }
+
+  // Request i of b on the host (nw_host.cpp): status and index as the device job returns them.
+  int answer(const Batch& b, size_t i, uint64_t* ix) {
+    *ix = 0;
+    switch (b.kind) {
+      case K_CERT:
+      case K_HEADER: {
+        const uint64_t* ho = b.header_offsets.as<uint64_t>();
+        const uint8_t* hb = b.header_bytes.p + ho[i];
+        const size_t hl = ho[i + 1] - ho[i];
+        const uint32_t np = b.payload_counts.as<uint32_t>()[i];
+        if (b.kind == K_HEADER)
+          return nw::host::header_verify(*hc, hb, hl, np, b.ids.p + 32 * i, b.header_sigs.p + 64 * i, ix);
+        const uint64_t* vo = b.vote_offsets.as<uint64_t>();
+        return nw::host::certificate_verify(*hc, hb, hl, np, b.ids.p + 32 * i,
+                                            b.header_sigs.p + 64 * i, b.vote_pks.p + 32 * vo[i],
+                                            b.vote_sigs.p + 64 * vo[i], vo[i + 1] - vo[i], nullptr,
+                                            ix);
+      }
+      case K_VOTE:
+        return nw::host::vote_verify(*hc, b.ids.p + 32 * i, b.rounds.as<uint64_t>()[i],
+                                     b.origins.p + 32 * i, b.authors.p + 32 * i,
+                                     b.header_sigs.p + 64 * i);
+      case K_STRICT:
+        return nw::host::verify_strict(b.digests.p + 32 * i, b.pks.p + 32 * i, b.sigs.p + 64 * i);
+      case K_BATCH: {
+        const uint64_t* bo = b.batch_offsets.as<uint64_t>();
+        return nw::host::verify_batch(b.digests.p + 32 * i, b.pks.p + 32 * bo[i],
+                                      b.sigs.p + 64 * bo[i], bo[i + 1] - bo[i], nullptr,
+                                      hc_ready.load(std::memory_order_acquire) ? hc : nullptr, ix);
+      }
+      default:
+        return NW_E_INVALID_ARG;
+    }
+  }
+
+  void hedge_worker() {
+    for (;;) {
+      Batch* b = nullptr;
+      size_t i = 0;
+      {
+        std::unique_lock<std::mutex> g(hm);
+        for (;;) {
+          if (!hq.empty()) {
+            b = hq.front();
+            i = b->hnext.fetch_add(1, std::memory_order_acq_rel);
+            if (i < b->n) {
+              b->hrefs.fetch_add(1, std::memory_order_acq_rel);
+              break;
+            }
+            hq.pop_front();   // every request claimed: the batch leaves the queue
+            hq_units -= b->units();
+            continue;
+          }
+          if (hworkers_stop) return;
+          cv_hw.wait(g);
+        }
+      }
+      b->wait_writers();
+      if (!b->is_answered(i)) {
+        uint64_t ix = 0;
+        const int st = answer(*b, i, &ix);
+        // a host error (no CSPRNG) is left to the device, unless there is no device job
+        if ((st >= 0 || b->host_only) && b->claim(i)) {
+          const Req& r = b->reqs.as<Req>()[i];
+          r.fn(r.arg, st, st >= 0 ? ix : 0);
+          n_host_first.fetch_add(1, std::memory_order_relaxed);
+          completed.fetch_add(1, std::memory_order_acq_rel);
+          { std::lock_guard<std::mutex> g(m); }   // no lost wake-up for a drain
+          cv_idle.notify_all();
+        }
+      }
+      b->hdone.fetch_add(1, std::memory_order_acq_rel);
+      b->hrefs.fetch_sub(1, std::memory_order_acq_rel);
+    }
+  }
+
+  // (Re)starts the hedge threads with the current parameters; the old ones first answer
+  // every request already queued.
+  void restart_hedge() {
+    stop_hedge();
+    {
+      std::lock_guard<std::mutex> g(hm);
+      hworkers_stop = false;
+    }
+    hedger_stop.store(false, std::memory_order_release);
+    if (!hedge_ns || !hedge_threads) return;
+    for (uint32_t t = 0; t < hedge_threads; ++t) hworkers.emplace_back([this] { hedge_worker(); });
+    hedger = std::thread([this] { hedger_main(); });
+  }
+  void stop_hedge() {
+    hedger_stop.store(true, std::memory_order_release);
+    {
+      std::lock_guard<std::mutex> g(m);
+    }
+    cv_hedger.notify_all();
+    if (hedger.joinable()) hedger.join();
+    {
+      std::lock_guard<std::mutex> g(hm);
+      hworkers_stop = true;
+    }
+    cv_hw.notify_all();
+    for (auto& t : hworkers) t.join();
+    std::lock_guard<std::mutex> g(hm);
+    hworkers.clear();
   }
 };
 
@@ -671,6 +967,11 @@ int nw_service_create(const nw_committee* committee, size_t max_items, uint32_t 
   s->debug = getenv("NW_SERVICE_DEBUG") != nullptr;
   if (s->debug && strchr(getenv("NW_SERVICE_DEBUG"), '/')) s->debug_path = getenv("NW_SERVICE_DEBUG");
   if (const char* e = getenv("NW_SERVICE_EAGER")) s->eager_jobs = std::max(1, atoi(e));
+  if (const char* e = getenv("NW_SERVICE_TEST_DELAY_US")) s->test_delay_ns = 1000ll * atoll(e);
+  // NW_SERVICE_HEDGE_US / _THREADS / _QUEUED: the hedge's defaults (nw_service_set_hedge)
+  if (const char* e = getenv("NW_SERVICE_HEDGE_US")) s->hedge_ns = 1000ll * atoll(e);
+  if (const char* e = getenv("NW_SERVICE_HEDGE_THREADS")) s->hedge_threads = (uint32_t)atoi(e);
+  if (const char* e = getenv("NW_SERVICE_HEDGE_QUEUED")) s->hedge_max_queued = strtoull(e, nullptr, 10);
   if (committee) {
     const size_t na = committee->nauth, nwk = na ? committee->worker_offsets[na] : 0;
     s->has_committee = true;
@@ -718,6 +1019,13 @@ int nw_service_create(const nw_committee* committee, size_t max_items, uint32_t 
   try {
     s->flusher = std::thread([s] { s->flusher_main(); });
     s->completer = std::thread([s] { s->completer_main(); });
+    // the committee's host tables for the hedge (~2-5 ms of a core per key), off this thread
+    if (s->has_committee)
+      s->hc_builder = std::thread([s] {
+        s->hc = nw::host::committee_new(&s->com);
+        s->hc_ready.store(s->hc != nullptr, std::memory_order_release);
+      });
+    s->restart_hedge();
   } catch (...) {
     {
       std::lock_guard<std::mutex> g(s->m);
@@ -726,6 +1034,9 @@ int nw_service_create(const nw_committee* committee, size_t max_items, uint32_t 
     s->cv_flush.notify_all();
     if (s->flusher.joinable()) s->flusher.join();
     if (s->completer.joinable()) s->completer.join();
+    s->stop_hedge();
+    if (s->hc_builder.joinable()) s->hc_builder.join();
+    nw::host::committee_free(s->hc);
     delete s;
     return set_err(NW_E_OUT_OF_MEMORY, "service threads");
   }
@@ -846,6 +1157,34 @@ int nw_service_drain(nw_service* s) {
   return 0;
 }
 
+int nw_service_set_hedge(nw_service* s, uint32_t deadline_us, uint32_t threads,
+                         uint64_t max_queued) {
+  if (!s) return set_err(NW_E_INVALID_ARG, "null service");
+  if (threads > 64) return set_err(NW_E_INVALID_ARG, "at most 64 hedge threads");
+  s->stop_hedge();
+  {
+    std::lock_guard<std::mutex> g(s->m);
+    s->hedge_ns = 1000ll * deadline_us;
+    s->hedge_threads = threads;
+    s->hedge_max_queued = max_queued;
+  }
+  try {
+    s->restart_hedge();
+  } catch (...) {
+    return set_err(NW_E_OUT_OF_MEMORY, "hedge threads");
+  }
+  return 0;
+}
+
+int nw_service_hedge_stats(nw_service* s, uint64_t* hedged, uint64_t* host_first,
+                           uint64_t* host_only_batches) {
+  if (!s) return set_err(NW_E_INVALID_ARG, "null service");
+  if (hedged) *hedged = s->n_hedged.load();
+  if (host_first) *host_first = s->n_host_first.load();
+  if (host_only_batches) *host_only_batches = s->n_host_only.load();
+  return 0;
+}
+
 int nw_service_stats(nw_service* s, uint64_t* requests, uint64_t* jobs) {
   if (!s) return set_err(NW_E_INVALID_ARG, "null service");
   std::lock_guard<std::mutex> g(s->m);
@@ -864,6 +1203,11 @@ void nw_service_destroy(nw_service* s) {
   s->cv_space.notify_all();
   s->flusher.join();
   s->completer.join();
+  // the hedge answers whatever it took for the host alone, then stops
+  s->stop_hedge();
+  if (s->hc_builder.joinable()) s->hc_builder.join();
+  nw::host::committee_free(s->hc);
+  s->hc = nullptr;
   if (getenv("NW_SERVICE_DEBUG"))
     fprintf(stderr,
             "[narwhal_amd] service: %llu requests, %llu jobs (%llu from callers' threads, "

@@ -11,6 +11,7 @@
  * start-up (d = -121665/121666, sqrt(-1) = 2^((p-1)/4), B.y = 4/5) rather than typed in.
  */
 #include "nw_oracle.h"
+#include "nw_dalek.h"
 
 #include <stdlib.h>
 #include <string.h>
@@ -952,9 +953,19 @@ void nwo_digest_72(const uint8_t x[32], uint64_t round, const uint8_t y[32], uin
   memcpy(out, h, 32);
 }
 
+/* The signature checks the message layer calls: the checker's (nwo_*) or the timed
+ * dalek-equivalent restatement's (nwd_*, nw_dalek.c). */
+typedef struct {
+  int (*strict)(const uint8_t*, size_t, const uint8_t*, const uint8_t*);
+  int (*batch)(const uint8_t*, const uint8_t*, const uint8_t*, size_t, const uint8_t*, size_t*);
+} sig_engine;
+static const sig_engine ENGINE_CHECK = {nwo_verify_strict, nwo_verify_batch};
+static const sig_engine ENGINE_DALEK = {nwd_verify_strict, nwd_verify_batch};
+
 /* Header::verify (messages.rs:48-67). hb = author || round || P x (digest || wid) || parents. */
-static int header_verify(const nwo_committee* c, const uint8_t* hb, size_t hlen, uint32_t np,
-                         const uint8_t id[32], const uint8_t sig[64], uint64_t* index) {
+static int header_verify(const sig_engine* E, const nwo_committee* c, const uint8_t* hb,
+                         size_t hlen, uint32_t np, const uint8_t id[32], const uint8_t sig[64],
+                         uint64_t* index) {
   uint8_t h[64];
   nwo_sha512(hb, hlen, h);
   if (memcmp(h, id, 32) != 0) return NWO_DAG_INVALID_HEADER_ID;
@@ -967,7 +978,7 @@ static int header_verify(const nwo_committee* c, const uint8_t* hb, size_t hlen,
       found |= c->worker_ids[w] == wid;
     if (!found) { *index = e; return NWO_DAG_MALFORMED_HEADER; }
   }
-  int st = nwo_verify_strict(id, 32, hb, sig);
+  int st = E->strict(id, 32, hb, sig);
   return st ? NWO_DAG_INVALID_SIGNATURE + st : 0;
 }
 
@@ -975,15 +986,16 @@ int nwo_header_verify(const nwo_committee* c, const uint8_t* hb, size_t hlen, ui
                       const uint8_t id[32], const uint8_t sig[64], uint64_t* index) {
   uint64_t ix = 0;
   ensure_init();
-  int st = header_verify(c, hb, hlen, np, id, sig, &ix);
+  int st = header_verify(&ENGINE_CHECK, c, hb, hlen, np, id, sig, &ix);
   if (index) *index = ix;
   return st;
 }
 
-int nwo_certificate_verify(const nwo_committee* c, const uint8_t* hb, size_t hlen,
-                           uint32_t np, const uint8_t id[32], const uint8_t hsig[64],
-                           const uint8_t* vote_pks, const uint8_t* vote_sigs, size_t nvotes,
-                           const uint8_t* z16, uint64_t* index) {
+static int certificate_verify(const sig_engine* E, const nwo_committee* c, const uint8_t* hb,
+                              size_t hlen, uint32_t np, const uint8_t id[32],
+                              const uint8_t hsig[64], const uint8_t* vote_pks,
+                              const uint8_t* vote_sigs, size_t nvotes, const uint8_t* z16,
+                              uint64_t* index) {
   uint64_t ix = 0;
   int st = 0;
   ensure_init();
@@ -993,7 +1005,7 @@ int nwo_certificate_verify(const nwo_committee* c, const uint8_t* hb, size_t hle
   int idzero = 1;
   for (int i = 0; i < 32; ++i) idzero &= id[i] == 0;
   if (idzero && round == 0 && committee_find(c, hb) >= 0) goto done;
-  st = header_verify(c, hb, hlen, np, id, hsig, &ix);
+  st = header_verify(E, c, hb, hlen, np, id, hsig, &ix);
   if (st) goto done;
   {
     uint32_t weight = 0;
@@ -1010,7 +1022,7 @@ int nwo_certificate_verify(const nwo_committee* c, const uint8_t* hb, size_t hle
     uint8_t cd[32];
     nwo_digest_72(id, round, hb, cd);
     size_t fi = 0;
-    int b = nwo_verify_batch(cd, vote_pks, vote_sigs, nvotes, z16, &fi);
+    int b = E->batch(cd, vote_pks, vote_sigs, nvotes, z16, &fi);
     if (b) { st = NWO_DAG_INVALID_VOTES + b; ix = fi; }
   }
 done:
@@ -1018,13 +1030,21 @@ done:
   return st;
 }
 
-void nwo_certificates_verify_many(const nwo_committee* c, const uint8_t* header_bytes,
-                                  const uint64_t* header_offsets, const uint32_t* payload_counts,
-                                  const uint8_t* ids, const uint8_t* header_sigs,
-                                  const uint64_t* vote_offsets, const uint8_t* vote_pks,
-                                  const uint8_t* vote_sigs, size_t n, const uint8_t* z16,
-                                  int headers_only, int32_t* status, uint64_t* index,
-                                  int nthreads) {
+int nwo_certificate_verify(const nwo_committee* c, const uint8_t* hb, size_t hlen,
+                           uint32_t np, const uint8_t id[32], const uint8_t hsig[64],
+                           const uint8_t* vote_pks, const uint8_t* vote_sigs, size_t nvotes,
+                           const uint8_t* z16, uint64_t* index) {
+  return certificate_verify(&ENGINE_CHECK, c, hb, hlen, np, id, hsig, vote_pks, vote_sigs,
+                            nvotes, z16, index);
+}
+
+static void certificates_verify_many(const sig_engine* E, const nwo_committee* c,
+                                     const uint8_t* header_bytes, const uint64_t* header_offsets,
+                                     const uint32_t* payload_counts, const uint8_t* ids,
+                                     const uint8_t* header_sigs, const uint64_t* vote_offsets,
+                                     const uint8_t* vote_pks, const uint8_t* vote_sigs, size_t n,
+                                     const uint8_t* z16, int headers_only, int32_t* status,
+                                     uint64_t* index, int nthreads) {
   ensure_init();
 #ifdef _OPENMP
   if (nthreads <= 0) nthreads = omp_get_max_threads();
@@ -1035,18 +1055,41 @@ void nwo_certificates_verify_many(const nwo_committee* c, const uint8_t* header_
     const size_t hl = header_offsets[i + 1] - header_offsets[i];
     uint64_t ix = 0;
     if (headers_only) {
-      status[i] = header_verify(c, hb, hl, payload_counts[i], ids + 32 * i, header_sigs + 64 * i,
-                                &ix);
+      status[i] = header_verify(E, c, hb, hl, payload_counts[i], ids + 32 * i,
+                                header_sigs + 64 * i, &ix);
     } else {
       const uint64_t vb = vote_offsets[i], nv = vote_offsets[i + 1] - vb;
-      status[i] = nwo_certificate_verify(c, hb, hl, payload_counts[i], ids + 32 * i,
-                                         header_sigs + 64 * i, vote_pks + 32 * vb,
-                                         vote_sigs + 64 * vb, nv, z16 ? z16 + 16 * vb : NULL,
-                                         &ix);
+      status[i] = certificate_verify(E, c, hb, hl, payload_counts[i], ids + 32 * i,
+                                     header_sigs + 64 * i, vote_pks + 32 * vb,
+                                     vote_sigs + 64 * vb, nv, z16 ? z16 + 16 * vb : NULL, &ix);
     }
     if (index) index[i] = ix;
   }
   (void)nthreads;
+}
+
+void nwo_certificates_verify_many(const nwo_committee* c, const uint8_t* header_bytes,
+                                  const uint64_t* header_offsets, const uint32_t* payload_counts,
+                                  const uint8_t* ids, const uint8_t* header_sigs,
+                                  const uint64_t* vote_offsets, const uint8_t* vote_pks,
+                                  const uint8_t* vote_sigs, size_t n, const uint8_t* z16,
+                                  int headers_only, int32_t* status, uint64_t* index,
+                                  int nthreads) {
+  certificates_verify_many(&ENGINE_CHECK, c, header_bytes, header_offsets, payload_counts, ids,
+                           header_sigs, vote_offsets, vote_pks, vote_sigs, n, z16, headers_only,
+                           status, index, nthreads);
+}
+
+void nwd_certificates_verify_many(const nwo_committee* c, const uint8_t* header_bytes,
+                                  const uint64_t* header_offsets, const uint32_t* payload_counts,
+                                  const uint8_t* ids, const uint8_t* header_sigs,
+                                  const uint64_t* vote_offsets, const uint8_t* vote_pks,
+                                  const uint8_t* vote_sigs, size_t n, const uint8_t* z16,
+                                  int headers_only, int32_t* status, uint64_t* index,
+                                  int nthreads) {
+  certificates_verify_many(&ENGINE_DALEK, c, header_bytes, header_offsets, payload_counts, ids,
+                           header_sigs, vote_offsets, vote_pks, vote_sigs, n, z16, headers_only,
+                           status, index, nthreads);
 }
 
 /* Vote::verify (messages.rs:131-142). */

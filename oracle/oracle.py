@@ -73,8 +73,33 @@ def lib() -> ctypes.CDLL:
         L.nwo_digest_72.argtypes = [P, ctypes.c_uint64, P, P]
         L.nwo_certificates_verify_many.argtypes = [P, P, P, P, P, P, P, P, P, S, P, I, P, P, I]
         L.nwo_votes_verify_many.argtypes = [P, P, P, P, P, P, S, P]
+        # the timed dalek-equivalent restatement (nw_dalek.c), same signatures
+        L.nwd_verify_strict.argtypes = [P, S, P, P]
+        L.nwd_verify_strict.restype = I
+        L.nwd_verify_strict_many.argtypes = [P, S, P, P, S, P, I]
+        L.nwd_verify_batch.argtypes = [P, P, P, S, P, ctypes.POINTER(S)]
+        L.nwd_verify_batch.restype = I
+        L.nwd_verify_batch_many.argtypes = [P, P, P, P, S, P, P, I]
+        L.nwd_double_base.argtypes = [P, P, P, P]
+        L.nwd_double_base.restype = I
+        L.nwd_certificates_verify_many.argtypes = [P, P, P, P, P, P, P, P, P, S, P, I, P, P, I]
         _lib = L
     return _lib
+
+
+# engine="check": the parity checker (nw_oracle.c); engine="dalek": the dalek-equivalent
+# restatement (nw_dalek.c: NAF-5 / affine NAF-8 double-base, Straus / Pippenger MSM), which
+# bench.py times as cpu_baseline. Same verdicts; tests/test_dalek_restatement.py checks it.
+DALEK_ALGORITHM = ("dalek-equivalent restatement (ed25519-dalek 1.0.1 / curve25519-dalek 3 u64 "
+                   "backend): radix-2^51 field, width-5 NAF of k over 8 cached odd multiples of "
+                   "-A, width-8 NAF of s over 64 affine odd multiples of B; verify_batch: "
+                   "vartime Straus (NAF-5) below 190 points, Pippenger w=6/7/8 (<500/<800/>=800)")
+
+
+def _fn(name: str, engine: str):
+    if engine not in ("check", "dalek"):
+        raise ValueError(f"unknown oracle engine {engine!r}")
+    return getattr(lib(), ("nwd_" if engine == "dalek" else "nwo_") + name)
 
 
 def _buf(b: bytes):
@@ -144,24 +169,25 @@ def sign_raw(a: bytes, prefix: bytes, A: bytes, msg: bytes) -> bytes:
     return out.raw
 
 
-def verify_strict(msg: bytes, pk: bytes, sig: bytes) -> int:
-    return lib().nwo_verify_strict(_buf(msg), len(msg), _buf(pk), _buf(sig))
+def verify_strict(msg: bytes, pk: bytes, sig: bytes, engine: str = "check") -> int:
+    return _fn("verify_strict", engine)(_buf(msg), len(msg), _buf(pk), _buf(sig))
 
 
 def verify_strict_many(msgs: np.ndarray, pks: np.ndarray, sigs: np.ndarray,
-                       shared_msg: bool = False, nthreads: int = 0) -> np.ndarray:
+                       shared_msg: bool = False, nthreads: int = 0,
+                       engine: str = "check") -> np.ndarray:
     msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
     pks = np.ascontiguousarray(pks, dtype=np.uint8)
     sigs = np.ascontiguousarray(sigs, dtype=np.uint8)
     n = pks.shape[0]
     st = np.zeros(n, dtype=np.int32)
-    lib().nwo_verify_strict_many(_np_ptr(msgs), 0 if shared_msg else 32, _np_ptr(pks),
-                                 _np_ptr(sigs), n, _np_ptr(st), nthreads)
+    _fn("verify_strict_many", engine)(_np_ptr(msgs), 0 if shared_msg else 32, _np_ptr(pks),
+                                      _np_ptr(sigs), n, _np_ptr(st), nthreads)
     return st
 
 
 def verify_batch(digest: bytes, pks: np.ndarray, sigs: np.ndarray,
-                 z16: np.ndarray | None = None) -> tuple[int, int]:
+                 z16: np.ndarray | None = None, engine: str = "check") -> tuple[int, int]:
     pks = np.ascontiguousarray(pks, dtype=np.uint8).reshape(-1, 32)
     sigs = np.ascontiguousarray(sigs, dtype=np.uint8).reshape(-1, 64)
     n = pks.shape[0]
@@ -170,14 +196,14 @@ def verify_batch(digest: bytes, pks: np.ndarray, sigs: np.ndarray,
     if z16 is not None:
         z16 = np.ascontiguousarray(z16, dtype=np.uint8).reshape(-1, 16)
         zp = _np_ptr(z16)
-    st = lib().nwo_verify_batch(_buf(digest), _np_ptr(pks), _np_ptr(sigs), n, zp,
-                                ctypes.byref(idx))
+    st = _fn("verify_batch", engine)(_buf(digest), _np_ptr(pks), _np_ptr(sigs), n, zp,
+                                     ctypes.byref(idx))
     return st, idx.value
 
 
 def verify_batch_many(digests: np.ndarray, pks: np.ndarray, sigs: np.ndarray,
                       offsets: np.ndarray, z16: np.ndarray | None = None,
-                      nthreads: int = 0) -> np.ndarray:
+                      nthreads: int = 0, engine: str = "check") -> np.ndarray:
     digests = np.ascontiguousarray(digests, dtype=np.uint8)
     pks = np.ascontiguousarray(pks, dtype=np.uint8)
     sigs = np.ascontiguousarray(sigs, dtype=np.uint8)
@@ -188,8 +214,8 @@ def verify_batch_many(digests: np.ndarray, pks: np.ndarray, sigs: np.ndarray,
     if z16 is not None:
         z16 = np.ascontiguousarray(z16, dtype=np.uint8)
         zp = _np_ptr(z16)
-    lib().nwo_verify_batch_many(_np_ptr(digests), _np_ptr(pks), _np_ptr(sigs),
-                                _np_ptr(offsets), nb, zp, _np_ptr(st), nthreads)
+    _fn("verify_batch_many", engine)(_np_ptr(digests), _np_ptr(pks), _np_ptr(sigs),
+                                     _np_ptr(offsets), nb, zp, _np_ptr(st), nthreads)
     return st
 
 
@@ -264,6 +290,12 @@ def _committee(c: dict) -> _Committee:
                       _np_ptr(c["worker_offsets"]), _np_ptr(c["worker_ids"]))
 
 
+def double_base(a: bytes, A: bytes, b: bytes) -> bytes | None:
+    """encode([a]A + [b]B) by the dalek-equivalent vartime_double_scalar_mul_basepoint."""
+    out = ctypes.create_string_buffer(32)
+    return out.raw if lib().nwd_double_base(_buf(a), _buf(A), _buf(b), out) else None
+
+
 def digest_72(x: bytes, round_: int, y: bytes) -> bytes:
     out = ctypes.create_string_buffer(32)
     lib().nwo_digest_72(_buf(x), round_, _buf(y), out)
@@ -271,8 +303,8 @@ def digest_72(x: bytes, round_: int, y: bytes) -> bytes:
 
 
 def certificates_verify_many(committee: dict, p: dict, z16: np.ndarray | None = None,
-                             headers_only: bool = False, nthreads: int = 0
-                             ) -> tuple[np.ndarray, np.ndarray]:
+                             headers_only: bool = False, nthreads: int = 0,
+                             engine: str = "check") -> tuple[np.ndarray, np.ndarray]:
     """Certificate::verify (or Header::verify) over a packed stream (same SoA layout as
     narwhal_amd.messages.pack_certificates / pack_committee)."""
     n = len(p["header_offsets"]) - 1
@@ -283,7 +315,7 @@ def certificates_verify_many(committee: dict, p: dict, z16: np.ndarray | None = 
     if z16 is not None:
         z16 = np.ascontiguousarray(z16, np.uint8)
         zp = _np_ptr(z16)
-    lib().nwo_certificates_verify_many(
+    _fn("certificates_verify_many", engine)(
         ctypes.byref(cc), _np_ptr(p["header_bytes"]), _np_ptr(p["header_offsets"]),
         _np_ptr(p["payload_counts"]), _np_ptr(p["ids"]), _np_ptr(p["header_sigs"]),
         _np_ptr(p["vote_offsets"]), _np_ptr(p["vote_pks"]), _np_ptr(p["vote_sigs"]), n, zp,

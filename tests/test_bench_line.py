@@ -97,3 +97,33 @@ def test_bench_gpus2_spawns_ranks():
     s = r["summary"]
     assert s["sha512"]["GB_s"] > 0 and s["cert_stream_Mcerts_s"]["N4"] > 0
     assert s["batch10k"]["resident_M_s"] > 0 and s["wire_Mcerts_s"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_gpus8_gloo_rehearsal():
+    """The driver's 8-GPU run rehearsed by process on the one-GPU box: `bench.py --gpus 8`
+    starts 8 ranks (all on device 0 over gloo), each verifies its shard of every timed leg
+    (strict, SHA-512, certificates, verify_batch, wire ingest) at toy sizes, and rank 0 checks
+    the gathered 8-shard verdict bitmap bit for bit."""
+    env = dict(os.environ, NW_BENCH_BACKEND="gloo",
+               NW_BENCH_DETAIL=os.path.join(ROOT, "gpurun_out", "bench_n8_detail.json"))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    # one 8 x 4096-item corpus, 8 shards; ragged / empty shards: tests/test_distributed.py
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8",
+                        "--steps", "2", "--warmup", "1", "--items-per-gpu", "4096",
+                        "--unique", "2048", "--sha-batches", "64", "--sha-unique", "8",
+                        "--certs", "512", "--cert-unique", "256", "--committees", "4",
+                        "--cert-invalid", "0", "--cert-payload-committees", "",
+                        "--batch-many", "1", "--wire-frames", "256", "--wire-steps", "1",
+                        "--no-worker", "--no-service", "--no-cpu-baseline"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 8 and r["parity"] == "ok", r
+    assert r["config"]["items_total"] == 8 * 4096 and r["config"]["parallelism"] == "shard8"
+    s = r["summary"]
+    assert s["sha512"]["GB_s"] > 0 and s["cert_stream_Mcerts_s"]["N4"] > 0
+    assert s["batch10k"]["resident_M_s"] > 0 and s["wire_Mcerts_s"] > 0

@@ -192,7 +192,9 @@ def test_wide_btab_entries(hc):
 
 @pytest.fixture(params=[16, 20])
 def keyw(request, hc):
-    """The key-comb widths the device builds (nw_api.cpp key_width: 20 bits up to 16 keys)."""
+    """The key-comb widths the device builds (nw_api.cpp key_width: 20 bits up to 64 keys,
+    otherwise 16; ntab = ceil(253 / W) tables plus a 2^128 A table when W does not divide
+    128, nw_kernels.h keyspec_for)."""
     hc.hc_set_key_width.restype = ctypes.c_int
     assert hc.hc_set_key_width(request.param) == 0
     yield request.param

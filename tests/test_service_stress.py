@@ -4,8 +4,10 @@ choices and the completer, driven by tools/service_stress.cpp with test doubles 
 the device entry points (each answers a request with a fingerprint of exactly the bytes
 that request supplied, and checks every batch's offsets). Several producer threads submit
 random certificates (0 .. 3,000 votes), headers, votes, Signature::verify and verify_batch
-requests; every request must get exactly one verdict and it must be its own. Also under
-ThreadSanitizer. No GPU."""
+requests; every request must get exactly one verdict and it must be its own. One job in 16
+is 3 ms late, so the hedge (nw_service_set_hedge: host doubles answering with the same
+fingerprints) delivers part of the verdicts, racing the completer for each request. Also
+under ThreadSanitizer. No GPU."""
 import json
 import os
 import shutil
@@ -35,6 +37,7 @@ def test_service_stress(producers, requests, max_items):
     assert r.returncode == 0, out
     assert out["accepted"] == producers * requests
     assert out["missing"] == out["duplicate"] == out["wrong"] == out["bad_shape"] == 0
+    assert out["hedged"] > 0 and 0 < out["host_first"] <= out["host_calls"]
 
 
 def test_service_stress_tsan():

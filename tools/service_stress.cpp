@@ -10,6 +10,9 @@
 //   service_stress PRODUCERS REQUESTS_PER_PRODUCER [MAX_ITEMS] [BENCH]
 // BENCH=1: certificates of 34 votes only, 100 us jobs, no hashing; prints the mean cost of one
 // nw_service_certificate call (the ingest path) instead of stressing shapes.
+// The hedge (nw_service_set_hedge) runs too: one job in 16 is 3 ms late, past the 1 ms
+// deadline, and nw::host::* are doubles that answer with the same fingerprints, so a verdict
+// is right whichever side delivers it; exactly one callback per request is still required.
 // Built with g++ (-fsanitize=thread in `make service_stress_tsan`); test/bench tooling.
 #include <stdio.h>
 #include <stdlib.h>
@@ -23,6 +26,7 @@
 #include <vector>
 
 #include "narwhal_amd.h"
+#include "nw_host.h"
 #include "nw_runtime.h"
 
 namespace {
@@ -46,7 +50,9 @@ nw_job* make_job() {
   thread_local std::mt19937_64 rng(std::hash<std::thread::id>()(std::this_thread::get_id()));
   Job* j = new Job;
   // bench: a fixed 100 us per job (a small-job launch), so batches accumulate as on a device
-  j->due = Clock::now() + std::chrono::microseconds(g_no_delay ? 100 : rng() % 200);
+  // one job in 16 is late (3 ms) so that the hedge answers part of the run
+  j->due = Clock::now() + std::chrono::microseconds(g_no_delay ? 100 : rng() % 16 == 0 ? 3000
+                                                                                       : rng() % 200);
   g_jobs.fetch_add(1);
   return reinterpret_cast<nw_job*>(j);
 }
@@ -158,6 +164,70 @@ int nw_submit_verify_batch_many(const uint8_t* digests, const uint8_t* pks, cons
   *job = make_job();
   return 0;
 }
+}  // extern "C"
+
+// ---- the host path (nw_host.cpp) as doubles: the same fingerprints as the device doubles ----
+namespace nw {
+namespace host {
+struct Committee {
+  int unused;
+};
+Committee* committee_new(const nw_committee*) { return new Committee{0}; }
+void committee_free(Committee* c) { delete c; }
+std::atomic<uint64_t> g_host_calls{0};
+int verify_strict(const uint8_t msg32[32], const uint8_t pk[32], const uint8_t sig[64]) {
+  g_host_calls.fetch_add(1);
+  uint64_t h = fnv(kFnv0, msg32, 32);
+  h = fnv(h, pk, 32);
+  h = fnv(h, sig, 64);
+  return (int32_t)(h & 0x7fffffff);
+}
+int verify_batch(const uint8_t digest[32], const uint8_t* pks, const uint8_t* sigs, size_t n,
+                 const uint8_t*, const Committee*, uint64_t* fail_index) {
+  g_host_calls.fetch_add(1);
+  uint64_t h = fnv(kFnv0, digest, 32);
+  h = fnv(h, pks, 32 * n);
+  h = fnv(h, sigs, 64 * n);
+  if (fail_index) *fail_index = h >> 31;
+  return (int32_t)(h & 0x7fffffff);
+}
+int header_verify(const Committee&, const uint8_t* hb, size_t hlen, uint32_t np,
+                  const uint8_t id[32], const uint8_t sig[64], uint64_t* index) {
+  g_host_calls.fetch_add(1);
+  uint64_t h = fnv(kFnv0, hb, hlen);
+  h = fnv(h, &np, 4);
+  h = fnv(h, id, 32);
+  h = fnv(h, sig, 64);
+  *index = h >> 31;
+  return (int32_t)(h & 0x7fffffff);
+}
+int vote_verify(const Committee&, const uint8_t id[32], uint64_t round, const uint8_t origin[32],
+                const uint8_t author[32], const uint8_t sig[64]) {
+  g_host_calls.fetch_add(1);
+  uint64_t h = fnv(kFnv0, id, 32);
+  h = fnv(h, &round, 8);
+  h = fnv(h, origin, 32);
+  h = fnv(h, author, 32);
+  h = fnv(h, sig, 64);
+  return (int32_t)(h & 0x7fffffff);
+}
+int certificate_verify(const Committee&, const uint8_t* hb, size_t hlen, uint32_t np,
+                       const uint8_t id[32], const uint8_t hsig[64], const uint8_t* vote_pks,
+                       const uint8_t* vote_sigs, size_t nvotes, const uint8_t*, uint64_t* index) {
+  g_host_calls.fetch_add(1);
+  uint64_t h = fnv(kFnv0, hb, hlen);
+  h = fnv(h, &np, 4);
+  h = fnv(h, id, 32);
+  h = fnv(h, hsig, 64);
+  h = fnv(h, vote_pks, 32 * nvotes);
+  h = fnv(h, vote_sigs, 64 * nvotes);
+  *index = h >> 31;
+  return (int32_t)(h & 0x7fffffff);
+}
+}  // namespace host
+}  // namespace nw
+
+extern "C" {
 int nw_job_poll(nw_job* job) {
   return Clock::now() >= reinterpret_cast<Job*>(job)->due ? 1 : 0;
 }
@@ -291,8 +361,9 @@ int main(int argc, char** argv) {
     });
   for (auto& t : th) t.join();
   nw_service_drain(s);
-  uint64_t reqs = 0, jobs = 0;
+  uint64_t reqs = 0, jobs = 0, hedged = 0, host_first = 0, host_only = 0;
   nw_service_stats(s, &reqs, &jobs);
+  nw_service_hedge_stats(s, &hedged, &host_first, &host_only);
   nw_service_destroy(s);
   size_t missing = 0, dup = 0, bad = 0;
   for (auto& e : ex) {
@@ -305,9 +376,12 @@ int main(int argc, char** argv) {
   for (double x : call_s) cs += x;
   printf("{\"producers\": %d, \"requests\": %zu, \"accepted\": %llu, \"jobs\": %llu, "
          "\"submit_errors\": %d, \"missing\": %zu, \"duplicate\": %zu, \"wrong\": %zu, "
-         "\"bad_shape\": %llu, \"cert_call_mean_us\": %.3f}\n",
+         "\"bad_shape\": %llu, \"cert_call_mean_us\": %.3f, \"hedged\": %llu, "
+         "\"host_first\": %llu, \"host_only_batches\": %llu, \"host_calls\": %llu}\n",
          P, ex.size(), (unsigned long long)reqs, (unsigned long long)jobs, submit_err.load(),
          missing, dup, bad, (unsigned long long)g_bad_shape.load(),
-         bench ? cs / ((double)P * R) * 1e6 : -1.0);
+         bench ? cs / ((double)P * R) * 1e6 : -1.0, (unsigned long long)hedged,
+         (unsigned long long)host_first, (unsigned long long)host_only,
+         (unsigned long long)nw::host::g_host_calls.load());
   return (missing || dup || bad || g_bad_shape.load() || submit_err.load()) ? 1 : 0;
 }
