@@ -278,9 +278,10 @@ int nw_service_stats(nw_service* s, uint64_t* requests, uint64_t* jobs);
 int nw_service_set_hedge(nw_service* s, uint32_t deadline_us, uint32_t threads,
                          uint64_t max_queued);
 /* Requests queued for the hedge, requests the host answered first, batches the host took
- * whole before submission (any pointer may be NULL). */
+ * whole before submission, and whether the committee's host tables are built (1) — until
+ * then only verify / verify_batch requests are hedged (any pointer may be NULL). */
 int nw_service_hedge_stats(nw_service* s, uint64_t* hedged, uint64_t* host_first,
-                           uint64_t* host_only_batches);
+                           uint64_t* host_only_batches, int* host_ready);
 /* Drain, stop the service threads and free the service. */
 void nw_service_destroy(nw_service* s);
 

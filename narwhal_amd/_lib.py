@@ -95,7 +95,7 @@ def lib() -> ctypes.CDLL:
         "nw_service_flush": ([P], I), "nw_service_drain": ([P], I),
         "nw_service_stats": ([P, P, P], I), "nw_service_destroy": ([P], None),
         "nw_service_set_hedge": ([P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64], I),
-        "nw_service_hedge_stats": ([P, P, P, P], I),
+        "nw_service_hedge_stats": ([P, P, P, P, P], I),
         "nw_host_verify_strict_many": ([P, S, P, P, S, P], I),
         "nw_host_verify_batch_many": ([P, P, P, P, S, P, P, P], I),
         "nw_host_certificates_verify_many": ([P, P, P, I, P, P], I),

@@ -12,8 +12,9 @@
 //
 // Work per signature on one core: a committee key's signature is a keyed comb check,
 // [s]B - [k]A from 8-bit comb tables (32 + 32 mixed additions, no doublings), then one
-// decompression of R (headers, votes) or one inversion (certificate votes, compressed-R
-// compare: nw_strict.hpp keyed_vote_check's argument); any other key takes the kernels'
+// decompression of R (headers, votes) or, for certificate votes, the compressed-R compare
+// of nw_strict.hpp keyed_vote_check with one inversion per certificate (Montgomery's trick);
+// any other key takes the kernels'
 // half-size strict ladder (nw_strict.hpp strict_verify_core<8>). A certificate whose votes
 // do not all pass exactly is re-verified as dalek's verify_batch with fresh CSPRNG z (Straus).
 #include <string.h>
@@ -387,34 +388,68 @@ int verify_strict_keyed(const KeyInfo& key, const uint8_t msg32[32], const uint8
 
 // A vote whose R == [s]B - [k]A exactly (and which dalek's verify_strict accepts) adds
 // nothing to ANY random linear combination: the compressed-R check of nw_strict.hpp
-// keyed_vote_check, finished with one inversion. false = decide by the full verify_batch.
-bool vote_passes(const KeyInfo& key, const uint8_t digest[32], const uint8_t pk[32],
-                 const uint8_t sig[64]) {
+// keyed_vote_check. Returns 0 = fails (decide by the full verify_batch), 1 = passes, or
+// 2 | sign = passes iff the parity of X'/Z' equals sign: the caller batches those
+// inversions (Montgomery's trick, as k_votes_keyed_inv does on the device).
+uint32_t vote_check(const KeyInfo& key, const uint8_t digest[32], const uint8_t pk[32],
+                    const uint8_t sig[64], fe& X, fe& Z) {
   const Consts& C = consts();
   if ((sig[63] & 0xE0) || !(key.flags & kKeyDecoded) || (key.flags & kKeySmall) ||
       (key.flags & kKeyLambdaMask))
-    return false;
+    return 0;
   sc s;
   load_sc(s, sig + 32);
-  if (!sc_is_canonical(s)) return false;
+  if (!sc_is_canonical(s)) return 0;
   uint32_t Rw[8];
   load8(Rw, sig);
   const uint32_t sign = Rw[7] >> 31;
   fe yR;
   fe_frombytes(yR, Rw);
-  if (small_order_by_y(yR, C.SK.small_y)) return false;
+  if (small_order_by_y(yR, C.SK.small_y)) return 0;
   sc k;
   hram(k, sig, pk, digest, 32);
   ge acc;
   comb_sum(acc, k, s, key.comb.data(), C.BC.data());
   fe t;
   fe_mul(t, yR, acc.Z);
-  if (!fe_eq(t, acc.Y)) return false;
-  if (fe_iszero(acc.X)) return true;
-  fe zi, x;
-  fe_invert(zi, acc.Z);
-  fe_mul(x, acc.X, zi);
-  return fe_isnegative(x) == sign;
+  if (!fe_eq(t, acc.Y)) return 0;
+  if (fe_iszero(acc.X)) return 1;
+  fe_copy(X, acc.X);
+  fe_copy(Z, acc.Z);
+  return 2 | sign;
+}
+
+// Every vote passes (each R == [s]B - [k]A with dalek's strict checks), the parities with
+// one inversion for all of them.
+bool votes_pass(const Committee& com, const uint8_t digest[32], const uint8_t* pks,
+                const uint8_t* sigs, size_t n) {
+  std::vector<fe> X(n), Z(n), pre(n);
+  std::vector<uint32_t> sign(n);
+  size_t m = 0;   // pending parities
+  for (size_t i = 0; i < n; ++i) {
+    const long a = com.find(pks + 32 * i);
+    if (a < 0) return false;
+    const uint32_t r = vote_check(com.keys[a], digest, pks + 32 * i, sigs + 64 * i, X[m], Z[m]);
+    if (r == 0) return false;
+    if (r & 2) sign[m++] = r & 1;
+  }
+  if (m == 0) return true;
+  fe_copy(pre[0], Z[0]);
+  for (size_t i = 1; i < m; ++i) fe_mul(pre[i], pre[i - 1], Z[i]);
+  fe inv;
+  fe_invert(inv, pre[m - 1]);
+  for (size_t i = m; i-- > 0;) {
+    fe zi, x;
+    if (i) {
+      fe_mul(zi, inv, pre[i - 1]);
+      fe_mul(inv, inv, Z[i]);
+    } else {
+      fe_copy(zi, inv);
+    }
+    fe_mul(x, X[i], zi);
+    if (fe_isnegative(x) != sign[i]) return false;
+  }
+  return true;
 }
 
 // dalek verify_batch, every step: per vote s high bits / A decode (first failure), s < l over
@@ -493,11 +528,7 @@ int verify_batch(const uint8_t digest[32], const uint8_t* pks, const uint8_t* si
                  const uint8_t* z16, const Committee* com, uint64_t* fail_index) {
   uint64_t fi = n;
   int st = NW_OK;
-  bool all = n > 0 && com != nullptr;
-  for (size_t i = 0; all && i < n; ++i) {
-    const long a = com->find(pks + 32 * i);
-    all = a >= 0 && vote_passes(com->keys[a], digest, pks + 32 * i, sigs + 64 * i);
-  }
+  const bool all = n > 0 && com != nullptr && votes_pass(*com, digest, pks, sigs, n);
   if (!all) st = verify_batch_full(digest, pks, sigs, n, z16, &fi);
   else fi = n;
   if (fail_index) *fail_index = fi;

@@ -1177,11 +1177,12 @@ int nw_service_set_hedge(nw_service* s, uint32_t deadline_us, uint32_t threads,
 }
 
 int nw_service_hedge_stats(nw_service* s, uint64_t* hedged, uint64_t* host_first,
-                           uint64_t* host_only_batches) {
+                           uint64_t* host_only_batches, int* host_ready) {
   if (!s) return set_err(NW_E_INVALID_ARG, "null service");
   if (hedged) *hedged = s->n_hedged.load();
   if (host_first) *host_first = s->n_host_first.load();
   if (host_only_batches) *host_only_batches = s->n_host_only.load();
+  if (host_ready) *host_ready = s->hc_ready.load(std::memory_order_acquire) ? 1 : 0;
   return 0;
 }
 

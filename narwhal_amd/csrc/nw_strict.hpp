@@ -620,6 +620,15 @@ NW_HD int strict_keyed_comb(const Src& src, const strict_consts& K, const BComb&
 // Status of one strict verification. wave_max maps this lane's ladder length (in 4-bit
 // windows) to the wave's maximum (identity on the host). tabA/tabR: 8 entries each of
 // per-lane scratch. bt: j*B and j*2^128 B, j = 0..2^(BW-1) (btab_pair / btab_wide).
+// NW_STRICT_STOP (instrumentation builds only, tools/strict_phases.sh; 0 = the kernel): cut
+// the verification after a phase so that PMC instruction counts of the cut builds split the
+// kernel's work by phase: 1 the two decompressions, 2 + the per-lane tables, 3 + SHA-512 and
+// Barrett (k), 4 + the scalar split and recodings, 5 + the ladder's doublings only (no
+// additions), 6 + the A and R additions (no B additions). The status is then a digest of the
+// state, not a verdict.
+#ifndef NW_STRICT_STOP
+#define NW_STRICT_STOP 0
+#endif
 template <int BW, class BTab, class Src, class WaveMax, class PF = pf_none, class Tab = ge_cached>
 NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab& bt,
                              Tab* tabA, Tab* tabR,
@@ -637,8 +646,11 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
     const bool ok = ge_frombytes(P, x, K.k);
     const bool small = small_order_by_y(P.Y, K.small_y);
     if (pt == 0) { okA = ok; smallA = small; } else { okR = ok; smallR = small; }
+    if (NW_STRICT_STOP == 1) continue;
     build_table8(pt ? tabR : tabA, P, K.k.d2);
   }
+  if (NW_STRICT_STOP == 1 || NW_STRICT_STOP == 2)
+    return (okA ? 1 : 0) + (okR ? 2 : 0) + (smallA ? 4 : 0) + (smallR ? 8 : 0);
 
   uint32_t Sw[8], kw[8];
   src.S(Sw);
@@ -647,6 +659,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
   sc s, k;
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s.w[j] = Sw[j]; k.w[j] = kw[j]; }
+  if (NW_STRICT_STOP == 3) return (int)((kw[0] ^ kw[7] ^ Sw[0]) & 15u) + (okA ? 16 : 0);
   const bool s_canon = sc_is_canonical(s);
   // v < 0: [v]R = [|v|](-R), taken as negated R digits (the table holds j * R)
   sc_half h;
@@ -683,6 +696,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
   int W = ((bu > bv ? bu : bv) + 3) / 4;
   if (W < 32) W = 32;
   W = wave_max(W);
+  if (NW_STRICT_STOP == 4) return W + (int)((ud[0] ^ vd[0] ^ wd[0] ^ wd[7]) & 15u) + (okR ? 64 : 0);
 
   // One rolled doubling and one addition routine serve every term (code size: the ladder
   // body stays inside the instruction cache). Per 4-bit window j: 4 doublings, then the
@@ -739,7 +753,7 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
       int d0;
       bool nl0;
       const void* s0 = slot_src(W - 1, 0, d0, nl0);
-      if (s0) pf.issue(s0, nl0 ? 8 : int(sizeof(Tab) / 16));
+      if (s0 && NW_STRICT_STOP != 5) pf.issue(s0, nl0 ? 8 : int(sizeof(Tab) / 16));
     }
 #pragma unroll 1
     for (int j = W - 1; j >= 0; --j) {
@@ -747,7 +761,8 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
 #pragma unroll 1
         for (int t = 0; t < 4; ++t) ge_dbl(acc, acc, t == 3);
       }
-      const int nslots = nslots_of(j);
+      if (NW_STRICT_STOP == 5) continue;
+      const int nslots = NW_STRICT_STOP == 6 ? 2 : nslots_of(j);
 #pragma unroll 1
       for (int slot = 0; slot < nslots; ++slot) {
         int d;

@@ -616,6 +616,18 @@ class NativeService:
               "nw_service_stats")
         return req.value, jobs.value
 
+    def set_hedge(self, deadline: float, threads: int = 4, max_queued: int = 512) -> None:
+        """Host hedge of late requests (nw_service_set_hedge): deadline in seconds (0 = off)."""
+        check(_lib.lib().nw_service_set_hedge(self._h, int(deadline * 1e6), threads, max_queued),
+              "nw_service_set_hedge")
+
+    def hedge_stats(self) -> tuple[int, int, int]:
+        """(requests hedged, requests the host answered first, batches the host took whole)."""
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        check(_lib.lib().nw_service_hedge_stats(self._h, ctypes.byref(a), ctypes.byref(b),
+                                                ctypes.byref(c), None), "nw_service_hedge_stats")
+        return a.value, b.value, c.value
+
     def close(self) -> None:
         if self._h.value is not None:
             _lib.lib().nw_service_destroy(self._h)   # drains: every callback has run

@@ -48,8 +48,10 @@ def test_compact_line_from_round4_record():
     s = back["summary"]
     assert s["batch10k"]["latency_ms"] == round(full["verify_batch_10k"]["latency_ms"], 3)
     assert set(s["cert_stream_Mcerts_s"]) == {"N4", "N10", "N50", "N100"}
-    # the service tail is reported with p90 and max, not only the good percentiles
-    assert len(s["service"]["N50"]["offered_achieved_p50_p90_p99_max_ms"][0]) == 6
+    # the service tail is reported with p90 and max, not only the good percentiles, and with
+    # the load generator's own lateness and the hedge's host answers beside them
+    row = s["service"]["N50"]["offered_achieved_p50_p90_p99_max_lagmax_ms_hostfirst"][0]
+    assert len(row) == 8 and row[6] is not None
 
 
 def test_compact_line_bounded_when_legs_grow():

@@ -65,6 +65,8 @@ extern "C" {
 // (a producer that cannot keep its schedule shows here before it shows as latency), then
 // the producers' CPU / wall time and their voluntary / involuntary context switches, and
 // the nw_service_certificate calls' mean and longest duration and the count above 20 us;
+// out[13..15]: the service's hedge during the timed run: requests hedged, requests the host
+// answered first, batches the host took whole (nw_service_hedge_stats);
 // out[11..12]: jobs that took the small-job launch and
 // the bulk pipeline during the timed run (nw_path_stats).
 int nw_loadgen_certificates(const nw_committee* com, const nw_certificates* corpus,
@@ -103,6 +105,13 @@ int nw_loadgen_certificates(const nw_committee* com, const nw_certificates* corp
     if (rc) {
       nw_service_destroy(s);
       return rc;
+    }
+    // the hedge's host tables of the committee (built in the background at create)
+    for (int t = 0; t < 4000; ++t) {
+      int ready = 0;
+      nw_service_hedge_stats(s, nullptr, nullptr, nullptr, &ready);
+      if (ready) break;
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
     }
   }
   rc = timed_run(s, corpus, exp_status, exp_index, rate, total, producers, lat_out, out);
@@ -152,6 +161,8 @@ int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_s
   uint64_t jobs0 = 0, sm0 = 0, pp0 = 0;
   nw_service_stats(s, nullptr, &jobs0);
   nw_path_stats(&sm0, &pp0);
+  uint64_t hq0 = 0, hf0 = 0, ho0 = 0;
+  nw_service_hedge_stats(s, &hq0, &hf0, &ho0, nullptr);
   run.t0 = Clock::now() + std::chrono::milliseconds(2);
   const double period = 1.0 / rate;
   for (uint64_t i = 0; i < total; ++i)
@@ -255,6 +266,11 @@ int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_s
   out[10] = sl;                                 // calls longer than 20 us
   out[11] = (double)(sm1 - sm0);                // small-job launches
   out[12] = (double)(pp1 - pp0);                // bulk-pipeline jobs
+  uint64_t hq1 = 0, hf1 = 0, ho1 = 0;
+  nw_service_hedge_stats(s, &hq1, &hf1, &ho1, nullptr);
+  out[13] = (double)(hq1 - hq0);                // requests hedged
+  out[14] = (double)(hf1 - hf0);                // answered by the host first
+  out[15] = (double)(ho1 - ho0);                // batches the host took whole
   return first_err.load();
 }
 }  // namespace

@@ -363,7 +363,7 @@ int main(int argc, char** argv) {
   nw_service_drain(s);
   uint64_t reqs = 0, jobs = 0, hedged = 0, host_first = 0, host_only = 0;
   nw_service_stats(s, &reqs, &jobs);
-  nw_service_hedge_stats(s, &hedged, &host_first, &host_only);
+  nw_service_hedge_stats(s, &hedged, &host_first, &host_only, nullptr);
   nw_service_destroy(s);
   size_t missing = 0, dup = 0, bad = 0;
   for (auto& e : ex) {
