@@ -1311,9 +1311,10 @@ def main():
     ap.add_argument("--service-hedge-us", type=int, default=1000,
                     help="service hedge deadline (us; 0 = off): late requests are also "
                          "verified on host threads, first verdict wins")
-    ap.add_argument("--service-hedge-threads", type=int, default=4)
+    ap.add_argument("--service-hedge-threads", type=int, default=6)
     ap.add_argument("--service-hedge-queued", type=int, default=512,
-                    help="units waiting for the hedge threads at most")
+                    help="units a batch still waiting for a job slot may join the host "
+                         "queue with (taken for the host alone)")
     ap.add_argument("--no-worker", action="store_true",
                     help="skip the worker Processor latency leg")
     ap.add_argument("--worker-rates", default="50,500,5000")

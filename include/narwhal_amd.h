@@ -262,16 +262,18 @@ int nw_service_flush(nw_service* s);
 int nw_service_drain(nw_service* s);
 /* Requests accepted and jobs submitted so far (either pointer may be NULL). */
 int nw_service_stats(nw_service* s, uint64_t* requests, uint64_t* jobs);
-/* Hedge (on by default: 1000 us, 4 threads, 512 units; NW_SERVICE_HEDGE_US / _THREADS /
+/* Hedge (on by default: 1000 us, 6 threads, 512 units; NW_SERVICE_HEDGE_US / _THREADS /
  * _QUEUED change the defaults). A request whose verdict has not arrived deadline_us after
  * its batch's first request (its device job is late, or its batch still waits for a job
  * slot) is verified on the host as well (the nw_host_* path below: the kernels' arithmetic
  * compiled for the CPU, same statuses and indices, fresh CSPRNG coefficients), and the
  * first verdict is delivered: fn is still called exactly once per request, but then from
- * one of the `threads` hedge threads, possibly before requests accepted earlier. At most
- * max_queued units (certificate = 1 + votes, batch = its votes, else 1) wait for the hedge
- * threads; later late requests wait for the device, so a stall under load costs at most
- * `threads` cores. deadline_us = 0 or threads = 0 turns hedging off. Why: the primary's Core
+ * one of the `threads` hedge threads, possibly before requests accepted earlier. The hedge
+ * threads take late requests oldest first while the device races them; a batch still
+ * waiting for a job slot is taken for the host alone (never submitted) only while fewer than
+ * max_queued units (certificate = 1 + votes, batch = its votes, else 1) wait for the host,
+ * so a stall under load costs at most `threads` cores and the host never owes more than it
+ * finishes quickly. deadline_us = 0 or threads = 0 turns hedging off. Why: the primary's Core
  * verifies inline on one task (primary/src/core.rs:338-346), so a late device job would
  * stall the primary. Header / vote / certificate requests are hedged once the committee's
  * host tables exist (built in the background at create, ~2-5 ms of a core per key). */

@@ -41,11 +41,12 @@
 //            (nw_host.cpp: the kernels' own arithmetic compiled for the CPU, same statuses
 //            and indices), and whichever verdict comes first is delivered, exactly once (one
 //            atomic flag per request). A hedger thread looks every deadline / 4 at the batches
-//            on the device or being submitted, and at batches still waiting for a job slot
-//            (those are then taken for the host alone and never submitted); `threads` host
-//            threads answer them, oldest first. At most `max_queued` units wait for those
-//            threads, so a device stall under heavy load costs at most `threads` cores and
-//            the rest waits for the device as before. Why: the primary verifies on its one
+//            on the device or being submitted, and at batches still waiting for a job slot;
+//            `threads` host threads answer them, oldest first, racing the device. A batch
+//            still waiting is taken for the host alone (never submitted) only while the host
+//            queue holds fewer than `max_queued` units, so the host never owes more than it
+//            finishes quickly; a device stall under heavy load costs at most `threads` cores
+//            and the rest waits for the device as before. Why: the primary verifies on its one
 //            Core task (primary/src/core.rs:338-346), so a device job that stalls for 10-40 ms
 //            (the box's host-memory access episodes) stalls the primary, while
 //            one certificate costs a host core well under a millisecond.
@@ -322,8 +323,8 @@ struct nw_service {
 
   // ---- hedge (nw_service_set_hedge) ----
   int64_t hedge_ns = 1000000;          // deadline after a batch's first request; 0 = off
-  uint32_t hedge_threads = 4;
-  uint64_t hedge_max_queued = 512;     // units (certificate = 1 + votes) waiting at most
+  uint32_t hedge_threads = 6;
+  uint64_t hedge_max_queued = 512;     // units a batch taken for the host alone may join
   // NW_SERVICE_TEST_DELAY_US (test hook): the completer holds every device verdict until this
   // long after its batch's first request, so the hedge answers first
   int64_t test_delay_ns = 0;
@@ -334,7 +335,6 @@ struct nw_service {
   std::condition_variable cv_hw;       // hedge threads: work queued / stop
   std::condition_variable cv_hedger;   // hedger: stop
   std::deque<Batch*> hq;               // batches the hedge threads answer, oldest first
-  uint64_t hq_units = 0;
   std::vector<std::unique_ptr<Batch>> hostonly;   // taken for the host alone (owned here)
   std::vector<std::unique_ptr<Batch>> retired;    // device-done hedged batches still entered
   std::vector<Batch*> submitting_b;    // batches inside launch() (under m)
@@ -726,7 +726,6 @@ struct nw_service {
       std::lock_guard<std::mutex> g(hm);
       auto it = std::find(hq.begin(), hq.end(), b.get());
       if (it != hq.end()) {
-        hq_units -= b->units();
         hq.erase(it);
       }
       if (b->hrefs.load(std::memory_order_acquire) > 0) {
@@ -737,14 +736,15 @@ struct nw_service {
     spare[b->kind].push_back(std::move(b));
   }
 
-  // Queue b for the hedge threads (under m); host_only: b was taken before submission and is
-  // owned by the hedge from now on. False when the budget has no room for it.
+  // Queue b for the hedge threads (under m); own != nullptr: b was taken before submission
+  // and is owned by the hedge from now on, and must fit the budget (the host answers it
+  // alone, so it must not queue more than the hedge threads finish quickly). A late batch on
+  // the device is always queued: the threads work oldest first and the device races them.
   bool queue_hedge(std::unique_ptr<Batch>* own, Batch* b) {
     std::lock_guard<std::mutex> g(hm);
-    if (hq_units + b->units() > hedge_max_queued || hworkers.empty()) return false;
+    if (hworkers.empty() || (own && host_queued() + b->units() > hedge_max_queued)) return false;
     b->hedged = true;
     hq.push_back(b);
-    hq_units += b->units();
     if (own) {
       b->host_only = true;
       hostonly.push_back(std::move(*own));
@@ -753,6 +753,16 @@ struct nw_service {
     n_hedged.fetch_add(b->n, std::memory_order_relaxed);
     cv_hw.notify_all();
     return true;
+  }
+
+  // units of the hedge queue not yet taken by a hedge thread (under hm)
+  uint64_t host_queued() const {
+    uint64_t u = 0;
+    for (const Batch* b : hq) {
+      const size_t next = std::min(b->hnext.load(std::memory_order_relaxed), b->n);
+      u += Batch::units_of(b->kind, b->n - next, b->n ? b->nv2 * (b->n - next) / b->n : 0);
+    }
+    return u;
   }
 
   bool hedgeable(const Batch& b, int64_t now) const {
@@ -821,7 +831,8 @@ struct nw_service {
         {
           std::lock_guard<std::mutex> g(hm);
           if (f == 0 || now - f < hedge_ns || hworkers.empty() ||
-              hq_units + Batch::units_of(static_cast<Kind>(k), c_req(c), c_v2(c)) > hedge_max_queued)
+              host_queued() + Batch::units_of(static_cast<Kind>(k), c_req(c), c_v2(c)) >
+                  hedge_max_queued)
             continue;
         }
         if (k != K_STRICT && k != K_BATCH && !hc_ready.load(std::memory_order_acquire)) continue;
@@ -888,8 +899,7 @@ struct nw_service {
               break;
             }
             hq.pop_front();   // every request claimed: the batch leaves the queue
-            hq_units -= b->units();
-            continue;
+                continue;
           }
           if (hworkers_stop) return;
           cv_hw.wait(g);

@@ -616,7 +616,7 @@ class NativeService:
               "nw_service_stats")
         return req.value, jobs.value
 
-    def set_hedge(self, deadline: float, threads: int = 4, max_queued: int = 512) -> None:
+    def set_hedge(self, deadline: float, threads: int = 6, max_queued: int = 512) -> None:
         """Host hedge of late requests (nw_service_set_hedge): deadline in seconds (0 = off)."""
         check(_lib.lib().nw_service_set_hedge(self._h, int(deadline * 1e6), threads, max_queued),
               "nw_service_set_hedge")

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Per-phase split of k_verify_strict, step 2 (GPU box): SQ_INSTS_VALU (+ its INT64 / INT32
 # parts) of one bench-size launch of the full kernel and of each phase-cut build
-# (exp/stop<k>, tools/strict_phases.sh), one rocprofv3 --pmc pass each. The cut builds'
+# (tools/r06/phases/stop<k>, tools/strict_phases.sh), one rocprofv3 --pmc pass each. The cut builds'
 # statuses are digests, not verdicts, so their bench parity fails by design (rc 1 is
 # expected; anything else stops the script). Summary: tools/strict_phases_summary.py.
 set -o pipefail
@@ -12,7 +12,7 @@ ARGS="--items-per-gpu 1048576 --steps 1 --warmup 0 --no-cpu-baseline --no-sha --
 mkdir -p $OUT
 for v in full stop1 stop2 stop3 stop4 stop5 stop6; do
   lib=narwhal_amd/libnarwhal_amd.so
-  [ $v != full ] && lib=exp/$v/libnarwhal_amd.so
+  [ $v != full ] && lib=tools/r06/phases/$v/libnarwhal_amd.so
   NW_LIB=$lib timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 SQ_WAVES \
     --output-format csv -d $OUT/$v -o p -- python bench.py $ARGS > $OUT/$v.log 2>&1
   rc=$?
