@@ -4,7 +4,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r06a; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_memory.py tests/test_bench_line.py -m gpu -v --timeout 280 --timeout-method thread > $O/newtests.log 2>&1 || { tail -60 $O/newtests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_hedge.py tests/test_gpu_memory.py tests/test_bench_line.py -m gpu -v --timeout 280 --timeout-method thread > $O/newtests.log 2>&1 || { tail -60 $O/newtests.log; exit 1; }
 tail -6 $O/newtests.log
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > $O/gputests.log 2>&1 || { tail -40 $O/gputests.log; exit 1; }
 tail -2 $O/gputests.log
