@@ -11,7 +11,8 @@
 // verdict wins; verdicts are the device's (same checks, same order, same status / index).
 //
 // Work per signature on one core: a committee key's signature is a keyed comb check,
-// [s]B - [k]A from 8-bit comb tables (32 + 32 mixed additions, no doublings), then one
+// [s]B - [k]A from 8-bit comb tables (32 + 32 mixed additions, no doublings; in five 51-bit
+// limbs, nw_host_f51.hpp, since a 64x64-bit product is the CPU's native one), then one
 // decompression of R (headers, votes) or, for certificate votes, the compressed-R compare
 // of nw_strict.hpp keyed_vote_check with one inversion per certificate (Montgomery's trick);
 // any other key takes the kernels'
@@ -27,6 +28,7 @@
 #include <vector>
 
 #include "nw_host.h"
+#include "nw_host_f51.hpp"
 #include "nw_consts.hpp"
 #include "nw_sha512.hpp"
 
@@ -191,8 +193,27 @@ struct Consts {
   strict_consts SK;
   ge_niels BT[129], B128[129];
   torsion_consts tc;
-  std::vector<ge_niels> BC;   // j * 2^(8 t) B
+  std::vector<f51::niels> BC;   // j * 2^(8 t) B
 };
+
+// the same field element in five 51-bit limbs (through its canonical bytes)
+void to51(f51::fe& h, const fe& f) {
+  uint32_t w[8];
+  fe_tobytes(w, f);
+  f51::frombytes(h, reinterpret_cast<const uint8_t*>(w));
+}
+void to51(f51::niels& h, const ge_niels& n) {
+  to51(h.ypx, n.ypx);
+  to51(h.ymx, n.ymx);
+  to51(h.xy2d, n.xy2d);
+}
+// comb8 into 51-bit limbs
+void comb8_51(std::vector<f51::niels>& out, const ge& P, const fe& d2) {
+  std::vector<ge_niels> t((size_t)kComb * kCombN);
+  comb8(t.data(), P, d2);
+  out.resize(t.size());
+  for (size_t i = 0; i < t.size(); ++i) to51(out[i], t[i]);
+}
 const Consts& consts() {
   static const Consts* c = [] {
     Consts* k = new Consts;
@@ -209,8 +230,7 @@ const Consts& consts() {
     fe_tobytes(yw, a);
     ge B;
     ge_frombytes(B, yw, k->SK.k);
-    k->BC.resize((size_t)kComb * kCombN);
-    comb8(k->BC.data(), B, k->SK.k.d2);
+    comb8_51(k->BC, B, k->SK.k.d2);
     return k;
   }();
   return *c;
@@ -234,22 +254,23 @@ inline int digit8(const uint32_t d[8], int m) {
 }
 
 // acc = [s]B - [k]A from the 8-bit combs of A (ka) and B: 64 mixed additions, no doublings
-void comb_sum(ge& acc, const sc& k, const sc& s, const ge_niels* ka, const ge_niels* bc) {
+void comb_sum(f51::pt& acc, const sc& k, const sc& s, const f51::niels* ka,
+              const f51::niels* bc) {
   uint32_t kd[8], sd[8];
   sc_recode(kd, k, 0x80808080u);
   sc_recode(sd, s, 0x80808080u);
-  ge_identity(acc);
+  f51::pt_identity(acc);
   for (int m = 0; m < kComb; ++m) {
     const int dk = digit8(kd, m), ds = digit8(sd, m);
     if (dk) {
-      ge_niels n = ka[kCombN * m + (dk < 0 ? -dk : dk)];
-      ge_niels_cneg(n, dk > 0);
-      ge_add_niels(acc, acc, n, true);
+      f51::niels n = ka[kCombN * m + (dk < 0 ? -dk : dk)];
+      f51::niels_cneg(n, dk > 0);
+      f51::add_niels(acc, acc, n);
     }
     if (ds) {
-      ge_niels n = bc[kCombN * m + (ds < 0 ? -ds : ds)];
-      ge_niels_cneg(n, ds < 0);
-      ge_add_niels(acc, acc, n, true);
+      f51::niels n = bc[kCombN * m + (ds < 0 ? -ds : ds)];
+      f51::niels_cneg(n, ds < 0);
+      f51::add_niels(acc, acc, n);
     }
   }
 }
@@ -261,7 +282,7 @@ void comb_sum(ge& acc, const sc& k, const sc& s, const ge_niels* ka, const ge_ni
 // ---------------------------------------------------------------------------------------
 struct KeyInfo {
   uint32_t flags = 0;          // kKeyDecoded | kKeySmall | lambda << kKeyLambdaShift
-  std::vector<ge_niels> comb;  // 32 x 129 when decoded
+  std::vector<f51::niels> comb;  // 32 x 129 when decoded
 };
 
 struct Committee {
@@ -310,8 +331,7 @@ void key_info(KeyInfo& ki, const uint8_t pk[32]) {
   const int j = torsion_index(acc, C.tc);
   const uint32_t lam = j > 0 ? (uint32_t)j : 0u;
   ki.flags = kKeyDecoded | (ge_is_small_order(A) ? kKeySmall : 0u) | (lam << kKeyLambdaShift);
-  ki.comb.resize((size_t)kComb * kCombN);
-  comb8(ki.comb.data(), A, C.SK.k.d2);
+  comb8_51(ki.comb, A, C.SK.k.d2);
 }
 }  // namespace
 
@@ -381,9 +401,16 @@ int verify_strict_keyed(const KeyInfo& key, const uint8_t msg32[32], const uint8
   if (key.flags & kKeySmall) return NW_ERR_A_SMALL_ORDER;
   sc k;
   hram(k, sig, pk, msg32, 32);
-  ge acc;
+  f51::pt acc;
   comb_sum(acc, k, s, key.comb.data(), C.BC.data());
-  return ge_eq_affine(acc, R) ? NW_OK : NW_ERR_EQUATION;
+  // projective equality against the affine R: X == x_R Z, Y == y_R Z
+  f51::fe xr, yr, t;
+  to51(xr, R.X);
+  to51(yr, R.Y);
+  f51::mul(t, xr, acc.Z);
+  if (!f51::eq(t, acc.X)) return NW_ERR_EQUATION;
+  f51::mul(t, yr, acc.Z);
+  return f51::eq(t, acc.Y) ? NW_OK : NW_ERR_EQUATION;
 }
 
 // A vote whose R == [s]B - [k]A exactly (and which dalek's verify_strict accepts) adds
@@ -392,7 +419,7 @@ int verify_strict_keyed(const KeyInfo& key, const uint8_t msg32[32], const uint8
 // 2 | sign = passes iff the parity of X'/Z' equals sign: the caller batches those
 // inversions (Montgomery's trick, as k_votes_keyed_inv does on the device).
 uint32_t vote_check(const KeyInfo& key, const uint8_t digest[32], const uint8_t pk[32],
-                    const uint8_t sig[64], fe& X, fe& Z) {
+                    const uint8_t sig[64], f51::fe& X, f51::fe& Z) {
   const Consts& C = consts();
   if ((sig[63] & 0xE0) || !(key.flags & kKeyDecoded) || (key.flags & kKeySmall) ||
       (key.flags & kKeyLambdaMask))
@@ -408,14 +435,17 @@ uint32_t vote_check(const KeyInfo& key, const uint8_t digest[32], const uint8_t 
   if (small_order_by_y(yR, C.SK.small_y)) return 0;
   sc k;
   hram(k, sig, pk, digest, 32);
-  ge acc;
+  f51::pt acc;
   comb_sum(acc, k, s, key.comb.data(), C.BC.data());
-  fe t;
-  fe_mul(t, yR, acc.Z);
-  if (!fe_eq(t, acc.Y)) return 0;
-  if (fe_iszero(acc.X)) return 1;
-  fe_copy(X, acc.X);
-  fe_copy(Z, acc.Z);
+  // y' == y_R: the encoding's y as given (bit 255 cleared, reduced mod p as dalek's
+  // decompression reads it)
+  f51::fe y51, t;
+  to51(y51, yR);
+  f51::mul(t, y51, acc.Z);
+  if (!f51::eq(t, acc.Y)) return 0;
+  if (f51::iszero(acc.X)) return 1;
+  X = acc.X;
+  Z = acc.Z;
   return 2 | sign;
 }
 
@@ -423,7 +453,7 @@ uint32_t vote_check(const KeyInfo& key, const uint8_t digest[32], const uint8_t 
 // one inversion for all of them.
 bool votes_pass(const Committee& com, const uint8_t digest[32], const uint8_t* pks,
                 const uint8_t* sigs, size_t n) {
-  std::vector<fe> X(n), Z(n), pre(n);
+  std::vector<f51::fe> X(n), Z(n), pre(n);
   std::vector<uint32_t> sign(n);
   size_t m = 0;   // pending parities
   for (size_t i = 0; i < n; ++i) {
@@ -434,20 +464,20 @@ bool votes_pass(const Committee& com, const uint8_t digest[32], const uint8_t* p
     if (r & 2) sign[m++] = r & 1;
   }
   if (m == 0) return true;
-  fe_copy(pre[0], Z[0]);
-  for (size_t i = 1; i < m; ++i) fe_mul(pre[i], pre[i - 1], Z[i]);
-  fe inv;
-  fe_invert(inv, pre[m - 1]);
+  pre[0] = Z[0];
+  for (size_t i = 1; i < m; ++i) f51::mul(pre[i], pre[i - 1], Z[i]);
+  f51::fe inv;
+  f51::invert(inv, pre[m - 1]);
   for (size_t i = m; i-- > 0;) {
-    fe zi, x;
+    f51::fe zi, x;
     if (i) {
-      fe_mul(zi, inv, pre[i - 1]);
-      fe_mul(inv, inv, Z[i]);
+      f51::mul(zi, inv, pre[i - 1]);
+      f51::mul(inv, inv, Z[i]);
     } else {
-      fe_copy(zi, inv);
+      zi = inv;
     }
-    fe_mul(x, X[i], zi);
-    if (fe_isnegative(x) != sign[i]) return false;
+    f51::mul(x, X[i], zi);
+    if (f51::isnegative(x) != sign[i]) return false;
   }
   return true;
 }

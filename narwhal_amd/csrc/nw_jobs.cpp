@@ -48,6 +48,9 @@ struct nw_job {
   char* dbuf = nullptr;   // device: same layout (+ workspace)
   size_t dcap = 0;
   char* hdev = nullptr;   // the device's address of hbuf (small jobs read it directly)
+  char* vbuf = nullptr;   // NW_SMALL_VRAM: fine-grained device memory for small jobs' inputs
+  char* vhost = nullptr;  // ... and the host's mapping of it (the CPU writes the inputs there)
+  size_t vcap = 0;
   uint32_t* dcnt = nullptr;   // small jobs' per-message arrival counters (kept zero)
   size_t ccap = 0;
   uint32_t* dfz = nullptr;    // config-1 fused launches' counters (the tail leaves them zero)
@@ -190,6 +193,45 @@ int job_reserve(nw_job* j, size_t hbytes, size_t dbytes) {
   return 0;
 }
 
+// NW_SMALL_VRAM=1 (A/B hook, read once): a small job's inputs travel as the CPU's writes into
+// fine-grained device memory mapped through the BAR, so its kernel reads device memory only
+// (the episodes in which the device's reads of pinned host memory stall).
+// Outputs stay in the pinned buffer. Falls back to the pinned inputs when the device memory
+// has no host mapping.
+bool small_vram() {
+  static const bool on = [] {
+    const char* e = getenv("NW_SMALL_VRAM");
+    return e && *e == '1';
+  }();
+  return on;
+}
+int job_reserve_vram(nw_job* j, size_t bytes) {
+  if (bytes <= j->vcap) return 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  if (j->vbuf) (void)hipFree(j->vbuf);
+  j->vbuf = j->vhost = nullptr;
+  j->vcap = 0;
+  const size_t cap = bytes < (1u << 20) ? (1u << 20) : bytes + bytes / 4;
+  void* p = nullptr;
+  hipError_t e = hipExtMallocWithFlags(&p, cap, hipDeviceMallocFinegrained);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return 1;
+  }
+  hipPointerAttribute_t at{};
+  e = hipPointerGetAttributes(&at, p);
+  if (e != hipSuccess || !at.hostPointer) {
+    (void)hipGetLastError();
+    (void)hipFree(p);
+    return 1;
+  }
+  j->vbuf = static_cast<char*>(p);
+  j->vhost = static_cast<char*>(at.hostPointer);
+  j->vcap = cap;
+  log_growth(3, cap, t0);
+  return 0;
+}
+
 void job_out(nw_job* j, void* dst, size_t off, size_t bytes) {
   if (dst && bytes) j->outs[j->nouts++] = {dst, off, bytes};
 }
@@ -261,6 +303,7 @@ int nw::rt::jobs_prewarm(int dev, int count, size_t hbytes, size_t dbytes) {
     // small jobs' arrival counters too: a first small job on a job without them would
     // allocate (hipMalloc + hipMemsetAsync) on the submitting thread in the middle of a burst
     if (!rc) rc = job_counters(j, 4096);
+    if (!rc && small_vram()) (void)job_reserve_vram(j, hbytes);
     if (!rc) ensure_fork(j);
   }
   for (nw_job* j : got) job_recycle(j);
@@ -622,6 +665,11 @@ int submit_small(int dev, uint32_t kind, const nw_committee* com, const nw_certi
     }
   }
   char* X = j->hdev;   // the device's view of the staging buffer
+  if (small_vram() && job_reserve_vram(j, o_st) == 0) {
+    memcpy(j->vhost, H, o_st);   // the inputs (everything before the outputs)
+    std::atomic_thread_fence(std::memory_order_seq_cst);   // drain the write-combining buffers
+    X = j->vbuf;
+  }
   nw::small_job_t J{};
   J.kind = kind;
   J.slots_per_wg = small_slots_per_wg(nslots);
@@ -658,8 +706,8 @@ int submit_small(int dev, uint32_t kind, const nw_committee* com, const nw_certi
   J.minfo = reinterpret_cast<nw::small_msg_info_t*>(j->dbuf + d_mi);
   J.srec = reinterpret_cast<uint32_t*>(j->dbuf + d_sr);
   J.mcount = j->dcnt;
-  J.status = reinterpret_cast<int32_t*>(X + o_st);
-  J.index = kind == nw::kSmallVotes ? nullptr : reinterpret_cast<uint64_t*>(X + o_ix);
+  J.status = reinterpret_cast<int32_t*>(j->hdev + o_st);
+  J.index = kind == nw::kSmallVotes ? nullptr : reinterpret_cast<uint64_t*>(j->hdev + o_ix);
   nw::rt::ReadLease rl;
   const void* tabs = nullptr;
   const uint32_t* ok = nullptr;

@@ -35,7 +35,7 @@ int os_random(void* buf, size_t n);
 // (nw_jobs.cpp; the aggregation service's start-up).
 int jobs_prewarm(int dev, int count, size_t hbytes, size_t dbytes);
 // Diagnostics (NW_SERVICE_DEBUG): job staging growths so far — pinned (kind 0), device
-// (kind 1), small-job counters (kind 2) — with their time (steady-clock ns), new capacity and
+// (kind 1), small-job counters (kind 2), NW_SMALL_VRAM input buffers (kind 3) — with their time (steady-clock ns), new capacity and
 // duration in us. Copies up to `max` of them into `out` (4 words each) and returns the count.
 size_t job_growth_log(uint64_t* out, size_t max);
 

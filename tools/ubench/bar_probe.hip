@@ -14,6 +14,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <setjmp.h>
+#include <signal.h>
+
 #include <algorithm>
 #include <chrono>
 #include <vector>
@@ -38,6 +41,43 @@ __global__ void k_sum(const uint4* __restrict__ in, uint32_t* __restrict__ out) 
 
 using Clock = std::chrono::steady_clock;
 
+// Is a device pointer mapped into the CPU's address space? The /proc/self/maps line that
+// holds it, then one guarded read and write through it (SIGSEGV / SIGBUS caught).
+static sigjmp_buf g_jb;
+static void on_fault(int) { siglongjmp(g_jb, 1); }
+static bool cpu_touch(volatile uint8_t* p) {
+  struct sigaction sa{}, o1{}, o2{};
+  sa.sa_handler = on_fault;
+  sigaction(SIGSEGV, &sa, &o1);
+  sigaction(SIGBUS, &sa, &o2);
+  bool ok = false;
+  if (sigsetjmp(g_jb, 1) == 0) {
+    const uint8_t v = p[0];
+    p[0] = (uint8_t)(v ^ 0x5a);
+    ok = p[0] == (uint8_t)(v ^ 0x5a);
+  }
+  sigaction(SIGSEGV, &o1, nullptr);
+  sigaction(SIGBUS, &o2, nullptr);
+  return ok;
+}
+static void maps_line(const void* p) {
+  FILE* f = fopen("/proc/self/maps", "r");
+  char line[512];
+  const uintptr_t a = (uintptr_t)p;
+  bool found = false;
+  while (f && fgets(line, sizeof line, f)) {
+    unsigned long lo = 0, hi = 0;
+    if (sscanf(line, "%lx-%lx", &lo, &hi) == 2 && a >= lo && a < hi) {
+      line[strcspn(line, "\n")] = 0;
+      printf("{\"maps\": \"%s\"}\n", line);
+      found = true;
+    }
+  }
+  if (f) fclose(f);
+  if (!found) printf("{\"maps\": null}\n");
+  fflush(stdout);
+}
+
 int main(int argc, char** argv) {
   const double secs = argc > 1 ? atof(argv[1]) : 20.0;
   void* bar = nullptr;
@@ -48,6 +88,13 @@ int main(int argc, char** argv) {
          at.devicePointer, at.hostPointer);
   fflush(stdout);
   uint8_t* bar_host = static_cast<uint8_t*>(at.hostPointer);
+  maps_line(bar);
+  if (!bar_host) {   // no host mapping reported: is the device address itself CPU-mapped?
+    const bool ok = cpu_touch(static_cast<volatile uint8_t*>(bar));
+    printf("{\"cpu_access_via_device_pointer\": %s}\n", ok ? "true" : "false");
+    fflush(stdout);
+    if (ok) bar_host = static_cast<uint8_t*>(bar);
+  }
   uint8_t* pinned = nullptr;
   CK(hipHostMalloc(reinterpret_cast<void**>(&pinned), kBytes, hipHostMallocMapped | hipHostMallocCoherent));
   void* pinned_dev = nullptr;
