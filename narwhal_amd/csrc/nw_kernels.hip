@@ -219,6 +219,24 @@ struct pf_lds {
     fe_unpack(e.Z2, p + 16);
     fe_unpack(e.T2d, p + 24);
   }
+  // A packed per-lane entry read as -entry when neg (NW_PF_SWAP): Y+X and Y-X trade places
+  // through the LDS address (chunks 0-1 <-> 2-3), so the caller negates only 2dT.
+  __device__ void get_signed(ge_cached& e, bool neg) const {
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    asm volatile("" ::: "memory");
+    const uint32_t l = threadIdx.x;
+    const uint32_t a = neg ? 2u : 0u;
+    uint32_t p[32];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint4 v = s_pf[k < 4 ? (k ^ a) : k][l];
+      p[4 * k] = v.x; p[4 * k + 1] = v.y; p[4 * k + 2] = v.z; p[4 * k + 3] = v.w;
+    }
+    fe_unpack(e.YpX, p);
+    fe_unpack(e.YmX, p + 8);
+    fe_unpack(e.Z2, p + 16);
+    fe_unpack(e.T2d, p + 24);
+  }
 };
 #endif
 

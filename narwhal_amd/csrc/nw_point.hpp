@@ -121,6 +121,31 @@ NW_HD void ge_add_any(ge& r, const ge& p, const ge_cached& q, bool affine, bool 
   if (want_t) fe_mul(r.T, e, h);
 }
 
+// ge_add_any with q's 2dT NEGATED by the caller (q = (Y+X, Y-X, 2Z, -2dT)): c' = -2dT T1,
+// so f = d + c' and g = d - c' need no carry pass (f <= L / P15 is the second operand of its
+// products, g = S(d) the first; every pair is one tests/test_field_bounds.py checks). The
+// ladder's sign selection already negates 2dT conditionally, so flipping its condition makes
+// this free (NW_ADD_NEGC).
+NW_HD void ge_add_any_negc(ge& r, const ge& p, const ge_cached& q, bool affine,
+                           bool want_t = true) {
+  fe a, b, c, d, e, f, g, h;
+  fe_sub_nc(a, p.Y, p.X);
+  fe_mul(a, a, q.YmX);
+  fe_add(b, p.Y, p.X);
+  fe_mul(b, b, q.YpX);
+  fe_mul(c, q.T2d, p.T);
+  if (affine) fe_add(d, p.Z, p.Z);
+  else fe_mul(d, p.Z, q.Z2);
+  fe_sub_nc(e, b, a);
+  fe_add(f, d, c);
+  fe_sub_nc(g, d, c);
+  fe_add(h, b, a);
+  fe_mul(r.X, e, f);
+  fe_mul(r.Z, g, f);
+  fe_mul(r.Y, g, h);
+  if (want_t) fe_mul(r.T, e, h);
+}
+
 // Conditionally negate a niels point: -(x, y) = (-x, y) -> swap y+x / y-x, negate 2dxy.
 NW_HD void ge_niels_cneg(ge_niels& n, bool neg) {
   fe t;
@@ -143,6 +168,19 @@ NW_HD void ge_cached_cneg(ge_cached& c, bool neg) {
   }
   fe_neg_nc(t, c.T2d);
   fe_cmov(c.T2d, t, neg);
+}
+// ge_cached_cneg for ge_add_any_negc: +-q with its 2dT negated (Y+X / Y-X swapped when neg,
+// 2dT negated when NOT neg)
+NW_HD void ge_cached_cneg_negc(ge_cached& c, bool neg) {
+  fe t;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    uint32_t a = c.YpX.v[i], b = c.YmX.v[i];
+    c.YpX.v[i] = neg ? b : a;
+    c.YmX.v[i] = neg ? a : b;
+  }
+  fe_neg_nc(t, c.T2d);
+  fe_cmov(c.T2d, t, !neg);
 }
 
 // r = 2p (dbl-2008-hwcd, a = -1, with E, G, H negated so every operand stays non-negative:

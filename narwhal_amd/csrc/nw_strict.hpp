@@ -384,6 +384,7 @@ struct pf_none {
   static constexpr bool lds_digits = false;
   NW_HD void issue(const void*, int) const {}
   NW_HD void get(ge_cached&, bool) const {}
+  NW_HD void get_signed(ge_cached&, bool) const {}
   NW_HD void dput(int, uint32_t) const {}
   NW_HD uint32_t dget(int) const { return 0; }
 };
@@ -629,6 +630,15 @@ NW_HD int strict_keyed_comb(const Src& src, const strict_consts& K, const BComb&
 #ifndef NW_STRICT_STOP
 #define NW_STRICT_STOP 0
 #endif
+// NW_PF_SWAP (A/B): a per-lane entry's sign taken in the prefetcher's LDS read (pf_lds::
+// get_signed) instead of 20 selects after it.
+#ifndef NW_PF_SWAP
+#define NW_PF_SWAP 0
+#endif
+// NW_ADD_NEGC (A/B): the ladder's additions as ge_add_any_negc (no carry pass on f).
+#ifndef NW_ADD_NEGC
+#define NW_ADD_NEGC 0
+#endif
 template <int BW, class BTab, class Src, class WaveMax, class PF = pf_none, class Tab = ge_cached>
 NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab& bt,
                              Tab* tabA, Tab* tabR,
@@ -769,7 +779,14 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
         bool niels;
         const void* cur = slot_src(j, slot, d, niels);
         ge_cached e;
+#if NW_PF_SWAP
+        if (cur) {
+          if (niels) pf.get(e, true);
+          else pf.get_signed(e, d < 0);
+        }
+#else
         if (cur) pf.get(e, niels);
+#endif
         // request the next addition's entry before this one runs
         const int j2 = slot + 1 < nslots ? j : j - 1, s2 = slot + 1 < nslots ? slot + 1 : 0;
         if (j2 >= 0) {
@@ -779,8 +796,23 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
           if (nx) pf.issue(nx, n2 ? 8 : int(sizeof(Tab) / 16));
         }
         if (cur) {
-          ge_cached_cneg(e, d < 0);
-          ge_add_any(acc, acc, e, niels, slot != nslots - 1);
+          // NW_ADD_NEGC: 2dT negated when the digit is positive (ge_add_any_negc)
+          const bool tneg = NW_ADD_NEGC ? d > 0 : d < 0;
+#if NW_PF_SWAP
+          if (niels) {
+            if (NW_ADD_NEGC) ge_cached_cneg_negc(e, d < 0);
+            else ge_cached_cneg(e, d < 0);
+          } else {   // Y+X / Y-X already swapped by the read: -2dT only
+            fe t;
+            fe_neg_nc(t, e.T2d);
+            fe_cmov(e.T2d, t, tneg);
+          }
+#else
+          if (NW_ADD_NEGC) ge_cached_cneg_negc(e, d < 0);
+          else ge_cached_cneg(e, d < 0);
+#endif
+          if (NW_ADD_NEGC) ge_add_any_negc(acc, acc, e, niels, slot != nslots - 1);
+          else ge_add_any(acc, acc, e, niels, slot != nslots - 1);
         }
       }
     }
@@ -816,8 +848,13 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
         } else {
           bt((slot == 3 || !has0) ? 1 : 0, ad, e);
         }
-        ge_cached_cneg(e, d < 0);
-        ge_add_any(acc, acc, e, slot >= 2, slot != nslots - 1);
+        if (NW_ADD_NEGC) {
+          ge_cached_cneg_negc(e, d < 0);
+          ge_add_any_negc(acc, acc, e, slot >= 2, slot != nslots - 1);
+        } else {
+          ge_cached_cneg(e, d < 0);
+          ge_add_any(acc, acc, e, slot >= 2, slot != nslots - 1);
+        }
       }
     }
   }

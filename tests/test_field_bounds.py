@@ -53,6 +53,13 @@ MUL_PAIRS = {
     "dbl Z3 = G*F (shared second operand F)": (T, P15),
     "add Z3 = g*f (shared second operand f)": (L, T),
     "generic": (T, T),
+    # ge_add_any_negc (NW_ADD_NEGC): f = d + c' (L cached, P15 affine d = 2Z) second,
+    # g = d - c' uncarried (S_T cached, S_L affine) first
+    "negc X3 = e*f (cached)": (S_T, L),
+    "negc Z3 = g*f, Y3 = g*h (cached)": (S_T, L),
+    "negc X3 = e*f (affine)": (S_T, P15),
+    "negc Z3 = g*f (affine)": (S_L, P15),
+    "negc Y3 = g*h (affine)": (S_L, L),
 }
 SQ_INPUTS = {"X, Y, Z": T, "X+Y": L}
 

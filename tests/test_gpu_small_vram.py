@@ -1,0 +1,29 @@
+"""Job inputs in device memory written by the CPU (nw_jobs.cpp job_reserve_vram): with
+NW_SMALL_VRAM=1 the small-job kernel's inputs, with NW_BATCH_VRAM=1 a lone fused
+verify_batch's inputs travel as the CPU's writes into host-mapped fine-grained device memory
+instead of pinned host memory (read across the bus, or copied by an H2D). The small-job
+parity file (tests/test_gpu_small.py: headers, votes, certificates, irregular committees) and
+the batch parity file (tests/test_gpu_batch.py: lone batches on both sides of the fused
+limit, every failure class) run in child processes with the hook on, against the oracle, and
+the library must report that it took the device-memory staging."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NOTICE = "job inputs written into host-mapped fine-grained device memory"
+
+
+@pytest.mark.parametrize("env,test", [("NW_SMALL_VRAM", "test_gpu_small.py"),
+                                      ("NW_BATCH_VRAM", "test_gpu_batch.py")])
+def test_inputs_in_device_memory(env, test):
+    r = subprocess.run([sys.executable, "-u", "-m", "pytest", "-x", "-q", "-s", "-p",
+                        "no:cacheprovider", os.path.join(ROOT, "tests", test)],
+                       cwd=ROOT, env=dict(os.environ, **{env: "1"}), capture_output=True,
+                       text=True, timeout=280)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert NOTICE in r.stdout + r.stderr
