@@ -205,10 +205,10 @@ bool small_vram() {
   }();
   return on;
 }
-bool batch_vram() {
+bool batch_vram() {   // on unless NW_BATCH_VRAM=0 (profiles/r06d: config 1 0.303 vs 0.321 ms)
   static const bool on = [] {
     const char* e = getenv("NW_BATCH_VRAM");
-    return e && *e == '1';
+    return !(e && *e == '0');
   }();
   return on;
 }
@@ -419,8 +419,9 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
                end = o_ws + a256(nw::batch_workspace_bytes(nbatches, nitems));
   rc = job_reserve(j, o_ws, end);
   if (rc) return job_abort(j, rc);
-  // NW_BATCH_VRAM=1 (A/B hook): a lone fused batch's inputs go straight from the caller's
-  // buffers into host-mapped fine-grained device memory (no pinned staging copy, no H2D)
+  // A lone fused batch's inputs go straight from the caller's buffers into host-mapped
+  // fine-grained device memory: no pinned staging copy, no H2D (NW_BATCH_VRAM=0: the pinned
+  // buffer and one H2D copy, as before round 6)
   const bool vram = direct && batch_vram() && job_reserve_vram(j, o_st) == 0;
   char* const stage = vram ? j->vhost : j->hbuf;
   memcpy(stage + o_d, digests, 32 * nbatches);
