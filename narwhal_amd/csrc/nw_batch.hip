@@ -2220,7 +2220,8 @@ __global__ __launch_bounds__(256) void k_pip_points_sorted(
     uint64_t i0, uint64_t i1, const uint32_t* __restrict__ pks,
     const uint32_t* __restrict__ sigs, const uint32_t* __restrict__ z16, z_key_t zkey,
     bv_item* __restrict__ items, ge_cached* __restrict__ tabs, uint32_t npb, uint32_t wv,
-    uint32_t ksort, uint32_t* __restrict__ ctr, uint64_t* __restrict__ stamps) {
+    uint32_t ksort, uint32_t* __restrict__ ctr, uint64_t* __restrict__ stamps,
+    input_gate_t gate) {
   __shared__ uint32_t s_ticket, s_ok;
   __shared__ uint32_t s_h[kPipSortBins], s_c[kPipSortBins];
   const int tid = (int)threadIdx.x;
@@ -2239,6 +2240,23 @@ __global__ __launch_bounds__(256) void k_pip_points_sorted(
     const uint64_t wi = (uint64_t)(t < nb0 ? t : t - nb0) * 4 + (uint64_t)(tid >> 6);
     const int which = t < nb0 ? 0 : 1 + (int)(wi & 1);
     const uint64_t grp64 = t < nb0 ? wi : wi >> 1;   // 64-vote group of the wave
+    if (gate.flags && grp64 < wv) {
+      // the CPU may still be writing this wave's votes (input_gate_t): lane 0 waits for
+      // their chunk's flag, then the whole wave acquires at system scope
+      if ((tid & 63) == 0) {
+        const uint32_t* f = gate.flags + (grp64 * 64) / gate.chunk;
+        const uint64_t g0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != gate.seq) {
+          __builtin_amdgcn_s_sleep(1);
+          if (__builtin_amdgcn_s_memrealtime() - g0 > kFuseSpinTicks) {
+            __hip_atomic_store(ctr + kFzError, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    }
     if (grp64 < wv)
       pip_point_do(which, grp64 * 64 + (uint64_t)(tid & 63), digests, offsets, bidx, bidx + 1,
                    i0, i1, 0, pks, sigs, z16, zkey, items, tabs, nogrp);
@@ -2277,7 +2295,7 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
                 const uint32_t* pks, const uint32_t* sigs, const uint32_t* z16,
                 const z_key_t& zkey, const bv_ws& w, int32_t* status, uint64_t* fail_index,
                 const pip_group_t& grp, hipStream_t stream,
-                uint32_t* fctr) {
+                uint32_t* fctr, const input_gate_t* gate = nullptr) {
   const bool group = grp.cert_vote_offsets != nullptr;
   const uint32_t extra = group ? grp.nkeys : 0;   // key sums
   const uint32_t roles = group ? 2 : 3;
@@ -2295,7 +2313,8 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
         (uint32_t)std::min<uint64_t>(8, std::max<uint64_t>(1, env_u64("NW_PIP_SORT_SPLIT", 2)));
     hipLaunchKernelGGL(k_pip_points_sorted, dim3(npb + kPipWin * ks), dim3(256), lds, stream,
                        digests, offsets, b, i0, i1, pks, sigs, z16, zkey, w.items, w.tabs, npb,
-                       (uint32_t)wv, ks, fctr, head_stamps(npb + kPipWin * ks));
+                       (uint32_t)wv, ks, fctr, head_stamps(npb + kPipWin * ks),
+                       gate ? *gate : input_gate_t{nullptr, 0u, 64u});
   } else {
     hipLaunchKernelGGL(k_pip_points, dim3((unsigned)((wv * roles * 64 + 255) / 256)), dim3(256),
                        0, stream, digests, offsets, b, e, i0, i1, pmin, pks, sigs, z16, zkey,
@@ -2383,7 +2402,11 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                int32_t* status, uint64_t* fail_index, hipStream_t stream,
                                const key_tables_t* keys, const uint32_t* skip_group_ok,
                                uint64_t skip_per_group, double active_frac,
-                               uint32_t* fuse_ctr) {
+                               uint32_t* fuse_ctr, const input_gate_t* gate) {
+  // a gate is honoured by the fused head only: refuse it anywhere else (its waves would
+  // read bytes the CPU has not written yet)
+  if (gate && !verify_batch_gate_ok(nbatches, nitems)) return hipErrorInvalidValue;
+  if (gate && (gate->chunk == 0 || gate->chunk % 64 != 0)) return hipErrorInvalidValue;
   const key_tables_t kt = keys ? *keys : key_tables_t{nullptr, nullptr, nullptr, {}};
   const batch_skip_t sk{skip_group_ok, skip_per_group ? skip_per_group : 1};
   if (nbatches == 0) return hipSuccess;
@@ -2465,7 +2488,7 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
     if (npip) {
       const hipError_t pe = launch_pip(digests, offsets, b, e, i0, i1, pmin, npip, pmax, pks,
                                        sigs, z16, zkey, w, status, fail_index, nogrp, stream,
-                                       own_ctr ? fuse_ctr : w.chunk_start);
+                                       own_ctr ? fuse_ctr : w.chunk_start, gate);
       if (pe != hipSuccess) return pe;
     }
     if (chunks)
@@ -2485,6 +2508,10 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
 }
 
 size_t verify_batch_fuse_ctr_bytes() { return 4ull * kFuseCtr; }
+
+bool verify_batch_gate_ok(uint64_t nbatches, uint64_t nitems) {
+  return verify_batch_outputs_direct(nbatches, nitems) && pip_fuse_head_on();
+}
 
 bool verify_batch_outputs_direct(uint64_t nbatches, uint64_t nitems) {
   return nbatches == 1 && pip_fuse_on() && pip_win_lp_max() >= 1 &&

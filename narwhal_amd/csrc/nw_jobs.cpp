@@ -51,6 +51,7 @@ struct nw_job {
   char* vbuf = nullptr;   // NW_SMALL_VRAM: fine-grained device memory for small jobs' inputs
   char* vhost = nullptr;  // ... and the host's mapping of it (the CPU writes the inputs there)
   size_t vcap = 0;
+  uint32_t vseq = 0;      // NW_BATCH_GATE: the last input-gate sequence number
   uint32_t* dcnt = nullptr;   // small jobs' per-message arrival counters (kept zero)
   size_t ccap = 0;
   uint32_t* dfz = nullptr;    // config-1 fused launches' counters (the tail leaves them zero)
@@ -205,6 +206,14 @@ bool small_vram() {
   }();
   return on;
 }
+constexpr uint64_t kGateChunk = 1024;   // votes per input-gate flag (a multiple of 64)
+bool batch_gate() {
+  static const bool on = [] {
+    const char* e = getenv("NW_BATCH_GATE");
+    return e && *e == '1';
+  }();
+  return on;
+}
 bool batch_vram() {   // on unless NW_BATCH_VRAM=0 (profiles/r06d: config 1 0.303 vs 0.321 ms)
   static const bool on = [] {
     const char* e = getenv("NW_BATCH_VRAM");
@@ -256,6 +265,9 @@ int job_reserve_vram(nw_job* j, size_t bytes) {
   j->vbuf = static_cast<char*>(p);
   j->vhost = static_cast<char*>(hp);
   j->vcap = cap;
+  memset(j->vhost, 0, cap);   // input-gate flags start below every sequence number
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  j->vseq = 0;
   static std::once_flag said;
   std::call_once(said, [] {
     fprintf(stderr, "[narwhal_amd] job inputs written into host-mapped fine-grained device "
@@ -422,19 +434,53 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
   // A lone fused batch's inputs go straight from the caller's buffers into host-mapped
   // fine-grained device memory: no pinned staging copy, no H2D (NW_BATCH_VRAM=0: the pinned
   // buffer and one H2D copy, as before round 6)
-  const bool vram = direct && batch_vram() && job_reserve_vram(j, o_st) == 0;
+  // NW_BATCH_GATE=1 (A/B hook): the kernels are queued first and the votes written after,
+  // chunk by chunk, each chunk released by a flag the head's waves wait for (input_gate_t):
+  // the launch and the head's first waves overlap the CPU's writes.
+  const uint64_t nchunks = (nitems + kGateChunk - 1) / kGateChunk;
+  const size_t o_gf = o_st;   // the flags follow the inputs in the device-memory buffer
+  const bool vram = direct && batch_vram() &&
+                    job_reserve_vram(j, o_st + (batch_gate() ? a256(4 * nchunks) : 0)) == 0;
+  const bool gate = vram && batch_gate() && nitems && nw::verify_batch_gate_ok(nbatches, nitems);
   char* const stage = vram ? j->vhost : j->hbuf;
   memcpy(stage + o_d, digests, 32 * nbatches);
   memcpy(stage + o_off, offsets, 8 * (nbatches + 1));
-  if (nitems) {
+  if (nitems && !gate) {
     memcpy(stage + o_pk, pks, 32 * nitems);
     memcpy(stage + o_sig, sigs, 64 * nitems);
     if (z16) memcpy(stage + o_z, z16, 16 * nitems);
   }
   if (vram) std::atomic_thread_fence(std::memory_order_seq_cst);   // drain write combining
+  uint32_t seq = 0;
+  if (gate) {
+    seq = ++j->vseq;
+    if (seq == 0) seq = j->vseq = 1;   // the flags were zeroed at allocation
+    static std::once_flag said;
+    std::call_once(said, [] {
+      fprintf(stderr, "[narwhal_amd] NW_BATCH_GATE: lone batches launched before their votes "
+              "are written (input gate)\n");
+    });
+  }
+  bool launched = false;
+  // the votes, chunk by chunk, each followed by its flag (fence between: write-combined
+  // stores are not ordered among themselves; PCIe keeps the posted writes in order)
+  const auto release_votes = [&]() {
+    volatile uint32_t* fl = reinterpret_cast<volatile uint32_t*>(j->vhost + o_gf);
+    for (uint64_t c = 0; c < nchunks; ++c) {
+      const uint64_t v0 = c * kGateChunk, v = std::min<uint64_t>(kGateChunk, nitems - v0);
+      memcpy(stage + o_pk + 32 * v0, pks + 32 * v0, 32 * v);
+      memcpy(stage + o_sig + 64 * v0, sigs + 64 * v0, 64 * v);
+      if (z16) memcpy(stage + o_z + 16 * v0, z16 + 16 * v0, 16 * v);
+      std::atomic_thread_fence(std::memory_order_seq_cst);
+      fl[c] = seq;
+    }
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+  };
   nw::z_key_t key;
   rc = fill_key(key);
   if (rc) return job_abort(j, rc);
+  const nw::input_gate_t gt{reinterpret_cast<const uint32_t*>(j->vbuf + o_gf), seq,
+                            (uint32_t)kGateChunk};
   // (planning reads the offsets on the host: the caller's array, never the mapped copy)
   const uint64_t* h_off = offsets;
   // (The Pippenger digit lanes and sorts on a second stream beside the decompressions
@@ -461,11 +507,14 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
         reinterpret_cast<const uint32_t*>(ibuf + o_sig), nitems,
         z16 ? reinterpret_cast<const uint32_t*>(ibuf + o_z) : nullptr, key, j->dbuf + o_ws,
         reinterpret_cast<int32_t*>(obuf + o_st), reinterpret_cast<uint64_t*>(obuf + o_fi),
-        j->stream, nullptr, nullptr, 0, 1.0, out_direct ? j->dfz : nullptr);
+        j->stream, nullptr, nullptr, 0, 1.0, out_direct ? j->dfz : nullptr,
+        gate ? &gt : nullptr);
     if (e != hipSuccess && out_direct) j->dfz_dirty = true;   // the head may have run
+    launched = gate && e == hipSuccess;
     JOB_HIP(e, "verify_batch launch");
     return 0;
   });
+  if (launched) release_votes();   // also on failure after the launch: no wave waits 2 s
   if (rc) return job_abort(j, rc);
   job_out(j, status_out, o_st, 4 * nbatches);
   job_out(j, fail_index_out, o_fi, 8 * nbatches);

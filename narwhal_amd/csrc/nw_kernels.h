@@ -115,6 +115,18 @@ bool verify_batch_outputs_direct(uint64_t nbatches, uint64_t nitems);
 // a zeroed device array of this size (fuse_ctr, e.g. shipped with its inputs' H2D copy),
 // which saves the kernel that would zero them.
 size_t verify_batch_fuse_ctr_bytes();
+// Input gate of a lone fused batch whose inputs the CPU is still writing into host-mapped
+// device memory when the launch is queued (nw_jobs.cpp submit_batch): the head's vote waves
+// wait until flags[vote / chunk] == seq (a system-scope load, then a system-scope acquire),
+// so the kernels start while the bytes are in flight. digests and offsets must be written
+// before the launch. verify_batch_gate_ok: the batch takes the fused head (the only launch
+// that honours the gate). chunk: a multiple of 64 votes.
+struct input_gate_t {
+  const uint32_t* flags;
+  uint32_t seq;
+  uint32_t chunk;
+};
+bool verify_batch_gate_ok(uint64_t nbatches, uint64_t nitems);
 // skip_group_ok (optional, device): batch b is settled (status Ok) when
 // skip_group_ok[b / skip_per_group] != 0 (launch_cert_groups, launch_votes_keyed);
 // active_frac: the caller's estimate of the fraction of votes not skipped (chunk sizing).
@@ -126,7 +138,8 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                const key_tables_t* keys = nullptr,
                                const uint32_t* skip_group_ok = nullptr,
                                uint64_t skip_per_group = 0, double active_frac = 1.0,
-                               uint32_t* fuse_ctr = nullptr);
+                               uint32_t* fuse_ctr = nullptr,
+                               const input_gate_t* gate = nullptr);
 
 // Certificate::verify vote batches merged over groups of certificates (nw_batch.hip):
 // cert_group_size() = certificates per group, 0 when the merge does not apply;

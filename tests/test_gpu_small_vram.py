@@ -7,7 +7,8 @@ the batch parity file (tests/test_gpu_batch.py: lone batches on both sides of th
 limit, every failure class) run in child processes against the oracle: small jobs with the
 opt-in staging (the library must report it), lone batches with the default staging turned
 OFF (NW_BATCH_VRAM=0: the pinned buffer and H2D path keeps its coverage; the default path is
-the one tests/test_gpu_batch.py runs in the suite itself)."""
+the one tests/test_gpu_batch.py runs in the suite itself), and lone batches with the input
+gate (NW_BATCH_GATE=1: the kernels queued before the votes are written, chunk flags)."""
 import os
 import subprocess
 import sys
@@ -20,14 +21,22 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NOTICE = "job inputs written into host-mapped fine-grained device memory"
 
 
-@pytest.mark.parametrize("env,value,test,staged", [
-    ("NW_SMALL_VRAM", "1", "test_gpu_small.py", True),     # opt-in for small jobs
-    ("NW_BATCH_VRAM", "0", "test_gpu_batch.py", False),    # lone batches: on by default
+GATE = "NW_BATCH_GATE: lone batches launched before their votes are written"
+
+
+@pytest.mark.parametrize("env,value,test,notice", [
+    ("NW_SMALL_VRAM", "1", "test_gpu_small.py", NOTICE),   # opt-in for small jobs
+    ("NW_BATCH_VRAM", "0", "test_gpu_batch.py", None),     # lone batches: on by default
+    ("NW_BATCH_GATE", "1", "test_gpu_batch.py", GATE),     # votes written after the launch
 ])
-def test_inputs_in_device_memory(env, value, test, staged):
+def test_inputs_in_device_memory(env, value, test, notice):
     r = subprocess.run([sys.executable, "-u", "-m", "pytest", "-x", "-q", "-s", "-p",
                         "no:cacheprovider", os.path.join(ROOT, "tests", test)],
                        cwd=ROOT, env=dict(os.environ, **{env: value}), capture_output=True,
                        text=True, timeout=280)
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
-    assert (NOTICE in r.stdout + r.stderr) == staged
+    out = r.stdout + r.stderr
+    if notice:
+        assert notice in out
+    else:
+        assert NOTICE not in out and GATE not in out
