@@ -206,6 +206,14 @@ bool small_vram() {
   }();
   return on;
 }
+bool test_fuse_abort() {
+  static std::atomic<long> left{[] {
+    const char* e = getenv("NW_TEST_FUSE_ABORT");
+    return e && *e ? atol(e) : 0L;
+  }()};
+  if (left.load(std::memory_order_relaxed) <= 0) return false;
+  return left.fetch_sub(1, std::memory_order_relaxed) > 0;
+}
 constexpr uint64_t kGateChunk = 1024;   // votes per input-gate flag (a multiple of 64)
 bool batch_gate() {
   static const bool on = [] {
@@ -516,6 +524,14 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
   });
   if (launched) release_votes();   // also on failure after the launch: no wave waits 2 s
   if (rc) return job_abort(j, rc);
+  if (out_direct && test_fuse_abort()) {
+    // test hook (NW_TEST_FUSE_ABORT=k: the first k such calls): a failure after the fused
+    // launches were queued, with their counters left non-zero — the job's next call must
+    // clear them (dfz_dirty, set by job_abort) instead of spinning on stale tickets
+    (void)hipStreamSynchronize(j->stream);
+    (void)hipMemsetAsync(j->dfz, 0x01, nw::verify_batch_fuse_ctr_bytes(), j->stream);
+    return job_abort(j, set_err(NW_E_DEVICE, "NW_TEST_FUSE_ABORT"));
+  }
   job_out(j, status_out, o_st, 4 * nbatches);
   job_out(j, fail_index_out, o_fi, 8 * nbatches);
   *job = j;
