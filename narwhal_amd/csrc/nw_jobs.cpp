@@ -230,17 +230,22 @@ bool batch_vram() {   // on unless NW_BATCH_VRAM=0 (profiles/r06d: config 1 0.30
   return on;
 }
 bool mapped_rw(const void* p, size_t bytes) {
+  // one whole /proc/self/maps line per read (getline: no line is split, however long its
+  // path), and only a writable shared mapping of a GPU device node counts
   FILE* f = fopen("/proc/self/maps", "r");
   if (!f) return false;
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  char line[512];
+  char* line = nullptr;
+  size_t cap = 0;
   bool ok = false;
-  while (!ok && fgets(line, sizeof line, f)) {
+  while (!ok && getline(&line, &cap, f) > 0) {
     unsigned long lo = 0, hi = 0;
     char perm[5] = {0};
     if (sscanf(line, "%lx-%lx %4s", &lo, &hi, perm) == 3 && a >= lo && a + bytes <= hi)
-      ok = perm[0] == 'r' && perm[1] == 'w';
+      ok = perm[0] == 'r' && perm[1] == 'w' && perm[3] == 's' &&
+           (strstr(line, "/dev/dri/") != nullptr || strstr(line, "/dev/kfd") != nullptr);
   }
+  free(line);
   fclose(f);
   return ok;
 }

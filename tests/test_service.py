@@ -538,7 +538,7 @@ def test_native_service_votes_not_starved_by_certificates():
     LG = loadgen_lib()
     cs = certificates_struct(m, len(rows))
     total = 400_000
-    lat_c, out3 = np.zeros(total), np.zeros(13)
+    lat_c, out3 = np.zeros(total), np.zeros(16)   # nw_loadgen.cpp writes out[0..15]
     res = {}
 
     def flood():

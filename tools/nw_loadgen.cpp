@@ -60,15 +60,16 @@ int timed_run(nw_service* s, const nw_certificates* corpus, const int32_t* exp_s
 extern "C" {
 
 // Returns 0 or the first negative NW_E_* from the service. lat_out: total seconds;
-// out (13 doubles): elapsed seconds (t0 .. last verdict), jobs, mismatches, and the
+// out (16 doubles — a caller's array must hold all 16): elapsed seconds (t0 .. last
+// verdict), jobs, mismatches, and the
 // producers' lateness: the largest and the mean (call time - due time) of a submit, seconds
 // (a producer that cannot keep its schedule shows here before it shows as latency), then
 // the producers' CPU / wall time and their voluntary / involuntary context switches, and
 // the nw_service_certificate calls' mean and longest duration and the count above 20 us;
-// out[13..15]: the service's hedge during the timed run: requests hedged, requests the host
-// answered first, batches the host took whole (nw_service_hedge_stats);
-// out[11..12]: jobs that took the small-job launch and
-// the bulk pipeline during the timed run (nw_path_stats).
+// out[11..12]: jobs that took the small-job launch and the bulk pipeline during the timed
+// run (nw_path_stats); out[13..15]: the service's hedge during the timed run: requests
+// hedged, requests the host answered first, batches the host took whole
+// (nw_service_hedge_stats).
 int nw_loadgen_certificates(const nw_committee* com, const nw_certificates* corpus,
                             const int32_t* exp_status, const uint64_t* exp_index, double rate,
                             uint64_t total, size_t max_items, uint32_t max_delay_us,
