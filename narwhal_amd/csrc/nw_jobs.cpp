@@ -214,6 +214,13 @@ bool test_fuse_abort() {
   if (left.load(std::memory_order_relaxed) <= 0) return false;
   return left.fetch_sub(1, std::memory_order_relaxed) > 0;
 }
+bool batch_stamps() {
+  static const bool on = [] {
+    const char* e = getenv("NW_BATCH_STAMPS");
+    return e && *e == '1';
+  }();
+  return on;
+}
 constexpr uint64_t kGateChunk = 1024;   // votes per input-gate flag (a multiple of 64)
 bool batch_gate() {
   static const bool on = [] {
@@ -456,6 +463,7 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
                     job_reserve_vram(j, o_st + (batch_gate() ? a256(4 * nchunks) : 0)) == 0;
   const bool gate = vram && batch_gate() && nitems && nw::verify_batch_gate_ok(nbatches, nitems);
   char* const stage = vram ? j->vhost : j->hbuf;
+  const auto ts0 = std::chrono::steady_clock::now();   // NW_BATCH_STAMPS (diagnostics)
   memcpy(stage + o_d, digests, 32 * nbatches);
   memcpy(stage + o_off, offsets, 8 * (nbatches + 1));
   if (nitems && !gate) {
@@ -464,6 +472,7 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
     if (z16) memcpy(stage + o_z, z16, 16 * nitems);
   }
   if (vram) std::atomic_thread_fence(std::memory_order_seq_cst);   // drain write combining
+  const auto ts1 = std::chrono::steady_clock::now();
   uint32_t seq = 0;
   if (gate) {
     seq = ++j->vseq;
@@ -527,8 +536,19 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
     JOB_HIP(e, "verify_batch launch");
     return 0;
   });
+  const auto ts2 = std::chrono::steady_clock::now();
   if (launched) release_votes();   // also on failure after the launch: no wave waits 2 s
   if (rc) return job_abort(j, rc);
+  if (batch_stamps()) {
+    const auto ts3 = std::chrono::steady_clock::now();
+    const auto us = [](std::chrono::steady_clock::time_point a,
+                       std::chrono::steady_clock::time_point b) {
+      return std::chrono::duration<double, std::micro>(b - a).count();
+    };
+    fprintf(stderr, "[narwhal_amd] batch stamps: n=%zu vram=%d gate=%d inputs %.1f us, "
+            "launch %.1f us, gated writes %.1f us\n", (size_t)nitems, (int)vram, (int)gate,
+            us(ts0, ts1), us(ts1, ts2), us(ts2, ts3));
+  }
   if (out_direct && test_fuse_abort()) {
     // test hook (NW_TEST_FUSE_ABORT=k: the first k such calls): a failure after the fused
     // launches were queued, with their counters left non-zero — the job's next call must
@@ -1448,7 +1468,12 @@ int nw_path_stats(uint64_t* small_jobs, uint64_t* pipeline_jobs) {
 // ---- blocking host-buffer entry points = submit + wait ------------------------------
 static int run_blocking(int rc, nw_job* j) {
   if (rc) return rc;
+  const auto t0 = std::chrono::steady_clock::now();
   rc = nw_job_wait(j);
+  if (batch_stamps())
+    fprintf(stderr, "[narwhal_amd] wait %.1f us\n",
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0)
+                .count());
   nw_job_release(j);
   return rc;
 }
