@@ -485,10 +485,12 @@ class NativeService:
 
     committee: messages.Committee, a packed committee dict, or None (verify / verify_batch
     only). Verdicts: (status, index) pairs as the bulk calls return them; a device failure
-    raises EngineError in every affected waiter."""
+    raises EngineError in every affected waiter. hedge: None keeps the library's hedge
+    (late requests also verified on the host, nw_service_set_hedge); 0 turns it off, so that
+    every verdict is the device's (the device-parity tests); a float sets its deadline."""
 
     def __init__(self, committee=None, max_items: int = 1 << 16, max_delay: float = 0.0005,
-                 max_inflight: int = 4):
+                 max_inflight: int = 4, hedge: float | None = None):
         from .messages import committee_struct
         L = _lib.lib()
         n = L.nw_init()
@@ -504,6 +506,8 @@ class NativeService:
                                   max_items, int(max_delay * 1e6), max_inflight,
                                   ctypes.byref(h)), "nw_service_create")
         self._h = h
+        if hedge is not None:
+            self.set_hedge(hedge)
         self._lock = threading.Lock()
         self._pending: dict[int, tuple] = {}
         self._ids = itertools.count(1)

@@ -145,7 +145,7 @@ def test_native_service_fans_out(fanout):
     from cert_cases import unpack
     rows = [S.CertRow(r["hb"], r["np"], r["id"], r["sig"], b"".join(pk for pk, _ in r["votes"]),
                       b"".join(sg for _, sg in r["votes"]), len(r["votes"])) for r in unpack(m)]
-    svc = S.NativeService(m["committee"], max_items=2000, max_delay=0.0005)
+    svc = S.NativeService(m["committee"], max_items=2000, max_delay=0.0005, hedge=0)
     got = [None] * len(rows)
 
     def worker(t):

@@ -148,7 +148,7 @@ def test_fuzz_certificates_through_service_vs_oracle():
     rows = _rows(d)
 
     async def main():
-        svc = S.NativeService(s["committee"], max_delay=0.0002)
+        svc = S.NativeService(s["committee"], max_delay=0.0002, hedge=0)
         got = await asyncio.gather(*[svc.certificate_status(r) for r in rows])
         svc.close()
         return got
@@ -240,7 +240,7 @@ def test_fuzz_irregular_committees_through_service():
     rows = _rows(d)
 
     async def main():
-        svc = S.NativeService(com, max_delay=0.0002)
+        svc = S.NativeService(com, max_delay=0.0002, hedge=0)
         got = await asyncio.gather(*[svc.certificate_status(r) for r in rows])
         got += await asyncio.gather(*[svc.certificate_status(r) for r in rows[::-1]])
         svc.close()

@@ -432,7 +432,8 @@ def test_native_service_certificates_from_threads_vs_oracle():
     m, mst, mix = W.mutate_votes(hon, np.arange(7, 2000, 100), seed=5)
     cases = [(com4, s4, st4, ix4), (m["committee"], m, mst, mix)]
     for com, s, est, eix in cases:
-        svc = S.NativeService(com, max_items=1 << 12, max_delay=0.0005, max_inflight=3)
+        svc = S.NativeService(com, max_items=1 << 12, max_delay=0.0005, max_inflight=3,
+                                 hedge=0)
         rows = _rows(s)
         got = [None] * len(rows)
         calls = [0] * len(rows)
@@ -476,8 +477,8 @@ def test_native_service_all_kinds_asyncio_vs_oracle():
               vp["authors"][i].tobytes(), vp["sigs"][i].tobytes()) for i in range(vn)]
 
     async def main():
-        svc = S.NativeService(com4, max_delay=0.001)
-        vsvc = S.NativeService(vcom, max_delay=0.001)
+        svc = S.NativeService(com4, max_delay=0.001, hedge=0)
+        vsvc = S.NativeService(vcom, max_delay=0.001, hedge=0)
         got = await asyncio.gather(*[svc.certificate_status(r) for r in rows],
                                    *[svc.header_status(r) for r in rows],
                                    *[vsvc.vote_status(v) for v in votes],
@@ -530,7 +531,8 @@ def test_native_service_votes_not_starved_by_certificates():
     vcom, vp, vn, vexp = votes_case(N=100, seed=62, count=40, keys=keys)
     for k in ("pks", "stakes", "worker_offsets", "worker_ids"):
         assert np.array_equal(vcom[k], m["committee"][k]), k
-    svc = S.NativeService(m["committee"], max_items=1 << 16, max_delay=0.0002, max_inflight=1)
+    svc = S.NativeService(m["committee"], max_items=1 << 16, max_delay=0.0002, max_inflight=1,
+                          hedge=0)
     rows = _rows(m)
     for r in rows[:8]:                                # warm: key tables, pools
         svc.submit_certificate(r, lambda st, ix: None)
