@@ -522,6 +522,9 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
   char* const obuf = out_direct ? j->hdev : j->dbuf;
   char* const ibuf = vram ? j->vbuf : j->dbuf;
   rc = job_run(j, vram ? 0 : o_st, o_st, out_direct ? 0 : o_ws - o_st, [&]() -> int {
+    // from here on a gated head may be queued (even if a later launch fails): the votes
+    // and their flags are written whatever happens, so no wave is left waiting
+    launched = gate;
     const hipError_t e = nw::launch_verify_batch(
         reinterpret_cast<const uint32_t*>(ibuf + o_d),
         reinterpret_cast<const uint64_t*>(ibuf + o_off), h_off, nbatches,
@@ -532,7 +535,6 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
         j->stream, nullptr, nullptr, 0, 1.0, out_direct ? j->dfz : nullptr,
         gate ? &gt : nullptr);
     if (e != hipSuccess && out_direct) j->dfz_dirty = true;   // the head may have run
-    launched = gate && e == hipSuccess;
     JOB_HIP(e, "verify_batch launch");
     return 0;
   });
