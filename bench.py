@@ -109,15 +109,19 @@ ALG_BYTES_PER_KEYED_VOTE = 96 + 27 * 128
 
 def pmc_issue_peak():
     """Issue-bound peak of k_verify_strict (verifies/s) from its committed PMC instruction mix
-    (profiles/r02d/pmc_mix.json, tools/pmc_mix.sh): per-verify 64-bit / 32-bit integer and
+    (the newest of profiles/r06m/pmc_mix.json — the round-6 kernel — and r02d's, written by
+    tools/pmc_mix.sh + tools/pmc_strict_json.py): per-verify 64-bit / 32-bit integer and
     other VALU lane-ops, each priced at its microbenchmarked issue rate
     (profiles/r01_ubench_valu_4wps.txt; 32-bit integer ops at the half rate, an upper bound
-    on their cost). None when the profile is absent."""
-    try:
-        m = json.load(open(os.path.join(ROOT, "profiles", "r02d", "pmc_mix.json")))
-    except (OSError, ValueError):
-        return None, None
-    return m["issue_peak_verifies_per_s"], "profiles/r02d/pmc_mix.json"
+    on their cost). None when no profile is present."""
+    for tag in ("r06m", "r02d"):
+        rel = os.path.join("profiles", tag, "pmc_mix.json")
+        try:
+            m = json.load(open(os.path.join(ROOT, rel)))
+        except (OSError, ValueError):
+            continue
+        return m["issue_peak_verifies_per_s"], rel
+    return None, None
 
 
 # One wave per SIMD (config 3: 65,536 messages = 1,024 waves): a lone wave issues one VALU
