@@ -1802,7 +1802,8 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
                                                         uint64_t* __restrict__ fail_index,
                                                         uint64_t* __restrict__ stamps,
                                                         const bv_item* __restrict__ items,
-                                                        int bsum_here) {
+                                                        int bsum_here, uint32_t* done,
+                                                        uint32_t done_seq) {
   __shared__ uint32_t s_ticket, s_ok;
   __shared__ uint32_t s_other[3][64];
   __shared__ uint32_t s_tmp[40];
@@ -1954,6 +1955,7 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
       status[bidx] = NW_E_DEVICE;
       if (fail_index) fail_index[bidx] = 0;
       __threadfence_system();
+      if (done) __hip_atomic_store(done, done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       fz_exit(ctr);
     }
     return;
@@ -1964,6 +1966,10 @@ __global__ __launch_bounds__(256) void k_pip_tail_fused(const uint64_t* __restri
   stamp(1, __builtin_amdgcn_s_memrealtime());
   stamp(2, 0x500u);
   if (lane == 0) __threadfence_system();   // outputs may be host-mapped (direct outputs)
+  // the verdict is out: tell a host spinning on `done` (NW_BATCH_SPIN), ahead of the
+  // kernel's completion signal (the other workgroups are counting out)
+  if (lane == 0 && done)
+    __hip_atomic_store(done, done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 inline size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -2295,7 +2301,8 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
                 const uint32_t* pks, const uint32_t* sigs, const uint32_t* z16,
                 const z_key_t& zkey, const bv_ws& w, int32_t* status, uint64_t* fail_index,
                 const pip_group_t& grp, hipStream_t stream,
-                uint32_t* fctr, const input_gate_t* gate = nullptr) {
+                uint32_t* fctr, const input_gate_t* gate = nullptr, uint32_t* done = nullptr,
+                uint32_t done_seq = 0) {
   const bool group = grp.cert_vote_offsets != nullptr;
   const uint32_t extra = group ? grp.nkeys : 0;   // key sums
   const uint32_t roles = group ? 2 : 3;
@@ -2345,7 +2352,7 @@ hipError_t launch_pip(const uint32_t* digests, const uint64_t* offsets, uint64_t
     const uint32_t nblk = nbk + 2 + kFuseTopParts + (kPipWin - 1) * kFuseParts;
     hipLaunchKernelGGL(k_pip_tail_fused, dim3(nblk), dim3(256), lds, stream, offsets, b, i0, lg,
                        nbk, w.tabs, fctr, status, fail_index, fuse_stamps(nblk), w.items,
-                       fuse_head ? 1 : 0);
+                       fuse_head ? 1 : 0, done, done_seq);
     return hipGetLastError();
   }
   const int xcd = npip >= 8;
@@ -2402,11 +2409,13 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                int32_t* status, uint64_t* fail_index, hipStream_t stream,
                                const key_tables_t* keys, const uint32_t* skip_group_ok,
                                uint64_t skip_per_group, double active_frac,
-                               uint32_t* fuse_ctr, const input_gate_t* gate) {
+                               uint32_t* fuse_ctr, const input_gate_t* gate,
+                               uint32_t* done, uint32_t done_seq) {
   // a gate is honoured by the fused head only: refuse it anywhere else (its waves would
   // read bytes the CPU has not written yet)
   if (gate && !verify_batch_gate_ok(nbatches, nitems)) return hipErrorInvalidValue;
   if (gate && (gate->chunk == 0 || gate->chunk % 64 != 0)) return hipErrorInvalidValue;
+  if (done && !verify_batch_outputs_direct(nbatches, nitems)) return hipErrorInvalidValue;
   const key_tables_t kt = keys ? *keys : key_tables_t{nullptr, nullptr, nullptr, {}};
   const batch_skip_t sk{skip_group_ok, skip_per_group ? skip_per_group : 1};
   if (nbatches == 0) return hipSuccess;
@@ -2488,7 +2497,8 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
     if (npip) {
       const hipError_t pe = launch_pip(digests, offsets, b, e, i0, i1, pmin, npip, pmax, pks,
                                        sigs, z16, zkey, w, status, fail_index, nogrp, stream,
-                                       own_ctr ? fuse_ctr : w.chunk_start, gate);
+                                       own_ctr ? fuse_ctr : w.chunk_start, gate, done,
+                                       done_seq);
       if (pe != hipSuccess) return pe;
     }
     if (chunks)

@@ -127,6 +127,9 @@ struct input_gate_t {
   uint32_t chunk;
 };
 bool verify_batch_gate_ok(uint64_t nbatches, uint64_t nitems);
+// done (optional, host-mapped; lone fused batches only, verify_batch_outputs_direct): the
+// fused tail stores done_seq there (system scope) right after the verdict, so a host may
+// spin on it instead of waiting for the launch's completion signal.
 // skip_group_ok (optional, device): batch b is settled (status Ok) when
 // skip_group_ok[b / skip_per_group] != 0 (launch_cert_groups, launch_votes_keyed);
 // active_frac: the caller's estimate of the fraction of votes not skipped (chunk sizing).
@@ -139,7 +142,8 @@ hipError_t launch_verify_batch(const uint32_t* digests, const uint64_t* offsets,
                                const uint32_t* skip_group_ok = nullptr,
                                uint64_t skip_per_group = 0, double active_frac = 1.0,
                                uint32_t* fuse_ctr = nullptr,
-                               const input_gate_t* gate = nullptr);
+                               const input_gate_t* gate = nullptr,
+                               uint32_t* done = nullptr, uint32_t done_seq = 0);
 
 // Certificate::verify vote batches merged over groups of certificates (nw_batch.hip):
 // cert_group_size() = certificates per group, 0 when the merge does not apply;

@@ -22,12 +22,15 @@ NOTICE = "job inputs written into host-mapped fine-grained device memory"
 
 
 GATE = "NW_BATCH_GATE: lone batches launched before their votes are written"
+SPIN = "NW_BATCH_SPIN: lone batches return on the tail's done word"
 
 
 @pytest.mark.parametrize("env,value,test,notice", [
     ("NW_SMALL_VRAM", "1", "test_gpu_small.py", NOTICE),   # opt-in for small jobs
     ("NW_BATCH_VRAM", "0", "test_gpu_batch.py", None),     # lone batches: on by default
     ("NW_BATCH_GATE", "1", "test_gpu_batch.py", GATE),     # votes written after the launch
+    ("NW_BATCH_SPIN", "1", "test_gpu_batch.py", SPIN),     # return on the tail's done word
+    ("NW_BATCH_SPIN", "1", "test_gpu_fused_abort.py", None),   # (its own child's output)
 ])
 def test_inputs_in_device_memory(env, value, test, notice):
     r = subprocess.run([sys.executable, "-u", "-m", "pytest", "-x", "-q", "-s", "-p",
@@ -39,4 +42,4 @@ def test_inputs_in_device_memory(env, value, test, notice):
     if notice:
         assert notice in out
     else:
-        assert NOTICE not in out and GATE not in out
+        assert NOTICE not in out and GATE not in out and SPIN not in out
