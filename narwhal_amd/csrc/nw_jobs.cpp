@@ -228,10 +228,10 @@ bool test_fuse_abort() {
   if (left.load(std::memory_order_relaxed) <= 0) return false;
   return left.fetch_sub(1, std::memory_order_relaxed) > 0;
 }
-bool batch_spin() {
+bool batch_spin() {   // on unless NW_BATCH_SPIN=0 (profiles/r06n: wait 258 vs 264 us)
   static const bool on = [] {
     const char* e = getenv("NW_BATCH_SPIN");
-    return e && *e == '1';
+    return !(e && *e == '0');
   }();
   return on;
 }
@@ -309,11 +309,7 @@ int job_reserve_vram(nw_job* j, size_t bytes) {
   memset(j->vhost, 0, cap);   // input-gate flags start below every sequence number
   std::atomic_thread_fence(std::memory_order_seq_cst);
   j->vseq = 0;
-  static std::once_flag said;
-  std::call_once(said, [] {
-    fprintf(stderr, "[narwhal_amd] job inputs written into host-mapped fine-grained device "
-            "memory (NW_SMALL_VRAM / NW_BATCH_VRAM)\n");
-  });
+
   log_growth(3, cap, t0);
   return 0;
 }
@@ -543,8 +539,9 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
   }
   char* const obuf = out_direct ? j->hdev : j->dbuf;
   char* const ibuf = vram ? j->vbuf : j->dbuf;
-  // NW_BATCH_SPIN=1 (A/B hook): the tail stores a fresh sequence number into the pinned
-  // done word after the verdict; nw_job_wait spins on it instead of the completion event
+  // The tail stores a fresh sequence number into the pinned done word right after the
+  // verdict; nw_job_wait spins on it instead of waiting for the launch's completion event
+  // (NW_BATCH_SPIN=0: the event only)
   uint32_t* done = nullptr;
   uint32_t dseq = 0;
   if (out_direct && batch_spin()) {
@@ -553,11 +550,6 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
     volatile uint32_t* dh = reinterpret_cast<volatile uint32_t*>(j->hbuf + o_dn);
     *dh = dseq - 1;   // anything but dseq
     done = reinterpret_cast<uint32_t*>(j->hdev + o_dn);
-    static std::once_flag said;
-    std::call_once(said, [] {
-      fprintf(stderr, "[narwhal_amd] NW_BATCH_SPIN: lone batches return on the tail's done "
-              "word\n");
-    });
   }
   rc = job_run(j, vram ? 0 : o_st, o_st, out_direct ? 0 : o_ws - o_st, [&]() -> int {
     // from here on a gated head may be queued (even if a later launch fails): the votes
@@ -840,6 +832,11 @@ int submit_small(int dev, uint32_t kind, const nw_committee* com, const nw_certi
   }
   char* X = j->hdev;   // the device's view of the staging buffer
   if (small_vram() && job_reserve_vram(j, o_st) == 0) {
+    static std::once_flag said;   // (the opt-in path announces itself once per process)
+    std::call_once(said, [] {
+      fprintf(stderr, "[narwhal_amd] NW_SMALL_VRAM: small jobs' inputs written into "
+              "host-mapped fine-grained device memory\n");
+    });
     memcpy(j->vhost, H, o_st);   // the inputs (everything before the outputs)
     std::atomic_thread_fence(std::memory_order_seq_cst);   // drain the write-combining buffers
     X = j->vbuf;

@@ -7,8 +7,11 @@ the batch parity file (tests/test_gpu_batch.py: lone batches on both sides of th
 limit, every failure class) run in child processes against the oracle: small jobs with the
 opt-in staging (the library must report it), lone batches with the default staging turned
 OFF (NW_BATCH_VRAM=0: the pinned buffer and H2D path keeps its coverage; the default path is
-the one tests/test_gpu_batch.py runs in the suite itself), and lone batches with the input
-gate (NW_BATCH_GATE=1: the kernels queued before the votes are written, chunk flags)."""
+the one tests/test_gpu_batch.py runs in the suite itself), lone batches with the input
+gate (NW_BATCH_GATE=1: the kernels queued before the votes are written, chunk flags), and
+lone batches that wait for the launch's completion event instead of the tail's done word
+(NW_BATCH_SPIN=0; the default spin path is the suite's own), also under the injected
+post-launch failure of tests/test_gpu_fused_abort.py."""
 import os
 import subprocess
 import sys
@@ -18,19 +21,18 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-NOTICE = "job inputs written into host-mapped fine-grained device memory"
+NOTICE = "NW_SMALL_VRAM: small jobs' inputs written into host-mapped fine-grained device memory"
 
 
 GATE = "NW_BATCH_GATE: lone batches launched before their votes are written"
-SPIN = "NW_BATCH_SPIN: lone batches return on the tail's done word"
 
 
 @pytest.mark.parametrize("env,value,test,notice", [
     ("NW_SMALL_VRAM", "1", "test_gpu_small.py", NOTICE),   # opt-in for small jobs
     ("NW_BATCH_VRAM", "0", "test_gpu_batch.py", None),     # lone batches: on by default
     ("NW_BATCH_GATE", "1", "test_gpu_batch.py", GATE),     # votes written after the launch
-    ("NW_BATCH_SPIN", "1", "test_gpu_batch.py", SPIN),     # return on the tail's done word
-    ("NW_BATCH_SPIN", "1", "test_gpu_fused_abort.py", None),   # (its own child's output)
+    ("NW_BATCH_SPIN", "0", "test_gpu_batch.py", None),     # the completion event only
+    ("NW_BATCH_SPIN", "0", "test_gpu_fused_abort.py", None),
 ])
 def test_inputs_in_device_memory(env, value, test, notice):
     r = subprocess.run([sys.executable, "-u", "-m", "pytest", "-x", "-q", "-s", "-p",
@@ -42,4 +44,4 @@ def test_inputs_in_device_memory(env, value, test, notice):
     if notice:
         assert notice in out
     else:
-        assert NOTICE not in out and GATE not in out and SPIN not in out
+        assert NOTICE not in out and GATE not in out
