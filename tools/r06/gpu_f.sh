@@ -3,7 +3,7 @@
 # the full -m gpu suite, smoke, the default bench line (the profile set: gpu_g.sh).
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r06f; mkdir -p $O
+O=${OUT:-gpurun_out/r06f}; mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 280 --timeout-method thread > $O/gputests.log 2>&1 || { tail -40 $O/gputests.log; exit 1; }
 tail -2 $O/gputests.log
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
