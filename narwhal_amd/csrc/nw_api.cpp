@@ -53,6 +53,12 @@ struct SharedDev {
   hipEvent_t last = nullptr;   // completion of the last leased launch sequence
   bool last_valid = false;
   std::vector<uint8_t> khost;  // host copy of the keys the tables hold (empty = unknown)
+  // 16-bit tables of the same committee for small jobs while ktabs are wider (Lease::
+  // small_tables): their allocation (keys), their ok words, the keys they hold (host)
+  void* stabs = nullptr;
+  uint32_t* sok = nullptr;
+  size_t scap = 0;
+  std::vector<uint8_t> shost;
   std::vector<hipEvent_t> readers;   // small jobs (ReadLease) queued since the last Lease
   std::vector<hipEvent_t> rpool;     // recycled reader events
 };
@@ -639,6 +645,8 @@ int cert_pipeline(int dev, const nw_committee& com, const nw_certificates& cs,
                                  ktabs, kok, s, ksaved, kflag, kforce),
            "k_key_tables");
     lease.keys_built(com.nauth, host_pks);
+    rc = lease.small_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth, host_pks);
+    if (rc) return rc;
   }
   NW_HIP(nw::launch_cert_prepare(dc, ds, headers_only, w.hdr_digest, w.authors, w.cert_digest,
                                  w.pre1, w.pre2, w.idx1, w.idx2,
@@ -813,6 +821,8 @@ int votes_pipeline(int dev, const nw_committee& com, size_t n, const uint8_t* id
                                  kforce),
            "k_key_tables");
     lease.keys_built(com.nauth, host_pks);
+    rc = lease.small_tables(reinterpret_cast<const uint32_t*>(com.pks), com.nauth, host_pks);
+    if (rc) return rc;
   }
   const nw::key_tables_t kt{static_cast<nw::ge_niels_pad*>(ktabs), kok, d_key, ks};
   NW_HIP(nw::launch_verify_strict(d_dig, 8, reinterpret_cast<const uint32_t*>(authors),
@@ -1002,6 +1012,13 @@ int ReadLease::acquire(int dev_index, hipStream_t stream, const uint8_t* pks, si
   dev_ = dev_index;
   stream_ = stream;
   held_ = true;
+  if (d.kW > 16 && d.stabs && d.shost.size() == 32 * nkeys &&
+      memcmp(d.shost.data(), pks, 32 * nkeys) == 0) {   // Lease::small_tables
+    *tabs = d.stabs;
+    *ok = d.sok;
+    *ks = nw::keyspec_for(16);
+    return 0;
+  }
   *tabs = d.ktabs;
   *ok = d.kok;
   *ks = nw::keyspec_for(d.kW);
@@ -1086,6 +1103,7 @@ static void free_key_tables(SharedDev& d) {
   d.kcap = d.ksaved_n = 0;
   d.kW = 0;
   d.khost.clear();
+  d.shost.clear();   // the small-job set describes no committee until rebuilt
 }
 
 // Key tables of width W for nkeys keys (room for 16 keys at 16 bits, 1 GB; for the committee
@@ -1145,6 +1163,43 @@ int Lease::key_tables(size_t nkeys, void** tabs, uint32_t** ok, nw::keyspec* ks,
   if (force) *force = d.ksaved_n != nkeys;
   d.ksaved_n = 0;   // until keys_built: a failed launch leaves no tables to keep
   d.khost.clear();
+  return 0;
+}
+
+int Lease::small_tables(const uint32_t* dpks, size_t nkeys, const uint8_t* host_pks) {
+  static const bool on = [] {
+    const char* e = getenv("NW_SMALL_KEYW16");
+    return !(e && *e == '0');
+  }();
+  SharedDev& d = g_shared[dev_];
+  if (!on || d.kW <= 16 || !host_pks || !nkeys || d.ksaved_n != nkeys) return 0;
+  if (d.shost.size() == 32 * nkeys && memcmp(d.shost.data(), host_pks, 32 * nkeys) == 0)
+    return 0;   // built for this committee (every earlier reader is ordered before us)
+  d.shost.clear();
+  const nw::keyspec ks = nw::keyspec_for(16);
+  if (nkeys > d.scap) {
+    if (d.stabs) (void)hipFree(d.stabs);
+    if (d.sok) (void)hipFree(d.sok);
+    d.stabs = nullptr;
+    d.sok = nullptr;
+    d.scap = 0;
+    hipError_t e = nw::table_malloc(&d.stabs, nw::key_tables_bytes(nkeys, ks));
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d.sok), 4 * nkeys);
+    if (e != hipSuccess) {   // no room: small jobs keep reading the wide tables
+      (void)hipGetLastError();
+      if (d.stabs) (void)hipFree(d.stabs);
+      if (d.sok) (void)hipFree(d.sok);
+      d.stabs = nullptr;
+      d.sok = nullptr;
+      return 0;
+    }
+    d.scap = nkeys;
+  }
+  const hipError_t e = nw::launch_key_tables(dpks, nkeys, ks,
+                                             static_cast<nw::ge_niels_pad*>(d.stabs), d.sok,
+                                             stream_, nullptr, nullptr, true);
+  if (e != hipSuccess) return ::set_err(NW_E_DEVICE, "k_key_tables (16-bit, small jobs)", e);
+  d.shost.assign(host_pks, host_pks + 32 * nkeys);
   return 0;
 }
 

@@ -99,6 +99,13 @@ class Lease {
   // After a successful launch_key_tables: the saved keys now describe the tables; host_pks
   // (nkeys x 32 bytes, optional) are those keys in host memory (small jobs compare them).
   void keys_built(size_t nkeys, const uint8_t* host_pks = nullptr);
+  // After keys_built: when the committee's tables are wider than 16 bits, also a 16-bit set
+  // of the same keys for the small-job kernel (ReadLease hands it out): lone requests read
+  // 67 MB per key instead of 940 MB (profiles/r06p: the 20-bit tables made ~3.5 % of N = 50
+  // single-certificate jobs take > 1 ms at low rates). dpks: the keys on the device. Skipped
+  // (small jobs keep the wide tables) without host keys, without memory, or with
+  // NW_SMALL_KEYW16=0.
+  int small_tables(const uint32_t* dpks, size_t nkeys, const uint8_t* host_pks);
   // Record the chain event on the stream and unlock (idempotent). 0 or NW_E_DEVICE.
   int release();
 
