@@ -59,6 +59,9 @@ struct nw_job {
   uint32_t spin_seq = 0;
   uint32_t dseq = 0;
   bool early = false;
+  // small jobs (NW_SMALL_DONE): one done flag per workgroup in the pinned buffer (host view)
+  volatile uint32_t* small_flags = nullptr;
+  uint32_t small_nwg = 0;
   uint32_t* dcnt = nullptr;   // small jobs' per-message arrival counters (kept zero)
   size_t ccap = 0;
   uint32_t* dfz = nullptr;    // config-1 fused launches' counters (the tail leaves them zero)
@@ -125,6 +128,7 @@ int job_acquire(int dev, nw_job** out) {
   j->pending = false;
   j->early = false;
   j->spin = nullptr;
+  j->small_flags = nullptr;
   *out = j;
   return 0;
 }
@@ -140,6 +144,7 @@ void job_recycle(nw_job* j) {
   if (!j->early) j->pending = false;   // an early job syncs on its next acquire
   j->nouts = 0;
   j->spin = nullptr;
+  j->small_flags = nullptr;
   std::lock_guard<std::mutex> g(g_pool[j->dev].m);
   g_pool[j->dev].free.push_back(j);
 }
@@ -227,6 +232,30 @@ bool test_fuse_abort() {
   }()};
   if (left.load(std::memory_order_relaxed) <= 0) return false;
   return left.fetch_sub(1, std::memory_order_relaxed) > 0;
+}
+bool small_done() {   // on unless NW_SMALL_DONE=0
+  static const bool on = [] {
+    const char* e = getenv("NW_SMALL_DONE");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+// Outputs delivered from a job whose kernels have written them (done word / flags) while the
+// launch may still be finishing: the job stays pending and is synchronised on its next
+// acquire (job_acquire), not at release.
+void job_deliver_early(nw_job* j) {
+  std::atomic_thread_fence(std::memory_order_acquire);
+  for (int i = 0; i < j->nouts; ++i)
+    memcpy(j->outs[i].dst, j->hbuf + j->outs[i].off, j->outs[i].bytes);
+  j->nouts = 0;
+  j->early = true;
+  j->spin = nullptr;
+  j->small_flags = nullptr;
+}
+bool small_flags_done(const nw_job* j) {
+  for (uint32_t w = 0; w < j->small_nwg; ++w)
+    if (j->small_flags[w] != j->spin_seq) return false;
+  return true;
 }
 bool batch_spin() {   // on unless NW_BATCH_SPIN=0 (profiles/r06n: wait 258 vs 264 us)
   static const bool on = [] {
@@ -790,7 +819,10 @@ int submit_small(int dev, uint32_t kind, const nw_committee* com, const nw_certi
     }
   }
   const size_t o_sl = P.add(sizeof(nw::small_slot_t) * nslots);
-  const size_t o_st = P.add(4 * n), o_ix = P.add(8 * n), hend = P.off;
+  const size_t o_st = P.add(4 * n), o_ix = P.add(8 * n);
+  const uint32_t S_wg = small_slots_per_wg(nslots);
+  const uint64_t nwg_all = (nslots + S_wg - 1) / S_wg;
+  const size_t o_df = P.add(4 * nwg_all), hend = P.off;   // NW_SMALL_DONE flags
   Packer D;
   const size_t d_mi = D.add(sizeof(nw::small_msg_info_t) * n), d_sr = D.add(4 * nslots);
   rc = job_reserve(j, hend, D.off);
@@ -879,6 +911,13 @@ int submit_small(int dev, uint32_t kind, const nw_committee* com, const nw_certi
   J.mcount = j->dcnt;
   J.status = reinterpret_cast<int32_t*>(j->hdev + o_st);
   J.index = kind == nw::kSmallVotes ? nullptr : reinterpret_cast<uint64_t*>(j->hdev + o_ix);
+  uint32_t dseq = 0;
+  if (small_done() && J.slots_per_wg == S_wg) {
+    dseq = ++j->dseq;
+    if (dseq == 0) dseq = j->dseq = 1;
+    J.done_flags = reinterpret_cast<uint32_t*>(j->hdev + o_df);
+    J.done_seq = dseq;
+  }
   nw::rt::ReadLease rl;
   const void* tabs = nullptr;
   const uint32_t* ok = nullptr;
@@ -942,6 +981,11 @@ int submit_small(int dev, uint32_t kind, const nw_committee* com, const nw_certi
   j->pending = true;
   job_out(j, status_out, o_st, 4 * n);
   if (kind != nw::kSmallVotes) job_out(j, index_out, o_ix, 8 * n);
+  if (J.done_flags) {
+    j->small_flags = reinterpret_cast<volatile uint32_t*>(H + o_df);
+    j->small_nwg = (uint32_t)nwg_all;
+    j->spin_seq = dseq;
+  }
   g_small_jobs.fetch_add(1, std::memory_order_relaxed);
   *job = j;
   return 0;
@@ -1312,6 +1356,11 @@ int nw_job_poll(nw_job* job) {
     return done;
   }
   if (!job->pending) return 1;
+  if (job->early) return 1;
+  if (job->small_flags && small_flags_done(job)) {   // every workgroup's writes are out
+    job_deliver_early(job);
+    return 1;
+  }
   hipError_t e = hipEventQuery(job->done);
   if (e == hipErrorNotReady) return 0;
   if (e != hipSuccess) {
@@ -1333,6 +1382,19 @@ int nw_job_wait(nw_job* job) {
     return first;
   }
   if (!job->pending) return 0;
+  if (job->early) return 0;
+  if (job->small_flags) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (!small_flags_done(job)) {
+      __builtin_ia32_pause();
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+    }
+    if (small_flags_done(job)) {
+      job_deliver_early(job);
+      return 0;
+    }
+    job->small_flags = nullptr;
+  }
   if (job->spin) {
     // NW_BATCH_SPIN: the tail's done word, for up to 20 ms (then the event, as usual)
     const auto t0 = std::chrono::steady_clock::now();
@@ -1341,12 +1403,7 @@ int nw_job_wait(nw_job* job) {
       if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
     }
     if (*job->spin == job->spin_seq) {
-      std::atomic_thread_fence(std::memory_order_acquire);
-      job->spin = nullptr;
-      job->early = true;   // pending stays set: the next acquire of this job synchronises
-      for (int i = 0; i < job->nouts; ++i)
-        memcpy(job->outs[i].dst, job->hbuf + job->outs[i].off, job->outs[i].bytes);
-      job->nouts = 0;
+      job_deliver_early(job);   // pending stays set: the next acquire synchronises
       return 0;
     }
     job->spin = nullptr;

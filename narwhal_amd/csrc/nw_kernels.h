@@ -296,6 +296,11 @@ struct small_job_t {
   int32_t* status;
   uint64_t* index;
   uint64_t* stamps;        // diagnostics (NW_SMALL_STAMPS): 8 phase times per workgroup, or null
+  // optional (pinned): workgroup w stores done_seq into done_flags[w] (system scope) after
+  // its last status / index write, so the host sees the job finished before its completion
+  // event (a workgroup that stored nothing just leaves the host waiting for the event)
+  uint32_t* done_flags;
+  uint32_t done_seq;
 };
 hipError_t upload_small_consts();
 hipError_t launch_small(const small_job_t& job, hipStream_t stream);

@@ -676,6 +676,9 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
     J.status[sl.m] = status;
     if (J.index) J.index[sl.m] = index;
     __threadfence_system();
+    if (lane == 0 && J.done_flags)
+      __hip_atomic_store(&J.done_flags[blockIdx.x], J.done_seq, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
     stamp(J, ST_END);
     return;
   }
@@ -773,6 +776,11 @@ __global__ __launch_bounds__(256) void k_small(small_job_t J) {
       if (J.index) J.index[m] = index;
       __threadfence_system();
     }
+  }
+  if (lane == 0 && J.done_flags) {   // this workgroup's writes are out (small_job_t)
+    __threadfence_system();
+    __hip_atomic_store(&J.done_flags[blockIdx.x], J.done_seq, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
   }
   stamp(J, ST_END);
 }

@@ -11,7 +11,8 @@ the one tests/test_gpu_batch.py runs in the suite itself), lone batches with the
 gate (NW_BATCH_GATE=1: the kernels queued before the votes are written, chunk flags), and
 lone batches that wait for the launch's completion event instead of the tail's done word
 (NW_BATCH_SPIN=0; the default spin path is the suite's own), also under the injected
-post-launch failure of tests/test_gpu_fused_abort.py."""
+post-launch failure of tests/test_gpu_fused_abort.py; and small jobs that wait for their
+completion event instead of their workgroups' done flags (NW_SMALL_DONE=0)."""
 import os
 import subprocess
 import sys
@@ -33,6 +34,7 @@ GATE = "NW_BATCH_GATE: lone batches launched before their votes are written"
     ("NW_BATCH_GATE", "1", "test_gpu_batch.py", GATE),     # votes written after the launch
     ("NW_BATCH_SPIN", "0", "test_gpu_batch.py", None),     # the completion event only
     ("NW_BATCH_SPIN", "0", "test_gpu_fused_abort.py", None),
+    ("NW_SMALL_DONE", "0", "test_gpu_small.py", None),     # small jobs: the event only
 ])
 def test_inputs_in_device_memory(env, value, test, notice):
     r = subprocess.run([sys.executable, "-u", "-m", "pytest", "-x", "-q", "-s", "-p",
