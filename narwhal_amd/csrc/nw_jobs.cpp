@@ -86,6 +86,10 @@ constexpr int kMaxDev = 64;
 struct DevPool {
   std::mutex m;
   std::vector<nw_job*> free;
+  // jobs released early (outputs delivered from done words / flags) whose launch may still be
+  // finishing: they rejoin `free` once their completion event has fired, so a submit never
+  // blocks on a launch that is counting out while an idle job exists
+  std::vector<nw_job*> retiring;
 };
 DevPool g_pool[kMaxDev];
 
@@ -104,9 +108,27 @@ int job_acquire(int dev, nw_job** out) {
   nw_job* j = nullptr;
   {
     std::lock_guard<std::mutex> g(p.m);
+    if (!p.retiring.empty()) {   // finished early releases rejoin the free list
+      size_t keep = 0;
+      for (nw_job* x : p.retiring) {
+        const hipError_t e = hipEventQuery(x->done);
+        if (e == hipErrorNotReady) {
+          p.retiring[keep++] = x;
+          continue;
+        }
+        if (e != hipSuccess && x->dfz) x->dfz_dirty = true;
+        x->pending = false;
+        x->early = false;
+        p.free.push_back(x);
+      }
+      p.retiring.resize(keep);
+    }
     if (!p.free.empty()) {
       j = p.free.back();
       p.free.pop_back();
+    } else if (!p.retiring.empty()) {   // none idle: the oldest early release (nearly done)
+      j = p.retiring.front();
+      p.retiring.erase(p.retiring.begin());
     }
   }
   if (!j) {
@@ -146,7 +168,8 @@ void job_recycle(nw_job* j) {
   j->spin = nullptr;
   j->small_flags = nullptr;
   std::lock_guard<std::mutex> g(g_pool[j->dev].m);
-  g_pool[j->dev].free.push_back(j);
+  if (j->early && j->pending) g_pool[j->dev].retiring.push_back(j);
+  else g_pool[j->dev].free.push_back(j);
 }
 
 // Fail a submit after work may have been queued: drain the stream, recycle, report.

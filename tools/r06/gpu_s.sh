@@ -3,7 +3,7 @@
 # NW_SMALL_DONE=0, alternating, two pairs.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r06s; mkdir -p $O
+O=${OUT:-gpurun_out/r06s}; mkdir -p $O
 timeout -k 10 900 python -u -m pytest -x -q --timeout 280 --timeout-method thread -m gpu tests/test_gpu_small.py tests/test_gpu_messages.py tests/test_service.py tests/test_gpu_fuzz.py tests/test_gpu_hedge.py tests/test_gpu_small_vram.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 for i in 1 2; do
