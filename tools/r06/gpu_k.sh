@@ -3,7 +3,7 @@
 # batch / strict corpus, each bounded.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r06k; mkdir -p $O
+O=${OUT:-gpurun_out/r06k}; mkdir -p $O
 timeout -k 10 500 python -u tools/fuzz_long.py 30000 150 irregular > $O/fuzz_irregular.json 2> $O/fuzz_irregular.err || { tail -20 $O/fuzz_irregular.err; exit 1; }
 cut -c1-500 $O/fuzz_irregular.json
 timeout -k 10 400 python -u tools/fuzz_long.py 20300 600 batch > $O/fuzz_batch.json 2> $O/fuzz_batch.err || { tail -20 $O/fuzz_batch.err; exit 1; }
