@@ -177,7 +177,11 @@ NW_HD void build_table8(Tab* tab, const ge& P, const fe& d2) {
     for (int st = 0; st < 7; ++st) {
       const bool dbl = st == 0 || st == 2 || st == 3 || st == 5;
       const int dst = st == 0 ? 1 : st == 1 ? 2 : st == 2 ? 5 : st == 3 ? 3 : st == 4 ? 4 : st == 5 ? 7 : 6;
-      if (st == 3 || st == 5) ge_from_cached_not(cur, tab[st == 3 ? 1 : 3]);
+      if (st == 3 || st == 5) {   // (the entry read back in whatever form the table holds)
+        ge_cached back;
+        tab_get(tab, st == 3 ? 1 : 3, back);
+        ge_from_cached_not(cur, back);
+      }
       if (st == 6) ge_cached_cneg(c1, true);
       if (dbl) ge_dbl(cur, cur, true);
       else ge_add_any(cur, cur, c1, true, true);
