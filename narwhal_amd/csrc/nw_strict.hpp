@@ -156,7 +156,7 @@ NW_HD void tab_get(const ge_cached_pk* t, int j, ge_cached& e) {
 }
 
 #ifndef NW_TAB_DBL
-#define NW_TAB_DBL 0   // 1: four doublings + three mixed additions (measured 0.5 % slower, r02b)
+#define NW_TAB_DBL 0   // 1: four doublings + three mixed additions (0.5 % / 0.9 % slower, r02b / r06w)
 #endif
 
 template <class Tab>
