@@ -885,6 +885,7 @@ def run_service_latency(args, rank, world, N: int, cache=None):
         total = max(1, int(rate * seconds))
         lat = np.zeros(total)
         bad = [0]
+        bad_first = []   # (request, got, expected) of the first mismatches
         done = loop.create_future()
         left = [total]
 
@@ -893,6 +894,8 @@ def run_service_latency(args, rank, world, N: int, cache=None):
                 lat[i] = loop.time() - t_arr
                 if f.result() != expect[i % uniq]:
                     bad[0] += 1
+                    if len(bad_first) < 10:
+                        bad_first.append([i, list(f.result()), list(expect[i % uniq])])
                 left[0] -= 1
                 if left[0] == 0:
                     done.set_result(None)
@@ -918,7 +921,8 @@ def run_service_latency(args, rank, world, N: int, cache=None):
                 "p99_ms": float(np.percentile(lat, 99) * 1e3),
                 "max_ms": float(lat.max() * 1e3), "jobs": jobs,
                 "certs_per_job": total / max(1, jobs),
-                "parity": "ok" if bad[0] == 0 else "FAIL"}
+                "parity": "ok" if bad[0] == 0 else "FAIL",
+                **({"mismatches": bad[0], "first_mismatches": bad_first} if bad[0] else {})}
 
     rates = [float(x) for x in args.service_rates.split(",") if x]
     loads = [native_load(r, min(args.service_seconds, args.service_max_certs / r)) for r in rates]
