@@ -57,7 +57,6 @@ struct nw_job {
   // out (the job is synchronised before its next use, job_acquire)
   volatile uint32_t* spin = nullptr;
   uint32_t spin_seq = 0;
-  uint32_t dseq = 0;
   bool early = false;
   // small jobs (NW_SMALL_DONE): one done flag per workgroup in the pinned buffer (host view)
   volatile uint32_t* small_flags = nullptr;
@@ -255,6 +254,14 @@ bool test_fuse_abort() {
   }()};
   if (left.load(std::memory_order_relaxed) <= 0) return false;
   return left.fetch_sub(1, std::memory_order_relaxed) > 0;
+}
+// Sequence numbers of done words / flags: unique across every job of the process (a job's own
+// counter would repeat values another job's stale flags still hold), never 0.
+uint32_t next_done_seq() {
+  static std::atomic<uint32_t> seq{0};
+  uint32_t v = seq.fetch_add(1, std::memory_order_relaxed) + 1;
+  if (v == 0) v = seq.fetch_add(1, std::memory_order_relaxed) + 1;
+  return v;
 }
 bool small_done() {   // on unless NW_SMALL_DONE=0
   static const bool on = [] {
@@ -597,8 +604,7 @@ int submit_batch(int dev, const uint8_t* digests, const uint8_t* pks, const uint
   uint32_t* done = nullptr;
   uint32_t dseq = 0;
   if (out_direct && batch_spin()) {
-    dseq = ++j->dseq;
-    if (dseq == 0) dseq = j->dseq = 1;
+    dseq = next_done_seq();
     volatile uint32_t* dh = reinterpret_cast<volatile uint32_t*>(j->hbuf + o_dn);
     *dh = dseq - 1;   // anything but dseq
     done = reinterpret_cast<uint32_t*>(j->hdev + o_dn);
@@ -936,8 +942,11 @@ int submit_small(int dev, uint32_t kind, const nw_committee* com, const nw_certi
   J.index = kind == nw::kSmallVotes ? nullptr : reinterpret_cast<uint64_t*>(j->hdev + o_ix);
   uint32_t dseq = 0;
   if (small_done() && J.slots_per_wg == S_wg) {
-    dseq = ++j->dseq;
-    if (dseq == 0) dseq = j->dseq = 1;
+    dseq = next_done_seq();
+    // the flag words start at 0 (never a sequence number): a staging buffer reallocated from
+    // another job's freed pinned memory may hold that job's old flags, and its sequence may
+    // equal ours (profiles/r06aa: rare stale verdicts before this line)
+    memset(H + o_df, 0, 4 * nwg_all);
     J.done_flags = reinterpret_cast<uint32_t*>(j->hdev + o_df);
     J.done_seq = dseq;
   }
