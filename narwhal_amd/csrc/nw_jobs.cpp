@@ -255,6 +255,15 @@ bool test_fuse_abort() {
   if (left.load(std::memory_order_relaxed) <= 0) return false;
   return left.fetch_sub(1, std::memory_order_relaxed) > 0;
 }
+bool test_stale_flags() {
+  static const bool on = [] {
+    const char* e = getenv("NW_TEST_STALE_FLAGS");
+    const bool v = e && *e == '1';
+    if (v) fprintf(stderr, "[narwhal_amd] NW_TEST_STALE_FLAGS: small-job flag words poisoned\n");
+    return v;
+  }();
+  return on;
+}
 // Sequence numbers of done words / flags: unique across every job of the process (a job's own
 // counter would repeat values another job's stale flags still hold), never 0.
 uint32_t next_done_seq() {
@@ -946,7 +955,15 @@ int submit_small(int dev, uint32_t kind, const nw_committee* com, const nw_certi
     // the flag words start at 0 (never a sequence number): a staging buffer reallocated from
     // another job's freed pinned memory may hold that job's old flags, and its sequence may
     // equal ours (profiles/r06aa: rare stale verdicts before this line)
+    if (test_stale_flags()) {
+      // test hook (NW_TEST_STALE_FLAGS=1): the buffer arrives holding this very sequence in
+      // every flag word, the worst a recycled buffer can hold; the memset below must clear it
+      uint32_t* f = reinterpret_cast<uint32_t*>(H + o_df);
+      for (uint64_t w = 0; w < nwg_all; ++w) f[w] = dseq;
+    }
+#ifndef NW_NO_FLAG_CLEAR   // negative control build only (tools/r06/gpu_ae.sh)
     memset(H + o_df, 0, 4 * nwg_all);
+#endif
     J.done_flags = reinterpret_cast<uint32_t*>(j->hdev + o_df);
     J.done_seq = dseq;
   }

@@ -12,7 +12,9 @@ gate (NW_BATCH_GATE=1: the kernels queued before the votes are written, chunk fl
 lone batches that wait for the launch's completion event instead of the tail's done word
 (NW_BATCH_SPIN=0; the default spin path is the suite's own), also under the injected
 post-launch failure of tests/test_gpu_fused_abort.py; and small jobs that wait for their
-completion event instead of their workgroups' done flags (NW_SMALL_DONE=0)."""
+completion event instead of their workgroups' done flags (NW_SMALL_DONE=0); and small jobs
+whose flag words arrive holding the job's own sequence number (NW_TEST_STALE_FLAGS=1, what a
+recycled pinned buffer can hold: the host must clear them before the launch, profiles/r06aa)."""
 import os
 import subprocess
 import sys
@@ -26,6 +28,7 @@ NOTICE = "NW_SMALL_VRAM: small jobs' inputs written into host-mapped fine-graine
 
 
 GATE = "NW_BATCH_GATE: lone batches launched before their votes are written"
+STALE = "NW_TEST_STALE_FLAGS: small-job flag words poisoned"
 
 
 @pytest.mark.parametrize("env,value,test,notice", [
@@ -35,6 +38,7 @@ GATE = "NW_BATCH_GATE: lone batches launched before their votes are written"
     ("NW_BATCH_SPIN", "0", "test_gpu_batch.py", None),     # the completion event only
     ("NW_BATCH_SPIN", "0", "test_gpu_fused_abort.py", None),
     ("NW_SMALL_DONE", "0", "test_gpu_small.py", None),     # small jobs: the event only
+    ("NW_TEST_STALE_FLAGS", "1", "test_gpu_small.py", STALE),   # poisoned flag words
 ])
 def test_inputs_in_device_memory(env, value, test, notice):
     r = subprocess.run([sys.executable, "-u", "-m", "pytest", "-x", "-q", "-s", "-p",
@@ -46,4 +50,4 @@ def test_inputs_in_device_memory(env, value, test, notice):
     if notice:
         assert notice in out
     else:
-        assert NOTICE not in out and GATE not in out
+        assert NOTICE not in out and GATE not in out and STALE not in out
