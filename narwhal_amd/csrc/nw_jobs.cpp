@@ -310,7 +310,12 @@ bool batch_stamps() {
   }();
   return on;
 }
-constexpr uint64_t kGateChunk = 1024;   // votes per input-gate flag (a multiple of 64)
+// votes per input-gate flag, a multiple of 64 (NW_GATE_CHUNK=k, A/B hook, rounded up to 64)
+const uint64_t kGateChunk = [] {
+  const char* e = getenv("NW_GATE_CHUNK");
+  const long v = e && *e ? atol(e) : 1024L;
+  return (uint64_t)(v < 64 ? 64 : (v + 63) / 64 * 64);
+}();
 bool batch_gate() {
   static const bool on = [] {
     const char* e = getenv("NW_BATCH_GATE");
