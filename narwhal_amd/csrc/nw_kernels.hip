@@ -120,6 +120,7 @@ __device__ __forceinline__ const T* opaque_ptr(const T* p) {
 
 // strict_verify_core's inputs for item i, fetched from global memory when needed.
 struct strict_src_global {
+  static constexpr bool kPre = false;
   const uint32_t* pk;    // 8 words
   const uint32_t* sig;   // 16 words: R || s
   const uint32_t* msg;   // 8 words
@@ -151,6 +152,26 @@ struct strict_src_global {
     sc_reduce512(k, hx);
 #pragma unroll
     for (int j = 0; j < 8; ++j) kw[j] = k.w[j];
+  }
+};
+
+// The same inputs with A's and R's x already decompressed (k_strict_triage): x limb k of
+// point pt (0 = A, 1 = R) of survivor q at xs[(10 pt + k) cap + q]. y is the encoding's own
+// (fe_frombytes), Z = 1, T = x y: exactly the point ge_frombytes returned.
+struct strict_src_pre : strict_src_global {
+  static constexpr bool kPre = true;
+  const uint32_t* xs;
+  uint64_t cap, q;
+  __device__ bool point(int pt, ge& P) const {
+    uint32_t w[8];
+    if (pt) R(w); else A(w);
+    fe_frombytes(P.Y, w);
+    const uint32_t* x = opaque_ptr(xs) + (uint64_t)(10 * pt) * cap + q;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) P.X.v[k] = x[(uint64_t)k * cap];
+    fe_1(P.Z);
+    fe_mul(P.T, P.X, P.Y);
+    return true;
   }
 };
 
@@ -306,6 +327,120 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
     if (list) continue;
     const uint64_t mask = __ballot(active && st == NW_OK);
     if ((threadIdx.x & 63) == 0 && gi < n) bitmap[gi >> 6] = mask;
+  }
+}
+
+// ---- config 4's strict verification in two passes (NW_STRICT_TRIAGE, default on) ----
+// Every check before the equation (s's high bits and canonical form, A's and R's
+// decompression and small order) needs only the two square roots, ~15 % of a verification;
+// an item that fails one of them (7 of the 12 invalid classes of the mixed corpus, ~6.5 % of
+// its items) still ran the whole ladder in k_verify_strict, whose lanes all take the same
+// path. k_strict_triage runs the checks for a slice of items, one lane per item, writes the
+// verdict of every item that fails one (same order as strict_verify_core: crypto/src/lib.rs
+// 201-202, then dalek's verify_strict), and appends the others to a list with the x of A and
+// R; k_verify_strict_pre runs strict_verify_core on the list, loading those points instead
+// of decompressing them (strict_src_pre). Statuses are the same codes for every item.
+__global__ __launch_bounds__(256) void k_strict_triage(
+    const uint32_t* __restrict__ msgs, uint32_t msg_stride_words, const uint32_t* __restrict__ pks,
+    const uint32_t* __restrict__ sigs, uint64_t i0, uint64_t ns, int32_t* __restrict__ status,
+    uint32_t* __restrict__ xs, uint64_t cap, uint32_t* __restrict__ list,
+    uint32_t* __restrict__ count) {
+  (void)msgs;
+  (void)msg_stride_words;
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = j < ns;
+  const uint64_t i = i0 + (active ? j : 0);
+  const curve_consts& K = g_consts.sk.k;   // as strict_verify_core
+  uint32_t Sw[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) Sw[t] = sigs[16 * i + 8 + t];
+  const bool s_high = (Sw[7] >> 29) != 0;
+  sc s;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) s.w[t] = Sw[t];
+  const bool s_canon = sc_is_canonical(s);
+  fe xa, xr;
+  bool okA, okR, smallA, smallR;
+  {
+    uint32_t w[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) w[t] = pks[8 * i + t];
+    ge P;
+    okA = ge_frombytes(P, w, K);
+    smallA = small_order_by_y(P.Y, g_consts.sk.small_y);
+    xa = P.X;
+  }
+  {
+    uint32_t w[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) w[t] = sigs[16 * i + t];
+    ge P;
+    okR = ge_frombytes(P, w, K);
+    smallR = small_order_by_y(P.Y, g_consts.sk.small_y);
+    xr = P.X;
+  }
+  const int st = s_high ? NW_ERR_S_HIGH_BITS : !okA ? NW_ERR_A_DECODE
+               : !s_canon ? NW_ERR_S_NONCANONICAL : !okR ? NW_ERR_R_DECODE
+               : smallR ? NW_ERR_R_SMALL_ORDER : smallA ? NW_ERR_A_SMALL_ORDER : NW_OK;
+  if (active && st != NW_OK) status[i] = st;
+  const bool keep = active && st == NW_OK;
+  const uint64_t m = __ballot(keep);
+  if (m == 0) return;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t rank = (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+  const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(count, (uint32_t)__builtin_popcountll(m));
+  base = (uint32_t)__shfl((int)base, (int)leader);
+  if (!keep) return;
+  const uint64_t pos = (uint64_t)base + rank;
+  list[pos] = (uint32_t)j;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    xs[(uint64_t)k * cap + pos] = xa.v[k];
+    xs[(uint64_t)(10 + k) * cap + pos] = xr.v[k];
+  }
+}
+
+// The list's items (persistent, as k_verify_strict): strict_verify_core on the points
+// k_strict_triage decompressed; *count is read on the device.
+__global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict_pre(
+    const uint32_t* __restrict__ msgs, uint32_t msg_stride_words, const uint32_t* __restrict__ pks,
+    const uint32_t* __restrict__ sigs, uint64_t i0, const uint32_t* __restrict__ list,
+    const uint32_t* __restrict__ count, const uint32_t* __restrict__ xs, uint64_t cap,
+    int32_t* __restrict__ status, ge_cached_pk* __restrict__ tabs,
+    const ge_niels_pad* __restrict__ btw) {
+  const uint64_t n = *count;
+#if NW_BWIN == 8
+  __shared__ ge_niels s_btab[129];
+  __shared__ ge_niels s_b128[129];
+  load_table(s_btab, g_consts.btab);
+  load_table(s_b128, g_consts.b128);
+  __syncthreads();
+  const btab_pair bt{s_btab, s_b128};
+  (void)btw;
+#else
+  const btab_wide bt{btw, bdigits<NW_BWIN>::ENTRIES};
+#endif
+  ge_cached_pk* tabA = tabs + 16 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  ge_cached_pk* tabR = tabA + 8;
+#pragma unroll 1
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n;
+       base += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t q0 = base + threadIdx.x;
+    const bool active = q0 < n;
+    const uint64_t q = active ? q0 : n - 1;
+    const uint64_t i = i0 + list[q];
+    const strict_src_pre src{{pks + 8 * i, sigs + 16 * i, msgs + (uint64_t)msg_stride_words * i},
+                             xs, cap, q};
+#if NW_STRICT_PF && NW_BWIN != 8
+    const int st = strict_verify_core<NW_BWIN>(src, g_consts.sk, bt, tabA, tabR, WaveMax{},
+                                               pf_lds{(uint32_t)__builtin_amdgcn_readfirstlane(
+                                                   threadIdx.x >> 6)});
+#else
+    const int st = strict_verify_core<NW_BWIN>(src, g_consts.sk, bt, tabA, tabR, WaveMax{});
+#endif
+    if (active) status[i] = st;
   }
 }
 
@@ -879,7 +1014,21 @@ static unsigned strict_grid() {
 constexpr uint64_t kKeyedSliceMax = 1ull << 22;
 // (sized for 160-byte entries; the packed ones use 128 of each 160)
 static size_t strict_tabs_bytes() { return (size_t)strict_grid() * 256 * 16 * sizeof(ge_cached); }
-size_t strict_workspace_bytes() { return strict_tabs_bytes() + 4 * kKeyedSliceMax + 256; }
+// The two-pass path's slice (k_strict_triage / k_verify_strict_pre): x of A and R (20 words)
+// and a list entry per item, after the keyed path's region. Large, so that the second pass's
+// last, partly filled round over the resident lanes is a small share of the slice.
+constexpr uint64_t kTriageSlice = 1ull << 23;
+static size_t strict_keyed_region_bytes() { return 4 * kKeyedSliceMax + 256; }
+size_t strict_workspace_bytes() {
+  return strict_tabs_bytes() + strict_keyed_region_bytes() + 84 * kTriageSlice + 256;
+}
+bool strict_triage_on() {   // NW_STRICT_TRIAGE=0: one pass (k_verify_strict), A/B hook
+  static const bool v = [] {
+    const char* e = getenv("NW_STRICT_TRIAGE");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
 
 hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
                                 const uint32_t* pks, const uint32_t* sigs, uint64_t n,
@@ -894,6 +1043,32 @@ hipError_t launch_verify_strict(const uint32_t* msgs, uint32_t msg_stride_words,
   if (eb == hipSuccess && kt.vote_key) eb = btab_for_current_device(1, &bcomb);
   if (eb != hipSuccess) return eb;
   const char* kf = getenv("NW_STRICT_KEYED_FAST");
+  if (!kt.vote_key && strict_triage_on()) {
+    char* const ws = static_cast<char*>(workspace);
+    char* const tri = ws + strict_tabs_bytes() + strict_keyed_region_bytes();
+    uint32_t* const xs = reinterpret_cast<uint32_t*>(tri);
+    uint32_t* const list = xs + 20 * kTriageSlice;
+    uint32_t* const count = list + kTriageSlice;
+    // equal slices of at most kTriageSlice items
+    const uint64_t nsl = (n + kTriageSlice - 1) / kTriageSlice;
+    const uint64_t per = (n + nsl - 1) / nsl;
+    for (uint64_t i0 = 0; i0 < n; i0 += per) {
+      const uint64_t ns = std::min(per, n - i0);
+      hipError_t e = hipMemsetAsync(count, 0, 4, stream);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(k_strict_triage, dim3(grid_for(ns, 256)), dim3(256), 0, stream, msgs,
+                         msg_stride_words, pks, sigs, i0, ns, status, xs, kTriageSlice, list,
+                         count);
+      hipLaunchKernelGGL(k_verify_strict_pre,
+                         dim3(std::min<uint64_t>(strict_grid(), grid_for(ns, 256))), dim3(256),
+                         0, stream, msgs, msg_stride_words, pks, sigs, i0, list, count, xs,
+                         kTriageSlice, status, static_cast<ge_cached_pk*>(workspace), btw);
+    }
+    if (bitmap)
+      hipLaunchKernelGGL(k_status_bitmap, dim3(grid_for(n, 256)), dim3(256), 0, stream, status,
+                         n, bitmap);
+    return hipGetLastError();
+  }
   if (!kt.vote_key) {
     hipLaunchKernelGGL(k_verify_strict<false>, dim3(grid), dim3(256), 0,
                        stream, msgs,

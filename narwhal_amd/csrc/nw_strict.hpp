@@ -210,6 +210,7 @@ NW_HD void build_table8(Tab* tab, const ge& P, const fe& d2) {
 // key, of R and of s; k(x) gives k = H(R || A || M) mod l. The kernel's source reloads
 // from global memory; the host self-check's returns copies of its arrays.
 struct strict_src_arrays {
+  static constexpr bool kPre = false;   // A and R decompressed here (see strict_verify_core)
   const uint32_t* a;
   const uint32_t* r;
   const uint32_t* s;
@@ -655,10 +656,16 @@ NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab&
   bool okA = false, smallA = false, okR = false, smallR = false;
 #pragma unroll 1
   for (int pt = 0; pt < 2; ++pt) {
-    uint32_t x[8];
-    if (pt) src.R(x); else src.A(x);
     ge P;
-    const bool ok = ge_frombytes(P, x, K.k);
+    bool ok;
+    if constexpr (Src::kPre) {
+      // the point was decompressed by an earlier pass (k_strict_triage): the same limbs
+      ok = src.point(pt, P);
+    } else {
+      uint32_t x[8];
+      if (pt) src.R(x); else src.A(x);
+      ok = ge_frombytes(P, x, K.k);
+    }
     const bool small = small_order_by_y(P.Y, K.small_y);
     if (pt == 0) { okA = ok; smallA = small; } else { okR = ok; smallR = small; }
     if (NW_STRICT_STOP == 1) continue;
