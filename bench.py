@@ -1404,7 +1404,9 @@ def main():
                          "traffic": traffic,
                          "traffic_unit": "HBM bytes per launch", "traffic_source": tsrc,
                          "algorithmic_bytes": r["n"] * (32 + 32 + 64 + 4) + r["n"] / 8,
-                         "kernel": "k_verify_strict", "kernel_ms": r["kernel_ms"],
+                         "kernel": ("k_verify_strict" if os.environ.get("NW_STRICT_TRIAGE") == "0"
+                                    else "k_strict_triage + k_verify_strict_pre + k_status_bitmap"),
+                         "kernel_ms": r["kernel_ms"],
                          "work_per_unit": f"{MAC_PER_STRICT_VERIFY} MAC/verify (SURVEY 8d)",
                          "issue_peak": issue_peak, "issue_unit": "verifies/s",
                          "issue_frac": (r["n"] / (r["kernel_ms"] * 1e-3) / issue_peak

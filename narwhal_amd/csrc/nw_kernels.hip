@@ -1015,9 +1015,10 @@ constexpr uint64_t kKeyedSliceMax = 1ull << 22;
 // (sized for 160-byte entries; the packed ones use 128 of each 160)
 static size_t strict_tabs_bytes() { return (size_t)strict_grid() * 256 * 16 * sizeof(ge_cached); }
 // The two-pass path's slice (k_strict_triage / k_verify_strict_pre): x of A and R (20 words)
-// and a list entry per item, after the keyed path's region. Large, so that the second pass's
-// last, partly filled round over the resident lanes is a small share of the slice.
-constexpr uint64_t kTriageSlice = 1ull << 23;
+// and a list entry per item, after the keyed path's region (1.4 GB, once per device). Large:
+// config 4's 12.5M items are one slice, so the second pass's last, partly filled round over
+// the resident lanes comes once per launch.
+constexpr uint64_t kTriageSlice = 1ull << 24;
 static size_t strict_keyed_region_bytes() { return 4 * kKeyedSliceMax + 256; }
 size_t strict_workspace_bytes() {
   return strict_tabs_bytes() + strict_keyed_region_bytes() + 84 * kTriageSlice + 256;

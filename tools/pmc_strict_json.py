@@ -4,7 +4,9 @@
 
     python tools/pmc_strict_json.py MIXDIR STALLDIR OUTDIR [--items N]
 
-Counters are summed over the k_verify_strict dispatches of the one-step bench run
+Counters are summed over the config-4 launch's dispatches of the one-step bench run (the
+two-pass path's k_strict_triage + k_verify_strict_pre + k_status_bitmap, or the one-pass
+k_verify_strict)
 (--items-per-gpu N, default 4,194,304). Lane-ops = instructions x 64 / items; the issue
 budget prices INT64 (v_mad_u64_u32, 64-bit shifts), INT32 (half-rate 32-bit) and the rest
 at the microbenchmarked rates (profiles/r01_ubench_valu_4wps.txt).
@@ -18,11 +20,14 @@ import sys
 RATES = {"int64": 32.39, "int32": 36.0, "other": 63.0}
 
 
-def collect(d, key="k_verify_strict"):
+STRICT = ("k_verify_strict", "k_strict_triage", "k_status_bitmap")
+
+
+def collect(d, keys=STRICT):
     agg = {}
     for f in glob.glob(os.path.join(d, "**", "p_counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if key in r["Kernel_Name"]:
+            if any(k in r["Kernel_Name"] for k in keys):
                 agg[r["Counter_Name"]] = agg.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     return agg
 
@@ -38,7 +43,8 @@ def main():
         i32 = m.get("SQ_INSTS_VALU_INT32", 0) * 64 / items
         lane = {"valu": valu, "int64": i64, "int32": i32, "other": valu - i64 - i32}
         ns = sum(lane[k] / (RATES[k] * 1e12) for k in RATES) * 1e9
-        json.dump({"kernel": "k_verify_strict", "items": items, "counters": m,
+        json.dump({"kernel": "config-4 launch (" + " + ".join(STRICT) + ")", "items": items,
+                   "counters": m,
                    "per_verify_lane_ops": lane,
                    "issue_rates_T_lane_ops_s": {**RATES,
                                                 "source": "profiles/r01_ubench_valu_4wps.txt"},
