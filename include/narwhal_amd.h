@@ -92,7 +92,7 @@ int nw_synchronize(void);
  * = 940 MB per key, 47 GB at 50 authorities; larger ones: 16-bit combs, 16 x 32,769 entries
  * = 67 MB per key, 6.7 GB at 100 authorities; NW_KEY_WIDTH=16 forces the small ones; built
  * by the first Header / Vote / Certificate call with that committee, ~0.4 s at N = 100) and
- * the strict workspace (~0.5 GB): ~21 GB in all at N = 100. Returns 0, or
+ * the strict workspace (~1.9 GB): ~22 GB in all at N = 100. Returns 0, or
  * NW_E_OUT_OF_MEMORY when a table does not fit; without the keyed comb or a committee's key
  * tables, Header / Vote / Certificate calls still run, unkeyed (the strict ladder and
  * per-certificate verify_batch: same verdicts, lower throughput). Optional: keeps the first
