@@ -340,7 +340,10 @@ __global__ __launch_bounds__(256, NW_STRICT_WAVES) void k_verify_strict(const ui
 // 201-202, then dalek's verify_strict), and appends the others to a list with the x of A and
 // R; k_verify_strict_pre runs strict_verify_core on the list, loading those points instead
 // of decompressing them (strict_src_pre). Statuses are the same codes for every item.
-__global__ __launch_bounds__(256) void k_strict_triage(
+#ifndef NW_TRIAGE_WAVES
+#define NW_TRIAGE_WAVES 4   // waves per SIMD (129 VGPRs unbounded: 3)
+#endif
+__global__ __launch_bounds__(256, NW_TRIAGE_WAVES) void k_strict_triage(
     const uint32_t* __restrict__ msgs, uint32_t msg_stride_words, const uint32_t* __restrict__ pks,
     const uint32_t* __restrict__ sigs, uint64_t i0, uint64_t ns, int32_t* __restrict__ status,
     uint32_t* __restrict__ xs, uint64_t cap, uint32_t* __restrict__ list,
@@ -359,25 +362,19 @@ __global__ __launch_bounds__(256) void k_strict_triage(
 #pragma unroll
   for (int t = 0; t < 8; ++t) s.w[t] = Sw[t];
   const bool s_canon = sc_is_canonical(s);
+  // A, then R, in one rolled loop (one copy of the square-root chain: registers, code size)
   fe xa, xr;
-  bool okA, okR, smallA, smallR;
-  {
+  bool okA = false, okR = false, smallA = false, smallR = false;
+#pragma unroll 1
+  for (int pt = 0; pt < 2; ++pt) {
+    const uint32_t* src = opaque_ptr(pt ? sigs + 16 * i : pks + 8 * i);
     uint32_t w[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) w[t] = pks[8 * i + t];
+    for (int t = 0; t < 8; ++t) w[t] = src[t];
     ge P;
-    okA = ge_frombytes(P, w, K);
-    smallA = small_order_by_y(P.Y, g_consts.sk.small_y);
-    xa = P.X;
-  }
-  {
-    uint32_t w[8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) w[t] = sigs[16 * i + t];
-    ge P;
-    okR = ge_frombytes(P, w, K);
-    smallR = small_order_by_y(P.Y, g_consts.sk.small_y);
-    xr = P.X;
+    const bool ok = ge_frombytes(P, w, K);
+    const bool small = small_order_by_y(P.Y, g_consts.sk.small_y);
+    if (pt == 0) { okA = ok; smallA = small; xa = P.X; } else { okR = ok; smallR = small; xr = P.X; }
   }
   const int st = s_high ? NW_ERR_S_HIGH_BITS : !okA ? NW_ERR_A_DECODE
                : !s_canon ? NW_ERR_S_NONCANONICAL : !okR ? NW_ERR_R_DECODE
