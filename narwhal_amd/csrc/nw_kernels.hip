@@ -353,32 +353,9 @@ __global__ __launch_bounds__(256, NW_TRIAGE_WAVES) void k_strict_triage(
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = j < ns;
   const uint64_t i = i0 + (active ? j : 0);
-  const curve_consts& K = g_consts.sk.k;   // as strict_verify_core
-  uint32_t Sw[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t) Sw[t] = sigs[16 * i + 8 + t];
-  const bool s_high = (Sw[7] >> 29) != 0;
-  sc s;
-#pragma unroll
-  for (int t = 0; t < 8; ++t) s.w[t] = Sw[t];
-  const bool s_canon = sc_is_canonical(s);
-  // A, then R, in one rolled loop (one copy of the square-root chain: registers, code size)
+  const strict_src_global src{pks + 8 * i, sigs + 16 * i, nullptr};
   fe xa, xr;
-  bool okA = false, okR = false, smallA = false, smallR = false;
-#pragma unroll 1
-  for (int pt = 0; pt < 2; ++pt) {
-    const uint32_t* src = opaque_ptr(pt ? sigs + 16 * i : pks + 8 * i);
-    uint32_t w[8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) w[t] = src[t];
-    ge P;
-    const bool ok = ge_frombytes(P, w, K);
-    const bool small = small_order_by_y(P.Y, g_consts.sk.small_y);
-    if (pt == 0) { okA = ok; smallA = small; xa = P.X; } else { okR = ok; smallR = small; xr = P.X; }
-  }
-  const int st = s_high ? NW_ERR_S_HIGH_BITS : !okA ? NW_ERR_A_DECODE
-               : !s_canon ? NW_ERR_S_NONCANONICAL : !okR ? NW_ERR_R_DECODE
-               : smallR ? NW_ERR_R_SMALL_ORDER : smallA ? NW_ERR_A_SMALL_ORDER : NW_OK;
+  const int st = strict_triage(src, g_consts.sk, xa, xr);
   if (active && st != NW_OK) status[i] = st;
   const bool keep = active && st == NW_OK;
   const uint64_t m = __ballot(keep);

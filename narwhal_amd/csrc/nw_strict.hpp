@@ -645,6 +645,36 @@ NW_HD int strict_keyed_comb(const Src& src, const strict_consts& K, const BComb&
 #ifndef NW_ADD_NEGC
 #define NW_ADD_NEGC 1
 #endif
+// The checks before the equation, as k_strict_triage runs them (config 4 in two passes,
+// nw_kernels.hip): s's high bits and canonical form, A's and R's decompression and small
+// order, in strict_verify_core's order. Returns the status of an item that fails one of
+// them, NW_OK otherwise; xa / xr get the x of A and R (the rest of each point is its
+// encoding's y, Z = 1 and T = x y: exactly what ge_frombytes returned).
+template <class Src>
+NW_HD int strict_triage(const Src& src, const strict_consts& K, fe& xa, fe& xr) {
+  uint32_t Sw[8];
+  src.S(Sw);
+  const bool s_high = (Sw[7] >> 29) != 0;
+  sc s;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) s.w[t] = Sw[t];
+  const bool s_canon = sc_is_canonical(s);
+  bool okA = false, okR = false, smallA = false, smallR = false;
+  // A, then R, in one rolled loop (one copy of the square-root chain: registers, code size)
+#pragma unroll 1
+  for (int pt = 0; pt < 2; ++pt) {
+    uint32_t w[8];
+    if (pt) src.R(w); else src.A(w);
+    ge P;
+    const bool ok = ge_frombytes(P, w, K.k);
+    const bool small = small_order_by_y(P.Y, K.small_y);
+    if (pt == 0) { okA = ok; smallA = small; xa = P.X; } else { okR = ok; smallR = small; xr = P.X; }
+  }
+  return s_high ? NW_ERR_S_HIGH_BITS : !okA ? NW_ERR_A_DECODE
+       : !s_canon ? NW_ERR_S_NONCANONICAL : !okR ? NW_ERR_R_DECODE
+       : smallR ? NW_ERR_R_SMALL_ORDER : smallA ? NW_ERR_A_SMALL_ORDER : NW_OK;
+}
+
 template <int BW, class BTab, class Src, class WaveMax, class PF = pf_none, class Tab = ge_cached>
 NW_HD int strict_verify_core(const Src& src, const strict_consts& K, const BTab& bt,
                              Tab* tabA, Tab* tabR,

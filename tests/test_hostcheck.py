@@ -31,7 +31,8 @@ def hc():
     _build()
     lib = ctypes.CDLL(LIB)
     for f in ("hc_decompress", "hc_is_small_order", "hc_dsm", "hc_verify_strict",
-              "hc_scalar_canonical", "hc_half_split", "hc_verify_strict_half"):
+              "hc_scalar_canonical", "hc_half_split", "hc_verify_strict_half",
+              "hc_verify_strict_twopass"):
         getattr(lib, f).restype = ctypes.c_int
     return lib
 
@@ -316,3 +317,30 @@ def test_strict_half_random_and_tampered(hc):
         want = O.verify_strict(m, pk, bytes(sig))
         for bw in (16, 8, 20, 24, -24):   # -24: packed per-lane table entries
             assert hc.hc_verify_strict_half(_b(pk), _b(bytes(sig)), _b(k), bw) == want
+
+
+@pytest.mark.parametrize("bw", [-16, -24])
+def test_strict_twopass_edge_corpus(hc, golden, bw):
+    """Config 4 in two passes (k_strict_triage, then k_verify_strict_pre on the points the
+    triage stored): the shared strict_triage + strict_verify_core over the stored x give the
+    golden status of every edge-corpus item, as the one-pass core does."""
+    for it in golden["edge_corpus"]["items"]:
+        m, pk, sig = (bytes.fromhex(it[k]) for k in ("msg", "pk", "sig"))
+        k = O.hram(sig[:32], pk, m)
+        assert hc.hc_verify_strict_twopass(_b(pk), _b(sig), _b(k), bw) == it["status"], it["class"]
+
+
+def test_strict_twopass_random_and_tampered(hc):
+    rng = np.random.Generator(np.random.PCG64(15))
+    for i in range(90):
+        pk, sk = O.keypair_from_seed(rng.bytes(32))
+        m = rng.bytes(32)
+        sig = bytearray(O.sign(sk, m))
+        if i % 3 == 1:
+            sig[32 + int(rng.integers(0, 31))] ^= 1 << int(rng.integers(0, 8))
+        elif i % 3 == 2:
+            sig[int(rng.integers(0, 32))] ^= 1 << int(rng.integers(0, 8))
+        k = O.hram(bytes(sig[:32]), pk, m)
+        want = O.verify_strict(m, pk, bytes(sig))
+        assert hc.hc_verify_strict_twopass(_b(pk), _b(bytes(sig)), _b(k), -24) == want
+        assert hc.hc_verify_strict_half(_b(pk), _b(bytes(sig)), _b(k), -24) == want

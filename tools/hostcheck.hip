@@ -151,6 +151,38 @@ int hc_verify_strict_half(const uint8_t pk[32], const uint8_t sig[64], const uin
   return strict_verify_core<16>(src, SK, btab_wide{BTW, BTW_N}, ta, tr, id);
 }
 
+// Config 4 in two passes, on the host: strict_triage (k_strict_triage's checks), then, for an
+// item that passes them, strict_verify_core on the stored x of A and R (the kPre source, as
+// k_verify_strict_pre's strict_src_pre) with B windows of |bw| bits and packed tables as
+// hc_verify_strict_half(bw < 0). Must equal the one-pass status for every input.
+struct src_arrays_pre : strict_src_arrays {
+  static constexpr bool kPre = true;
+  fe xa, xr;
+  bool point(int pt, ge& P) const {
+    uint32_t w[8];
+    if (pt) R(w); else A(w);
+    fe_frombytes(P.Y, w);
+    P.X = pt ? xr : xa;
+    fe_1(P.Z);
+    fe_mul(P.T, P.X, P.Y);
+    return true;
+  }
+};
+int hc_verify_strict_twopass(const uint8_t pk[32], const uint8_t sig[64], const uint8_t k32[32],
+                             int bw) {
+  init();
+  uint32_t Aw[8], Rw[8], Sw[8], kw[8];
+  load8(Aw, pk); load8(Rw, sig); load8(Sw, sig + 32); load8(kw, k32);
+  src_arrays_pre src{};
+  src.a = Aw; src.r = Rw; src.s = Sw; src.k = kw;
+  const int st = strict_triage(static_cast<const strict_src_arrays&>(src), SK, src.xa, src.xr);
+  if (st != NW_OK) return st;
+  ge_cached_pk pa[8], pr[8];
+  auto id = [](int w) { return w; };
+  if (bw == -24) return strict_verify_core<24>(src, SK, btab_lazy{BT, &SK.k.d2}, pa, pr, id);
+  return strict_verify_core<16>(src, SK, btab_wide{BTW, BTW_N}, pa, pr, id);
+}
+
 // The keyed strict path (nw_strict.hpp strict_keyed_comb): the key's comb table entries
 // j * 2^(W t) A computed per lookup (keytab_lazy) by the definition the device's k_key_base /
 // k_key_tabs tabulate, the B comb likewise. Returns the status; -1 when A does not decode is reported through the
