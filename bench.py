@@ -109,13 +109,13 @@ ALG_BYTES_PER_KEYED_VOTE = 96 + 27 * 128
 
 def pmc_issue_peak():
     """Issue-bound peak of k_verify_strict (verifies/s) from its committed PMC instruction mix
-    (the newest of profiles/r06ap/pmc_mix.json — round 6's final two-pass launch (r06ak before it), k_strict_triage +
+    (the newest of profiles/r06as/pmc_mix.json — round 6's final two-pass launch (r06ap, r06ak before it), k_strict_triage +
     k_verify_strict_pre —, r06m's — the one-pass kernel — and r02d's, written by
     tools/pmc_mix.sh + tools/pmc_strict_json.py): per-verify 64-bit / 32-bit integer and
     other VALU lane-ops, each priced at its microbenchmarked issue rate
     (profiles/r01_ubench_valu_4wps.txt; 32-bit integer ops at the half rate, an upper bound
     on their cost). None when no profile is present."""
-    tags = ("r06m", "r02d") if os.environ.get("NW_STRICT_TRIAGE") == "0" else ("r06ap", "r06ak", "r06m", "r02d")
+    tags = ("r06m", "r02d") if os.environ.get("NW_STRICT_TRIAGE") == "0" else ("r06as", "r06ap", "r06ak", "r06m", "r02d")
     for tag in tags:
         rel = os.path.join("profiles", tag, "pmc_mix.json")
         try:
